@@ -1,0 +1,298 @@
+// extern "C" boundary of libfastscnn_hip.so (declared in include/fastscnn.h).
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/fastscnn.h"
+#include "net.hpp"
+
+namespace fscnn {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+const char* last_error() { return g_err; }
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return E_HIP;
+  }
+  return OK;
+}
+
+}  // namespace fscnn
+
+using namespace fscnn;
+
+struct fscnn_net {
+  Net net;
+};
+struct fscnn_plan {
+  Plan plan;
+};
+
+#define GUARD(expr)                                   \
+  try {                                               \
+    return (expr);                                    \
+  } catch (const std::exception& e) {                 \
+    set_error("exception: %s", e.what());             \
+    return E_INVALID;                                 \
+  }
+
+static hipStream_t S(void* s) { return (hipStream_t)s; }
+
+extern "C" {
+
+const char* fscnn_version(void) { return "fastscnn-hip 0.1 (gfx950)"; }
+const char* fscnn_last_error(void) { return last_error(); }
+
+int fscnn_net_create(int num_classes, int aux, fscnn_net** out) {
+  if (!out) { set_error("fscnn_net_create: null out"); return E_INVALID; }
+  fscnn_net* n = new (std::nothrow) fscnn_net();
+  if (!n) { set_error("fscnn_net_create: out of host memory"); return E_INVALID; }
+  int rc = net_build(num_classes, aux, n->net);
+  if (rc) { delete n; return rc; }
+  *out = n;
+  return OK;
+}
+void fscnn_net_destroy(fscnn_net* net) { delete net; }
+
+int fscnn_net_param_count(const fscnn_net* net, int* count, long long* total) {
+  if (!net) { set_error("null net"); return E_INVALID; }
+  if (count) *count = (int)net->net.params.size();
+  if (total) *total = net->net.p_total;
+  return OK;
+}
+int fscnn_net_param_info(const fscnn_net* net, int i, const char** name, long long* offset,
+                         long long* numel) {
+  if (!net || i < 0 || i >= (int)net->net.params.size()) { set_error("bad param index %d", i); return E_INVALID; }
+  const TSpec& t = net->net.params[i];
+  if (name) *name = t.name.c_str();
+  if (offset) *offset = t.off;
+  if (numel) *numel = t.numel;
+  return OK;
+}
+int fscnn_net_buffer_count(const fscnn_net* net, int* count, long long* total, int* num_bn) {
+  if (!net) { set_error("null net"); return E_INVALID; }
+  if (count) *count = (int)net->net.buffers.size();
+  if (total) *total = net->net.r_total;
+  if (num_bn) *num_bn = net->net.n_bn;
+  return OK;
+}
+int fscnn_net_buffer_info(const fscnn_net* net, int i, const char** name, long long* offset,
+                          long long* numel) {
+  if (!net || i < 0 || i >= (int)net->net.buffers.size()) { set_error("bad buffer index %d", i); return E_INVALID; }
+  const TSpec& t = net->net.buffers[i];
+  if (name) *name = t.name.c_str();
+  if (offset) *offset = t.off;
+  if (numel) *numel = t.numel;
+  return OK;
+}
+int fscnn_net_stage_range(const fscnn_net* net, int stage, long long* begin, long long* end) {
+  if (!net || stage < 0 || stage > 3) { set_error("bad stage %d", stage); return E_INVALID; }
+  const Net& n = net->net;
+  *begin = n.stage_p_begin[stage];
+  *end = stage == 0 ? n.p_total : n.stage_p_begin[stage - 1];
+  return OK;
+}
+
+int fscnn_plan_create(const fscnn_net* net, int N, int H, int W, int dtype, int train,
+                      fscnn_plan** out) {
+  if (!net || !out) { set_error("fscnn_plan_create: null argument"); return E_INVALID; }
+  fscnn_plan* p = new (std::nothrow) fscnn_plan();
+  if (!p) { set_error("out of host memory"); return E_INVALID; }
+  int rc = plan_build(net->net, N, H, W, dtype, train, p->plan);
+  if (rc) { delete p; return rc; }
+  *out = p;
+  return OK;
+}
+void fscnn_plan_destroy(fscnn_plan* plan) { delete plan; }
+int fscnn_plan_workspace(const fscnn_plan* plan, long long* fwd, long long* bwd) {
+  if (!plan) { set_error("null plan"); return E_INVALID; }
+  if (fwd) *fwd = (long long)plan->plan.ws_bytes;
+  if (bwd) *bwd = (long long)plan->plan.bws_bytes;
+  return OK;
+}
+int fscnn_plan_shapes(const fscnn_plan* plan, int* d) {
+  if (!plan || !d) { set_error("null plan"); return E_INVALID; }
+  const Plan& p = plan->plan;
+  int v[10] = {p.H1, p.W1, p.H2, p.W2, p.H3, p.W3, p.H4, p.W4, p.H5, p.W5};
+  memcpy(d, v, sizeof v);
+  return OK;
+}
+
+int fscnn_forward(const fscnn_plan* plan, const void* x, int x_dtype, void* out, int out_dtype,
+                  const float* params, float* running, long long* nbt, void* ws,
+                  unsigned long long seed, float dropout_p, float momentum, void* stream) {
+  if (!plan || !x || !out || !params || !running || !ws) {
+    set_error("fscnn_forward: null argument");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.x = x; r.x_dtype = x_dtype; r.out = out; r.out_dtype = out_dtype;
+  r.P = params; r.R = running; r.NBT = nbt; r.ws = ws;
+  r.seed = seed; r.dropout_p = dropout_p; r.momentum = momentum; r.st = S(stream);
+  GUARD(net_forward(plan->plan, r));
+}
+
+int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int x_dtype,
+                   const float* params, float* grads, void* ws, void* bws,
+                   unsigned long long seed, float dropout_p, int stage_from, int stage_to,
+                   void* stream) {
+  if (!plan || !dout || !x || !params || !grads || !ws || !bws) {
+    set_error("fscnn_backward: null argument");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.dout = dout; r.x = x; r.x_dtype = x_dtype; r.P = params; r.G = grads; r.ws = ws; r.bws = bws;
+  r.seed = seed; r.dropout_p = dropout_p; r.st = S(stream);
+  GUARD(net_backward(plan->plan, r, stage_from, stage_to));
+}
+
+long long fscnn_ce_parts(int N, long long HW) { return ce_parts(N, HW); }
+
+int fscnn_ce_fwd(const void* logits, int dtype, const long long* target, int N, int C,
+                 long long HW, long long ignore_index, float* part, float* out2, void* stream) {
+  CeArgs a{};
+  a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target;
+  a.ignore_index = ignore_index; a.part = part;
+  return ce_fwd(a, out2, dtype, S(stream));
+}
+int fscnn_ce_bwd(const void* logits, int dtype, const long long* target, int N, int C,
+                 long long HW, long long ignore_index, const float* grad_out, const float* out2,
+                 void* dlogits, void* stream) {
+  CeArgs a{};
+  a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target;
+  a.ignore_index = ignore_index; a.dlogits = dlogits;
+  return ce_bwd(a, grad_out, out2, dtype, S(stream));
+}
+int fscnn_sgd(float* p, const float* g, float* buf, long long n, float lr, float momentum,
+              float dampening, float weight_decay, int nesterov, int first, float grad_scale,
+              void* stream) {
+  SgdArgs a{};
+  a.n = n; a.p = p; a.g = g; a.buf = buf; a.lr = lr; a.momentum = momentum;
+  a.dampening = dampening; a.weight_decay = weight_decay; a.nesterov = nesterov; a.first = first;
+  a.grad_scale = grad_scale;
+  return sgd(a, S(stream));
+}
+
+int fscnn_conv0_fwd(const void* x, int x_dtype, int N, int H, int W, const float* w,
+                    const float* scale, const float* shift, int relu, void* y, int y_dtype,
+                    void* stream) {
+  Conv0Args a{};
+  a.x = x; a.x_bf16 = x_dtype == DT_BF16; a.N = N; a.H = H; a.W = W;
+  a.Ho = (H - 3) / 2 + 1; a.Wo = (W - 3) / 2 + 1; a.w = w; a.scale = scale; a.shift = shift;
+  a.relu = relu; a.y = y;
+  return conv0_fwd(a, y_dtype, S(stream));
+}
+
+int fscnn_dw3x3_fwd(const void* x, int dtype, int N, int H, int W, int C, int stride,
+                    const float* w, const float* scale, const float* shift, int relu, void* y,
+                    void* stream) {
+  DwArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.stride = stride;
+  a.Ho = (H - 1) / stride + 1; a.Wo = (W - 1) / stride + 1;
+  a.x = x; a.w = w; a.scale = scale; a.shift = shift; a.relu = relu; a.y = y;
+  return dw_fwd(a, dtype, S(stream));
+}
+int fscnn_dw3x3_dgrad(const void* dy, int dtype, int N, int H, int W, int C, int stride,
+                      const float* w, void* dx, void* stream) {
+  DwBwdArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.stride = stride;
+  a.Ho = (H - 1) / stride + 1; a.Wo = (W - 1) / stride + 1;
+  a.dy = dy; a.w = w; a.dx = dx;
+  return dw_dgrad(a, dtype, S(stream));
+}
+long long fscnn_dw3x3_wgrad_slab_floats(int N, int H, int W, int C, int stride, int dtype) {
+  int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  return (long long)dw_wgrad_parts(N, Ho, Wo, C, dtype) * 9 * C;
+}
+int fscnn_dw3x3_wgrad(const void* x, const void* dy, int dtype, int N, int H, int W, int C,
+                      int stride, float* slab, float* dw, void* stream) {
+  DwBwdArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.stride = stride;
+  a.Ho = (H - 1) / stride + 1; a.Wo = (W - 1) / stride + 1;
+  a.x = x; a.dy = dy; a.slab = slab;
+  int rc = dw_wgrad(a, dtype, S(stream));
+  if (rc) return rc;
+  return dw_wgrad_reduce(slab, dw_wgrad_parts(N, a.Ho, a.Wo, C, dtype), C, dw, S(stream));
+}
+
+int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                  int b_trans, const float* scale, const float* shift, const void* R, int ldr,
+                  int relu, void* C, int ldc, float* stats_part, int dtype, void* stream) {
+  GemmArgs a{};
+  a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.b_trans = b_trans;
+  a.scale = scale; a.shift = shift; a.R = R; a.ldr = ldr; a.relu = relu; a.C = C; a.ldc = ldc;
+  a.part = stats_part;
+  return gemm_nt(a, dtype, S(stream));
+}
+long long fscnn_pw_wgrad_slab_floats(int M, int N, int K) {
+  return (long long)gemm_tn_splits(M, N, K) * N * K;
+}
+int fscnn_pw_wgrad(int M, int N, int K, const void* D, int ldd, const void* X, int ldx,
+                   float* slab, float* dW, int dtype, void* stream) {
+  GemmTnArgs a{};
+  a.M = M; a.N = N; a.K = K; a.D = D; a.ldd = ldd; a.X = X; a.ldx = ldx; a.slab = slab;
+  int s = gemm_tn_splits(M, N, K);
+  int rc = gemm_tn(a, s, dtype, S(stream));
+  if (rc) return rc;
+  return reduce_slabs(slab, s, (long long)N * K, (long long)N * K, dW, 0, S(stream));
+}
+
+int fscnn_bn_finalize(const float* part, int P, int C, const float* gamma, const float* beta,
+                      float* rmean, float* rvar, long long* nbt, float momentum, float* mean,
+                      float* invstd, float* scale, float* shift, void* stream) {
+  BnFinalizeArgs a{};
+  a.part = part; a.P = P; a.C = C; a.gamma = gamma; a.beta = beta; a.rmean = rmean;
+  a.rvar = rvar; a.nbt = nbt; a.momentum = momentum; a.mean = mean; a.invstd = invstd;
+  a.scale = scale; a.shift = shift;
+  return bn_finalize(a, S(stream));
+}
+
+int fscnn_bilinear_ac_fwd(const void* x, int dtype, int N, int Hi, int Wi, int C, int Ho, int Wo,
+                          void* y, int out_nchw, int out_dtype, void* stream) {
+  UpArgs a{};
+  a.N = N; a.Hi = Hi; a.Wi = Wi; a.C = C; a.Ho = Ho; a.Wo = Wo; a.x = x; a.ldx = C; a.y = y;
+  a.ldy = C;
+  if (out_nchw) return up_nchw(a, dtype, out_dtype, S(stream));
+  return up_nhwc(a, dtype, S(stream));
+}
+int fscnn_bilinear_ac_bwd(const void* dy, int dtype, int N, int Hi, int Wi, int C, int Ho, int Wo,
+                          float* tmp, void* dx, void* stream) {
+  AxisBwdArgs a{};
+  a.n_o1 = (long long)N * Ho; a.n_o2 = 1; a.Lout = Wo; a.Lin = Wi; a.n_in = C;
+  a.g = dy; a.g_s1 = (long long)Wo * C; a.g_idx = C; a.g_in = 1;
+  a.d = tmp; a.d_s1 = (long long)Wi * C; a.d_idx = C; a.d_in = 1;
+  int rc = axis_bwd(a, dtype, DT_F32, S(stream));
+  if (rc) return rc;
+  AxisBwdArgs b{};
+  b.n_o1 = N; b.n_o2 = 1; b.Lout = Ho; b.Lin = Hi; b.n_in = (long long)Wi * C;
+  b.g = tmp; b.g_s1 = (long long)Ho * Wi * C; b.g_idx = (long long)Wi * C; b.g_in = 1;
+  b.d = dx; b.d_s1 = (long long)Hi * Wi * C; b.d_idx = (long long)Wi * C; b.d_in = 1;
+  return axis_bwd(b, DT_F32, dtype, S(stream));
+}
+int fscnn_pyramid_pool_fwd(const void* x, int dtype, int N, int H, int W, int C, int ldx,
+                           void* pooled, void* stream) {
+  PoolArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.x = x; a.ldx = ldx; a.pooled = pooled;
+  return pyramid_pool(a, dtype, S(stream));
+}
+int fscnn_pyramid_pool_bwd(const void* dpooled, int dtype, int N, int H, int W, int C, void* dx,
+                           int lddx, int accumulate, void* stream) {
+  PoolBwdArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.dpooled = dpooled; a.dx = dx; a.lddx = lddx;
+  a.accumulate = accumulate;
+  return pyramid_pool_bwd(a, dtype, S(stream));
+}
+
+}  // extern "C"

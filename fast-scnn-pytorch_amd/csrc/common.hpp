@@ -1,0 +1,135 @@
+// Shared device/host helpers for the Fast-SCNN gfx950 kernels.
+//
+// Layout conventions: activations are NHWC ("[M rows = N*H*W][C channels]",
+// channels contiguous) in the storage type T (float or bf16); every kernel computes in fp32.
+// Per-channel BatchNorm statistics travel as "partial records" [part][3][C] = (mean, M2, count)
+// merged with Chan's parallel formula, so every reduction is deterministic (fixed order) and
+// free of the E[x^2]-E[x]^2 cancellation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace fscnn {
+
+enum DType : int { DT_F32 = 0, DT_BF16 = 1 };
+
+struct bf16 {
+  uint16_t x;
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);  // RNE; lowers to v_cvt_pk_bf16_f32 on gfx950
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+// Elements per 16-byte vector.
+template <typename T> struct VecW;
+template <> struct VecW<float> { static constexpr int V = 4; };
+template <> struct VecW<bf16> { static constexpr int V = 8; };
+
+// ---- scalar load/store in storage type -------------------------------------------------------
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16* p) { return bf2f(p->x); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16* p, float v) { p->x = f2bf(v); }
+
+// ---- 16-byte vector load/store (p must be 16 B aligned) --------------------------------------
+__device__ __forceinline__ void ldv(const float* p, float (&v)[4]) {
+  float4 t = *reinterpret_cast<const float4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+__device__ __forceinline__ void ldv(const bf16* p, float (&v)[8]) {
+  uint4 t = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+__device__ __forceinline__ void stv(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void stv(bf16* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ---- Chan parallel merge of (count, mean, M2) ------------------------------------------------
+struct Welford {
+  double n, mean, m2;
+};
+__device__ __forceinline__ Welford wf_merge(Welford a, Welford b) {
+  double n = a.n + b.n;
+  if (n == 0.0) return a;
+  double d = b.mean - a.mean;
+  double f = b.n / n;
+  Welford r;
+  r.n = n;
+  r.mean = a.mean + d * f;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * f;
+  return r;
+}
+
+// ---- dropout keep-mask: a pure function of (seed, NCHW linear index) -------------------------
+// Must match oracle/fast_scnn_ref.py:dropout_mask bit for bit.
+// keep iff (hash >> 40) >= thr, thr = ceil(p * 2^24)  (<=> 24-bit uniform u >= p)
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
+  uint64_t z = idx * 0x9E3779B97F4A7C15ull + seed;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  return (uint32_t)(z >> 40) >= thr;
+}
+inline uint32_t dropout_threshold(float p) {
+  double t = (double)p * 16777216.0;
+  uint32_t k = (uint32_t)t;
+  return ((double)k < t) ? k + 1 : k;
+}
+
+// ---- align_corners=True source index (aten compute_source_index_and_lambda) ------------------
+struct Lerp {
+  int i0, i1;
+  float l0, l1;
+};
+__host__ __device__ __forceinline__ float ac_scale(int in, int out) {
+  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.0f;
+}
+__host__ __device__ __forceinline__ Lerp ac_lerp(int o, int in, int out, float scale) {
+  Lerp r;
+  if (in == out) {
+    r.i0 = o; r.i1 = o; r.l0 = 1.0f; r.l1 = 0.0f;
+    return r;
+  }
+  float real = scale * (float)o;
+  int i0 = (int)floorf(real);
+  if (i0 > in - 1) i0 = in - 1;
+  float lam = real - (float)i0;
+  lam = lam < 0.f ? 0.f : (lam > 1.f ? 1.f : lam);
+  r.i0 = i0;
+  r.i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  r.l1 = lam;
+  r.l0 = 1.0f - lam;
+  return r;
+}
+
+// ---- error reporting ----------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+const char* last_error();
+int check_launch(const char* what);
+
+enum Status : int { OK = 0, E_INVALID = -1, E_UNSUPPORTED = -2, E_HIP = -3 };
+
+__host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace fscnn

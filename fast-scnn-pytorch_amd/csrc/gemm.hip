@@ -1,0 +1,508 @@
+// Pointwise 1x1 convolution as MFMA-tiled channel contractions (every nn.Conv2d(k=1) of
+// models/fast_scnn.py: :73 _DSConv pw, :103/:107 bottleneck expand/project, :124-128 PPM,
+// :198/:202 FFM, :230 classifier).  NHWC makes a 1x1 conv the row-major GEMM
+//     C[m][n] = sum_k A[m][k] * W[n][k]      (m = pixel, k = Cin, n = Cout)
+// with both operands k-contiguous ("NT"), which is exactly the operand order MFMA fragments
+// want: lane l holds A[row l&15][8 consecutive k] (bf16 16x16x32) or A[row l&15][k] (fp32
+// 16x16x4), so every fragment is one ds_read_b128 from a [row][k] LDS image.
+//
+// gemm_nt   forward and dgrad (dgrad reads W^T through the "b_trans" staging path).  Tile
+//           128 rows x 16*NT cols, 4 waves of 32 rows, K staged in 128-B chunks (32 fp32 /
+//           64 bf16), register-staged double-buffered LDS.  Epilogue fuses conv bias, BN
+//           (scale/shift), residual add, ReLU and, in train mode, the per-channel BN statistics
+//           (mean, M2, count) of the output tile.
+// gemm_tn   weight gradient dW[n][k] = sum_m dY[m][n] X[m][k], split over m into partial
+//           slabs reduced in fixed order (deterministic).
+//
+// fp32 storage uses v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulate); bf16 storage
+// uses v_mfma_f32_16x16x32_bf16 with f32 accumulation.  Roofline: MFMA-bound only when the
+// tile's K and N are large; most Fast-SCNN 1x1 convs are HBM-bound.
+#include "kernels.hpp"
+
+namespace fscnn {
+
+
+constexpr int G_BM = 128;
+constexpr int G_VROW = 8;   // 16-B vectors per row per K chunk (128 B)
+constexpr int G_VPAD = 9;   // LDS row stride in vectors
+
+template <typename T>
+struct MfmaOp;
+
+template <>
+struct MfmaOp<float> {
+  // one 16-B vector per lane = 4 k-steps of 16x16x4
+  static __device__ __forceinline__ void run(const uint4& a, const uint4& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+
+template <>
+struct MfmaOp<bf16> {
+  static __device__ __forceinline__ void run(const uint4& a, const uint4& b, f32x4& acc) {
+    i16x8 av, bv;
+    __builtin_memcpy(&av, &a, 16);
+    __builtin_memcpy(&bv, &b, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ uint4 zero_tail(uint4 v, int valid) {
+  // zero the elements >= valid (valid in [0, V)) of a 16-B vector
+  constexpr int V = VecW<T>::V;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if (V == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j >= valid) w[j] = 0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j >= valid) w[j >> 1] &= (j & 1) ? 0x0000FFFFu : 0xFFFF0000u;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <typename T, int NT, bool BT>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
+  constexpr int V = VecW<T>::V;
+  constexpr int BN = 16 * NT;
+  constexpr int KC = G_VROW * V;  // k elements per chunk
+  __shared__ uint4 sA[2][G_BM * G_VPAD];
+  __shared__ uint4 sB[2][BN * G_VPAD];
+  __shared__ float s_red[4][BN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int m0 = blockIdx.x * G_BM;
+  const int n0 = blockIdx.y * BN;
+  const T* A = (const T*)a.A;
+  const T* B = (const T*)a.B;
+  const int nchunks = (a.K + KC - 1) / KC;
+
+  // ---- staging registers --------------------------------------------------------------------
+  constexpr int A_PER = G_BM * G_VROW / 256;            // 4
+  constexpr int B_PER = (BN * G_VROW + 255) / 256;      // vectors per thread (non-trans)
+  uint4 ra[A_PER];
+  uint4 rb[BT ? 1 : B_PER];
+  // transposed-B staging: KC rows (k) x BN cols (n) of scalars, held as raw 16-B vectors along n
+  constexpr int BT_VEC = KC * BN / V;                   // vectors per chunk
+  constexpr int BT_PER = (BT_VEC + 255) / 256;
+  uint4 rbt[BT ? BT_PER : 1];
+
+  auto load_chunk = [&](int c) {
+    const int k0 = c * KC;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int id = tid + 256 * i;
+      int row = id >> 3, vv = id & 7;
+      int m = m0 + row, k = k0 + vv * V;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < a.M && k < a.K) {
+        v = *reinterpret_cast<const uint4*>(A + (size_t)m * a.lda + k);
+        if (k + V > a.K) v = zero_tail<T>(v, a.K - k);
+      }
+      ra[i] = v;
+    }
+    if (!BT) {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        int id = tid + 256 * i;
+        int row = id >> 3, vv = id & 7;
+        int n = n0 + row, k = k0 + vv * V;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (id < BN * G_VROW && n < a.N && k < a.K) {
+          v = *reinterpret_cast<const uint4*>(B + (size_t)n * a.ldb + k);
+          if (k + V > a.K) v = zero_tail<T>(v, a.K - k);
+        }
+        rb[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BT_PER; ++i) {
+        int id = tid + 256 * i;
+        int kk = id / (BN / V), nv = id - kk * (BN / V);
+        int k = k0 + kk, n = n0 + nv * V;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (id < BT_VEC && k < a.K && n < a.N) {
+          v = *reinterpret_cast<const uint4*>(B + (size_t)k * a.ldb + n);
+          if (n + V > a.N) v = zero_tail<T>(v, a.N - n);
+        }
+        rbt[i] = v;
+      }
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int id = tid + 256 * i;
+      sA[buf][(id >> 3) * G_VPAD + (id & 7)] = ra[i];
+    }
+    if (!BT) {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        int id = tid + 256 * i;
+        if (id < BN * G_VROW) sB[buf][(id >> 3) * G_VPAD + (id & 7)] = rb[i];
+      }
+    } else {
+      T* sbs = reinterpret_cast<T*>(&sB[buf][0]);
+#pragma unroll
+      for (int i = 0; i < BT_PER; ++i) {
+        int id = tid + 256 * i;
+        if (id < BT_VEC) {
+          int kk = id / (BN / V), nv = id - kk * (BN / V);
+          const T* e = reinterpret_cast<const T*>(&rbt[i]);
+#pragma unroll
+          for (int j = 0; j < V; ++j) sbs[(nv * V + j) * G_VPAD * V + kk] = e[j];
+        }
+      }
+    }
+  };
+
+  f32x4 acc[2][NT];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunks) load_chunk(c + 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int vv = lq + 4 * h;
+      uint4 af[2], bfv[NT];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) af[mt] = sA[buf][(wave * 32 + mt * 16 + li) * G_VPAD + vv];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB[buf][(nt * 16 + li) * G_VPAD + vv];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
+    }
+    if (c + 1 < nchunks) store_chunk(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue -------------------------------------------------------------------------------
+  T* Cp = (T*)a.C;
+  const T* Rp = (const T*)a.R;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = n0 + nt * 16 + li;
+    const bool nok = n < a.N;
+    const float sc = (nok && a.scale) ? a.scale[n] : 1.f;
+    const float sh = (nok && a.shift) ? a.shift[n] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
+        float v = acc[mt][nt][r] * sc + sh;
+        if (nok && m < a.M) {
+          if (Rp) v += ld1(Rp + (size_t)m * a.ldr + n);
+          if (a.relu) v = fmaxf(v, 0.f);
+          st1(Cp + (size_t)m * a.ldc + n, v);
+        }
+        acc[mt][nt][r] = v;
+      }
+    }
+  }
+  if (a.part == nullptr) return;
+
+  // ---- train-mode BN statistics of the output tile (per column: mean, M2, count) ----------
+  const int valid_rows = min(G_BM, a.M - m0);
+  float mean_c[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    float s = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
+        s += (m < a.M) ? acc[mt][nt][r] : 0.f;
+      }
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (lq == 0) s_red[wave][nt * 16 + li] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    int col = nt * 16 + li;
+    mean_c[nt] = (s_red[0][col] + s_red[1][col] + s_red[2][col] + s_red[3][col]) / (float)valid_rows;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    float s = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
+        float d = acc[mt][nt][r] - mean_c[nt];
+        s += (m < a.M) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (lq == 0) s_red[wave][nt * 16 + li] = s;
+  }
+  __syncthreads();
+  if (wave == 0 && lq == 0) {
+    float* rec = a.part + (size_t)blockIdx.x * 3 * a.N;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      int col = nt * 16 + li, n = n0 + col;
+      if (n < a.N) {
+        rec[n] = mean_c[nt];
+        rec[a.N + n] = s_red[0][col] + s_red[1][col] + s_red[2][col] + s_red[3][col];
+        rec[2 * a.N + n] = (float)valid_rows;
+      }
+    }
+  }
+}
+
+static int pick_nt(int N) {
+  if (N <= 32) return 2;
+  if (N <= 48) return 3;
+  if (N <= 64) return 4;
+  if (N % 96 == 0) return 6;
+  return 8;
+}
+
+int gemm_parts(int M) { return cdiv(M, G_BM); }
+
+template <typename T, bool BT>
+static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
+  dim3 grid(cdiv(a.M, G_BM), cdiv(a.N, 16 * nt));
+  switch (nt) {
+    case 2: gemm_nt_kernel<T, 2, BT><<<grid, 256, 0, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT><<<grid, 256, 0, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT><<<grid, 256, 0, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT><<<grid, 256, 0, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT><<<grid, 256, 0, st>>>(a); break;
+  }
+}
+
+int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
+  const int V = dtype == DT_F32 ? 4 : 8;
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) {
+    set_error("gemm_nt: empty problem M=%d N=%d K=%d", a.M, a.N, a.K);
+    return E_INVALID;
+  }
+  if (a.lda % V || (uintptr_t)a.A % 16 || (uintptr_t)a.B % 16 || a.ldb % V ||
+      (a.b_trans && a.N % 1)) {
+    set_error("gemm_nt: operands must be 16-B aligned with ld multiple of %d (lda=%d ldb=%d)", V,
+              a.lda, a.ldb);
+    return E_INVALID;
+  }
+  if (a.part && cdiv(a.N, 16 * pick_nt(a.N)) > 0 && a.R) {
+    set_error("gemm_nt: statistics with residual not supported");
+    return E_UNSUPPORTED;
+  }
+  int nt = pick_nt(a.N);
+  if (dtype == DT_F32) {
+    if (a.b_trans) launch_nt<float, true>(a, nt, st);
+    else launch_nt<float, false>(a, nt, st);
+  } else {
+    if (a.b_trans) launch_nt<bf16, true>(a, nt, st);
+    else launch_nt<bf16, false>(a, nt, st);
+  }
+  return check_launch("gemm_nt");
+}
+
+// =============================================================================================
+// Weight gradient: dW[n][k] = sum_m D[m][n] * X[m][k]  (D = dY, X = layer input activation)
+// =============================================================================================
+
+constexpr int TN_T = 64;    // output tile 64 (n) x 64 (k)
+constexpr int TN_MC = 32;   // rows per staged chunk
+constexpr int TN_PAD = 8;   // elements of row padding in LDS
+
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
+  constexpr int V = VecW<T>::V;
+  constexpr int LDS_LD = TN_T + TN_PAD;
+  __shared__ T sD[TN_MC * LDS_LD];
+  __shared__ T sX[TN_MC * LDS_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int tiles_k = cdiv(a.K, TN_T);
+  const int tn = blockIdx.x / tiles_k, tk = blockIdx.x - tn * tiles_k;
+  const int n0 = tn * TN_T, k0 = tk * TN_T;
+  const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;  // wave sub-tile
+  const int mb = blockIdx.y * a.rows_per_split;
+  const int me = min(a.M, mb + a.rows_per_split);
+  const T* D = (const T*)a.D;
+  const T* X = (const T*)a.X;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int VPR = TN_T / V;                 // vectors per staged row
+  constexpr int PER = TN_MC * VPR / 256;        // vectors per thread per operand (2 f32 / 1 bf16)
+  for (int mc = mb; mc < me; mc += TN_MC) {
+    uint4 rd[PER], rx[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int id = tid + 256 * i;
+      int r = id / VPR, vv = id - r * VPR;
+      int m = mc + r;
+      int n = n0 + vv * V, k = k0 + vv * V;
+      uint4 d = make_uint4(0, 0, 0, 0), x = make_uint4(0, 0, 0, 0);
+      if (m < me) {
+        if (n < a.N) {
+          d = *reinterpret_cast<const uint4*>(D + (size_t)m * a.ldd + n);
+          if (n + V > a.N) d = zero_tail<T>(d, a.N - n);
+        }
+        if (k < a.K) {
+          x = *reinterpret_cast<const uint4*>(X + (size_t)m * a.ldx + k);
+          if (k + V > a.K) x = zero_tail<T>(x, a.K - k);
+        }
+      }
+      rd[i] = d;
+      rx[i] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int id = tid + 256 * i;
+      int r = id / VPR, vv = id - r * VPR;
+      *reinterpret_cast<uint4*>(&sD[r * LDS_LD + vv * V]) = rd[i];
+      *reinterpret_cast<uint4*>(&sX[r * LDS_LD + vv * V]) = rx[i];
+    }
+    __syncthreads();
+    if constexpr (V == 4) {
+      // fp32: 8 steps of 16x16x4, step s covers rows 4s..4s+3 (row 4s+lq for this lane)
+#pragma unroll
+      for (int s = 0; s < TN_MC / 4; ++s) {
+        const int r = 4 * s + lq;
+        float av[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) av[i] = sD[r * LDS_LD + wn + i * 16 + li];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = sX[r * LDS_LD + wk + j * 16 + li];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // bf16: one 16x16x32 step; lane needs rows 8*lq .. 8*lq+7 of its column
+      i16x8 av[2], bv[2];
+      const short* sd = reinterpret_cast<const short*>(sD);
+      const short* sx = reinterpret_cast<const short*>(sX);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * lq + j;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          av[i][j] = sd[r * LDS_LD + wn + i * 16 + li];
+          bv[i][j] = sx[r * LDS_LD + wk + i * 16 + li];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // write the block's partial tile: slab[split][n][k]; acc[i][j][r]: n = wn+i*16+lq*4+r, k = wk+j*16+li
+  float* sl = a.slab + (size_t)blockIdx.y * a.N * a.K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int n = n0 + wn + i * 16 + lq * 4 + r, k = k0 + wk + j * 16 + li;
+        if (n < a.N && k < a.K) sl[(size_t)n * a.K + k] = acc[i][j][r];
+      }
+}
+
+int gemm_tn_splits(int M, int N, int K) {
+  int tiles = cdiv(N, TN_T) * cdiv(K, TN_T);
+  int s = 2048 / tiles;
+  int smax = cdiv(M, 256);
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  return s;
+}
+
+int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
+  const int V = dtype == DT_F32 ? 4 : 8;
+  if (a.ldd % V || a.ldx % V || (uintptr_t)a.D % 16 || (uintptr_t)a.X % 16) {
+    set_error("gemm_tn: operands must be 16-B aligned (ldd=%d ldx=%d)", a.ldd, a.ldx);
+    return E_INVALID;
+  }
+  a.rows_per_split = cdiv(cdiv(a.M, splits), TN_MC) * TN_MC;
+  dim3 grid(cdiv(a.N, TN_T) * cdiv(a.K, TN_T), splits);
+  if (dtype == DT_F32) gemm_tn_kernel<float><<<grid, 256, 0, st>>>(a);
+  else gemm_tn_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  return check_launch("gemm_tn");
+}
+
+// out[i] = sum_{s<S} slab[s*stride + i]  (fixed order), optionally out += (accumulate)
+__global__ void reduce_slabs_kernel(const float* slab, int S, long long stride, long long count,
+                                    float* out, int accumulate) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += slab[(size_t)k * stride + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+int reduce_slabs(const float* slab, int S, long long stride, long long count, float* out,
+                 int accumulate, hipStream_t st) {
+  reduce_slabs_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slab, S, stride, count, out,
+                                                                        accumulate);
+  return check_launch("reduce_slabs");
+}
+
+// per-block column sums of D [M][N] (ld) -> part [P][N]  (bias gradients)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* D, int M, int N, int ld,
+                                                     int rows_per_block, float* part) {
+  int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  int g = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (n < N) {
+    int mb = blockIdx.y * rows_per_block, me = min(M, mb + rows_per_block);
+    for (int m = mb + g; m < me; m += 4) s += ld1(D + (size_t)m * ld + n);
+  }
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && n < N)
+    part[(size_t)blockIdx.y * N + n] = red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                       red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+int colsum_parts(int M) { int p = cdiv(M, 1024); return p > 1024 ? 1024 : p; }
+
+int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStream_t st) {
+  int P = colsum_parts(M);
+  int rpb = cdiv(M, P);
+  dim3 grid(cdiv(N, 64), P);
+  if (dtype == DT_F32) colsum_kernel<float><<<grid, 256, 0, st>>>((const float*)D, M, N, ld, rpb, part);
+  else colsum_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)D, M, N, ld, rpb, part);
+  return check_launch("colsum");
+}
+
+}  // namespace fscnn

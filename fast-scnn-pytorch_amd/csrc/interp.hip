@@ -1,0 +1,305 @@
+// Bilinear upsampling with align_corners=True (models/fast_scnn.py:40 final logits, :135 PPM
+// features, :212 FFM lower-resolution branch) and the pyramid pooling reduce
+// AdaptiveAvgPool2d(1,2,3,6) (:130-132, overlapping windows).
+//
+// The source index / lambda law is aten's compute_source_index_and_lambda in fp32
+// (common.hpp ac_lerp), so the GPU reproduces the CPU oracle's weights exactly.
+// Backward passes are separable GATHERS along one axis at a time (no atomics, deterministic):
+// for input index i the contributing outputs form the contiguous range [lo(i), hi(i)) found by
+// binary search on the monotone i0(o).
+#include "kernels.hpp"
+
+namespace fscnn {
+
+// ---- forward NHWC -> NHWC (optionally into a channel slice of a wider buffer) ---------------
+
+template <typename T>
+__global__ __launch_bounds__(256) void up_nhwc_kernel(UpArgs a) {
+  constexpr int V = VecW<T>::V;
+  const int CV = a.C / V;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)a.N * a.Ho * a.Wo * CV;
+  if (i >= total) return;
+  int cv = (int)(i % CV);
+  long long pix = i / CV;
+  int wo = (int)(pix % a.Wo);
+  long long r = pix / a.Wo;
+  int ho = (int)(r % a.Ho);
+  int n = (int)(r / a.Ho);
+  Lerp lh = ac_lerp(ho, a.Hi, a.Ho, ac_scale(a.Hi, a.Ho));
+  Lerp lw = ac_lerp(wo, a.Wi, a.Wo, ac_scale(a.Wi, a.Wo));
+  const T* xb = (const T*)a.x + (size_t)n * a.Hi * a.Wi * a.ldx + cv * V;
+  float p00[V], p01[V], p10[V], p11[V], o[V];
+  ldv(xb + ((size_t)lh.i0 * a.Wi + lw.i0) * a.ldx, p00);
+  ldv(xb + ((size_t)lh.i0 * a.Wi + lw.i1) * a.ldx, p01);
+  ldv(xb + ((size_t)lh.i1 * a.Wi + lw.i0) * a.ldx, p10);
+  ldv(xb + ((size_t)lh.i1 * a.Wi + lw.i1) * a.ldx, p11);
+#pragma unroll
+  for (int j = 0; j < V; ++j)
+    o[j] = lh.l0 * (lw.l0 * p00[j] + lw.l1 * p01[j]) + lh.l1 * (lw.l0 * p10[j] + lw.l1 * p11[j]);
+  stv((T*)a.y + pix * a.ldy + cv * V, o);
+}
+
+int up_nhwc(const UpArgs& a, int dtype, hipStream_t st) {
+  int V = dtype == DT_F32 ? 4 : 8;
+  if (a.C % V || a.ldx % V || a.ldy % V) {
+    set_error("up_nhwc: C=%d ldx=%d ldy=%d must be multiples of %d", a.C, a.ldx, a.ldy, V);
+    return E_INVALID;
+  }
+  long long total = (long long)a.N * a.Ho * a.Wo * (a.C / V);
+  unsigned grid = (unsigned)((total + 255) / 256);
+  if (dtype == DT_F32) up_nhwc_kernel<float><<<grid, 256, 0, st>>>(a);
+  else up_nhwc_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  return check_launch("up_nhwc");
+}
+
+// ---- forward NHWC (padded channels) -> NCHW logits (the final F.interpolate) -----------------
+// One thread per output pixel; lanes run along wo so every per-class plane store is coalesced.
+template <typename TI, typename TO, int CMAX>
+__global__ __launch_bounds__(256) void up_nchw_kernel(UpArgs a) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)a.N * a.Ho * a.Wo;
+  if (i >= total) return;
+  int wo = (int)(i % a.Wo);
+  long long r = i / a.Wo;
+  int ho = (int)(r % a.Ho);
+  int n = (int)(r / a.Ho);
+  Lerp lh = ac_lerp(ho, a.Hi, a.Ho, ac_scale(a.Hi, a.Ho));
+  Lerp lw = ac_lerp(wo, a.Wi, a.Wo, ac_scale(a.Wi, a.Wo));
+  const TI* xb = (const TI*)a.x + (size_t)n * a.Hi * a.Wi * a.ldx;
+  const TI* q00 = xb + ((size_t)lh.i0 * a.Wi + lw.i0) * a.ldx;
+  const TI* q01 = xb + ((size_t)lh.i0 * a.Wi + lw.i1) * a.ldx;
+  const TI* q10 = xb + ((size_t)lh.i1 * a.Wi + lw.i0) * a.ldx;
+  const TI* q11 = xb + ((size_t)lh.i1 * a.Wi + lw.i1) * a.ldx;
+  TO* yb = (TO*)a.y + (size_t)n * a.C * a.Ho * a.Wo + (size_t)ho * a.Wo + wo;
+  const size_t plane = (size_t)a.Ho * a.Wo;
+#pragma unroll 4
+  for (int c = 0; c < a.C; ++c) {
+    float o = lh.l0 * (lw.l0 * ld1(q00 + c) + lw.l1 * ld1(q01 + c)) +
+              lh.l1 * (lw.l0 * ld1(q10 + c) + lw.l1 * ld1(q11 + c));
+    st1(yb + c * plane, o);
+  }
+}
+
+int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
+  long long total = (long long)a.N * a.Ho * a.Wo;
+  unsigned grid = (unsigned)((total + 255) / 256);
+  if (in_dtype == DT_F32 && out_dtype == DT_F32) up_nchw_kernel<float, float, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) up_nchw_kernel<bf16, bf16, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_BF16 && out_dtype == DT_F32) up_nchw_kernel<bf16, float, 0><<<grid, 256, 0, st>>>(a);
+  else up_nchw_kernel<float, bf16, 0><<<grid, 256, 0, st>>>(a);
+  return check_launch("up_nchw");
+}
+
+// ---- backward: gather along one axis --------------------------------------------------------
+// Element (o1, o2, i, x) of the grad wrt the forward INPUT (i < Lin along the interpolated axis)
+// is the sum over forward outputs p (< Lout) that read index i of w(p, i) * g(o1, o2, p, x).
+// Every coordinate has its own stride on both sides, so the same kernel serves NCHW logits and
+// NHWC activations.  Threads run fastest along x.
+
+__device__ __forceinline__ int first_out_with_i0_ge(int i, int Lin, int Lout, float sc) {
+  // smallest p with i0(p) >= i (i0 monotone non-decreasing in p)
+  int lo = 0, hi = Lout;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (ac_lerp(mid, Lin, Lout, sc).i0 >= i) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+template <typename TG, typename TD>
+__global__ __launch_bounds__(256) void axis_bwd_kernel(AxisBwdArgs a) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = a.n_o1 * a.n_o2 * a.Lin * a.n_in;
+  if (t >= total) return;
+  long long x = t % a.n_in;
+  long long r = t / a.n_in;
+  int i = (int)(r % a.Lin);
+  long long o = r / a.Lin;
+  long long o2 = o % a.n_o2, o1 = o / a.n_o2;
+  const float sc = ac_scale(a.Lin, a.Lout);
+  // contributors: outputs p with i0(p) in {i-1, i}  (i1 = i0 or i0+1)
+  int p_lo = first_out_with_i0_ge(i - 1, a.Lin, a.Lout, sc);
+  int p_hi = first_out_with_i0_ge(i + 1, a.Lin, a.Lout, sc);
+  const TG* gb = (const TG*)a.g + o1 * a.g_s1 + o2 * a.g_s2 + x * a.g_in;
+  float s = 0.f;
+  for (int p = p_lo; p < p_hi; ++p) {
+    Lerp l = ac_lerp(p, a.Lin, a.Lout, sc);
+    float w = (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
+    s += w * ld1(gb + (size_t)p * a.g_idx);
+  }
+  TD* dp = (TD*)a.d + o1 * a.d_s1 + o2 * a.d_s2 + (long long)i * a.d_idx + x * a.d_in;
+  if (a.accumulate) s += ld1(dp);
+  st1(dp, s);
+}
+
+int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st) {
+  long long total = a.n_o1 * a.n_o2 * a.Lin * a.n_in;
+  unsigned grid = (unsigned)((total + 255) / 256);
+  if (g_dtype == DT_F32 && d_dtype == DT_F32) axis_bwd_kernel<float, float><<<grid, 256, 0, st>>>(a);
+  else if (g_dtype == DT_BF16 && d_dtype == DT_BF16) axis_bwd_kernel<bf16, bf16><<<grid, 256, 0, st>>>(a);
+  else if (g_dtype == DT_BF16 && d_dtype == DT_F32) axis_bwd_kernel<bf16, float><<<grid, 256, 0, st>>>(a);
+  else axis_bwd_kernel<float, bf16><<<grid, 256, 0, st>>>(a);
+  return check_launch("axis_bwd");
+}
+
+// ---- pyramid pooling: AdaptiveAvgPool2d(1), (2), (3), (6) in one launch ----------------------
+// pooled layout: [N][50 bins][C] with bins ordered level-major (1x1, 2x2, 3x3, 6x6), row-major.
+constexpr int PP_LEVELS[4] = {1, 2, 3, 6};
+__device__ __forceinline__ void pp_bin(int b, int& k, int& bi, int& bj) {
+  if (b < 1) { k = 1; b -= 0; }
+  else if (b < 5) { k = 2; b -= 1; }
+  else if (b < 14) { k = 3; b -= 5; }
+  else { k = 6; b -= 14; }
+  bi = b / k;
+  bj = b - bi * k;
+}
+__host__ __device__ __forceinline__ int pp_start(int i, int in, int k) { return (i * in) / k; }
+__host__ __device__ __forceinline__ int pp_end(int i, int in, int k) { return ((i + 1) * in + k - 1) / k; }
+
+
+template <typename T>
+__global__ __launch_bounds__(128) void pyramid_pool_kernel(PoolArgs a) {
+  const int b = blockIdx.x, n = blockIdx.y;
+  int k, bi, bj;
+  pp_bin(b, k, bi, bj);
+  int h0 = pp_start(bi, a.H, k), h1 = pp_end(bi, a.H, k);
+  int w0 = pp_start(bj, a.W, k), w1 = pp_end(bj, a.W, k);
+  float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+  const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.ldx;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float s = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) s += ld1(xb + ((size_t)h * a.W + w) * a.ldx + c);
+    st1((T*)a.pooled + ((size_t)b * a.N + n) * a.C + c, s * inv);
+  }
+}
+
+int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
+  dim3 grid(50, a.N);
+  if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 128, 0, st>>>(a);
+  else pyramid_pool_kernel<bf16><<<grid, 128, 0, st>>>(a);
+  return check_launch("pyramid_pool");
+}
+
+// backward: dx[n,h,w,c] (+)= sum_levels sum_{bins containing (h,w)} dpooled[bin,n,c] / area
+
+template <typename T>
+__global__ __launch_bounds__(256) void pyramid_pool_bwd_kernel(PoolBwdArgs a) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)a.N * a.H * a.W * a.C;
+  if (t >= total) return;
+  int c = (int)(t % a.C);
+  long long pix = t / a.C;
+  int w = (int)(pix % a.W);
+  long long r = pix / a.W;
+  int h = (int)(r % a.H);
+  int n = (int)(r / a.H);
+  float s = 0.f;
+  int base = 0;
+#pragma unroll
+  for (int lv = 0; lv < 4; ++lv) {
+    const int k = PP_LEVELS[lv];
+    // all bins whose (possibly overlapping, possibly > input size) window holds (h, w)
+    for (int bi = 0; bi < k; ++bi) {
+      int h0 = pp_start(bi, a.H, k), h1 = pp_end(bi, a.H, k);
+      if (h < h0 || h >= h1) continue;
+      for (int bj = 0; bj < k; ++bj) {
+        int w0 = pp_start(bj, a.W, k), w1 = pp_end(bj, a.W, k);
+        if (w < w0 || w >= w1) continue;
+        s += ld1((const T*)a.dpooled + ((size_t)(base + bi * k + bj) * a.N + n) * a.C + c) /
+             (float)((h1 - h0) * (w1 - w0));
+      }
+    }
+    base += k * k;
+  }
+  T* dp = (T*)a.dx + pix * a.lddx + c;
+  if (a.accumulate) s += ld1(dp);
+  st1(dp, s);
+}
+
+int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st) {
+  long long total = (long long)a.N * a.H * a.W * a.C;
+  unsigned grid = (unsigned)((total + 255) / 256);
+  if (dtype == DT_F32) pyramid_pool_bwd_kernel<float><<<grid, 256, 0, st>>>(a);
+  else pyramid_pool_bwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  return check_launch("pyramid_pool_bwd");
+}
+
+// ---- PPM feature upsampling: all 4 levels into the concat buffer in one launch --------------
+// feats: bin-major [50][N][CF] (CF = 32); y: concat NHWC [N,H,W] with row stride ldy, level i
+// written to channels [coff + i*CF, coff + (i+1)*CF).   (models/fast_scnn.py:139-143)
+
+template <typename T>
+__global__ __launch_bounds__(256) void ppm_up_fwd_kernel(PpmUpArgs a) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int CT = 4 * a.CF;
+  long long total = (long long)a.N * a.H * a.W * CT;
+  if (t >= total) return;
+  int cc = (int)(t % CT);
+  long long pix = t / CT;
+  int w = (int)(pix % a.W);
+  long long r = pix / a.W;
+  int h = (int)(r % a.H);
+  int n = (int)(r / a.H);
+  int lv = cc / a.CF, c = cc - lv * a.CF;
+  const int k = PP_LEVELS[lv];
+  const int base = lv == 0 ? 0 : (lv == 1 ? 1 : (lv == 2 ? 5 : 14));
+  Lerp lh = ac_lerp(h, k, a.H, ac_scale(k, a.H));
+  Lerp lw = ac_lerp(w, k, a.W, ac_scale(k, a.W));
+  const T* f = (const T*)a.feats;
+  auto F = [&](int i, int j) { return ld1(f + ((size_t)(base + i * k + j) * a.N + n) * a.CF + c); };
+  float o = lh.l0 * (lw.l0 * F(lh.i0, lw.i0) + lw.l1 * F(lh.i0, lw.i1)) +
+            lh.l1 * (lw.l0 * F(lh.i1, lw.i0) + lw.l1 * F(lh.i1, lw.i1));
+  st1((T*)a.y + pix * a.ldy + a.coff + cc, o);
+}
+
+int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
+  long long total = (long long)a.N * a.H * a.W * 4 * a.CF;
+  unsigned grid = (unsigned)((total + 255) / 256);
+  if (dtype == DT_F32) ppm_up_fwd_kernel<float><<<grid, 256, 0, st>>>(a);
+  else ppm_up_fwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  return check_launch("ppm_up_fwd");
+}
+
+// backward: dfeats[bin][n][c] = sum_{h,w} wy(h,bi) wx(w,bj) dy[n,h,w,coff+lv*CF+c]  (gather)
+template <typename T>
+__global__ __launch_bounds__(256) void ppm_up_bwd_kernel(PpmUpArgs a, void* dfeats) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = 50LL * a.N * a.CF;
+  if (t >= total) return;
+  int c = (int)(t % a.CF);
+  long long r = t / a.CF;
+  int n = (int)(r % a.N);
+  int b = (int)(r / a.N);
+  int k, bi, bj;
+  pp_bin(b, k, bi, bj);
+  const int lv = k == 1 ? 0 : (k == 2 ? 1 : (k == 3 ? 2 : 3));
+  const float sh = ac_scale(k, a.H), sw = ac_scale(k, a.W);
+  const T* g = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * a.CF + c;
+  float s = 0.f;
+  for (int h = 0; h < a.H; ++h) {
+    Lerp lh = ac_lerp(h, k, a.H, sh);
+    float wy = (lh.i0 == bi ? lh.l0 : 0.f) + (lh.i1 == bi ? lh.l1 : 0.f);
+    if (wy == 0.f) continue;
+    float sr = 0.f;
+    for (int w = 0; w < a.W; ++w) {
+      Lerp lw = ac_lerp(w, k, a.W, sw);
+      float wx = (lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f);
+      if (wx != 0.f) sr += wx * ld1(g + ((size_t)h * a.W + w) * a.ldy);
+    }
+    s += wy * sr;
+  }
+  st1((T*)dfeats + ((size_t)b * a.N + n) * a.CF + c, s);
+}
+
+int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
+  long long total = 50LL * a.N * a.CF;
+  unsigned grid = (unsigned)((total + 255) / 256);
+  if (dtype == DT_F32) ppm_up_bwd_kernel<float><<<grid, 256, 0, st>>>(a, dfeats);
+  else ppm_up_bwd_kernel<bf16><<<grid, 256, 0, st>>>(a, dfeats);
+  return check_launch("ppm_up_bwd");
+}
+
+}  // namespace fscnn

@@ -1,0 +1,251 @@
+// Argument structs and host launchers of every Fast-SCNN HIP kernel (csrc/*.hip).
+// The executor (net.cpp) and the C ABI (capi.cpp) call these; each returns 0 or a negative
+// fscnn::Status with the message available from fscnn::last_error().
+#pragma once
+#include "common.hpp"
+
+namespace fscnn {
+
+constexpr int MAX_FOLD = 64;
+
+struct Conv0Args {
+  const void* x;       // NCHW [N,3,H,W]
+  int x_bf16;
+  int N, H, W, Ho, Wo;
+  const float* w;      // [32][3][3][3]
+  const float* scale;  // [32] or null (eval BN fold)
+  const float* shift;  // [32] or null
+  int relu;
+  void* y;             // NHWC [N,Ho,Wo,32]
+  float* part;         // BN partial records [part][3][32] or null
+};
+
+struct Conv0WgradArgs {
+  const void* x;
+  int x_bf16;
+  int N, H, W, Ho, Wo;
+  const void* dz;  // NHWC [N,Ho,Wo,32]
+  float* slab;     // [parts][864]
+  int rows_per_block;
+};
+
+struct DwArgs {
+  int N, H, W, C, Ho, Wo, stride;
+  const void* x;   // NHWC [N,H,W,C] (input activation)
+  const float* w;  // [C][3][3] fp32 master weights
+  const float* scale;  // eval BN fold, or null
+  const float* shift;
+  int relu;
+  void* y;         // NHWC [N,Ho,Wo,C]
+  float* part;     // BN partial records [parts][3][C] or null
+};
+
+struct DwBwdArgs {
+  int N, H, W, C, Ho, Wo, stride;
+  const void* x;    // forward input activation (wgrad)
+  const void* dy;   // NHWC [N,Ho,Wo,C]
+  const float* w;   // [C][9]
+  void* dx;         // NHWC [N,H,W,C] (dgrad)
+  float* slab;      // [parts][9][C] (wgrad)
+};
+
+struct GemmArgs {
+  int M, N, K;
+  const void* A;
+  int lda;
+  const void* B;
+  int ldb;
+  int b_trans;          // 0: Bk(n,k) = B[n*ldb+k]   1: Bk(n,k) = B[k*ldb+n]
+  const float* scale;   // [N] or null
+  const float* shift;   // [N] or null
+  const void* R;        // residual [M][N] (ldr) or null; may alias C
+  int ldr;
+  int relu;
+  void* C;
+  int ldc;
+  float* part;          // BN partial records [gridDim.x][3][N] or null
+};
+
+struct GemmTnArgs {
+  int M, N, K;
+  const void* D;
+  int ldd;
+  const void* X;
+  int ldx;
+  float* slab;   // [splits][N][K]
+  int rows_per_split;
+};
+
+struct FoldEntry {
+  const float* gamma;
+  const float* beta;
+  const float* rmean;
+  const float* rvar;
+  const float* bias;  // conv bias folded in, or null
+  float* scale;
+  float* shift;
+  int C;
+};
+
+struct FoldTable {
+  int n;
+  FoldEntry e[MAX_FOLD];
+};
+
+struct BnFinalizeArgs {
+  const float* part;  // [P][3][C] (mean, M2, count)
+  int P, C;
+  const float* gamma;
+  const float* beta;
+  float* rmean;       // running stats, updated in place (or null)
+  float* rvar;
+  long long* nbt;     // num_batches_tracked (or null)
+  float momentum;
+  const float* bias;  // conv bias to add to the batch mean (stats taken before the bias) or null
+  float* mean;        // [C] saved for backward
+  float* invstd;      // [C]
+  float* scale;       // [C] gamma*invstd
+  float* shift;       // [C] beta - mean*scale
+};
+
+struct BnApplyArgs {
+  long long M;
+  int C;
+  const void* z;  int ldz;
+  const float* scale; const float* shift;
+  const void* z2; int ldz2;           // optional second affine branch (FFM)
+  const float* scale2; const float* shift2;
+  const void* res; int ldres;         // optional residual (LinearBottleneck shortcut)
+  int relu;
+  void* y; int ldy;
+};
+
+struct BnBwdArgs {
+  long long M;
+  int C;
+  const void* dy; int lddy;
+  const void* mask; int ldmask;   // null: no ReLU
+  const void* z; int ldz;
+  const float* mean; const float* invstd; const float* scale;
+  float* part;                    // [P][2][C]: sum dy_r, sum dy_r*xhat
+  int rows_per_block;
+  // apply
+  const float* coef;              // [2][C]: mean(dy_r), mean(dy_r*xhat) (train) — null in eval
+  void* dz; int lddz;
+};
+
+struct UpArgs {
+  int N, Hi, Wi, C, Ho, Wo;
+  const void* x; int ldx;   // NHWC, ldx = row stride (elements) >= C
+  void* y; int ldy;         // NHWC slice, ldy >= C
+};
+
+struct AxisBwdArgs {
+  long long n_o1;
+  int n_o2;
+  int Lout, Lin;
+  long long n_in;
+  const void* g;
+  long long g_s1, g_s2, g_idx, g_in;
+  void* d;
+  long long d_s1, d_s2, d_idx, d_in;
+  int accumulate;
+};
+
+struct PoolArgs {
+  int N, H, W, C;
+  const void* x; int ldx;   // NHWC (channel slice)
+  void* pooled;             // bin-major [50][N][C], storage type
+};
+
+struct PoolBwdArgs {
+  int N, H, W, C;
+  const void* dpooled;  // bin-major [50][N][C]
+  void* dx; int lddx;
+  int accumulate;
+};
+
+struct PpmUpArgs {
+  int N, H, W, CF;
+  const void* feats;
+  void* y; int ldy; int coff;
+};
+
+struct CeArgs {
+  int N, C;
+  long long HW;
+  const void* logits;     // [N][C][HW]
+  const long long* target;  // [N][HW]
+  long long ignore_index;
+  float* part;            // [P][2]: sum of loss, count of valid pixels
+  // backward
+  const float* scale;     // device scalar: grad_out / count (computed by ce_finalize)
+  void* dlogits;          // [N][C][HW] or null
+};
+
+struct DropArgs {
+  int N, H, W, C;
+  const void* x; int ldx;
+  void* y; int ldy;
+  uint64_t seed;
+  float p;
+};
+
+struct SgdArgs {
+  long long n;
+  float* p;
+  const float* g;
+  float* buf;
+  float lr, momentum, dampening, weight_decay;
+  int nesterov, first;
+  float grad_scale;  // multiply g first (e.g. 1/world_size); 1 = none
+};
+
+// ---- launchers ----------------------------------------------------------------------------
+int conv0_parts(int N, int Ho, int Wo);
+int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st);
+int conv0_wgrad_parts(int N, int Ho, int Wo, int rows_per_block);
+int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
+
+int dw_parts(int N, int Ho, int Wo, int C, int dtype);
+int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
+int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
+int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype);
+int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
+int dw_wgrad_reduce(const float* slab, int P, int C, float* dw, hipStream_t st);
+
+int gemm_parts(int M);
+int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st);
+int gemm_tn_splits(int M, int N, int K);
+int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st);
+int reduce_slabs(const float* slab, int S, long long stride, long long count, float* out,
+                 int accumulate, hipStream_t st);
+int colsum_parts(int M);
+int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStream_t st);
+
+int bn_fold(const FoldTable& t, hipStream_t st);
+int bn_finalize(const BnFinalizeArgs& a, hipStream_t st);
+int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st);
+int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
+int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);
+int bn_bwd_finalize(const float* part, int P, int C, double count, float* dgamma, float* dbeta,
+                    float* coef, hipStream_t st);
+int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st);
+
+int up_nhwc(const UpArgs& a, int dtype, hipStream_t st);
+int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st);
+int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st);
+int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st);
+int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st);
+int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st);
+int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st);
+
+int ce_parts(int N, long long HW);
+int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st);
+int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hipStream_t st);
+int dropout(const DropArgs& a, int dtype, hipStream_t st);
+int sgd(const SgdArgs& a, hipStream_t st);
+int cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st);
+int fill_f32(float* x, long long n, float v, hipStream_t st);
+
+}  // namespace fscnn

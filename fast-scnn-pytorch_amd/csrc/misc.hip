@@ -1,0 +1,187 @@
+// Train-step kernels around the network: cross-entropy with ignore_index (nn.CrossEntropyLoss
+// as wrapped by utils/loss.py:103-124; train.py:183-192), classifier Dropout(0.1)
+// (models/fast_scnn.py:229), the fused multi-tensor SGD over the flat parameter arena
+// (torch.optim.SGD momentum 0.9 / wd 1e-4, train.py:195-198) and fp32 -> bf16 weight casts.
+#include "kernels.hpp"
+
+namespace fscnn {
+
+// ---- cross entropy over NCHW logits, ignore_index --------------------------------------------
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(CeArgs a) {
+  __shared__ float r1[256], r2[256];
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)a.N * a.HW;
+  float loss = 0.f, cnt = 0.f;
+  if (i < total) {
+    long long n = i / a.HW, p = i - n * a.HW;
+    long long t = a.target[i];
+    if (t != a.ignore_index && t >= 0 && t < a.C) {
+      const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
+      float mx = -INFINITY;
+      for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
+      float se = 0.f;
+      for (int c = 0; c < a.C; ++c) se += expf(ld1(lb + (size_t)c * a.HW) - mx);
+      loss = mx + logf(se) - ld1(lb + (size_t)t * a.HW);
+      cnt = 1.f;
+    }
+  }
+  r1[threadIdx.x] = loss;
+  r2[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      r1[threadIdx.x] += r1[threadIdx.x + off];
+      r2[threadIdx.x] += r2[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.part[2 * blockIdx.x] = r1[0];
+    a.part[2 * blockIdx.x + 1] = r2[0];
+  }
+}
+
+// merge partials (fp64, fixed order) -> out[0] = mean loss, out[1] = count
+__global__ __launch_bounds__(256) void ce_finalize_kernel(const float* part, int P, float* out) {
+  __shared__ double r1[256], r2[256];
+  double s1 = 0.0, s2 = 0.0;
+  for (int p = threadIdx.x; p < P; p += 256) {
+    s1 += part[2 * p];
+    s2 += part[2 * p + 1];
+  }
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      r1[threadIdx.x] += r1[threadIdx.x + off];
+      r2[threadIdx.x] += r2[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = r2[0] > 0 ? (float)(r1[0] / r2[0]) : NAN;  // aten: mean over zero valid -> nan
+    out[1] = (float)r2[0];
+  }
+}
+
+int ce_parts(int N, long long HW) { return (int)(((long long)N * HW + 255) / 256); }
+
+int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st) {
+  int P = ce_parts(a.N, a.HW);
+  if (dtype == DT_F32) ce_fwd_kernel<float><<<P, 256, 0, st>>>(a);
+  else ce_fwd_kernel<bf16><<<P, 256, 0, st>>>(a);
+  int rc = check_launch("ce_fwd");
+  if (rc) return rc;
+  ce_finalize_kernel<<<1, 256, 0, st>>>(a.part, P, out);
+  return check_launch("ce_finalize");
+}
+
+// dlogits = (softmax - onehot) * grad_out / count ; 0 for ignored pixels
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(CeArgs a, const float* gout, const float* stats) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)a.N * a.HW;
+  if (i >= total) return;
+  long long n = i / a.HW, p = i - n * a.HW;
+  long long t = a.target[i];
+  const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
+  T* db = (T*)a.dlogits + (size_t)n * a.C * a.HW + p;
+  if (t == a.ignore_index || t < 0 || t >= a.C) {
+    for (int c = 0; c < a.C; ++c) st1(db + (size_t)c * a.HW, 0.f);
+    return;
+  }
+  float g = gout[0] / stats[1];
+  float mx = -INFINITY;
+  for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
+  float se = 0.f;
+  for (int c = 0; c < a.C; ++c) se += expf(ld1(lb + (size_t)c * a.HW) - mx);
+  float inv = 1.f / se;
+  for (int c = 0; c < a.C; ++c) {
+    float pr = expf(ld1(lb + (size_t)c * a.HW) - mx) * inv;
+    st1(db + (size_t)c * a.HW, (pr - (c == t ? 1.f : 0.f)) * g);
+  }
+}
+
+int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hipStream_t st) {
+  int P = ce_parts(a.N, a.HW);
+  if (dtype == DT_F32) ce_bwd_kernel<float><<<P, 256, 0, st>>>(a, gout, stats);
+  else ce_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, gout, stats);
+  return check_launch("ce_bwd");
+}
+
+// ---- dropout on an NHWC activation, mask indexed in NCHW order (matches the oracle) ----------
+
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)a.N * a.H * a.W * a.C;
+  if (i >= total) return;
+  int c = (int)(i % a.C);
+  long long pix = i / a.C;
+  long long hw = pix % ((long long)a.H * a.W);
+  long long n = pix / ((long long)a.H * a.W);
+  uint64_t nchw = ((uint64_t)n * a.C + c) * (uint64_t)a.H * a.W + hw;
+  float v = ld1((const T*)a.x + pix * a.ldx + c);
+  float s = 1.f / (1.f - a.p);
+  st1((T*)a.y + pix * a.ldy + c, dropout_keep(a.seed, nchw, thr) ? v * s : 0.f);
+}
+
+int dropout(const DropArgs& a, int dtype, hipStream_t st) {
+  long long total = (long long)a.N * a.H * a.W * a.C;
+  unsigned grid = (unsigned)((total + 255) / 256);
+  uint32_t thr = dropout_threshold(a.p);
+  if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr);
+  else dropout_kernel<bf16><<<grid, 256, 0, st>>>(a, thr);
+  return check_launch("dropout");
+}
+
+// ---- fused SGD over a flat fp32 arena ------------------------------------------------------
+// d = g + wd*p; buf = first ? d : momentum*buf + (1-dampening)*d; d = nesterov ? d + m*buf : buf;
+// p -= lr*d     (torch.optim.SGD semantics)
+
+__global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
+  long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= a.n) return;
+  int cnt = (int)min((long long)4, a.n - i);
+  for (int j = 0; j < cnt; ++j) {
+    float p = a.p[i + j];
+    float d = a.g[i + j] * a.grad_scale + a.weight_decay * p;
+    if (a.momentum != 0.f) {
+      float b = a.first ? d : a.momentum * a.buf[i + j] + (1.f - a.dampening) * d;
+      a.buf[i + j] = b;
+      d = a.nesterov ? d + a.momentum * b : b;
+    }
+    a.p[i + j] = p - a.lr * d;
+  }
+}
+
+int sgd(const SgdArgs& a, hipStream_t st) {
+  unsigned grid = (unsigned)((a.n + 1023) / 1024);
+  sgd_kernel<<<grid, 256, 0, st>>>(a);
+  return check_launch("sgd");
+}
+
+// ---- casts ------------------------------------------------------------------------------------
+__global__ void cast_f32_bf16_kernel(const float* x, uint16_t* y, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = f2bf(x[i]);
+}
+int cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st) {
+  cast_f32_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(x, (uint16_t*)y, n);
+  return check_launch("cast_f32_bf16");
+}
+
+__global__ void fill_kernel(float* x, long long n, float v) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+int fill_f32(float* x, long long n, float v, hipStream_t st) {
+  if (n <= 0) return OK;
+  fill_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(x, n, v);
+  return check_launch("fill");
+}
+
+}  // namespace fscnn

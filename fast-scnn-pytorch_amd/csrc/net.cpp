@@ -1,0 +1,766 @@
+// Native executor: builds the layer table, plans the workspace for a (N, H, W, dtype, mode)
+// and issues the forward / backward kernel sequences on the caller's stream.
+//
+// Forward dataflow (models/fast_scnn.py:33-46), NHWC activations:
+//   conv0 → dsconv1 → dsconv2 (= higher_res_features)        LearningToDownsample :157-161
+//   9 × LinearBottleneck                                     GlobalFeatureExtractor :182-187
+//   PPM: pool(1,2,3,6) → 4 × 1x1 → upsample into concat[:,128:256]; out 1x1(256→128)  :137-145
+//   FFM: up(x4, ac) → dw → 1x1+bias+BN  (+)  1x1+bias+BN(higher) → ReLU    :207-218
+//   Classifier: 2 × DSConv → Dropout → 1x1(+bias) → final bilinear to NCHW   :233-237, :40
+// eval : BN folded into every producer's epilogue (one bn_fold launch per forward)
+// train: producer writes raw z + per-block statistics → bn_finalize → bn_apply (+res / ReLU)
+#include "net.hpp"
+
+#include <cstdio>
+#include <cstring>
+
+namespace fscnn {
+
+// ======================================================================================
+// layer table
+// ======================================================================================
+namespace {
+struct Builder {
+  Net& n;
+  explicit Builder(Net& net) : n(net) {}
+  long long palloc(const std::string& name, std::vector<int> shape) {
+    long long numel = 1;
+    for (int s : shape) numel *= s;
+    long long off = (n.p_total + 15) / 16 * 16;  // 64-B aligned tensors (16-B vector loads)
+    n.params.push_back({name, shape, off, numel});
+    n.p_total = off + numel;
+    return off;
+  }
+  long long ralloc(const std::string& name, int C) {
+    long long off = (n.r_total + 15) / 16 * 16;
+    n.buffers.push_back({name, {C}, off, C});
+    n.r_total = off + C;
+    return off;
+  }
+  ConvL conv(const std::string& key, int cin, int cout, int k = 1, int groups = 1, bool bias = false) {
+    ConvL c;
+    c.cin = cin; c.cout = cout; c.k = k; c.groups = groups;
+    c.w = palloc(key + ".weight", {cout, cin / groups, k, k});
+    if (bias) c.b = palloc(key + ".bias", {cout});
+    return c;
+  }
+  BnL bn(const std::string& key, int C) {
+    BnL b;
+    b.C = C;
+    b.g = palloc(key + ".weight", {C});
+    b.b = palloc(key + ".bias", {C});
+    b.rm = ralloc(key + ".running_mean", C);
+    b.rv = ralloc(key + ".running_var", C);
+    b.nbt = n.n_bn;
+    b.id = n.n_bn;
+    n.buffers.push_back({key + ".num_batches_tracked", {}, (long long)n.n_bn, 1});
+    n.n_bn++;
+    return b;
+  }
+  DsL dsconv(const std::string& p, int cin, int cout) {
+    DsL d;
+    d.dw = conv(p + ".conv.0", cin, cin, 3, cin);
+    d.bdw = bn(p + ".conv.1", cin);
+    d.pw = conv(p + ".conv.3", cin, cout);
+    d.bpw = bn(p + ".conv.4", cout);
+    return d;
+  }
+};
+}  // namespace
+
+int net_build(int num_classes, int aux, Net& net) {
+  if (num_classes < 1 || num_classes > 1024) {
+    set_error("net_build: num_classes=%d out of range", num_classes);
+    return E_INVALID;
+  }
+  net = Net();
+  net.num_classes = num_classes;
+  net.aux = aux;
+  Builder b(net);
+  // models/fast_scnn.py:20 LearningToDownsample(32, 48, 64)
+  net.c0 = b.conv("learning_to_downsample.conv.conv.0", 3, 32, 3);
+  net.b0 = b.bn("learning_to_downsample.conv.conv.1", 32);
+  net.ltd1 = b.dsconv("learning_to_downsample.dsconv1", 32, 48);
+  net.ltd2 = b.dsconv("learning_to_downsample.dsconv2", 48, 64);
+  // :21 GlobalFeatureExtractor(64, [64, 96, 128], 128, 6, [3, 3, 3])
+  static const int cin_[9] = {64, 64, 64, 64, 96, 96, 96, 128, 128};
+  static const int cout_[9] = {64, 64, 64, 96, 96, 96, 128, 128, 128};
+  static const int s_[9] = {2, 1, 1, 2, 1, 1, 1, 1, 1};
+  net.stage_p_begin[3] = 0;
+  for (int i = 0; i < 9; ++i) {
+    char pfx[128];
+    snprintf(pfx, sizeof pfx, "global_feature_extractor.bottleneck%d.%d", i / 3 + 1, i % 3);
+    std::string p(pfx);
+    int e = cin_[i] * 6;
+    if (i == 3) net.stage_p_begin[2] = (net.p_total + 15) / 16 * 16;
+    if (i == 6) net.stage_p_begin[1] = (net.p_total + 15) / 16 * 16;
+    LbL& l = net.lb[i];
+    l.cin = cin_[i]; l.cout = cout_[i]; l.stride = s_[i];
+    l.e = b.conv(p + ".block.0.conv.0", cin_[i], e);
+    l.be = b.bn(p + ".block.0.conv.1", e);
+    l.d = b.conv(p + ".block.1.conv.0", e, e, 3, e);
+    l.bd = b.bn(p + ".block.1.conv.1", e);
+    l.p = b.conv(p + ".block.2", e, cout_[i]);
+    l.bp = b.bn(p + ".block.3", cout_[i]);
+  }
+  net.stage_p_begin[0] = (net.p_total + 15) / 16 * 16;
+  for (int i = 0; i < 4; ++i) {
+    char pfx[128];
+    snprintf(pfx, sizeof pfx, "global_feature_extractor.ppm.conv%d.conv", i + 1);
+    std::string p(pfx);
+    net.ppm_c[i] = b.conv(p + ".0", 128, 32);
+    net.ppm_b[i] = b.bn(p + ".1", 32);
+  }
+  net.ppm_o = b.conv("global_feature_extractor.ppm.out.conv.0", 256, 128);
+  net.ppm_ob = b.bn("global_feature_extractor.ppm.out.conv.1", 128);
+  // :22 FeatureFusionModule(64, 128, 128)
+  net.ffm_dw = b.conv("feature_fusion.dwconv.conv.0", 128, 128, 3, 128);
+  net.ffm_bdw = b.bn("feature_fusion.dwconv.conv.1", 128);
+  net.ffm_low = b.conv("feature_fusion.conv_lower_res.0", 128, 128, 1, 1, true);
+  net.ffm_blow = b.bn("feature_fusion.conv_lower_res.1", 128);
+  net.ffm_high = b.conv("feature_fusion.conv_higher_res.0", 64, 128, 1, 1, true);
+  net.ffm_bhigh = b.bn("feature_fusion.conv_higher_res.1", 128);
+  // :23 Classifer(128, num_classes)
+  net.cls1 = b.dsconv("classifier.dsconv1", 128, 128);
+  net.cls2 = b.dsconv("classifier.dsconv2", 128, 128);
+  net.cls_out = b.conv("classifier.conv.1", 128, num_classes, 1, 1, true);
+  if (aux) {
+    net.aux0 = b.conv("auxlayer.0", 64, 32, 3);
+    net.aux1 = b.bn("auxlayer.1", 32);
+    net.aux4 = b.conv("auxlayer.4", 32, num_classes, 1, 1, true);
+  }
+  net.p_total = (net.p_total + 15) / 16 * 16;
+  net.r_total = (net.r_total + 15) / 16 * 16;
+  return OK;
+}
+
+// ======================================================================================
+// planning
+// ======================================================================================
+namespace {
+struct Alloc {
+  size_t top = 0;
+  size_t get(size_t bytes) {
+    size_t off = (top + 255) / 256 * 256;
+    top = off + (bytes ? bytes : 1);
+    return off;
+  }
+};
+
+int dwout(int h, int s) { return (h - 1) / s + 1; }
+}  // namespace
+
+int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl) {
+  if (net.aux) {
+    set_error("plan_build: aux head is not implemented on the HIP path yet");
+    return E_UNSUPPORTED;
+  }
+  if (N < 1 || H < 3 || W < 3) {
+    set_error("plan_build: bad input shape N=%d H=%d W=%d", N, H, W);
+    return E_INVALID;
+  }
+  if (dtype != DT_F32 && dtype != DT_BF16) {
+    set_error("plan_build: unsupported dtype %d", dtype);
+    return E_UNSUPPORTED;
+  }
+  pl = Plan();
+  pl.net = &net;
+  pl.N = N; pl.H = H; pl.W = W; pl.dtype = dtype; pl.train = train;
+  pl.H1 = (H - 3) / 2 + 1; pl.W1 = (W - 3) / 2 + 1;  // first conv, padding 0
+  pl.H2 = dwout(pl.H1, 2); pl.W2 = dwout(pl.W1, 2);
+  pl.H3 = dwout(pl.H2, 2); pl.W3 = dwout(pl.W2, 2);
+  pl.H4 = dwout(pl.H3, 2); pl.W4 = dwout(pl.W3, 2);
+  pl.H5 = dwout(pl.H4, 2); pl.W5 = dwout(pl.W4, 2);
+  const int V = dtype == DT_F32 ? 4 : 8;
+  const size_t E = dtype == DT_F32 ? 4 : 2;
+  pl.Cp = (net.num_classes + V - 1) / V * V;
+  Alloc A, B;  // forward (saved) and backward (scratch) workspaces
+  auto unit = [&](Unit& u, long long M, int C, int nparts, size_t a_override = (size_t)-1,
+                  int ld = 0) {
+    u.M = M; u.C = C; u.ld = ld ? ld : C;
+    u.a = a_override != (size_t)-1 ? a_override : A.get((size_t)M * u.ld * E);
+    u.z = train ? A.get((size_t)M * C * E) : u.a;
+    u.nparts = nparts;
+    if (train) u.part = A.get((size_t)nparts * 3 * C * 4);
+    u.mean = A.get(C * 4); u.invstd = A.get(C * 4);
+    u.scale = A.get(C * 4); u.shift = A.get(C * 4);
+  };
+  auto gunit = [&](Unit& u, size_t ga_override = (size_t)-1, int ld = 0) {
+    u.ga_ld = ld ? ld : u.C;
+    u.ga = ga_override != (size_t)-1 ? ga_override : B.get((size_t)u.M * u.ga_ld * E);
+  };
+  const long long M0 = (long long)N * pl.H1 * pl.W1, M1 = (long long)N * pl.H2 * pl.W2,
+                  M2 = (long long)N * pl.H3 * pl.W3, M4 = (long long)N * pl.H4 * pl.W4,
+                  M5 = (long long)N * pl.H5 * pl.W5;
+  if (M0 > 0x7fffffffLL / 32) {
+    set_error("plan_build: batch too large for 32-bit row indexing");
+    return E_INVALID;
+  }
+  if (dtype == DT_BF16) pl.pbf = A.get((size_t)net.p_total * 2);
+  unit(pl.c0, M0, 32, conv0_parts(N, pl.H1, pl.W1));
+  unit(pl.l1dw, M1, 32, dw_parts(N, pl.H2, pl.W2, 32, dtype));
+  unit(pl.l1pw, M1, 48, gemm_parts((int)M1));
+  unit(pl.l2dw, M2, 48, dw_parts(N, pl.H3, pl.W3, 48, dtype));
+  unit(pl.l2pw, M2, 64, gemm_parts((int)M2));
+  pl.concat = A.get((size_t)M5 * 256 * E);
+  for (int i = 0; i < 9; ++i) {
+    const LbL& l = net.lb[i];
+    long long Min = i == 0 ? M2 : (i <= 3 ? M4 : M5);
+    long long Mout = i < 3 ? M4 : M5;
+    int Ho = i < 3 ? pl.H4 : pl.H5, Wo = i < 3 ? pl.W4 : pl.W5;
+    int e = l.cin * 6;
+    unit(pl.lbe[i], Min, e, gemm_parts((int)Min));
+    unit(pl.lbd[i], Mout, e, dw_parts(N, Ho, Wo, e, dtype));
+    if (i == 8) unit(pl.lbp[i], Mout, l.cout, gemm_parts((int)Mout), pl.concat, 256);
+    else unit(pl.lbp[i], Mout, l.cout, gemm_parts((int)Mout));
+  }
+  // PPM: pooled / feats are bin-major [50][N][C]
+  pl.pooled = A.get((size_t)50 * N * 128 * E);
+  pl.feats_a = A.get((size_t)50 * N * 32 * E);
+  static const int kk[4] = {1, 2, 3, 6}, base[4] = {0, 1, 5, 14};
+  for (int i = 0; i < 4; ++i) {
+    long long M = (long long)kk[i] * kk[i] * N;
+    unit(pl.ppk[i], M, 32, gemm_parts((int)M), pl.feats_a + (size_t)base[i] * N * 32 * E, 32);
+  }
+  unit(pl.po, M5, 128, gemm_parts((int)M5));
+  pl.up_low = A.get((size_t)M2 * 128 * E);
+  unit(pl.fdw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype));
+  pl.f = A.get((size_t)M2 * 128 * E);
+  unit(pl.flow, M2, 128, gemm_parts((int)M2), pl.f);    // a = f (combined), z own
+  unit(pl.fhigh, M2, 128, gemm_parts((int)M2), pl.f);
+  unit(pl.c1dw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype));
+  unit(pl.c1pw, M2, 128, gemm_parts((int)M2));
+  unit(pl.c2dw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype));
+  unit(pl.c2pw, M2, 128, gemm_parts((int)M2));
+  pl.drop = train ? A.get((size_t)M2 * 128 * E) : pl.c2pw.a;
+  pl.logits = A.get((size_t)M2 * pl.Cp * E);
+  pl.ws_bytes = A.top;
+
+  if (train) {
+    const int C = net.num_classes;
+    pl.g_logits = B.get((size_t)M2 * pl.Cp * E);
+    pl.t_up = B.get((size_t)N * C * H * pl.W3 * 4);
+    pl.g_drop = B.get((size_t)M2 * 128 * E);
+    gunit(pl.c2pw);
+    gunit(pl.c2dw);
+    gunit(pl.c1pw);
+    gunit(pl.c1dw);
+    pl.g_f = B.get((size_t)M2 * 128 * E);
+    gunit(pl.fdw);
+    pl.g_up = B.get((size_t)M2 * 128 * E);
+    pl.t_up2 = B.get((size_t)N * pl.H3 * pl.W5 * 128 * 4);
+    gunit(pl.po);
+    pl.g_concat = B.get((size_t)M5 * 256 * E);
+    pl.g_feats = B.get((size_t)50 * N * 32 * E);
+    for (int i = 0; i < 4; ++i)
+      gunit(pl.ppk[i], pl.g_feats + (size_t)base[i] * N * 32 * E, 32);
+    pl.g_pooled = B.get((size_t)50 * N * 128 * E);
+    for (int i = 8; i >= 0; --i) {
+      gunit(pl.lbd[i]);
+      gunit(pl.lbe[i]);
+      if (i == 8) gunit(pl.lbp[i], pl.g_concat, 256);
+      else gunit(pl.lbp[i]);
+    }
+    gunit(pl.l2pw);
+    gunit(pl.l2dw);
+    gunit(pl.l1pw);
+    gunit(pl.l1dw);
+    gunit(pl.c0);
+    // scratch sized for the largest consumer
+    long long max_mc = 0;
+    auto upd = [&](const Unit& u) { if (u.M * u.C > max_mc) max_mc = u.M * u.C; };
+    upd(pl.c0); upd(pl.l1dw); upd(pl.l1pw); upd(pl.l2dw); upd(pl.l2pw);
+    for (int i = 0; i < 9; ++i) { upd(pl.lbe[i]); upd(pl.lbd[i]); upd(pl.lbp[i]); }
+    upd(pl.po); upd(pl.fdw); upd(pl.flow); upd(pl.c1dw); upd(pl.c1pw);
+    pl.dz = B.get((size_t)max_mc * E);
+    // weight-gradient slabs: max over pw convs of splits*N*K, dw parts*9*C, conv0 parts*864
+    size_t slab = 0;
+    auto pw_slab = [&](long long M, int n, int k) {
+      size_t s = (size_t)gemm_tn_splits((int)M, n, k) * n * k;
+      if (s > slab) slab = s;
+    };
+    auto dw_slab = [&](int Ho, int Wo, int Cc) {
+      size_t s = (size_t)dw_wgrad_parts(N, Ho, Wo, Cc, dtype) * 9 * Cc;
+      if (s > slab) slab = s;
+    };
+    pw_slab(M1, 48, 32); pw_slab(M2, 64, 48);
+    dw_slab(pl.H2, pl.W2, 32); dw_slab(pl.H3, pl.W3, 48);
+    for (int i = 0; i < 9; ++i) {
+      const LbL& l = net.lb[i];
+      long long Min = pl.lbe[i].M, Mout = pl.lbd[i].M;
+      int Ho = i < 3 ? pl.H4 : pl.H5, Wo = i < 3 ? pl.W4 : pl.W5;
+      pw_slab(Min, l.cin * 6, l.cin);
+      pw_slab(Mout, l.cout, l.cin * 6);
+      dw_slab(Ho, Wo, l.cin * 6);
+    }
+    for (int i = 0; i < 4; ++i) pw_slab(pl.ppk[i].M, 32, 128);
+    pw_slab(M5, 128, 256);
+    dw_slab(pl.H3, pl.W3, 128);
+    pw_slab(M2, 128, 128); pw_slab(M2, 128, 64); pw_slab(M2, C, 128);
+    size_t c0s = (size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864;
+    if (c0s > slab) slab = c0s;
+    pl.slab = B.get(slab * 4);
+    // BN backward partials: max P*2*C
+    size_t bnp = 0;
+    auto bn_upd = [&](const Unit& u) {
+      int rpb;
+      size_t s = (size_t)bn_bwd_parts(u.M, u.C, dtype, &rpb) * 2 * u.C;
+      if (s > bnp) bnp = s;
+    };
+    bn_upd(pl.c0); bn_upd(pl.l1dw); bn_upd(pl.l1pw); bn_upd(pl.l2dw); bn_upd(pl.l2pw);
+    for (int i = 0; i < 9; ++i) { bn_upd(pl.lbe[i]); bn_upd(pl.lbd[i]); bn_upd(pl.lbp[i]); }
+    for (int i = 0; i < 4; ++i) bn_upd(pl.ppk[i]);
+    bn_upd(pl.po); bn_upd(pl.fdw); bn_upd(pl.flow); bn_upd(pl.c1dw); bn_upd(pl.c1pw);
+    pl.bnpart = B.get(bnp * 4);
+    pl.coef = B.get(2 * 1024 * 4);
+    pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
+    pl.bws_bytes = B.top;
+  }
+  return OK;
+}
+
+// ======================================================================================
+// execution
+// ======================================================================================
+namespace {
+
+#define TRY(x)                 \
+  do {                         \
+    int rc__ = (x);            \
+    if (rc__) return rc__;     \
+  } while (0)
+
+struct Exec {
+  const Plan& pl;
+  const Net& net;
+  const RunArgs& r;
+  char* ws;
+  char* bws;
+  int dt;
+  size_t E;
+  bool train;
+  Exec(const Plan& p, const RunArgs& ra)
+      : pl(p), net(*p.net), r(ra), ws((char*)ra.ws), bws((char*)ra.bws), dt(p.dtype),
+        E(p.dtype == DT_F32 ? 4 : 2), train(p.train != 0) {}
+
+  void* W(size_t off) const { return ws + off; }
+  void* Bw(size_t off) const { return bws + off; }
+  float* Wf(size_t off) const { return (float*)(ws + off); }
+  const float* P(long long off) const { return off < 0 ? nullptr : r.P + off; }
+  float* G(long long off) const { return off < 0 ? nullptr : r.G + off; }
+  // GEMM weight operand in the storage dtype
+  const void* Wg(const ConvL& c) const {
+    if (dt == DT_F32) return r.P + c.w;
+    return ws + pl.pbf + (size_t)c.w * 2;
+  }
+
+  // ---- BN glue -----------------------------------------------------------------------
+  int finalize(const Unit& u, const BnL& bn) {
+    BnFinalizeArgs f{};
+    f.part = Wf(u.part); f.P = u.nparts; f.C = u.C;
+    f.gamma = P(bn.g); f.beta = P(bn.b);
+    f.rmean = r.R + bn.rm; f.rvar = r.R + bn.rv;
+    f.nbt = r.NBT ? r.NBT + bn.nbt : nullptr;
+    f.momentum = r.momentum;
+    f.bias = nullptr;
+    f.mean = Wf(u.mean); f.invstd = Wf(u.invstd); f.scale = Wf(u.scale); f.shift = Wf(u.shift);
+    return bn_finalize(f, r.st);
+  }
+  int apply(const Unit& u, bool relu, const void* res = nullptr, int ldres = 0) {
+    BnApplyArgs a{};
+    a.M = u.M; a.C = u.C;
+    a.z = W(u.z); a.ldz = u.C;
+    a.scale = Wf(u.scale); a.shift = Wf(u.shift);
+    a.res = res; a.ldres = ldres;
+    a.relu = relu;
+    a.y = W(u.a); a.ldy = u.ld;
+    return bn_apply(a, dt, r.st);
+  }
+
+  // ---- conv + BN (+ReLU) producers -------------------------------------------------------
+  // pointwise conv on X [M][K] (ld ldx); eval: fused BN(+res,+relu); train: stats → apply
+  int pw(const Unit& u, const ConvL& c, const BnL* bn, const void* X, int ldx, bool relu,
+         const void* res = nullptr, int ldres = 0) {
+    GemmArgs g{};
+    g.M = (int)u.M; g.N = c.cout; g.K = c.cin;
+    g.A = X; g.lda = ldx;
+    g.B = Wg(c); g.ldb = c.cin; g.b_trans = 0;
+    if (!train || !bn) {
+      g.scale = bn ? Wf(u.scale) : nullptr;
+      g.shift = bn ? Wf(u.shift) : P(c.b);
+      g.R = res; g.ldr = ldres;
+      g.relu = relu;
+      g.C = W(u.a); g.ldc = u.ld;
+      return gemm_nt(g, dt, r.st);
+    }
+    g.scale = nullptr; g.shift = P(c.b);
+    g.C = W(u.z); g.ldc = u.C;
+    g.part = Wf(u.part);
+    TRY(gemm_nt(g, dt, r.st));
+    TRY(finalize(u, *bn));
+    return apply(u, relu, res, ldres);
+  }
+  int dw(const Unit& u, const ConvL& c, const BnL& bn, const void* X, int H, int Wd, int Ho, int Wo,
+         int stride) {
+    DwArgs d{};
+    d.N = pl.N; d.H = H; d.W = Wd; d.C = u.C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
+    d.x = X; d.w = P(c.w);
+    if (!train) {
+      d.scale = Wf(u.scale); d.shift = Wf(u.shift); d.relu = 1; d.y = W(u.a);
+      return dw_fwd(d, dt, r.st);
+    }
+    d.relu = 0; d.y = W(u.z); d.part = Wf(u.part);
+    TRY(dw_fwd(d, dt, r.st));
+    TRY(finalize(u, bn));
+    return apply(u, true);
+  }
+
+  int fold_all() {
+    FoldTable t{};
+    auto add = [&](const BnL& bn, const Unit& u, const ConvL* conv) {
+      FoldEntry& e = t.e[t.n++];
+      e.gamma = P(bn.g); e.beta = P(bn.b); e.rmean = r.R + bn.rm; e.rvar = r.R + bn.rv;
+      e.bias = (conv && conv->b >= 0) ? P(conv->b) : nullptr;
+      e.scale = Wf(u.scale); e.shift = Wf(u.shift); e.C = bn.C;
+    };
+    add(net.b0, pl.c0, nullptr);
+    add(net.ltd1.bdw, pl.l1dw, nullptr); add(net.ltd1.bpw, pl.l1pw, nullptr);
+    add(net.ltd2.bdw, pl.l2dw, nullptr); add(net.ltd2.bpw, pl.l2pw, nullptr);
+    for (int i = 0; i < 9; ++i) {
+      add(net.lb[i].be, pl.lbe[i], nullptr);
+      add(net.lb[i].bd, pl.lbd[i], nullptr);
+      add(net.lb[i].bp, pl.lbp[i], nullptr);
+    }
+    for (int i = 0; i < 4; ++i) add(net.ppm_b[i], pl.ppk[i], nullptr);
+    add(net.ppm_ob, pl.po, nullptr);
+    add(net.ffm_bdw, pl.fdw, nullptr);
+    add(net.ffm_blow, pl.flow, &net.ffm_low);
+    add(net.ffm_bhigh, pl.fhigh, &net.ffm_high);
+    add(net.cls1.bdw, pl.c1dw, nullptr); add(net.cls1.bpw, pl.c1pw, nullptr);
+    add(net.cls2.bdw, pl.c2dw, nullptr); add(net.cls2.bpw, pl.c2pw, nullptr);
+    return bn_fold(t, r.st);
+  }
+
+  // ================================ forward ================================================
+  int forward() {
+    const int N = pl.N;
+    if (dt == DT_BF16) TRY(cast_f32_bf16(r.P, W(pl.pbf), net.p_total, r.st));
+    if (!train) TRY(fold_all());
+    // ---- LearningToDownsample ----
+    {
+      Conv0Args c{};
+      c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
+      c.N = N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
+      c.w = P(net.c0.w);
+      if (!train) { c.scale = Wf(pl.c0.scale); c.shift = Wf(pl.c0.shift); c.relu = 1; c.y = W(pl.c0.a); }
+      else { c.relu = 0; c.y = W(pl.c0.z); c.part = Wf(pl.c0.part); }
+      TRY(conv0_fwd(c, dt, r.st));
+      if (train) { TRY(finalize(pl.c0, net.b0)); TRY(apply(pl.c0, true)); }
+    }
+    TRY(dw(pl.l1dw, net.ltd1.dw, net.ltd1.bdw, W(pl.c0.a), pl.H1, pl.W1, pl.H2, pl.W2, 2));
+    TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, W(pl.l1dw.a), 32, true));
+    TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, W(pl.l1pw.a), pl.H2, pl.W2, pl.H3, pl.W3, 2));
+    TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, W(pl.l2dw.a), 48, true));
+    // ---- bottlenecks ----
+    const void* x = W(pl.l2pw.a);
+    int xld = 64;
+    int Hc = pl.H3, Wc = pl.W3;
+    for (int i = 0; i < 9; ++i) {
+      const LbL& l = net.lb[i];
+      int Ho = dwout(Hc, l.stride), Wo = dwout(Wc, l.stride);
+      TRY(pw(pl.lbe[i], l.e, &l.be, x, xld, true));
+      TRY(dw(pl.lbd[i], l.d, l.bd, W(pl.lbe[i].a), Hc, Wc, Ho, Wo, l.stride));
+      bool shortcut = l.stride == 1 && l.cin == l.cout;
+      TRY(pw(pl.lbp[i], l.p, &l.bp, W(pl.lbd[i].a), l.cin * 6, false,
+             shortcut ? x : nullptr, shortcut ? xld : 0));
+      x = W(pl.lbp[i].a);
+      xld = pl.lbp[i].ld;
+      Hc = Ho; Wc = Wo;
+    }
+    // ---- PPM ----
+    {
+      PoolArgs p{};
+      p.N = N; p.H = pl.H5; p.W = pl.W5; p.C = 128; p.x = W(pl.concat); p.ldx = 256;
+      p.pooled = W(pl.pooled);
+      TRY(pyramid_pool(p, dt, r.st));
+      static const int base[4] = {0, 1, 5, 14};
+      for (int i = 0; i < 4; ++i) {
+        const void* xin = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
+        TRY(pw(pl.ppk[i], net.ppm_c[i], &net.ppm_b[i], xin, 128, true));
+      }
+      PpmUpArgs u{};
+      u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = W(pl.feats_a);
+      u.y = W(pl.concat); u.ldy = 256; u.coff = 128;
+      TRY(ppm_up_fwd(u, dt, r.st));
+      TRY(pw(pl.po, net.ppm_o, &net.ppm_ob, W(pl.concat), 256, true));
+    }
+    // ---- FFM ----
+    {
+      UpArgs u{};
+      u.N = N; u.Hi = pl.H5; u.Wi = pl.W5; u.C = 128; u.Ho = pl.H3; u.Wo = pl.W3;
+      u.x = W(pl.po.a); u.ldx = 128; u.y = W(pl.up_low); u.ldy = 128;
+      TRY(up_nhwc(u, dt, r.st));
+      TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+      if (!train) {
+        // f = BN_h(conv_h(hr)) ; f = relu(BN_l(conv_l(dw)) + f)
+        TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, W(pl.l2pw.a), 64, false));
+        TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, W(pl.fdw.a), 128, true,
+               W(pl.f), 128));
+      } else {
+        GemmArgs g{};
+        g.M = (int)pl.flow.M; g.N = 128; g.K = 128; g.A = W(pl.fdw.a); g.lda = 128;
+        g.B = Wg(net.ffm_low); g.ldb = 128; g.shift = P(net.ffm_low.b);
+        g.C = W(pl.flow.z); g.ldc = 128; g.part = Wf(pl.flow.part);
+        TRY(gemm_nt(g, dt, r.st));
+        TRY(finalize(pl.flow, net.ffm_blow));
+        g.K = 64; g.A = W(pl.l2pw.a); g.lda = 64; g.B = Wg(net.ffm_high); g.ldb = 64;
+        g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z); g.part = Wf(pl.fhigh.part);
+        TRY(gemm_nt(g, dt, r.st));
+        TRY(finalize(pl.fhigh, net.ffm_bhigh));
+        BnApplyArgs a{};
+        a.M = pl.flow.M; a.C = 128;
+        a.z = W(pl.flow.z); a.ldz = 128; a.scale = Wf(pl.flow.scale); a.shift = Wf(pl.flow.shift);
+        a.z2 = W(pl.fhigh.z); a.ldz2 = 128; a.scale2 = Wf(pl.fhigh.scale); a.shift2 = Wf(pl.fhigh.shift);
+        a.relu = 1; a.y = W(pl.f); a.ldy = 128;
+        TRY(bn_apply(a, dt, r.st));
+      }
+    }
+    // ---- Classifier ----
+    TRY(dw(pl.c1dw, net.cls1.dw, net.cls1.bdw, W(pl.f), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+    TRY(pw(pl.c1pw, net.cls1.pw, &net.cls1.bpw, W(pl.c1dw.a), 128, true));
+    TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, W(pl.c1pw.a), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+    TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, W(pl.c2dw.a), 128, true));
+    const void* cls_in = W(pl.c2pw.a);
+    if (train && r.dropout_p > 0.f) {
+      DropArgs d{};
+      d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = W(pl.c2pw.a); d.ldx = 128;
+      d.y = W(pl.drop); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
+      TRY(dropout(d, dt, r.st));
+      cls_in = W(pl.drop);
+    }
+    {
+      GemmArgs g{};
+      g.M = (int)pl.c2pw.M; g.N = net.num_classes; g.K = 128; g.A = cls_in; g.lda = 128;
+      g.B = Wg(net.cls_out); g.ldb = 128; g.shift = P(net.cls_out.b);
+      g.C = W(pl.logits); g.ldc = pl.Cp;
+      TRY(gemm_nt(g, dt, r.st));
+    }
+    // ---- final bilinear (align_corners) to NCHW ----
+    UpArgs u{};
+    u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
+    u.x = W(pl.logits); u.ldx = pl.Cp; u.y = r.out; u.ldy = 0;
+    return up_nchw(u, dt, r.out_dtype, r.st);
+  }
+
+  // ================================ backward ===============================================
+  // BN backward of unit u: dy = u.ga (ld u.ga_ld), mask = relu output (or null) → dz scratch
+  int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
+             int ldmask, void* dz) {
+    BnBwdArgs b{};
+    b.M = u.M; b.C = u.C;
+    b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
+    b.z = W(u.z); b.ldz = u.C;
+    b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
+    b.part = (float*)Bw(pl.bnpart);
+    TRY(bn_bwd_reduce(b, dt, r.st));
+    int rpb;
+    int P = bn_bwd_parts(u.M, u.C, dt, &rpb);
+    float* coef = (float*)Bw(pl.coef);
+    TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b), coef, r.st));
+    b.coef = coef;
+    b.dz = dz; b.lddz = u.C;
+    return bn_bwd_apply(b, dt, r.st);
+  }
+  // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
+  int pw_bwd(const ConvL& c, long long M, const void* dz, int lddz, const void* X, int ldx,
+             void* dX, int lddx, const void* R = nullptr, int ldr = 0) {
+    GemmTnArgs t{};
+    t.M = (int)M; t.N = c.cout; t.K = c.cin; t.D = dz; t.ldd = lddz; t.X = X; t.ldx = ldx;
+    t.slab = (float*)Bw(pl.slab);
+    int S = gemm_tn_splits((int)M, c.cout, c.cin);
+    TRY(gemm_tn(t, S, dt, r.st));
+    TRY(reduce_slabs(t.slab, S, (long long)c.cout * c.cin, (long long)c.cout * c.cin, G(c.w), 0, r.st));
+    if (c.b >= 0) {
+      float* part = (float*)Bw(pl.cspart);
+      TRY(colsum(dz, (int)M, c.cout, lddz, part, dt, r.st));
+      TRY(reduce_slabs(part, colsum_parts((int)M), c.cout, c.cout, G(c.b), 0, r.st));
+    }
+    if (!dX) return OK;
+    GemmArgs g{};
+    g.M = (int)M; g.N = c.cin; g.K = c.cout; g.A = dz; g.lda = lddz;
+    g.B = Wg(c); g.ldb = c.cin; g.b_trans = 1;
+    g.R = R; g.ldr = ldr;
+    g.C = dX; g.ldc = lddx;
+    return gemm_nt(g, dt, r.st);
+  }
+  // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
+  int dw_bwd(const ConvL& c, int C, const void* dz, const void* X, int H, int Wd, int Ho, int Wo,
+             int stride, void* dX) {
+    DwBwdArgs d{};
+    d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
+    d.x = X; d.dy = dz; d.w = P(c.w); d.dx = dX; d.slab = (float*)Bw(pl.slab);
+    TRY(dw_wgrad(d, dt, r.st));
+    TRY(dw_wgrad_reduce(d.slab, dw_wgrad_parts(pl.N, Ho, Wo, C, dt), C, G(c.w), r.st));
+    return dw_dgrad(d, dt, r.st);
+  }
+
+  int backward_head() {
+    const int N = pl.N, C = net.num_classes;
+    void* dz = Bw(pl.dz);
+    // final upsample: W pass (NCHW rows) then H pass into NHWC low-res logits grad
+    {
+      AxisBwdArgs a{};
+      a.n_o1 = (long long)N * C * pl.H; a.n_o2 = 1; a.Lout = pl.W; a.Lin = pl.W3; a.n_in = 1;
+      a.g = r.dout; a.g_s1 = pl.W; a.g_s2 = 0; a.g_idx = 1; a.g_in = 0;
+      a.d = Bw(pl.t_up); a.d_s1 = pl.W3; a.d_s2 = 0; a.d_idx = 1; a.d_in = 0;
+      TRY(axis_bwd(a, dt, DT_F32, r.st));
+      AxisBwdArgs b{};
+      b.n_o1 = N; b.n_o2 = C; b.Lout = pl.H; b.Lin = pl.H3; b.n_in = pl.W3;
+      b.g = Bw(pl.t_up); b.g_s1 = (long long)C * pl.H * pl.W3; b.g_s2 = (long long)pl.H * pl.W3;
+      b.g_idx = pl.W3; b.g_in = 1;
+      b.d = Bw(pl.g_logits); b.d_s1 = (long long)pl.H3 * pl.W3 * pl.Cp; b.d_s2 = 1;
+      b.d_idx = (long long)pl.W3 * pl.Cp; b.d_in = pl.Cp;
+      TRY(axis_bwd(b, DT_F32, dt, r.st));
+    }
+    // classifier 1x1 (+bias), dropout
+    const bool drop = r.dropout_p > 0.f;
+    TRY(pw_bwd(net.cls_out, pl.c2pw.M, Bw(pl.g_logits), pl.Cp, drop ? W(pl.drop) : W(pl.c2pw.a), 128,
+               drop ? Bw(pl.g_drop) : Bw(pl.c2pw.ga), 128));
+    if (drop) {
+      DropArgs d{};
+      d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = Bw(pl.g_drop); d.ldx = 128;
+      d.y = Bw(pl.c2pw.ga); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
+      TRY(dropout(d, dt, r.st));
+    }
+    // classifier dsconv2, dsconv1
+    TRY(bn_bwd(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, W(pl.c2pw.a), 128, dz));
+    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, W(pl.c2dw.a), 128, Bw(pl.c2dw.ga), 128));
+    TRY(bn_bwd(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, W(pl.c2dw.a), 128, dz));
+    TRY(dw_bwd(net.cls2.dw, 128, dz, W(pl.c1pw.a), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
+    TRY(bn_bwd(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, W(pl.c1pw.a), 128, dz));
+    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, W(pl.c1dw.a), 128, Bw(pl.c1dw.ga), 128));
+    TRY(bn_bwd(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, W(pl.c1dw.a), 128, dz));
+    TRY(dw_bwd(net.cls1.dw, 128, dz, W(pl.f), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
+    // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
+    TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
+    TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, W(pl.fdw.a), 128, Bw(pl.fdw.ga), 128));
+    TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
+    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, W(pl.l2pw.a), 64, Bw(pl.l2pw.ga), 64));
+    TRY(bn_bwd(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, W(pl.fdw.a), 128, dz));
+    TRY(dw_bwd(net.ffm_dw, 128, dz, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_up)));
+    // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
+    {
+      AxisBwdArgs a{};
+      a.n_o1 = (long long)N * pl.H3; a.n_o2 = 1; a.Lout = pl.W3; a.Lin = pl.W5; a.n_in = 128;
+      a.g = Bw(pl.g_up); a.g_s1 = (long long)pl.W3 * 128; a.g_s2 = 0; a.g_idx = 128; a.g_in = 1;
+      a.d = Bw(pl.t_up2); a.d_s1 = (long long)pl.W5 * 128; a.d_s2 = 0; a.d_idx = 128; a.d_in = 1;
+      TRY(axis_bwd(a, dt, DT_F32, r.st));
+      AxisBwdArgs b{};
+      b.n_o1 = N; b.n_o2 = 1; b.Lout = pl.H3; b.Lin = pl.H5; b.n_in = (long long)pl.W5 * 128;
+      b.g = Bw(pl.t_up2); b.g_s1 = (long long)pl.H3 * pl.W5 * 128; b.g_s2 = 0;
+      b.g_idx = (long long)pl.W5 * 128; b.g_in = 1;
+      b.d = Bw(pl.po.ga); b.d_s1 = (long long)pl.H5 * pl.W5 * 128; b.d_s2 = 0;
+      b.d_idx = (long long)pl.W5 * 128; b.d_in = 1;
+      TRY(axis_bwd(b, DT_F32, dt, r.st));
+    }
+    // PPM out 1x1 (256→128) over the concat buffer
+    TRY(bn_bwd(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, W(pl.po.a), 128, dz));
+    TRY(pw_bwd(net.ppm_o, pl.po.M, dz, 128, W(pl.concat), 256, Bw(pl.g_concat), 256));
+    {
+      PpmUpArgs u{};
+      u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = nullptr;
+      u.y = Bw(pl.g_concat); u.ldy = 256; u.coff = 128;
+      TRY(ppm_up_bwd(u, Bw(pl.g_feats), dt, r.st));
+      static const int base[4] = {0, 1, 5, 14};
+      for (int i = 0; i < 4; ++i) {
+        const Unit& u4 = pl.ppk[i];
+        size_t off = (size_t)base[i] * N;
+        TRY(bn_bwd(u4, net.ppm_b[i], (char*)Bw(pl.g_feats) + off * 32 * E, 32,
+                   (char*)W(pl.feats_a) + off * 32 * E, 32, dz));
+        TRY(pw_bwd(net.ppm_c[i], u4.M, dz, 32, (char*)W(pl.pooled) + off * 128 * E, 128,
+                   (char*)Bw(pl.g_pooled) + off * 128 * E, 128));
+      }
+      PoolBwdArgs p{};
+      p.N = N; p.H = pl.H5; p.W = pl.W5; p.C = 128; p.dpooled = Bw(pl.g_pooled);
+      p.dx = Bw(pl.g_concat); p.lddx = 256; p.accumulate = 1;
+      TRY(pyramid_pool_bwd(p, dt, r.st));
+    }
+    return OK;
+  }
+
+  int backward_block(int i) {
+    const LbL& l = net.lb[i];
+    void* dz = Bw(pl.dz);
+    const Unit &ue = pl.lbe[i], &ud = pl.lbd[i], &up = pl.lbp[i];
+    int Hin = i == 0 ? pl.H3 : (i <= 3 ? pl.H4 : pl.H5);
+    int Win = i == 0 ? pl.W3 : (i <= 3 ? pl.W4 : pl.W5);
+    int Ho = i < 3 ? pl.H4 : pl.H5, Wo = i < 3 ? pl.W4 : pl.W5;
+    const void* x = i == 0 ? W(pl.l2pw.a) : W(pl.lbp[i - 1].a);
+    int xld = i == 0 ? 64 : pl.lbp[i - 1].ld;
+    void* gx = i == 0 ? Bw(pl.l2pw.ga) : Bw(pl.lbp[i - 1].ga);
+    int gxld = i == 0 ? 64 : pl.lbp[i - 1].ga_ld;
+    bool shortcut = l.stride == 1 && l.cin == l.cout;
+    const int e = l.cin * 6;
+    TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz));
+    TRY(pw_bwd(l.p, up.M, dz, l.cout, W(ud.a), e, Bw(ud.ga), e));
+    TRY(bn_bwd(ud, l.bd, Bw(ud.ga), e, W(ud.a), e, dz));
+    TRY(dw_bwd(l.d, e, dz, W(ue.a), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
+    TRY(bn_bwd(ue, l.be, Bw(ue.ga), e, W(ue.a), e, dz));
+    // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
+    const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
+    int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
+    return pw_bwd(l.e, ue.M, dz, e, x, xld, gx, gxld, R, ldr);
+  }
+
+  int backward_ltd() {
+    void* dz = Bw(pl.dz);
+    TRY(bn_bwd(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, W(pl.l2pw.a), 64, dz));
+    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, W(pl.l2dw.a), 48, Bw(pl.l2dw.ga), 48));
+    TRY(bn_bwd(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, W(pl.l2dw.a), 48, dz));
+    TRY(dw_bwd(net.ltd2.dw, 48, dz, W(pl.l1pw.a), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
+    TRY(bn_bwd(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, W(pl.l1pw.a), 48, dz));
+    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, W(pl.l1dw.a), 32, Bw(pl.l1dw.ga), 32));
+    TRY(bn_bwd(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, W(pl.l1dw.a), 32, dz));
+    TRY(dw_bwd(net.ltd1.dw, 32, dz, W(pl.c0.a), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
+    TRY(bn_bwd(pl.c0, net.b0, Bw(pl.c0.ga), 32, W(pl.c0.a), 32, dz));
+    Conv0WgradArgs c{};
+    c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
+    c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
+    c.dz = dz; c.slab = (float*)Bw(pl.slab); c.rows_per_block = 8;
+    TRY(conv0_wgrad(c, dt, r.st));
+    int S = conv0_wgrad_parts(pl.N, pl.H1, pl.W1, 8);
+    return reduce_slabs(c.slab, S, 864, 864, G(net.c0.w), 0, r.st);
+  }
+};
+
+}  // namespace
+
+int net_forward(const Plan& pl, const RunArgs& r) {
+  Exec ex(pl, r);
+  return ex.forward();
+}
+
+// stages: 0 = head (upsample, classifier, FFM, PPM), 1 = bottleneck3, 2 = bottleneck2,
+//         3 = bottleneck1 + LearningToDownsample
+int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to) {
+  if (!pl.train) {
+    set_error("net_backward: the plan was built for inference (train=0)");
+    return E_INVALID;
+  }
+  Exec ex(pl, r);
+  for (int s = stage_from; s <= stage_to; ++s) {
+    switch (s) {
+      case 0: TRY(ex.backward_head()); break;
+      case 1: for (int i = 8; i >= 6; --i) TRY(ex.backward_block(i)); break;
+      case 2: for (int i = 5; i >= 3; --i) TRY(ex.backward_block(i)); break;
+      case 3:
+        for (int i = 2; i >= 0; --i) TRY(ex.backward_block(i));
+        TRY(ex.backward_ltd());
+        break;
+      default: set_error("net_backward: bad stage %d", s); return E_INVALID;
+    }
+  }
+  return OK;
+}
+
+}  // namespace fscnn

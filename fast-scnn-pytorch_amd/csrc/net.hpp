@@ -1,0 +1,111 @@
+// Native executor of the Fast-SCNN hot path: layer table (state_dict schema of
+// models/fast_scnn.py), workspace planning and the forward / backward launch sequences.
+// It never allocates device memory: the caller passes the parameter / buffer / gradient arenas
+// and workspaces (see include/fastscnn.h).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+namespace fscnn {
+
+struct TSpec {
+  std::string name;
+  std::vector<int> shape;
+  long long off;    // element offset in its arena
+  long long numel;
+};
+
+struct ConvL {
+  long long w = -1, b = -1;  // offsets into P (floats), -1 = none
+  int cin = 0, cout = 0, k = 1, groups = 1;
+};
+struct BnL {
+  long long g = -1, b = -1;   // P offsets
+  long long rm = -1, rv = -1; // R offsets
+  int nbt = -1;               // index into the num_batches_tracked arena
+  int C = 0;
+  int id = -1;                // BN ordinal
+};
+struct DsL { ConvL dw; BnL bdw; ConvL pw; BnL bpw; };
+struct LbL { ConvL e; BnL be; ConvL d; BnL bd; ConvL p; BnL bp; int cin, cout, stride; };
+
+struct Net {
+  int num_classes = 0, aux = 0;
+  std::vector<TSpec> params;   // P arena (fp32), named_parameters() order
+  std::vector<TSpec> buffers;  // R arena (fp32 running_mean/var) + nbt entries (off = index)
+  long long p_total = 0, r_total = 0;
+  int n_bn = 0;
+  ConvL c0; BnL b0;
+  DsL ltd1, ltd2, cls1, cls2;
+  LbL lb[9];
+  ConvL ppm_c[4]; BnL ppm_b[4];
+  ConvL ppm_o; BnL ppm_ob;
+  ConvL ffm_dw; BnL ffm_bdw;
+  ConvL ffm_low; BnL ffm_blow;
+  ConvL ffm_high; BnL ffm_bhigh;
+  ConvL cls_out;
+  ConvL aux0; BnL aux1; ConvL aux4;
+  long long stage_p_begin[4];  // P offset where each backward stage's parameters start
+};
+
+int net_build(int num_classes, int aux, Net& net);
+
+// A conv(+BN) output in the workspace.
+struct Unit {
+  long long M = 0;
+  int C = 0, ld = 0;
+  size_t z = 0, a = 0;      // raw conv output / activation (same in eval)
+  size_t part = 0;          // BN partial records
+  int nparts = 0;
+  size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
+  size_t ga = 0;            // backward: grad wrt a (bwd workspace)
+  int ga_ld = 0;
+};
+
+struct Plan {
+  const Net* net = nullptr;
+  int N = 0, H = 0, W = 0, dtype = DT_F32, train = 0;
+  int H1, W1, H2, W2, H3, W3, H4, W4, H5, W5;
+  int Cp = 0;   // padded class count (row stride of the low-res logits)
+  size_t ws_bytes = 0, bws_bytes = 0;
+  // forward units
+  Unit c0, l1dw, l1pw, l2dw, l2pw;
+  Unit lbe[9], lbd[9], lbp[9];
+  Unit ppk[4], po;
+  Unit fdw, flow, fhigh;
+  Unit c1dw, c1pw, c2dw, c2pw;
+  Unit aux0;
+  size_t concat = 0, pooled = 0, feats_a = 0, feats_z = 0, up_low = 0, f = 0, drop = 0,
+         logits = 0, aux_drop = 0, aux_logits = 0, pbf = 0, fold_tmp = 0;
+  // backward workspace
+  size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
+         g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
+         g_aux = 0, g_auxlog = 0;
+};
+
+int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl);
+
+struct RunArgs {
+  const void* x; int x_dtype;     // NCHW input image
+  void* out; int out_dtype;       // NCHW logits [N][C][H][W]
+  void* aux_out;                  // NCHW aux logits or null
+  const float* P;                 // parameter arena
+  float* R;                       // running stats arena
+  long long* NBT;                 // num_batches_tracked arena
+  float* G;                       // gradient arena (backward)
+  void* ws;                       // forward workspace (persists until backward)
+  void* bws;                      // backward workspace
+  const void* dout;               // grad wrt out (backward)
+  const void* daux;               // grad wrt aux_out (backward) or null
+  unsigned long long seed;        // dropout seed
+  float dropout_p;
+  float momentum;
+  hipStream_t st;
+};
+
+int net_forward(const Plan& pl, const RunArgs& r);
+int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to);
+
+}  // namespace fscnn

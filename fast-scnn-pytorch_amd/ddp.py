@@ -1,0 +1,79 @@
+"""Data parallelism for the HIP Fast-SCNN: one process per GPU, gradient all-reduce over RCCL.
+
+Replaces ``torch.nn.DataParallel(model, device_ids=[0, 1, 2])`` (train.py:170-171), which
+replicated parameters, scattered the batch and gathered full-resolution logits to cuda:0 every
+step.  Here every rank owns its own shard of the batch and computes its loss locally; the only
+exchange is the gradient all-reduce.  The native backward runs in four stages (head / bottleneck3
+/ bottleneck2 / bottleneck1+LTD, the buckets of SURVEY.md §8(e)); as soon as a stage has been
+enqueued its contiguous slice of the flat gradient arena is all-reduced on a communication
+stream, overlapping the remaining backward (depthwise and GEMM) kernels.
+
+BatchNorm statistics stay per rank (no SyncBN), like DataParallel's per-replica statistics;
+running statistics are those of each rank (rank 0's are the ones to checkpoint).
+"""
+import torch
+import torch.distributed as dist
+
+
+class DistributedFastSCNN(torch.nn.Module):
+    def __init__(self, model, process_group=None, broadcast=True):
+        super().__init__()
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed must be initialised (one process per GPU)")
+        self.module = model
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group)
+        self.backend = dist.get_backend(process_group)
+        self.comm_stream = torch.cuda.Stream() if self._on_gpu() else None
+        self._works = []
+        if broadcast:
+            self.broadcast_parameters()
+        model.grad_stage_hook = self._stage_hook
+
+    def _on_gpu(self):
+        return next(self.module.parameters()).is_cuda
+
+    @torch.no_grad()
+    def broadcast_parameters(self):
+        """Make every rank start from rank 0's parameters and buffers (one call per arena)."""
+        if self._on_gpu():
+            ar = self.module.arena()
+            for t in (ar["P"], ar["R"], ar["NBT"]):
+                dist.broadcast(t, 0, group=self.pg)
+        else:
+            for t in list(self.module.parameters()) + list(self.module.buffers()):
+                dist.broadcast(t.data, 0, group=self.pg)
+
+    def _stage_hook(self, stage, G, begin, end):
+        bucket = G[begin:end]
+        if self.comm_stream is None:
+            self._reduce(bucket)
+            return
+        cur = torch.cuda.current_stream()
+        self.comm_stream.wait_stream(cur)
+        with torch.cuda.stream(self.comm_stream):
+            self._works.append(self._reduce(bucket, async_op=True))
+        if stage == 3:
+            for w in self._works:
+                if w is not None:
+                    w.wait()
+            self._works = []
+            cur.wait_stream(self.comm_stream)
+
+    def _reduce(self, bucket, async_op=False):
+        if self.world == 1:
+            return None
+        if self.backend == "nccl":
+            return dist.all_reduce(bucket, op=dist.ReduceOp.AVG, group=self.pg, async_op=async_op)
+        w = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.pg)
+        bucket.div_(self.world)
+        return w
+
+    def allreduce_grads(self):
+        """Explicit gradient averaging for models that do not run the native staged backward."""
+        for p in self.module.parameters():
+            if p.grad is not None:
+                self._reduce(p.grad)
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)

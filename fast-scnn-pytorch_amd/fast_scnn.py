@@ -1,0 +1,404 @@
+"""Fast-SCNN with the reference interface, executed by the gfx950 HIP library.
+
+Drop-in for ``models/fast_scnn.py`` of Shinokawa/Fast-SCNN-pytorch:
+
+* ``__all__ = ['FastSCNN', 'get_fast_scnn']`` (reference :13);
+* ``FastSCNN(num_classes, aux=False, **kwargs)`` (:16-17) with the same submodule tree, so
+  ``state_dict()`` keys / shapes (Appendix A of SURVEY.md) and attribute paths such as
+  ``model.classifier.conv[1].out_channels`` or ``ppm.conv1.conv[0]`` are unchanged;
+* ``forward(x)`` returns a ``tuple`` of NCHW logits at the input resolution (:33-46);
+* ``get_fast_scnn(dataset, pretrained, root, map_cpu, **kwargs)`` (:240-256) with a static
+  NUM_CLASS table instead of importing the data loaders (no torchvision dependency).
+
+The parameters are re-homed into one flat fp32 arena (64-B aligned tensors, layout owned by the
+C++ executor), running statistics into a second arena; ``.grad`` tensors returned by backward
+are views of one flat gradient arena, so the fused SGD and the RCCL all-reduce each touch a
+single buffer.  The submodules are parameter containers only: the whole network runs as one
+native forward and one staged native backward.  CPU tensors raise — there is no fallback.
+"""
+import os
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .arch import NUM_CLASS
+
+__all__ = ["FastSCNN", "get_fast_scnn"]
+
+
+# ---------------------------------------------------------------------------------------------
+# parameter containers (attribute schema of models/fast_scnn.py:49-237)
+# ---------------------------------------------------------------------------------------------
+class _Container(nn.Module):
+    def forward(self, *args, **kwargs):  # pragma: no cover - guard
+        raise RuntimeError("%s is a parameter container; call the FastSCNN module"
+                           % type(self).__name__)
+
+
+def _seq_conv_bn_relu(cin, cout, k, stride, padding, groups=1):
+    return nn.Sequential(nn.Conv2d(cin, cout, k, stride, padding, groups=groups, bias=False),
+                         nn.BatchNorm2d(cout), nn.ReLU(True))
+
+
+class _ConvBNReLU(_Container):
+    """models/fast_scnn.py:49-61 (padding defaults to 0)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=0, **kwargs):
+        super().__init__()
+        self.conv = _seq_conv_bn_relu(in_channels, out_channels, kernel_size, stride, padding)
+
+
+class _DSConv(_Container):
+    """models/fast_scnn.py:64-79: dw3x3 → BN → ReLU → pw → BN → ReLU."""
+
+    def __init__(self, dw_channels, out_channels, stride=1, **kwargs):
+        super().__init__()
+        dw = _seq_conv_bn_relu(dw_channels, dw_channels, 3, stride, 1, groups=dw_channels)
+        pw = _seq_conv_bn_relu(dw_channels, out_channels, 1, 1, 0)
+        self.conv = nn.Sequential(*dw, *pw)
+
+
+class _DWConv(_Container):
+    """models/fast_scnn.py:82-92."""
+
+    def __init__(self, dw_channels, out_channels, stride=1, **kwargs):
+        super().__init__()
+        self.conv = _seq_conv_bn_relu(dw_channels, out_channels, 3, stride, 1, groups=dw_channels)
+
+
+class LinearBottleneck(_Container):
+    """models/fast_scnn.py:95-115 (t = 6, shortcut iff stride 1 and Cin == Cout)."""
+
+    def __init__(self, in_channels, out_channels, t=6, stride=2, **kwargs):
+        super().__init__()
+        self.use_shortcut = stride == 1 and in_channels == out_channels
+        e = in_channels * t
+        self.block = nn.Sequential(_ConvBNReLU(in_channels, e, 1), _DWConv(e, e, stride),
+                                   nn.Conv2d(e, out_channels, 1, bias=False),
+                                   nn.BatchNorm2d(out_channels))
+
+
+class PyramidPooling(_Container):
+    """models/fast_scnn.py:118-145."""
+
+    def __init__(self, in_channels, out_channels, **kwargs):
+        super().__init__()
+        inter = int(in_channels / 4)
+        for i in range(1, 5):
+            setattr(self, "conv%d" % i, _ConvBNReLU(in_channels, inter, 1))
+        self.out = _ConvBNReLU(in_channels * 2, out_channels, 1)
+
+
+class LearningToDownsample(_Container):
+    """models/fast_scnn.py:148-161."""
+
+    def __init__(self, dw_channels1=32, dw_channels2=48, out_channels=64, **kwargs):
+        super().__init__()
+        self.conv = _ConvBNReLU(3, dw_channels1, 3, 2)
+        self.dsconv1 = _DSConv(dw_channels1, dw_channels2, 2)
+        self.dsconv2 = _DSConv(dw_channels2, out_channels, 2)
+
+
+class GlobalFeatureExtractor(_Container):
+    """models/fast_scnn.py:164-187."""
+
+    def __init__(self, in_channels=64, block_channels=(64, 96, 128), out_channels=128, t=6,
+                 num_blocks=(3, 3, 3), **kwargs):
+        super().__init__()
+        strides = (2, 2, 1)
+        cin = in_channels
+        for i, (cout, n, s) in enumerate(zip(block_channels, num_blocks, strides)):
+            blocks = [LinearBottleneck(cin if j == 0 else cout, cout, t, s if j == 0 else 1)
+                      for j in range(n)]
+            setattr(self, "bottleneck%d" % (i + 1), nn.Sequential(*blocks))
+            cin = cout
+        self.ppm = PyramidPooling(block_channels[2], out_channels)
+
+
+class FeatureFusionModule(_Container):
+    """models/fast_scnn.py:190-218."""
+
+    def __init__(self, highter_in_channels, lower_in_channels, out_channels, scale_factor=4,
+                 **kwargs):
+        super().__init__()
+        self.scale_factor = scale_factor
+        self.dwconv = _DWConv(lower_in_channels, out_channels, 1)
+        self.conv_lower_res = nn.Sequential(nn.Conv2d(out_channels, out_channels, 1),
+                                            nn.BatchNorm2d(out_channels))
+        self.conv_higher_res = nn.Sequential(nn.Conv2d(highter_in_channels, out_channels, 1),
+                                             nn.BatchNorm2d(out_channels))
+        self.relu = nn.ReLU(True)
+
+
+class Classifer(_Container):
+    """models/fast_scnn.py:221-237 (reference spelling kept)."""
+
+    def __init__(self, dw_channels, num_classes, stride=1, **kwargs):
+        super().__init__()
+        self.dsconv1 = _DSConv(dw_channels, dw_channels, stride)
+        self.dsconv2 = _DSConv(dw_channels, dw_channels, stride)
+        self.conv = nn.Sequential(nn.Dropout(0.1), nn.Conv2d(dw_channels, num_classes, 1))
+
+
+# ---------------------------------------------------------------------------------------------
+# native network handle + plans
+# ---------------------------------------------------------------------------------------------
+class _Native:
+    """Owns the C++ fscnn_net and a cache of fscnn_plan handles."""
+
+    def __init__(self, num_classes, aux):
+        lib = _lib.load()
+        h = _lib.c_vp()
+        _lib.check(lib.fscnn_net_create(num_classes, int(aux), _lib.ctypes.byref(h)),
+                   "fscnn_net_create")
+        self.h = h
+        self.lib = lib
+        n, tot = _lib.c_int(), _lib.c_ll()
+        _lib.check(lib.fscnn_net_param_count(h, _lib.ctypes.byref(n), _lib.ctypes.byref(tot)))
+        self.p_total = tot.value
+        self.params = [self._info("fscnn_net_param_info", i) for i in range(n.value)]
+        nb, rtot, nbn = _lib.c_int(), _lib.c_ll(), _lib.c_int()
+        _lib.check(lib.fscnn_net_buffer_count(h, _lib.ctypes.byref(nb), _lib.ctypes.byref(rtot),
+                                              _lib.ctypes.byref(nbn)))
+        self.r_total, self.n_bn = rtot.value, nbn.value
+        self.buffers = [self._info("fscnn_net_buffer_info", i) for i in range(nb.value)]
+        self.stage_ranges = []
+        for s in range(4):
+            b, e = _lib.c_ll(), _lib.c_ll()
+            _lib.check(lib.fscnn_net_stage_range(h, s, _lib.ctypes.byref(b), _lib.ctypes.byref(e)))
+            self.stage_ranges.append((b.value, e.value))
+        self.plans = {}
+
+    def _info(self, fn, i):
+        name, off, numel = _lib.c_char_p(), _lib.c_ll(), _lib.c_ll()
+        _lib.check(getattr(self.lib, fn)(self.h, i, _lib.ctypes.byref(name), _lib.ctypes.byref(off),
+                                         _lib.ctypes.byref(numel)), fn)
+        return name.value.decode(), off.value, numel.value
+
+    def plan(self, N, H, W, dtype_code, train):
+        key = (N, H, W, dtype_code, int(train))
+        p = self.plans.get(key)
+        if p is None:
+            h = _lib.c_vp()
+            _lib.check(self.lib.fscnn_plan_create(self.h, N, H, W, dtype_code, int(train),
+                                                  _lib.ctypes.byref(h)), "fscnn_plan_create")
+            fw, bw = _lib.c_ll(), _lib.c_ll()
+            _lib.check(self.lib.fscnn_plan_workspace(h, _lib.ctypes.byref(fw),
+                                                     _lib.ctypes.byref(bw)))
+            p = (h, fw.value, bw.value)
+            self.plans[key] = p
+        return p
+
+    def __del__(self):
+        try:
+            for h, _, _ in self.plans.values():
+                self.lib.fscnn_plan_destroy(h)
+            self.lib.fscnn_net_destroy(self.h)
+        except Exception:
+            pass
+
+
+class _FastSCNNFunction(torch.autograd.Function):
+    """Whole-network forward / staged backward; grads are views of one flat arena."""
+
+    @staticmethod
+    def forward(ctx, x, model, *params):
+        out, ws, seed, dt = model._run_forward(x, train=True)
+        ctx.model = model
+        ctx.ws, ctx.seed, ctx.dt = ws, seed, dt
+        ctx.save_for_backward(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x,) = ctx.saved_tensors
+        grads = ctx.model._run_backward(gout, x, ctx.ws, ctx.seed, ctx.dt)
+        ctx.ws = None
+        return (None, None) + tuple(grads)
+
+
+class FastSCNN(nn.Module):
+    """Fast-SCNN (models/fast_scnn.py:16-46) on the MI355X HIP path."""
+
+    def __init__(self, num_classes, aux=False, **kwargs):
+        super().__init__()
+        self.aux = aux
+        self.learning_to_downsample = LearningToDownsample(32, 48, 64)
+        self.global_feature_extractor = GlobalFeatureExtractor(64, [64, 96, 128], 128, 6, [3, 3, 3])
+        self.feature_fusion = FeatureFusionModule(64, 128, 128)
+        self.classifier = Classifer(128, num_classes)
+        if self.aux:
+            self.auxlayer = nn.Sequential(nn.Conv2d(64, 32, 3, padding=1, bias=False),
+                                          nn.BatchNorm2d(32), nn.ReLU(True), nn.Dropout(0.1),
+                                          nn.Conv2d(32, num_classes, 1))
+        self.num_classes = num_classes
+        object.__setattr__(self, "_native", None)
+        object.__setattr__(self, "_arena", None)
+        object.__setattr__(self, "grad_stage_hook", None)
+
+    # ---- arenas ----------------------------------------------------------------------------
+    def native(self):
+        if self._native is None:
+            object.__setattr__(self, "_native", _Native(self.num_classes, self.aux))
+            nat = self._native
+            names = [n for n, _ in self.named_parameters()]
+            if names != [p[0] for p in nat.params]:
+                raise RuntimeError("FastSCNN: parameter table mismatch with the native executor")
+        return self._native
+
+    def _apply(self, fn, recurse=True):
+        r = super()._apply(fn, recurse)
+        object.__setattr__(self, "_arena", None)
+        return r
+
+    def _pack_arena(self):
+        """Re-home params / buffers into the executor's flat arenas on their current device."""
+        nat = self.native()
+        params = list(self.parameters())
+        dev = params[0].device
+        P = torch.zeros(nat.p_total, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, (_, off, numel) in zip(params, nat.params):
+                if p.numel() != numel or p.dtype != torch.float32:
+                    raise RuntimeError("FastSCNN: parameter %s has unexpected shape/dtype" % (_,))
+                P[off:off + numel].copy_(p.detach().reshape(-1))
+                p.data = P[off:off + numel].view(p.shape)
+            R = torch.zeros(nat.r_total, dtype=torch.float32, device=dev)
+            NBT = torch.zeros(nat.n_bn, dtype=torch.int64, device=dev)
+            mods = dict(self.named_modules())
+            for name, off, numel in nat.buffers:
+                mname, bname = name.rsplit(".", 1)
+                m = mods[mname]
+                cur = m._buffers[bname]
+                if bname == "num_batches_tracked":
+                    NBT[off].copy_(cur.reshape(()))
+                    m._buffers[bname] = NBT[off]
+                else:
+                    R[off:off + numel].copy_(cur.reshape(-1))
+                    m._buffers[bname] = R[off:off + numel]
+        arena = {"P": P, "R": R, "NBT": NBT, "params": params,
+                 "ptrs": (params[0].data_ptr(), params[-1].data_ptr())}
+        object.__setattr__(self, "_arena", arena)
+        return arena
+
+    def arena(self):
+        a = self._arena
+        params = None
+        if a is not None:
+            params = a["params"]
+            if (params[0].data_ptr(), params[-1].data_ptr()) != a["ptrs"] or \
+                    params[0].data_ptr() != a["P"].data_ptr():
+                a = None
+        if a is None:
+            a = self._pack_arena()
+        return a
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        r = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        if assign:
+            object.__setattr__(self, "_arena", None)
+        return r
+
+    # ---- execution ----------------------------------------------------------------------------
+    def _compute_dtype(self, x):
+        if x.dtype == torch.bfloat16:
+            return torch.bfloat16
+        if torch.is_autocast_enabled("cuda"):
+            # AMP (train.py:269 uses fp16 autocast): this path computes in bf16 with fp32 master
+            # weights and fp32 statistics
+            return torch.bfloat16
+        if x.dtype in (torch.float32, torch.float16):
+            return torch.float32
+        raise RuntimeError("FastSCNN: unsupported input dtype %s" % (x.dtype,))
+
+    def _momentum(self):
+        m = self.learning_to_downsample.conv.conv[1].momentum
+        if m is None:
+            raise RuntimeError("FastSCNN: BatchNorm momentum=None (cumulative) is not supported")
+        return float(m)
+
+    def _dropout_p(self):
+        return float(self.classifier.conv[0].p)
+
+    def _run_forward(self, x, train):
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise RuntimeError("FastSCNN: expected input [N, 3, H, W], got %s" % (tuple(x.shape),))
+        if not x.is_cuda:
+            raise RuntimeError("FastSCNN: the HIP path needs a ROCm device tensor (got %s); "
+                               "move the model and input to 'cuda'" % (x.device,))
+        nat = self.native()
+        ar = self.arena()
+        if ar["P"].device != x.device:
+            raise RuntimeError("FastSCNN: input on %s but parameters on %s"
+                               % (x.device, ar["P"].device))
+        N, _, H, W = x.shape
+        if H < 32 or W < 32:
+            raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
+        dt = self._compute_dtype(x)
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        if train and N < 2:
+            # the reference raises from the PPM 1x1 BatchNorm in train mode (SURVEY §0 trap 5)
+            raise ValueError("Expected more than 1 value per channel when training, got input "
+                             "size torch.Size([1, 32, 1, 1])")
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), train)
+        ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
+        out = torch.empty((N, self.num_classes, H, W), dtype=dt, device=x.device)
+        p = self._dropout_p() if train else 0.0
+        seed = 0
+        if train and p > 0:
+            fixed = getattr(self, "_dropout_seed", None)  # tests pin the mask (oracle parity)
+            seed = int(fixed) if fixed is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
+        _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(out),
+                  _lib.dtype_code(dt), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]),
+                  _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p), _lib.c_float(self._momentum()),
+                  _lib.stream_ptr(x.device))
+        return out, ws, seed, dt
+
+    def _run_backward(self, gout, x, ws, seed, dt):
+        nat = self.native()
+        ar = self.arena()
+        N, _, H, W = x.shape
+        plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), True)
+        gout = gout.to(dt).contiguous()
+        G = torch.zeros(nat.p_total, dtype=torch.float32, device=x.device)
+        bws = torch.empty(max(bw, 1), dtype=torch.uint8, device=x.device)
+        p = self._dropout_p()
+        hook = self.grad_stage_hook
+        for s in range(4):
+            _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x), _lib.dtype_code(x.dtype),
+                      _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws), _lib.ptr(bws), _lib.c_ull(seed),
+                      _lib.c_float(p), s, s, _lib.stream_ptr(x.device))
+            if hook is not None:
+                b, e = nat.stage_ranges[s]
+                hook(s, G, b, e)
+        return [G[off:off + numel].view(prm.shape)
+                for prm, (_, off, numel) in zip(ar["params"], nat.params)]
+
+    def forward(self, x):
+        train = self.training
+        needs_grad = train and torch.is_grad_enabled()
+        if needs_grad:
+            ar = self.arena() if x.is_cuda else None
+            if ar is None:
+                self._run_forward(x, train)  # raises the device error
+            out = _FastSCNNFunction.apply(x, self, *ar["params"])
+        else:
+            out = self._run_forward(x, train)[0]
+        return (out,)
+
+
+def get_fast_scnn(dataset="citys", pretrained=False, root="./weights", map_cpu=False, **kwargs):
+    """models/fast_scnn.py:240-256 without the torchvision-importing data_loader lookup."""
+    acronyms = {"pascal_voc": "voc", "pascal_aug": "voc", "ade20k": "ade", "coco": "coco",
+                "citys": "citys", "tusimple": "tusimple"}
+    if dataset not in NUM_CLASS:
+        raise KeyError(dataset)
+    model = FastSCNN(NUM_CLASS[dataset], **kwargs)
+    if pretrained:
+        path = os.path.join(root, "fast_scnn_%s.pth" % acronyms[dataset])
+        sd = torch.load(path, map_location="cpu" if map_cpu else None, weights_only=True)
+        model.load_state_dict(sd)
+    return model

@@ -1,0 +1,83 @@
+"""Fused multi-tensor SGD (torch.optim.SGD semantics, train.py:195-198) on the HIP path.
+
+When every parameter of a group is a view of one flat arena and every ``.grad`` a view of one
+flat gradient buffer at the same offsets (what ``FastSCNN`` produces), the whole step is ONE
+kernel over the arena.  Otherwise it falls back to one launch per tensor (still the HIP kernel).
+State keeps torch's ``momentum_buffer`` key so ``state_dict()`` interoperates.
+"""
+import torch
+
+from . import _lib
+
+
+def _flat_base(tensors):
+    """(base tensor storage pointer, [offsets]) if all tensors are contiguous views of one
+    storage, else None."""
+    st = tensors[0].untyped_storage().data_ptr()
+    offs = []
+    for t in tensors:
+        if not t.is_contiguous() or t.untyped_storage().data_ptr() != st:
+            return None
+        offs.append(t.storage_offset())
+    return st, offs
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-2, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                 nesterov=False, grad_scale=1.0):
+        if lr < 0.0:
+            raise ValueError("Invalid learning rate: {}".format(lr))
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening,
+                        weight_decay=weight_decay, nesterov=nesterov, grad_scale=grad_scale)
+        super().__init__(params, defaults)
+
+    def _launch(self, p, g, buf, n, group, first):
+        _lib.call("fscnn_sgd", _lib.c_vp(p), _lib.c_vp(g), _lib.c_vp(buf), n,
+                  _lib.c_float(group["lr"]), _lib.c_float(group["momentum"]),
+                  _lib.c_float(group["dampening"]), _lib.c_float(group["weight_decay"]),
+                  int(group["nesterov"]), int(first), _lib.c_float(group["grad_scale"]),
+                  _lib.stream_ptr())
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            for p in params:
+                if not p.is_cuda or p.dtype != torch.float32:
+                    raise RuntimeError("FusedSGD needs fp32 ROCm parameters")
+            grads = [p.grad for p in params]
+            first = any("momentum_buffer" not in self.state[p] for p in params)
+            pb, gb = _flat_base([p.data for p in params]), _flat_base(grads)
+            fused = (pb is not None and gb is not None and pb[1] == gb[1] and
+                     all(p.grad.dtype == torch.float32 for p in params) and
+                     not any(("momentum_buffer" in self.state[p]) != (not first) for p in params))
+            if fused:
+                lo = min(pb[1])
+                hi = max(o + p.numel() for o, p in zip(pb[1], params))
+                key = "_flat_buf"
+                flat = group.get(key)
+                if flat is None or flat.numel() != hi - lo or first:
+                    flat = torch.zeros(hi - lo, dtype=torch.float32, device=params[0].device)
+                    group[key] = flat
+                    for o, p in zip(pb[1], params):
+                        self.state[p]["momentum_buffer"] = flat[o - lo:o - lo + p.numel()].view_as(p)
+                self._launch(pb[0] + lo * 4, gb[0] + lo * 4, flat.data_ptr(), hi - lo, group,
+                             first)
+            else:
+                for p in params:
+                    st = self.state[p]
+                    f = "momentum_buffer" not in st
+                    if f:
+                        st["momentum_buffer"] = torch.zeros_like(p)
+                    g = p.grad.float().contiguous()
+                    self._launch(p.data_ptr(), g.data_ptr(), st["momentum_buffer"].data_ptr(),
+                                 p.numel(), group, f)
+        return loss

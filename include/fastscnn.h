@@ -1,0 +1,121 @@
+/* fastscnn.h — C ABI of libfastscnn_hip.so, the MI355X (gfx950) Fast-SCNN hot path.
+ *
+ * Plain pointers and sizes only (no torch types).  Every function returns 0 on success or a
+ * negative status (-1 invalid argument, -2 unsupported, -3 HIP error); fscnn_last_error()
+ * returns the thread-local message of the last failure.  The library never allocates device
+ * memory: the caller passes arenas and workspaces.  Launches go to the caller's hipStream_t
+ * (passed as void*), so calls are graph-capturable and overlap with RCCL on other streams.
+ *
+ * dtype codes: 0 = fp32, 1 = bf16.  Activations are NHWC; images and logits are NCHW.
+ *
+ * Reference interfaces replaced (Shinokawa/Fast-SCNN-pytorch):
+ *   fscnn_net_* / fscnn_plan_* / fscnn_forward   FastSCNN.__init__ / forward
+ *                                                 (models/fast_scnn.py:16-46)
+ *   fscnn_backward                                autograd backward of that forward
+ *                                                 (train.py:273 / :280 loss.backward())
+ *   fscnn_ce_fwd / fscnn_ce_bwd                   nn.CrossEntropyLoss(ignore_index=-1)
+ *                                                 (utils/loss.py:103-124, train.py:191)
+ *   fscnn_sgd                                     torch.optim.SGD.step (train.py:195-198,274)
+ *   fscnn_conv0_fwd                               _ConvBNReLU(3,32,3,2) (models/fast_scnn.py:153)
+ *   fscnn_dw3x3_*                                 nn.Conv2d(groups=C, k=3, pad=1) (:70, :86)
+ *   fscnn_pw_gemm / fscnn_pw_wgrad                nn.Conv2d(k=1) (:73, :103, :107, :124-128,
+ *                                                 :198, :202, :230)
+ *   fscnn_bn_*                                    nn.BatchNorm2d (:56, :71, :74, :87, :108)
+ *   fscnn_bilinear_ac_*                           F.interpolate(bilinear, align_corners=True)
+ *                                                 (:40, :135, :212)
+ *   fscnn_pyramid_pool_*                          AdaptiveAvgPool2d(1,2,3,6) (:130-132)
+ */
+#ifndef FASTSCNN_H
+#define FASTSCNN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fscnn_net fscnn_net;
+typedef struct fscnn_plan fscnn_plan;
+
+const char* fscnn_version(void);
+const char* fscnn_last_error(void);
+
+/* ---- network: layer table + arena layout ------------------------------------------------ */
+int fscnn_net_create(int num_classes, int aux, fscnn_net** out);
+void fscnn_net_destroy(fscnn_net* net);
+/* parameter arena (fp32, 64-B aligned tensors, named_parameters() order) */
+int fscnn_net_param_count(const fscnn_net* net, int* count, long long* total_floats);
+int fscnn_net_param_info(const fscnn_net* net, int i, const char** name, long long* offset,
+                         long long* numel);
+/* buffer arena: running_mean / running_var in a fp32 arena, num_batches_tracked in an int64
+ * arena (for those entries *offset is the index into the int64 arena) */
+int fscnn_net_buffer_count(const fscnn_net* net, int* count, long long* total_floats, int* num_bn);
+int fscnn_net_buffer_info(const fscnn_net* net, int i, const char** name, long long* offset,
+                          long long* numel);
+/* backward stage s (0..3) finalises the gradients of parameters [begin, end) of the arena */
+int fscnn_net_stage_range(const fscnn_net* net, int stage, long long* begin, long long* end);
+
+/* ---- plan: shapes + workspace sizes for one (N, H, W, dtype, mode) ---------------------- */
+int fscnn_plan_create(const fscnn_net* net, int N, int H, int W, int dtype, int train,
+                      fscnn_plan** out);
+void fscnn_plan_destroy(fscnn_plan* plan);
+int fscnn_plan_workspace(const fscnn_plan* plan, long long* fwd_bytes, long long* bwd_bytes);
+int fscnn_plan_shapes(const fscnn_plan* plan, int* dims /* 10: H1 W1 H2 W2 H3 W3 H4 W4 H5 W5 */);
+
+/* ---- whole-network forward / backward ----------------------------------------------------- */
+int fscnn_forward(const fscnn_plan* plan, const void* x, int x_dtype, void* out, int out_dtype,
+                  const float* params, float* running, long long* nbt, void* ws,
+                  unsigned long long dropout_seed, float dropout_p, float momentum,
+                  void* stream);
+int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int x_dtype,
+                   const float* params, float* grads, void* ws, void* bws,
+                   unsigned long long dropout_seed, float dropout_p, int stage_from,
+                   int stage_to, void* stream);
+
+/* ---- loss / optimizer ------------------------------------------------------------------- */
+/* out2[0] = mean loss over valid pixels, out2[1] = valid count; part: ce_parts*2 floats */
+long long fscnn_ce_parts(int N, long long HW);
+int fscnn_ce_fwd(const void* logits, int dtype, const long long* target, int N, int C,
+                 long long HW, long long ignore_index, float* part, float* out2, void* stream);
+int fscnn_ce_bwd(const void* logits, int dtype, const long long* target, int N, int C,
+                 long long HW, long long ignore_index, const float* grad_out,
+                 const float* out2, void* dlogits, void* stream);
+int fscnn_sgd(float* p, const float* g, float* buf, long long n, float lr, float momentum,
+              float dampening, float weight_decay, int nesterov, int first, float grad_scale,
+              void* stream);
+
+/* ---- individual kernels (per-op parity tests) ------------------------- */
+int fscnn_conv0_fwd(const void* x, int x_dtype, int N, int H, int W, const float* w,
+                    const float* scale, const float* shift, int relu, void* y, int y_dtype,
+                    void* stream);
+int fscnn_dw3x3_fwd(const void* x, int dtype, int N, int H, int W, int C, int stride,
+                    const float* w, const float* scale, const float* shift, int relu, void* y,
+                    void* stream);
+int fscnn_dw3x3_dgrad(const void* dy, int dtype, int N, int H, int W, int C, int stride,
+                      const float* w, void* dx, void* stream);
+long long fscnn_dw3x3_wgrad_slab_floats(int N, int H, int W, int C, int stride, int dtype);
+int fscnn_dw3x3_wgrad(const void* x, const void* dy, int dtype, int N, int H, int W, int C,
+                      int stride, float* slab, float* dw, void* stream);
+/* C[M][N] = act((A[M][K] . B^T) * scale + shift (+ R)); B is [N][K] (b_trans=0) or [K][N] */
+int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                  int b_trans, const float* scale, const float* shift, const void* R, int ldr,
+                  int relu, void* C, int ldc, float* stats_part, int dtype, void* stream);
+long long fscnn_pw_wgrad_slab_floats(int M, int N, int K);
+/* dW[N][K] = sum_m D[m][n] X[m][k] */
+int fscnn_pw_wgrad(int M, int N, int K, const void* D, int ldd, const void* X, int ldx,
+                   float* slab, float* dW, int dtype, void* stream);
+int fscnn_bn_finalize(const float* part, int P, int C, const float* gamma, const float* beta,
+                      float* rmean, float* rvar, long long* nbt, float momentum, float* mean,
+                      float* invstd, float* scale, float* shift, void* stream);
+int fscnn_bilinear_ac_fwd(const void* x, int dtype, int N, int Hi, int Wi, int C, int Ho, int Wo,
+                          void* y, int out_nchw, int out_dtype, void* stream);
+/* NHWC grad wrt output [N][Ho][Wo][C] -> NHWC grad wrt input [N][Hi][Wi][C] (fp32 tmp) */
+int fscnn_bilinear_ac_bwd(const void* dy, int dtype, int N, int Hi, int Wi, int C, int Ho, int Wo,
+                          float* tmp, void* dx, void* stream);
+int fscnn_pyramid_pool_fwd(const void* x, int dtype, int N, int H, int W, int C, int ldx,
+                           void* pooled, void* stream);
+int fscnn_pyramid_pool_bwd(const void* dpooled, int dtype, int N, int H, int W, int C, void* dx,
+                           int lddx, int accumulate, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -141,7 +141,7 @@ def dropout_mask(seed, shape, p):
     """Keep-mask for the classifier Dropout, a pure function of (seed, NCHW linear index).
 
     The HIP path computes the identical hash (csrc/common.hpp ``dropout_keep``), so train-mode
-    parity holds with dropout active.  u = splitmix64-like hash → 24-bit uniform; keep iff u >= p.
+    parity holds with dropout active.  24-bit uniform from a splitmix64 hash; keep iff u >= p.
     """
     n = int(np.prod(shape))
     idx = np.arange(n, dtype=np.uint64)
@@ -150,8 +150,9 @@ def dropout_mask(seed, shape, p):
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
-    u = (z >> np.uint64(40)).astype(np.float64) * (1.0 / float(1 << 24))
-    return torch.from_numpy((u >= p).reshape(shape))
+    # keep iff 24-bit uniform u >= p  <=>  (z >> 40) >= ceil(p * 2^24)
+    thr = int(np.ceil(np.float64(np.float32(p)) * float(1 << 24)))
+    return torch.from_numpy(((z >> np.uint64(40)) >= np.uint64(thr)).reshape(shape))
 
 
 def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
