@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Fast-SCNN MI355X benchmark — BASELINE.json metric:
+    "images/sec fwd+bwd @1024x2048 bs=8 per GPU; 1/2/4/8-GPU scaling"
+
+Workload (BASELINE.json configs[2] / [3]): one training step = forward + cross-entropy +
+backward + fused SGD (lr 0.01, momentum 0.9, wd 1e-4) of Fast-SCNN (19 classes) on a synthetic
+Cityscapes-shaped batch of 8 x 3 x 1024 x 2048 per GPU, bf16 activations with fp32 master
+weights and fp32 statistics.  Weights come from the portable generator (random init, PyTorch
+default law), inputs/targets from the same generator with rank-dependent seeds (5 % ignore).
+N > 1: one process per GPU (torchrun), gradients all-reduced over RCCL in four buckets
+overlapped with the staged backward; weak scaling (8 images per GPU).
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+Rank 0 prints ONE JSON line.  Extra objects: roofline of the dominant kernel family (HIP events
+on its launch stream over the timed region, algorithmic bytes per SURVEY.md §8(d)),
+cpu_baseline (the oracle restatement timed on this host's cores on a bounded sample), and the
+forward-only fp32 inference rate (cfg2) for the north-star forward target.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec fwd+bwd @1024x2048 bs=8 per GPU; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0
+MFMA_PEAK_TFS = {"bf16": 2500.0, "fp32": 157.3}
+PROF_KINDS = {1: "conv0_fwd", 2: "dw_fwd", 3: "dw_dgrad", 4: "dw_wgrad", 5: "gemm_nt",
+              6: "gemm_tn", 9: "upsample"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=2048)
+    ap.add_argument("--classes", type=int, default=19)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--profile-kind", type=int, default=0, help="0 = dominant (census)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-forward", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def prof(lib, kind, fn, max_launches):
+    import torch
+    from fast_scnn_pytorch_amd import _lib
+    _lib.check(lib.fscnn_prof_begin(kind, max_launches), "fscnn_prof_begin")
+    fn()
+    torch.cuda.synchronize()
+    ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
+    _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
+                                  ctypes.byref(f)), "fscnn_prof_end")
+    return ms.value, n.value, b.value, f.value
+
+
+def cpu_baseline(args):
+    """Oracle restatement (port) of one train step on a bounded sample, timed on host cores."""
+    import numpy as np
+    import torch
+    from fast_scnn_pytorch_amd import arch, portable_init
+    from oracle import fast_scnn_ref as ref  # checker / CPU baseline only
+    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    nb = 2
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+          arch.portable_state_dict(args.classes, seed=0).items()}
+    for k, v in sd.items():
+        if v.is_floating_point() and "running" not in k:
+            v.requires_grad_(True)
+    x = torch.from_numpy(portable_init.input_tensor(1, (nb, 3, args.height, args.width)))
+    t = torch.from_numpy(portable_init.target_tensor(3, (nb, args.height, args.width),
+                                                     args.classes, 0.05))
+
+    def step():
+        for v in sd.values():
+            v.grad = None
+        outs, _, _ = ref.forward(sd, x, args.classes, training=True, dropout_seed=5)
+        ref.cross_entropy(outs[0], t).backward()
+
+    step()
+    times = []
+    t_end = time.perf_counter() + 25.0
+    while len(times) < 3 and (not times or time.perf_counter() < t_end):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(nb / med, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": "oracle/fast_scnn_ref.py train step (fwd+CE+bwd, fp32) on %d x 3 x %d x %d, "
+                      "median of %d after 1 warm-up, torch CPU %d threads"
+                      % (nb, args.height, args.width, len(times), threads)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import _fscnn_boot
+    _fscnn_boot.load()
+    import numpy as np
+    from fast_scnn_pytorch_amd import _lib, arch, portable_init
+    from fast_scnn_pytorch_amd.loss import cross_entropy
+    from fast_scnn_pytorch_amd.optim import FusedSGD
+    from models.fast_scnn import FastSCNN
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    lib = _lib.load()
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    model = FastSCNN(args.classes)
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+          arch.portable_state_dict(args.classes, seed=0).items()}
+    model.load_state_dict(sd)
+    model = model.to(dev).train()
+    net = model
+    if world > 1:
+        from fast_scnn_pytorch_amd.ddp import DistributedFastSCNN
+        net = DistributedFastSCNN(model)
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    B, H, W = args.batch, args.height, args.width
+    x = torch.from_numpy(portable_init.input_tensor(1 + rank, (B, 3, H, W))).to(dev).to(dt)
+    t = torch.from_numpy(portable_init.target_tensor(3 + rank, (B, H, W), args.classes,
+                                                     0.05)).to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = net(x)[0]
+        loss = cross_entropy(out, t)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        loss = step()
+    barrier()
+    first_loss = float(loss.item())
+
+    # census (untimed): which kernel family dominates the step
+    kind = args.profile_kind
+    census = {}
+    if kind == 0:
+        for k, name in PROF_KINDS.items():
+            ms, n, b, f = prof(lib, k, step, 4096)
+            census[name] = round(ms, 4)
+        kind = max(PROF_KINDS, key=lambda k: census[PROF_KINDS[k]])
+    barrier()
+
+    # ---- timed region: K steps, events on the dominant family's launches -------------------
+    _lib.check(lib.fscnn_prof_begin(kind, 512 * max(1, args.steps)), "fscnn_prof_begin")
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
+    _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
+                                  ctypes.byref(f)), "fscnn_prof_end")
+    last_loss = float(loss.item())
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    value = world * B * args.steps / elapsed
+    avg_ms = ms.value / max(1, n.value)
+    bytes_per_launch = b.value / max(1, n.value)
+    flops_per_launch = f.value / max(1, n.value)
+    ach_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    ach_tfs = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    mfma_peak = MFMA_PEAK_TFS[args.dtype]
+    kname = PROF_KINDS.get(kind, str(kind))
+    if kname in ("gemm_nt", "gemm_tn") and ach_tfs / mfma_peak > ach_gbs / HBM_PEAK_GBS:
+        roof = {"bound": "mfma", "achieved": round(ach_tfs, 3), "peak": mfma_peak,
+                "unit": "TFLOP/s", "frac": round(ach_tfs / mfma_peak, 4)}
+    else:
+        roof = {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach_gbs / HBM_PEAK_GBS, 4)}
+    roof.update({"kernel": kname, "launches": n.value, "avg_launch_us": round(avg_ms * 1e3, 2),
+                 "algo_bytes_per_launch": round(bytes_per_launch),
+                 "algo_flops_per_launch": round(flops_per_launch), "traffic": None})
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (kname, args.dtype))
+    if os.path.exists(pmc):
+        try:
+            roof["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (portable counter-based generator; random-init weights, default law)",
+        "config": {"workload": "cfg3 train step: fwd + CE(ignore -1) + bwd + fused SGD",
+                   "model": "FastSCNN (19 classes)", "global_batch": world * B,
+                   "per_gpu_batch": B, "resolution": [H, W], "parallelism": "dp%d" % world},
+        "roofline": roof,
+        "loss": {"after_warmup": round(first_loss, 5), "final": round(last_loss, 5)},
+    }
+    if census:
+        result["kernel_ms_per_step_census"] = census
+
+    # forward-only fp32 inference (cfg2): north-star forward target (rank 0, N=1 only)
+    if rank == 0 and world == 1 and not args.no_forward:
+        model.eval()
+        x32 = x.float()
+        with torch.no_grad():
+            for _ in range(3):
+                model(x32)
+            torch.cuda.synchronize()
+            nrep = max(5, args.steps // 2)
+            t1 = time.perf_counter()
+            for _ in range(nrep):
+                model(x32)
+            torch.cuda.synchronize()
+            fe = time.perf_counter() - t1
+            fms, fn, fb, ff = prof(lib, 2, lambda: model(x32), 256)
+        dw_gbs = fb / max(fn, 1) / (fms / max(fn, 1) * 1e-3) / 1e9 if fms > 0 else 0
+        result["forward_fp32"] = {"value": round(B * nrep / fe, 2), "unit": "images/s",
+                                  "ms_per_batch": round(1e3 * fe / nrep, 3),
+                                  "config": "cfg2 eval fp32 %dx3x%dx%d" % (B, H, W),
+                                  "dw_fwd_GBps": round(dw_gbs, 1),
+                                  "dw_fwd_hbm_frac": round(dw_gbs / HBM_PEAK_GBS, 4)}
+        model.train()
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -32,10 +32,15 @@ SIGNATURES = {
     "fscnn_plan_destroy": (None, [c_vp]),
     "fscnn_plan_workspace": (c_int, [c_vp, P_ll, P_ll]),
     "fscnn_plan_shapes": (c_int, [c_vp, P_int]),
+    "fscnn_plan_buffer": (c_int, [c_vp, c_char_p, P_ll, P_ll, P_int, P_int, P_int]),
     "fscnn_forward": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_ull,
                               c_float, c_float, c_vp]),
     "fscnn_backward": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_ull, c_float,
                                c_int, c_int, c_vp]),
+    "fscnn_prof_begin": (c_int, [c_int, c_int]),
+    "fscnn_prof_end": (c_int, [ctypes.POINTER(ctypes.c_double), P_ll, ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double)]),
+    "fscnn_prof_kind_name": (c_char_p, [c_int]),
     "fscnn_ce_parts": (c_ll, [c_int, c_ll]),
     "fscnn_ce_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp, c_vp]),
     "fscnn_ce_bwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp, c_vp,

@@ -29,9 +29,80 @@ int check_launch(const char* what) {
   return OK;
 }
 
+// ---- launch profiler --------------------------------------------------------------------
+int g_prof_kind = PK_NONE;
+namespace {
+struct ProfState {
+  std::vector<hipEvent_t> ev;  // pairs
+  size_t used = 0;
+  double bytes = 0, flops = 0;
+  long long launches = 0;
+  bool overflow = false;
+} g_prof;
+}  // namespace
+
+void prof_start(hipStream_t st) {
+  if (g_prof.used + 2 > g_prof.ev.size()) { g_prof.overflow = true; return; }
+  hipEventRecord(g_prof.ev[g_prof.used], st);
+}
+void prof_stop(hipStream_t st, double bytes, double flops) {
+  if (g_prof.used + 2 > g_prof.ev.size()) return;
+  hipEventRecord(g_prof.ev[g_prof.used + 1], st);
+  g_prof.used += 2;
+  g_prof.bytes += bytes;
+  g_prof.flops += flops;
+  g_prof.launches++;
+}
+
 }  // namespace fscnn
 
 using namespace fscnn;
+
+extern "C" int fscnn_prof_begin(int kind, int max_launches) {
+  if (kind <= PK_NONE || kind >= PK_COUNT || max_launches <= 0) {
+    set_error("fscnn_prof_begin: bad kind %d", kind);
+    return E_INVALID;
+  }
+  size_t need = (size_t)max_launches * 2;
+  while (g_prof.ev.size() < need) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) { set_error("hipEventCreate failed"); return E_HIP; }
+    g_prof.ev.push_back(e);
+  }
+  g_prof.used = 0; g_prof.bytes = 0; g_prof.flops = 0; g_prof.launches = 0;
+  g_prof.overflow = false;
+  g_prof_kind = kind;
+  return OK;
+}
+
+// Synchronises on the recorded events; returns summed kernel time (ms), launches and the
+// algorithmic bytes / flops of those launches.
+extern "C" int fscnn_prof_end(double* total_ms, long long* launches, double* bytes, double* flops) {
+  g_prof_kind = PK_NONE;
+  double tot = 0;
+  for (size_t i = 0; i + 1 < g_prof.used; i += 2) {
+    float ms = 0;
+    if (hipEventSynchronize(g_prof.ev[i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, g_prof.ev[i], g_prof.ev[i + 1]) != hipSuccess) {
+      set_error("fscnn_prof_end: event query failed");
+      return E_HIP;
+    }
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = g_prof.launches;
+  if (bytes) *bytes = g_prof.bytes;
+  if (flops) *flops = g_prof.flops;
+  if (g_prof.overflow) { set_error("fscnn_prof_end: event pool overflow"); return E_INVALID; }
+  return OK;
+}
+
+extern "C" const char* fscnn_prof_kind_name(int kind) {
+  static const char* names[PK_COUNT] = {"none", "conv0_fwd", "dw_fwd", "dw_dgrad", "dw_wgrad",
+                                        "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
+                                        "upsample_bwd", "cross_entropy"};
+  return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
+}
 
 struct fscnn_net {
   Net net;
@@ -296,3 +367,20 @@ int fscnn_pyramid_pool_bwd(const void* dpooled, int dtype, int N, int H, int W, 
 }
 
 }  // extern "C"
+
+extern "C" int fscnn_plan_buffer(const fscnn_plan* plan, const char* name, long long* offset,
+                                 long long* rows, int* cols, int* ld, int* in_bws) {
+  if (!plan || !name) { set_error("fscnn_plan_buffer: null argument"); return E_INVALID; }
+  for (const auto& b : plan->plan.named) {
+    if (b.name == name) {
+      if (offset) *offset = (long long)b.off;
+      if (rows) *rows = b.rows;
+      if (cols) *cols = b.cols;
+      if (ld) *ld = b.ld;
+      if (in_bws) *in_bws = b.bws;
+      return OK;
+    }
+  }
+  set_error("fscnn_plan_buffer: no buffer named '%s' in this plan", name);
+  return E_INVALID;
+}

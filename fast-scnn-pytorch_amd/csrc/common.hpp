@@ -130,6 +130,27 @@ int check_launch(const char* what);
 
 enum Status : int { OK = 0, E_INVALID = -1, E_UNSUPPORTED = -2, E_HIP = -3 };
 
+// ---- in-library launch profiler (bench.py roofline: HIP events on the launch stream) ---------
+enum ProfKind : int {
+  PK_NONE = 0, PK_CONV0_FWD, PK_DW_FWD, PK_DW_DGRAD, PK_DW_WGRAD, PK_GEMM_NT, PK_GEMM_TN,
+  PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_COUNT
+};
+extern int g_prof_kind;  // kind being recorded (PK_NONE = off)
+void prof_start(hipStream_t st);
+void prof_stop(hipStream_t st, double bytes, double flops);
+struct ProfScope {
+  bool on;
+  hipStream_t st;
+  double bytes, flops;
+  ProfScope(int kind, hipStream_t s, double b, double f)
+      : on(g_prof_kind == kind), st(s), bytes(b), flops(f) {
+    if (on) prof_start(st);
+  }
+  ~ProfScope() {
+    if (on) prof_stop(st, bytes, flops);
+  }
+};
+
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace fscnn

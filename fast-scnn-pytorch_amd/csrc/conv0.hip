@@ -136,6 +136,10 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
     return E_INVALID;
   }
   dim3 grid(cdiv(a.Wo, C0_TILE), a.N * a.Ho);
+  const double px = (double)a.N * a.Ho * a.Wo;
+  ProfScope ps(PK_CONV0_FWD, st,
+               (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (y_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
+               2.0 * 27 * 32 * px);
   if (y_dtype == DT_F32)
     conv0_fwd_kernel<float><<<grid, 256, 0, st>>>(a);
   else

@@ -116,7 +116,14 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     s_red[ty * BX * V + tx * V + j] = s[j];
   }
   __shared__ float s_cnt[256];
-  s_cnt[ty] = (float)npx_strip;  // identical for all tx (same strip)
+  // pixels of this strip, independent of whether this thread's channel vector exists (all tx of a
+  // row write the same value — no race between active and padding threads)
+  int strip_px = 0;
+  if (strip < nstrips) {
+    int ws_ = (int)(strip % nstrip_w);
+    strip_px = min(DW_WS, a.Wo - ws_ * DW_WS);
+  }
+  s_cnt[ty] = (float)strip_px;
   __syncthreads();
   float cnt = 0.f;
   float mean[V];
@@ -174,6 +181,9 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   dim3 grid(cdiv(a.C / V, bx), (unsigned)((nstrips + by - 1) / by));
   dim3 block(bx, by);
   size_t shm = a.part ? (size_t)bx * by * V * sizeof(float) : 0;
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
+  ProfScope ps(PK_DW_FWD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
   if (dtype == DT_F32) {
     if (a.stride == 1) dw_fwd_kernel<float, 1><<<grid, block, shm, st>>>(a);
     else dw_fwd_kernel<float, 2><<<grid, block, shm, st>>>(a);
@@ -230,6 +240,9 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   int V = dtype == DT_F32 ? 4 : 8;
   long long total = (long long)a.N * a.H * a.W * (a.C / V);
   dim3 grid((unsigned)((total + 255) / 256));
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
+  ProfScope ps(PK_DW_DGRAD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
   if (dtype == DT_F32) {
     if (a.stride == 1) dw_dgrad_kernel<float, 1><<<grid, 256, 0, st>>>(a);
     else dw_dgrad_kernel<float, 2><<<grid, 256, 0, st>>>(a);
@@ -335,6 +348,9 @@ int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   dim3 grid(cdiv(a.C / V, bx), dw_wgrad_parts(a.N, a.Ho, a.Wo, a.C, dtype));
   dim3 block(bx, by);
   size_t shm = (size_t)bx * by * V * sizeof(float);
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
+  ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el), 18.0 * out_el);
   if (dtype == DT_F32) {
     if (a.stride == 1) dw_wgrad_kernel<float, 1><<<grid, block, shm, st>>>(a);
     else dw_wgrad_kernel<float, 2><<<grid, block, shm, st>>>(a);

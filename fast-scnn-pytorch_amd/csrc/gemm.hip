@@ -301,17 +301,19 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     set_error("gemm_nt: empty problem M=%d N=%d K=%d", a.M, a.N, a.K);
     return E_INVALID;
   }
-  if (a.lda % V || (uintptr_t)a.A % 16 || (uintptr_t)a.B % 16 || a.ldb % V ||
-      (a.b_trans && a.N % 1)) {
+  if (a.lda % V || (uintptr_t)a.A % 16 || (uintptr_t)a.B % 16 || a.ldb % V) {
     set_error("gemm_nt: operands must be 16-B aligned with ld multiple of %d (lda=%d ldb=%d)", V,
               a.lda, a.ldb);
     return E_INVALID;
   }
-  if (a.part && cdiv(a.N, 16 * pick_nt(a.N)) > 0 && a.R) {
+  if (a.part && a.R) {
     set_error("gemm_nt: statistics with residual not supported");
     return E_UNSUPPORTED;
   }
   int nt = pick_nt(a.N);
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  const double M = a.M, N = a.N, K = a.K;
+  ProfScope ps(PK_GEMM_NT, st, E * (M * K + M * N * (a.R ? 2 : 1) + N * K), 2.0 * M * N * K);
   if (dtype == DT_F32) {
     if (a.b_trans) launch_nt<float, true>(a, nt, st);
     else launch_nt<float, false>(a, nt, st);
@@ -334,8 +336,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int LDS_LD = TN_T + TN_PAD;
-  __shared__ T sD[TN_MC * LDS_LD];
-  __shared__ T sX[TN_MC * LDS_LD];
+  __shared__ __attribute__((aligned(16))) T sD[TN_MC * LDS_LD];
+  __shared__ __attribute__((aligned(16))) T sX[TN_MC * LDS_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int tiles_k = cdiv(a.K, TN_T);
@@ -453,6 +455,9 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
   }
   a.rows_per_split = cdiv(cdiv(a.M, splits), TN_MC) * TN_MC;
   dim3 grid(cdiv(a.N, TN_T) * cdiv(a.K, TN_T), splits);
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  const double M = a.M, N = a.N, K = a.K;
+  ProfScope ps(PK_GEMM_TN, st, E * (M * N + M * K) + 4.0 * N * K, 2.0 * M * N * K);
   if (dtype == DT_F32) gemm_tn_kernel<float><<<grid, 256, 0, st>>>(a);
   else gemm_tn_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("gemm_tn");

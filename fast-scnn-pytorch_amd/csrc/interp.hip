@@ -84,6 +84,10 @@ __global__ __launch_bounds__(256) void up_nchw_kernel(UpArgs a) {
 int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
   long long total = (long long)a.N * a.Ho * a.Wo;
   unsigned grid = (unsigned)((total + 255) / 256);
+  ProfScope ps(PK_UP, st,
+               (in_dtype == DT_F32 ? 4.0 : 2.0) * a.N * a.C * a.Hi * a.Wi +
+                   (out_dtype == DT_F32 ? 4.0 : 2.0) * (double)a.N * a.C * a.Ho * a.Wo,
+               7.0 * a.N * a.C * a.Ho * a.Wo);
   if (in_dtype == DT_F32 && out_dtype == DT_F32) up_nchw_kernel<float, float, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) up_nchw_kernel<bf16, bf16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_F32) up_nchw_kernel<bf16, float, 0><<<grid, 256, 0, st>>>(a);

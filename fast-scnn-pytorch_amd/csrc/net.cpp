@@ -235,6 +235,31 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   pl.drop = train ? A.get((size_t)M2 * 128 * E) : pl.c2pw.a;
   pl.logits = A.get((size_t)M2 * pl.Cp * E);
   pl.ws_bytes = A.top;
+  auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
+    pl.named.push_back({n, off, rows, cols, ld, bws});
+  };
+  auto nu = [&](const std::string& n, const Unit& u) {
+    pl.named.push_back({n + ".a", u.a, u.M, u.C, u.ld, 0});
+    pl.named.push_back({n + ".z", u.z, u.M, u.C, u.C, 0});
+    pl.named.push_back({n + ".scale", u.scale, 1, u.C, u.C, 0});
+    pl.named.push_back({n + ".shift", u.shift, 1, u.C, u.C, 0});
+    pl.named.push_back({n + ".mean", u.mean, 1, u.C, u.C, 0});
+    pl.named.push_back({n + ".invstd", u.invstd, 1, u.C, u.C, 0});
+  };
+  nu("c0", pl.c0); nu("l1dw", pl.l1dw); nu("l1pw", pl.l1pw); nu("l2dw", pl.l2dw); nu("l2pw", pl.l2pw);
+  for (int i = 0; i < 9; ++i) {
+    nu("lbe" + std::to_string(i), pl.lbe[i]);
+    nu("lbd" + std::to_string(i), pl.lbd[i]);
+    nu("lbp" + std::to_string(i), pl.lbp[i]);
+  }
+  for (int i = 0; i < 4; ++i) nu("ppk" + std::to_string(i), pl.ppk[i]);
+  nu("po", pl.po); nu("fdw", pl.fdw); nu("flow", pl.flow); nu("fhigh", pl.fhigh);
+  nu("c1dw", pl.c1dw); nu("c1pw", pl.c1pw); nu("c2dw", pl.c2dw); nu("c2pw", pl.c2pw);
+  nm("concat", pl.concat, M5, 256, 256, 0);
+  nm("up_low", pl.up_low, M2, 128, 128, 0);
+  nm("f", pl.f, M2, 128, 128, 0);
+  nm("drop", pl.drop, M2, 128, 128, 0);
+  nm("logits", pl.logits, M2, net.num_classes, pl.Cp, 0);
 
   if (train) {
     const int C = net.num_classes;
@@ -315,6 +340,22 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.coef = B.get(2 * 1024 * 4);
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
     pl.bws_bytes = B.top;
+    auto gu = [&](const std::string& n, const Unit& u) {
+      pl.named.push_back({n + ".ga", u.ga, u.M, u.C, u.ga_ld, 1});
+    };
+    gu("c0", pl.c0); gu("l1dw", pl.l1dw); gu("l1pw", pl.l1pw); gu("l2dw", pl.l2dw); gu("l2pw", pl.l2pw);
+    for (int i = 0; i < 9; ++i) {
+      gu("lbe" + std::to_string(i), pl.lbe[i]);
+      gu("lbd" + std::to_string(i), pl.lbd[i]);
+      gu("lbp" + std::to_string(i), pl.lbp[i]);
+    }
+    gu("po", pl.po); gu("fdw", pl.fdw); gu("c1dw", pl.c1dw); gu("c1pw", pl.c1pw);
+    gu("c2dw", pl.c2dw); gu("c2pw", pl.c2pw);
+    nm("g_logits", pl.g_logits, M2, C, pl.Cp, 1);
+    nm("g_f", pl.g_f, M2, 128, 128, 1);
+    nm("g_up", pl.g_up, M2, 128, 128, 1);
+    nm("g_concat", pl.g_concat, M5, 256, 256, 1);
+    nm("dz", pl.dz, M0, 32, 32, 1);
   }
   return OK;
 }

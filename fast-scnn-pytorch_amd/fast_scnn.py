@@ -355,7 +355,27 @@ class FastSCNN(nn.Module):
                   _lib.dtype_code(dt), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]),
                   _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p), _lib.c_float(self._momentum()),
                   _lib.stream_ptr(x.device))
+        if getattr(self, "_keep_ws", False):
+            self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return out, ws, seed, dt
+
+    def debug_buffer(self, name):
+        """Tensor view of a named plan buffer of the last forward/backward (set ``_keep_ws``).
+
+        Debug / stage-level parity helper: returns [rows, cols] in the compute dtype."""
+        d = self._debug
+        off, rows, cols, ld, inb = (_lib.c_ll(), _lib.c_ll(), _lib.c_int(), _lib.c_int(),
+                                    _lib.c_int())
+        _lib.check(_lib.load().fscnn_plan_buffer(d["plan"], name.encode(), _lib.ctypes.byref(off),
+                                                 _lib.ctypes.byref(rows), _lib.ctypes.byref(cols),
+                                                 _lib.ctypes.byref(ld), _lib.ctypes.byref(inb)),
+                   "fscnn_plan_buffer")
+        base = d["bws"] if inb.value else d["ws"]
+        dt = d["dt"] if not name.endswith((".scale", ".shift", ".mean", ".invstd")) else torch.float32
+        esz = torch.tensor([], dtype=dt).element_size()
+        n = (rows.value - 1) * ld.value + cols.value
+        flat = base[off.value:off.value + n * esz].view(dt)
+        return flat.as_strided((rows.value, cols.value), (ld.value, 1))
 
     def _run_backward(self, gout, x, ws, seed, dt):
         nat = self.native()
@@ -366,6 +386,8 @@ class FastSCNN(nn.Module):
         G = torch.zeros(nat.p_total, dtype=torch.float32, device=x.device)
         bws = torch.empty(max(bw, 1), dtype=torch.uint8, device=x.device)
         p = self._dropout_p()
+        if getattr(self, "_keep_ws", False):
+            self._debug["bws"] = bws
         hook = self.grad_stage_hook
         for s in range(4):
             _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x), _lib.dtype_code(x.dtype),

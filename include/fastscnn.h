@@ -59,6 +59,10 @@ int fscnn_plan_create(const fscnn_net* net, int N, int H, int W, int dtype, int 
 void fscnn_plan_destroy(fscnn_plan* plan);
 int fscnn_plan_workspace(const fscnn_plan* plan, long long* fwd_bytes, long long* bwd_bytes);
 int fscnn_plan_shapes(const fscnn_plan* plan, int* dims /* 10: H1 W1 H2 W2 H3 W3 H4 W4 H5 W5 */);
+/* debug / stage-level parity: location of a named activation (e.g. "c2pw.a", "g_logits") in
+ * the forward (in_bws = 0) or backward (in_bws = 1) workspace; rows x cols with row stride ld */
+int fscnn_plan_buffer(const fscnn_plan* plan, const char* name, long long* offset, long long* rows,
+                      int* cols, int* ld, int* in_bws);
 
 /* ---- whole-network forward / backward ----------------------------------------------------- */
 int fscnn_forward(const fscnn_plan* plan, const void* x, int x_dtype, void* out, int out_dtype,
@@ -69,6 +73,15 @@ int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int 
                    const float* params, float* grads, void* ws, void* bws,
                    unsigned long long dropout_seed, float dropout_p, int stage_from,
                    int stage_to, void* stream);
+
+/* ---- launch profiler (bench.py roofline) --------------------------------------------------
+ * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 9 upsample.
+ * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
+ * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes
+ * and flops of those launches (SURVEY.md §8(d) formulas). */
+int fscnn_prof_begin(int kind, int max_launches);
+int fscnn_prof_end(double* total_ms, long long* launches, double* bytes, double* flops);
+const char* fscnn_prof_kind_name(int kind);
 
 /* ---- loss / optimizer ------------------------------------------------------------------- */
 /* out2[0] = mean loss over valid pixels, out2[1] = valid count; part: ce_parts*2 floats */

@@ -56,8 +56,9 @@ def test_conv0_fwd(dt, shape):
     Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
     y = torch.empty(N, Ho, Wo, 32, dtype=dt, device=DEV)
     xd = x.to(dt).to(DEV)
-    _lib.call("fscnn_conv0_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, _lib.ptr(w.to(DEV)),
-              _lib.ptr(sc.to(DEV)), _lib.ptr(sh.to(DEV)), 1, _lib.ptr(y), _lib.dtype_code(dt), S())
+    wd, scd, shd = w.to(DEV), sc.to(DEV), sh.to(DEV)
+    _lib.call("fscnn_conv0_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, _lib.ptr(wd),
+              _lib.ptr(scd), _lib.ptr(shd), 1, _lib.ptr(y), _lib.dtype_code(dt), S())
     sync()
     close(nchw(y), ref, TOL[dt])
 
@@ -69,7 +70,7 @@ def test_dw3x3_fwd_bwd(dt, N, H, W, C, s):
     x = rnd(N, C, H, W, seed=5)
     w = rnd(C, 1, 3, 3, seed=6, scale=0.5)
     sc, sh = rnd(C, seed=7).abs() + 0.5, rnd(C, seed=8)
-    xq = x.to(dt).float().requires_grad_(True)
+    xq = x.to(dt).float().clone().requires_grad_(True)
     wq = w.clone().requires_grad_(True)
     z = F.conv2d(xq, wq, stride=s, padding=1, groups=C)
     ref = F.relu(z * sc[None, :, None, None] + sh[None, :, None, None])
@@ -77,8 +78,9 @@ def test_dw3x3_fwd_bwd(dt, N, H, W, C, s):
     xd = nhwc(x.to(dt)).to(DEV)
     y = torch.empty(N, Ho, Wo, C, dtype=dt, device=DEV)
     wd = w.to(DEV).contiguous()
+    scd, shd = sc.to(DEV), sh.to(DEV)
     _lib.call("fscnn_dw3x3_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, C, s, _lib.ptr(wd),
-              _lib.ptr(sc.to(DEV)), _lib.ptr(sh.to(DEV)), 1, _lib.ptr(y), S())
+              _lib.ptr(scd), _lib.ptr(shd), 1, _lib.ptr(y), S())
     sync()
     close(nchw(y), ref.detach(), TOL[dt])
     # backward of the raw conv
@@ -114,8 +116,9 @@ def test_pw_gemm(dt, M, N, K):
     Rd = torch.zeros(M, ldc, dtype=dt, device=DEV)
     Rd[:, :N] = R.to(dt).to(DEV)
     Ad, Bd = A.to(dt).to(DEV), B.to(dt).to(DEV)
-    _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(Ad), K, _lib.ptr(Bd), K, 0, _lib.ptr(sc.to(DEV)),
-              _lib.ptr(sh.to(DEV)), _lib.ptr(Rd), ldc, 1, _lib.ptr(C), ldc, None,
+    scd, shd = sc.to(DEV), sh.to(DEV)
+    _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(Ad), K, _lib.ptr(Bd), K, 0, _lib.ptr(scd),
+              _lib.ptr(shd), _lib.ptr(Rd), ldc, 1, _lib.ptr(C), ldc, None,
               _lib.dtype_code(dt), S())
     sync()
     close(C[:, :N], ref, TOL[dt] * (10 if dt == torch.float32 else 1))
@@ -151,14 +154,15 @@ def test_gemm_bn_statistics(dt):
     parts = (M + 127) // 128
     part = torch.empty(parts * 3 * N, dtype=torch.float32, device=DEV)
     C = torch.empty(M, N, dtype=dt, device=DEV)
-    _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(A.to(dt).to(DEV)), K, _lib.ptr(B.to(dt).to(DEV)),
+    Ad, Bd = A.to(dt).to(DEV), B.to(dt).to(DEV)
+    _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(Ad), K, _lib.ptr(Bd),
               K, 0, None, None, None, 0, 0, _lib.ptr(C), N, _lib.ptr(part), _lib.dtype_code(dt), S())
-    gamma, beta = rnd(N, seed=22).abs() + 0.5, rnd(N, seed=23)
+    gamma, beta = (rnd(N, seed=22).abs() + 0.5).to(DEV), rnd(N, seed=23).to(DEV)
     rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
     nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
     mean, invstd, scale, shift = (torch.empty(N, device=DEV) for _ in range(4))
-    _lib.call("fscnn_bn_finalize", _lib.ptr(part), parts, N, _lib.ptr(gamma.to(DEV)),
-              _lib.ptr(beta.to(DEV)), _lib.ptr(rm), _lib.ptr(rv), _lib.ptr(nbt), _lib.c_float(0.1),
+    _lib.call("fscnn_bn_finalize", _lib.ptr(part), parts, N, _lib.ptr(gamma),
+              _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), _lib.ptr(nbt), _lib.c_float(0.1),
               _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(scale), _lib.ptr(shift), S())
     sync()
     tol = 1e-5 if dt == torch.float32 else 2e-3
@@ -176,7 +180,7 @@ def test_gemm_bn_statistics(dt):
 def test_bilinear_ac(dt, Hi, Wi, Ho, Wo, C):
     N = 2
     x = rnd(N, C, Hi, Wi, seed=30)
-    xq = x.to(dt).float().requires_grad_(True)
+    xq = x.to(dt).float().clone().requires_grad_(True)
     ref = F.interpolate(xq, (Ho, Wo), mode="bilinear", align_corners=True)
     xd = nhwc(x.to(dt)).to(DEV)
     y = torch.empty(N, Ho, Wo, C, dtype=dt, device=DEV)
@@ -187,12 +191,13 @@ def test_bilinear_ac(dt, Hi, Wi, Ho, Wo, C):
               _lib.ptr(y2), 1, _lib.DT_F32, S())
     sync()
     close(nchw(y), ref.detach(), TOL[dt])
-    close(y2, ref.detach(), 2e-6 if dt == torch.float32 else 1e-6)
+    close(y2, ref.detach(), 1e-5)  # fp32 out: only FMA-contraction / order differences
     g = rnd(N, C, Ho, Wo, seed=31).to(dt)
     ref.backward(g.float())
     tmp = torch.empty(N * Ho * Wi * C, dtype=torch.float32, device=DEV)
     dx = torch.empty(N, Hi, Wi, C, dtype=dt, device=DEV)
-    _lib.call("fscnn_bilinear_ac_bwd", _lib.ptr(nhwc(g).to(DEV)), _lib.dtype_code(dt), N, Hi, Wi, C,
+    gd = nhwc(g).to(DEV)
+    _lib.call("fscnn_bilinear_ac_bwd", _lib.ptr(gd), _lib.dtype_code(dt), N, Hi, Wi, C,
               Ho, Wo, _lib.ptr(tmp), _lib.ptr(dx), S())
     sync()
     close(nchw(dx), xq.grad, TOL[dt] * 5)
@@ -203,10 +208,11 @@ def test_bilinear_ac(dt, Hi, Wi, Ho, Wo, C):
 def test_pyramid_pool(dt, H, W):
     N, C = 2, 128
     x = rnd(N, C, H, W, seed=40)
-    xq = x.to(dt).float().requires_grad_(True)
+    xq = x.to(dt).float().clone().requires_grad_(True)
     refs = [F.adaptive_avg_pool2d(xq, k) for k in (1, 2, 3, 6)]
     pooled = torch.empty(50, N, C, dtype=dt, device=DEV)
-    _lib.call("fscnn_pyramid_pool_fwd", _lib.ptr(nhwc(x.to(dt)).to(DEV)), _lib.dtype_code(dt), N, H,
+    xd = nhwc(x.to(dt)).to(DEV)
+    _lib.call("fscnn_pyramid_pool_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H,
               W, C, C, _lib.ptr(pooled), S())
     sync()
     base = 0
@@ -233,10 +239,10 @@ def test_cross_entropy(dt):
     x = rnd(N, C, H, W, seed=50, scale=4)
     t = torch.randint(0, C, (N, H, W), generator=torch.Generator().manual_seed(51))
     t[:, ::7, ::5] = -1
-    xq = x.to(dt).float().requires_grad_(True)
+    xq = x.to(dt).float().clone().requires_grad_(True)
     ref = F.cross_entropy(xq, t, ignore_index=-1)
     ref.backward()
-    xd = x.to(dt).to(DEV).requires_grad_(True)
+    xd = x.detach().to(dt).to(DEV).requires_grad_(True)
     loss = cross_entropy(xd, t.to(DEV), -1)
     loss.backward()
     sync()
