@@ -92,10 +92,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(BnApplyArgs a) {
   constexpr int V = VecW<T>::V;
   const int CV = a.C / V;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.M * CV) return;
-  long long m = i / CV;
-  int c = (int)(i - m * CV) * V;
+  // 32-bit index math (M*C/V < 2^31 is enforced by the planner)
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (unsigned)a.M * (unsigned)CV) return;
+  const unsigned mu = i / (unsigned)CV;
+  const int c = (int)(i - mu * (unsigned)CV) * V;
+  const long long m = mu;
   float z[V], o[V];
   ldv((const T*)a.z + m * a.ldz + c, z);
 #pragma unroll
@@ -260,10 +262,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int CV = a.C / V;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.M * CV) return;
-  long long m = i / CV;
-  int c = (int)(i - m * CV) * V;
+  // 32-bit index math (M*C/V < 2^31 is enforced by the planner)
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (unsigned)a.M * (unsigned)CV) return;
+  const unsigned mu = i / (unsigned)CV;
+  const int c = (int)(i - mu * (unsigned)CV) * V;
+  const long long m = mu;
   float g[V], z[V], o[V];
   ldv((const T*)a.dy + m * a.lddy + c, g);
   if (a.mask) {

@@ -1,13 +1,17 @@
 // Depthwise 3x3 convolution, pad 1, stride 1 or 2, NHWC (models/fast_scnn.py:70 _DSConv,
-// :86 _DWConv; used by LTD.dsconv1/2, the 9 bottleneck expansions, FFM.dwconv and the
-// classifier dsconvs — 14 layers).
+// :86 _DWConv; LTD.dsconv1/2, the 9 bottleneck expansions, FFM.dwconv, classifier dsconvs —
+// 14 layers).
 //
-// Workgroup = blockDim.x channel vectors (16 B each: 4 fp32 / 8 bf16 channels) x blockDim.y
-// output strips; a strip is WS consecutive output pixels of one row.  Lanes run along the
-// channel vectors, so every load/store of a wave is a run of contiguous 16 B vectors.  The
-// WS-wide strip reuses each loaded input column for up to 3 (s=1) taps in registers; the 3x
-// vertical reuse is served by L1/L2 since neighbouring rows are processed by neighbouring
-// workgroups at the same time.
+// Workgroup = blockDim.x channel vectors (16 B: 4 fp32 / 8 bf16 channels) x blockDim.y column
+// tiles.  Each thread owns a register tile of HS=2 output rows x WS=4 output columns of its
+// channel vector: it streams the (HS-1)*s+3 input rows once, and every 16-B input vector it loads
+// feeds all the taps of the tile that read it (stride 1: 24 loads for 8 outputs instead of 72).
+// Lanes run along channels, so each wave-wide load is a run of contiguous 16-B vectors.
+// Grids are 3-D (channel chunk, column tile, row band) — no 64-bit index division.
+//
+// dgrad, stride 1 = the same kernel with the 3x3 taps flipped (correlation of dy);
+// dgrad, stride 2 = parity-aware gather (a 2x4 dx tile reads 2 dy rows x 3 dy columns).
+// wgrad = per-block partial [part][9][C] sums, reduced by the deterministic two-pass reducer.
 //
 // Roofline: HBM-bound.  Algorithmic bytes per layer = e*(N*C*Hi*Wi + N*C*Ho*Wo) + 9*C*4,
 // flops = 18*N*C*Ho*Wo.
@@ -15,8 +19,8 @@
 
 namespace fscnn {
 
-
-constexpr int DW_WS = 4;
+constexpr int DW_WS = 4;  // output columns per thread
+constexpr int DW_HS = 2;  // output rows per thread
 
 __host__ __device__ inline void dw_block_shape(int C, int V, int& bx, int& by) {
   int cv = C / V;
@@ -25,108 +29,118 @@ __host__ __device__ inline void dw_block_shape(int C, int V, int& bx, int& by) {
   if (by < 1) by = 1;
 }
 
-template <typename T, int S>
+struct DwGeom {
+  int gx, gy, gz;  // channel chunks, column tiles, row bands
+};
+static DwGeom dw_geom(int N, int Ho, int Wo, int C, int V) {
+  int bx, by;
+  dw_block_shape(C, V, bx, by);
+  DwGeom g;
+  g.gx = cdiv(C / V, bx);
+  g.gy = cdiv(Wo, by * DW_WS);
+  g.gz = N * cdiv(Ho, DW_HS);
+  return g;
+}
+
+// ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
+template <typename T, int S, bool FLIP>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   constexpr int V = VecW<T>::V;
-  constexpr int NIN = (DW_WS - 1) * S + 3;  // input columns touched by a strip
-  extern __shared__ float s_red[];          // [blockDim.y][blockDim.x*V]
-  const int cv = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int NR = (DW_HS - 1) * S + 3;  // input rows touched
+  constexpr int NC = (DW_WS - 1) * S + 3;  // input cols touched
+  extern __shared__ float s_red[];         // [by][bx*V] (train statistics)
+  __shared__ float s_cnt[256];
+  const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
+  const int cv = blockIdx.x * BX + tx;
   const int CV = a.C / V;
-  const int nstrip_w = (a.Wo + DW_WS - 1) / DW_WS;
-  const long long strip = (long long)blockIdx.y * blockDim.y + threadIdx.y;
-  const long long nstrips = (long long)a.N * a.Ho * nstrip_w;
-  const bool active = (cv < CV) && (strip < nstrips);
+  const int nb = (a.Ho + DW_HS - 1) / DW_HS;
+  const int n = blockIdx.z / nb;
+  const int ho0 = (blockIdx.z - n * nb) * DW_HS;
+  const int wo0 = (blockIdx.y * BY + ty) * DW_WS;
+  const int nrow = min(DW_HS, a.Ho - ho0);
+  const int ncol = wo0 < a.Wo ? min(DW_WS, a.Wo - wo0) : 0;
+  const bool active = cv < CV && ncol > 0;
 
-  float acc[DW_WS][V];
+  float acc[DW_HS][DW_WS][V];
 #pragma unroll
-  for (int p = 0; p < DW_WS; ++p)
+  for (int r = 0; r < DW_HS; ++r)
 #pragma unroll
-    for (int j = 0; j < V; ++j) acc[p][j] = 0.f;
-  int n = 0, ho = 0, wo0 = 0;
+    for (int p = 0; p < DW_WS; ++p)
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[r][p][j] = 0.f;
   if (active) {
-    int ws = (int)(strip % nstrip_w);
-    long long r = strip / nstrip_w;
-    ho = (int)(r % a.Ho);
-    n = (int)(r / a.Ho);
-    wo0 = ws * DW_WS;
-    // taps: w[c][kh][kw] for this thread's V channels (9*V contiguous floats)
     float wt[9][V];
     const float* wp = a.w + (size_t)cv * V * 9;
 #pragma unroll
     for (int j = 0; j < V; ++j)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wt[t][j] = wp[j * 9 + t];
+      for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = wp[j * 9 + t];
     const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.C + (size_t)cv * V;
-    const int wi0 = wo0 * S - 1;
+    const int hi0 = ho0 * S - 1, wi0 = wo0 * S - 1;
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      int hi = ho * S - 1 + kh;
+    for (int rr = 0; rr < NR; ++rr) {
+      const int hi = hi0 + rr;
       if (hi < 0 || hi >= a.H) continue;
       const T* xr = xb + (size_t)hi * a.W * a.C;
 #pragma unroll
-      for (int ci = 0; ci < NIN; ++ci) {
-        int wi = wi0 + ci;
+      for (int ci = 0; ci < NC; ++ci) {
+        const int wi = wi0 + ci;
         if (wi < 0 || wi >= a.W) continue;
         float v[V];
         ldv(xr + (size_t)wi * a.C, v);
 #pragma unroll
-        for (int p = 0; p < DW_WS; ++p) {
-          int kw = ci - p * S;
-          if (kw >= 0 && kw < 3) {
+        for (int r = 0; r < DW_HS; ++r) {
+          const int kh = rr - r * S;
+          if (kh < 0 || kh > 2) continue;
 #pragma unroll
-            for (int j = 0; j < V; ++j) acc[p][j] = fmaf(v[j], wt[kh * 3 + kw][j], acc[p][j]);
+          for (int p = 0; p < DW_WS; ++p) {
+            const int kw = ci - p * S;
+            if (kw < 0 || kw > 2) continue;
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[r][p][j] = fmaf(v[j], wt[kh * 3 + kw][j], acc[r][p][j]);
           }
         }
       }
     }
-  }
-  const int npx_strip = active ? min(DW_WS, a.Wo - wo0) : 0;
-  if (active) {
     float sc[V], sh[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       sc[j] = a.scale ? a.scale[cv * V + j] : 1.f;
       sh[j] = a.scale ? a.shift[cv * V + j] : 0.f;
     }
-    T* yb = (T*)a.y + (((size_t)n * a.Ho + ho) * a.Wo + wo0) * a.C + (size_t)cv * V;
 #pragma unroll
-    for (int p = 0; p < DW_WS; ++p) {
-      if (p < npx_strip) {
+    for (int r = 0; r < DW_HS; ++r) {
+      if (r >= nrow) continue;
+      T* yb = (T*)a.y + (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0) * a.C + (size_t)cv * V;
+#pragma unroll
+      for (int p = 0; p < DW_WS; ++p) {
+        if (p >= ncol) continue;
         float o[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) {
-          float t = acc[p][j] * sc[j] + sh[j];
+          float t = acc[r][p][j] * sc[j] + sh[j];
           o[j] = a.relu ? fmaxf(t, 0.f) : t;
-          acc[p][j] = o[j];
+          acc[r][p][j] = o[j];
         }
         stv(yb + (size_t)p * a.C, o);
       }
     }
   }
   if (a.part == nullptr) return;
-  // ---- per-channel (mean, M2, count) over the block's pixels (train-mode BN statistics) ----
-  const int BX = blockDim.x, BY = blockDim.y;
-  const int tx = threadIdx.x, ty = threadIdx.y;
-  float s[V];
+  // ---- per-channel (mean, M2, count) over the block's outputs (train-mode BN statistics) -----
+  const int npx = nrow * ncol;  // identical for every tx of this ty
 #pragma unroll
   for (int j = 0; j < V; ++j) {
-    s[j] = 0.f;
+    float s = 0.f;
 #pragma unroll
-    for (int p = 0; p < DW_WS; ++p) s[j] += (p < npx_strip) ? acc[p][j] : 0.f;
-    s_red[ty * BX * V + tx * V + j] = s[j];
+    for (int r = 0; r < DW_HS; ++r)
+#pragma unroll
+      for (int p = 0; p < DW_WS; ++p) s += (r < nrow && p < ncol) ? acc[r][p][j] : 0.f;
+    s_red[ty * BX * V + tx * V + j] = s;
   }
-  __shared__ float s_cnt[256];
-  // pixels of this strip, independent of whether this thread's channel vector exists (all tx of a
-  // row write the same value — no race between active and padding threads)
-  int strip_px = 0;
-  if (strip < nstrips) {
-    int ws_ = (int)(strip % nstrip_w);
-    strip_px = min(DW_WS, a.Wo - ws_ * DW_WS);
-  }
-  s_cnt[ty] = (float)strip_px;
+  s_cnt[ty] = (float)npx;
   __syncthreads();
-  float cnt = 0.f;
-  float mean[V];
+  float cnt = 0.f, mean[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) mean[j] = 0.f;
   for (int k = 0; k < BY; ++k) {
@@ -141,15 +155,17 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   for (int j = 0; j < V; ++j) {
     float m2 = 0.f;
 #pragma unroll
-    for (int p = 0; p < DW_WS; ++p) {
-      float d = acc[p][j] - mean[j];
-      m2 += (p < npx_strip) ? d * d : 0.f;
-    }
+    for (int r = 0; r < DW_HS; ++r)
+#pragma unroll
+      for (int p = 0; p < DW_WS; ++p) {
+        float d = acc[r][p][j] - mean[j];
+        m2 += (r < nrow && p < ncol) ? d * d : 0.f;
+      }
     s_red[ty * BX * V + tx * V + j] = m2;
   }
   __syncthreads();
   if (ty == 0 && cv < CV) {
-    float* rec = a.part + (size_t)blockIdx.y * 3 * a.C;
+    float* rec = a.part + ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * 3 * a.C;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       float m2 = 0.f;
@@ -162,10 +178,30 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 }
 
 int dw_parts(int N, int Ho, int Wo, int C, int dtype) {
-  int V = dtype == DT_F32 ? 4 : 8, bx, by;
-  dw_block_shape(C, V, bx, by);
-  long long nstrips = (long long)N * Ho * cdiv(Wo, DW_WS);
-  return (int)((nstrips + by - 1) / by);
+  DwGeom g = dw_geom(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8);
+  return g.gy * g.gz;
+}
+
+template <bool FLIP>
+static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
+  const int V = dtype == DT_F32 ? 4 : 8;
+  int bx, by;
+  dw_block_shape(a.C, V, bx, by);
+  DwGeom g = dw_geom(a.N, a.Ho, a.Wo, a.C, V);
+  if (g.gz > 65535 || g.gy > 65535) {
+    set_error("dw: grid too large (N*Ho/2=%d)", g.gz);
+    return E_UNSUPPORTED;
+  }
+  dim3 grid(g.gx, g.gy, g.gz), block(bx, by);
+  size_t shm = a.part ? (size_t)bx * by * V * sizeof(float) : 0;
+  if (dtype == DT_F32) {
+    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP><<<grid, block, shm, st>>>(a);
+    else dw_fwd_kernel<float, 2, FLIP><<<grid, block, shm, st>>>(a);
+  } else {
+    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP><<<grid, block, shm, st>>>(a);
+    else dw_fwd_kernel<bf16, 2, FLIP><<<grid, block, shm, st>>>(a);
+  }
+  return check_launch("dw_fwd");
 }
 
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
@@ -175,144 +211,164 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     set_error("dw_fwd: bad args C=%d stride=%d H=%d Ho=%d", a.C, a.stride, a.H, a.Ho);
     return E_INVALID;
   }
-  int bx, by;
-  dw_block_shape(a.C, V, bx, by);
-  long long nstrips = (long long)a.N * a.Ho * cdiv(a.Wo, DW_WS);
-  dim3 grid(cdiv(a.C / V, bx), (unsigned)((nstrips + by - 1) / by));
-  dim3 block(bx, by);
-  size_t shm = a.part ? (size_t)bx * by * V * sizeof(float) : 0;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_FWD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
-  if (dtype == DT_F32) {
-    if (a.stride == 1) dw_fwd_kernel<float, 1><<<grid, block, shm, st>>>(a);
-    else dw_fwd_kernel<float, 2><<<grid, block, shm, st>>>(a);
-  } else {
-    if (a.stride == 1) dw_fwd_kernel<bf16, 1><<<grid, block, shm, st>>>(a);
-    else dw_fwd_kernel<bf16, 2><<<grid, block, shm, st>>>(a);
-  }
-  return check_launch("dw_fwd");
+  return dw_launch_fwd<false>(a, dtype, st);
 }
 
-// ---- input gradient (gather form, no atomics) ----------------------------------------------
+// ---- input gradient ---------------------------------------------------------------------------
 // dX[n,h,w,c] = sum_{kh,kw} dY[n,ho,wo,c] * w[c,kh,kw] with h = ho*s-1+kh, w = wo*s-1+kw.
-
-template <typename T, int S>
-__global__ __launch_bounds__(256) void dw_dgrad_kernel(DwBwdArgs a) {
+// stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even):
+//   row h0   <- dy row h0/2 (kh=1);  row h0+1 <- dy rows h0/2+1 (kh=0) and h0/2 (kh=2)
+//   col w0+q <- dy cols w0/2 + (q+1-kw)/2 for the kw of matching parity
+template <typename T>
+__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   constexpr int V = VecW<T>::V;
+  const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
+  const int cv = blockIdx.x * BX + tx;
   const int CV = a.C / V;
-  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = (long long)a.N * a.H * a.W * CV;
-  if (idx >= total) return;
-  int cv = (int)(idx % CV);
-  long long pix = idx / CV;
-  int wi = (int)(pix % a.W);
-  long long r = pix / a.W;
-  int hi = (int)(r % a.H);
-  int n = (int)(r / a.H);
-  float acc[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  const int nb = (a.H + 1) / 2;
+  const int n = blockIdx.z / nb;
+  const int h0 = (blockIdx.z - n * nb) * 2;
+  const int w0 = (blockIdx.y * BY + ty) * 4;
+  if (cv >= CV || w0 >= a.W) return;
+  float wt[9][V];
   const float* wp = a.w + (size_t)cv * V * 9;
-  const T* dyb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cv * V;
 #pragma unroll
-  for (int kh = 0; kh < 3; ++kh) {
-    int hn = hi + 1 - kh;
-    if (hn < 0 || (S == 2 && (hn & 1))) continue;
-    int ho = hn / S;
+  for (int j = 0; j < V; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t][j] = wp[j * 9 + t];
+  float acc[2][4][V];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[r][q][j] = 0.f;
+  const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cv * V;
+  const int hb = h0 / 2, wb = w0 / 2;
+#pragma unroll
+  for (int dr = 0; dr < 2; ++dr) {       // dy rows hb, hb+1
+    const int ho = hb + dr;
     if (ho >= a.Ho) continue;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      int wn = wi + 1 - kw;
-      if (wn < 0 || (S == 2 && (wn & 1))) continue;
-      int wo = wn / S;
+    for (int dc = 0; dc < 3; ++dc) {     // dy cols wb, wb+1, wb+2
+      const int wo = wb + dc;
       if (wo >= a.Wo) continue;
-      float v[V];
-      ldv(dyb + ((size_t)ho * a.Wo + wo) * a.C, v);
+      float g[V];
+      ldv(gb + ((size_t)ho * a.Wo + wo) * a.C, g);
 #pragma unroll
-      for (int j = 0; j < V; ++j) acc[j] = fmaf(v[j], wp[j * 9 + kh * 3 + kw], acc[j]);
+      for (int r = 0; r < 2; ++r) {
+        // dx row h0+r reads dy row ho with kh = (h0 + r) + 1 - 2*ho
+        const int kh = r + 1 - 2 * dr;
+        if (kh < 0 || kh > 2) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kw = q + 1 - 2 * dc;
+          if (kw < 0 || kw > 2) continue;
+#pragma unroll
+          for (int j = 0; j < V; ++j) acc[r][q][j] = fmaf(g[j], wt[kh * 3 + kw][j], acc[r][q][j]);
+        }
+      }
     }
   }
-  stv((T*)a.dx + (size_t)pix * a.C + (size_t)cv * V, acc);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (h0 + r >= a.H) continue;
+    T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + (size_t)cv * V;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (w0 + q < a.W) stv(db + (size_t)q * a.C, acc[r][q]);
+  }
 }
 
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
-  int V = dtype == DT_F32 ? 4 : 8;
-  long long total = (long long)a.N * a.H * a.W * (a.C / V);
-  dim3 grid((unsigned)((total + 255) / 256));
+  const int V = dtype == DT_F32 ? 4 : 8;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_DGRAD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
-  if (dtype == DT_F32) {
-    if (a.stride == 1) dw_dgrad_kernel<float, 1><<<grid, 256, 0, st>>>(a);
-    else dw_dgrad_kernel<float, 2><<<grid, 256, 0, st>>>(a);
-  } else {
-    if (a.stride == 1) dw_dgrad_kernel<bf16, 1><<<grid, 256, 0, st>>>(a);
-    else dw_dgrad_kernel<bf16, 2><<<grid, 256, 0, st>>>(a);
+  if (a.stride == 1) {
+    // correlation of dy with the flipped taps, same geometry as the forward
+    DwArgs f{};
+    f.N = a.N; f.H = a.Ho; f.W = a.Wo; f.C = a.C; f.Ho = a.H; f.Wo = a.W; f.stride = 1;
+    f.x = a.dy; f.w = a.w; f.y = a.dx;
+    return dw_launch_fwd<true>(f, dtype, st);
   }
+  int bx, by;
+  dw_block_shape(a.C, V, bx, by);
+  dim3 grid(cdiv(a.C / V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
+  if (dtype == DT_F32) dw_dgrad_s2_kernel<float><<<grid, block, 0, st>>>(a);
+  else dw_dgrad_s2_kernel<bf16><<<grid, block, 0, st>>>(a);
   return check_launch("dw_dgrad");
 }
 
-// ---- weight gradient: per-block partial [part][9][C], reduced deterministically later --------
+// ---- weight gradient: per-block partial [part][9][C] -----------------------------------------
+// Blocks walk (row band, column tile) pairs grid-stride so the partial count stays bounded.
 template <typename T, int S>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(DwBwdArgs a) {
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(DwBwdArgs a, int gy, int gz) {
   constexpr int V = VecW<T>::V;
+  constexpr int NR = (DW_HS - 1) * S + 3;
+  constexpr int NC = (DW_WS - 1) * S + 3;
   extern __shared__ float s_red[];  // [BY][BX*V]
-  const int cv = blockIdx.x * blockDim.x + threadIdx.x;
+  const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
+  const int cv = blockIdx.x * BX + tx;
   const int CV = a.C / V;
-  const int nstrip_w = (a.Wo + DW_WS - 1) / DW_WS;
-  const long long nstrips = (long long)a.N * a.Ho * nstrip_w;
+  const int nb = (a.Ho + DW_HS - 1) / DW_HS;
   float acc[9][V];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[t][j] = 0.f;
-  // grid-stride over strips: the number of partial records is gridDim.y (bounded), not the
-  // number of strips, so the final fixed-order reduction stays short.
-  for (long long strip = (long long)blockIdx.y * blockDim.y + threadIdx.y;
-       cv < CV && strip < nstrips; strip += (long long)gridDim.y * blockDim.y) {
-    int ws = (int)(strip % nstrip_w);
-    long long r = strip / nstrip_w;
-    int ho = (int)(r % a.Ho);
-    int n = (int)(r / a.Ho);
-    int wo0 = ws * DW_WS;
-    int npx = min(DW_WS, a.Wo - wo0);
-    float g[DW_WS][V];
-    const T* dyb = (const T*)a.dy + (((size_t)n * a.Ho + ho) * a.Wo + wo0) * a.C + (size_t)cv * V;
+  const int ntiles = gy * gz;
+  for (int tile = blockIdx.y; cv < CV && tile < ntiles; tile += gridDim.y) {
+    const int tz = tile / gy, tyy = tile - tz * gy;
+    const int n = tz / nb;
+    const int ho0 = (tz - n * nb) * DW_HS;
+    const int wo0 = (tyy * BY + ty) * DW_WS;
+    if (wo0 >= a.Wo) continue;
+    const int nrow = min(DW_HS, a.Ho - ho0), ncol = min(DW_WS, a.Wo - wo0);
+    float g[DW_HS][DW_WS][V];
+    const T* gb = (const T*)a.dy + (((size_t)n * a.Ho + ho0) * a.Wo + wo0) * a.C + (size_t)cv * V;
 #pragma unroll
-    for (int p = 0; p < DW_WS; ++p) {
-      if (p < npx) ldv(dyb + (size_t)p * a.C, g[p]);
-      else {
+    for (int r = 0; r < DW_HS; ++r)
 #pragma unroll
-        for (int j = 0; j < V; ++j) g[p][j] = 0.f;
+      for (int p = 0; p < DW_WS; ++p) {
+        if (r < nrow && p < ncol) ldv(gb + ((size_t)r * a.Wo + p) * a.C, g[r][p]);
+        else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) g[r][p][j] = 0.f;
+        }
       }
-    }
-    constexpr int NIN = (DW_WS - 1) * S + 3;
     const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.C + (size_t)cv * V;
-    const int wi0 = wo0 * S - 1;
+    const int hi0 = ho0 * S - 1, wi0 = wo0 * S - 1;
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      int hi = ho * S - 1 + kh;
+    for (int rr = 0; rr < NR; ++rr) {
+      const int hi = hi0 + rr;
       if (hi < 0 || hi >= a.H) continue;
       const T* xr = xb + (size_t)hi * a.W * a.C;
 #pragma unroll
-      for (int ci = 0; ci < NIN; ++ci) {
-        int wi = wi0 + ci;
+      for (int ci = 0; ci < NC; ++ci) {
+        const int wi = wi0 + ci;
         if (wi < 0 || wi >= a.W) continue;
         float v[V];
         ldv(xr + (size_t)wi * a.C, v);
 #pragma unroll
-        for (int p = 0; p < DW_WS; ++p) {
-          int kw = ci - p * S;
-          if (kw >= 0 && kw < 3) {
+        for (int r = 0; r < DW_HS; ++r) {
+          const int kh = rr - r * S;
+          if (kh < 0 || kh > 2) continue;
 #pragma unroll
-            for (int j = 0; j < V; ++j) acc[kh * 3 + kw][j] = fmaf(v[j], g[p][j], acc[kh * 3 + kw][j]);
+          for (int p = 0; p < DW_WS; ++p) {
+            const int kw = ci - p * S;
+            if (kw < 0 || kw > 2) continue;
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+              acc[kh * 3 + kw][j] = fmaf(v[j], g[r][p][j], acc[kh * 3 + kw][j]);
           }
         }
       }
     }
   }
-  const int BX = blockDim.x, BY = blockDim.y, tx = threadIdx.x, ty = threadIdx.y;
   for (int t = 0; t < 9; ++t) {
 #pragma unroll
     for (int j = 0; j < V; ++j) s_red[ty * BX * V + tx * V + j] = acc[t][j];
@@ -331,49 +387,37 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(DwBwdArgs a) {
 }
 
 int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype) {
-  int V = dtype == DT_F32 ? 4 : 8, bx, by;
-  dw_block_shape(C, V, bx, by);
-  long long nstrips = (long long)N * Ho * cdiv(Wo, DW_WS);
-  long long gy = (nstrips + by - 1) / by;
-  int gx = cdiv(C / V, bx);
-  long long cap = 2048 / gx;
+  DwGeom g = dw_geom(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8);
+  long long tiles = (long long)g.gy * g.gz;
+  long long cap = 2048 / g.gx;
   if (cap < 1) cap = 1;
-  return (int)(gy < cap ? gy : cap);
+  return (int)(tiles < cap ? tiles : cap);
 }
 
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   int V = dtype == DT_F32 ? 4 : 8;
   int bx, by;
   dw_block_shape(a.C, V, bx, by);
-  dim3 grid(cdiv(a.C / V, bx), dw_wgrad_parts(a.N, a.Ho, a.Wo, a.C, dtype));
+  DwGeom g = dw_geom(a.N, a.Ho, a.Wo, a.C, V);
+  dim3 grid(g.gx, dw_wgrad_parts(a.N, a.Ho, a.Wo, a.C, dtype));
   dim3 block(bx, by);
   size_t shm = (size_t)bx * by * V * sizeof(float);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el), 18.0 * out_el);
   if (dtype == DT_F32) {
-    if (a.stride == 1) dw_wgrad_kernel<float, 1><<<grid, block, shm, st>>>(a);
-    else dw_wgrad_kernel<float, 2><<<grid, block, shm, st>>>(a);
+    if (a.stride == 1) dw_wgrad_kernel<float, 1><<<grid, block, shm, st>>>(a, g.gy, g.gz);
+    else dw_wgrad_kernel<float, 2><<<grid, block, shm, st>>>(a, g.gy, g.gz);
   } else {
-    if (a.stride == 1) dw_wgrad_kernel<bf16, 1><<<grid, block, shm, st>>>(a);
-    else dw_wgrad_kernel<bf16, 2><<<grid, block, shm, st>>>(a);
+    if (a.stride == 1) dw_wgrad_kernel<bf16, 1><<<grid, block, shm, st>>>(a, g.gy, g.gz);
+    else dw_wgrad_kernel<bf16, 2><<<grid, block, shm, st>>>(a, g.gy, g.gz);
   }
   return check_launch("dw_wgrad");
 }
 
-// slab [P][9][C] -> dW [C][9] (native PyTorch [C,1,3,3] layout), fixed-order sum over P
-__global__ void dw_wgrad_reduce_kernel(const float* slab, int P, int C, float* dw) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 9 * C) return;
-  int t = i / C, c = i - t * C;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += slab[((size_t)p * 9 + t) * C + c];
-  dw[c * 9 + t] = s;
-}
-
-int dw_wgrad_reduce(const float* slab, int P, int C, float* dw, hipStream_t st) {
-  dw_wgrad_reduce_kernel<<<cdiv(9 * C, 256), 256, 0, st>>>(slab, P, C, dw);
-  return check_launch("dw_wgrad_reduce");
+// slab [P][9][C] -> dW [C][9] (native PyTorch [C,1,3,3] layout): two-pass fixed-order reduction
+int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st) {
+  return reduce_slabs_ex(slab, P, 9LL * C, 9LL * C, dw, 0, C, st);
 }
 
 }  // namespace fscnn

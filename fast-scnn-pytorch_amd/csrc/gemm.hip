@@ -463,21 +463,49 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
   return check_launch("gemm_tn");
 }
 
-// out[i] = sum_{s<S} slab[s*stride + i]  (fixed order), optionally out += (accumulate)
-__global__ void reduce_slabs_kernel(const float* slab, int S, long long stride, long long count,
-                                    float* out, int accumulate) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+// Deterministic two-pass reduction of S partial slabs: out[i] = sum_{s<S} slab[s*stride + i].
+// Pass 1 folds slab k into slab (k mod Q) IN PLACE (thread (i, q) owns every slab[k*stride+i]
+// with k = q mod Q, so there is no race), giving Q*count-way parallelism; pass 2 sums the Q
+// survivors.  Fixed assignment and order => bitwise reproducible.  `transpose9` writes
+// out[(i % C9) * 9 + i / C9] (depthwise [9][C] partials -> PyTorch [C][3][3]).
+constexpr int RED_Q = 64;
+
+__global__ void reduce_fold_kernel(float* slab, int S, int Q, long long stride, int count) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int q = blockIdx.y;
+  if (i >= count) return;
+  float s = 0.f;
+  for (int k = q; k < S; k += Q) s += slab[(size_t)k * stride + i];
+  slab[(size_t)q * stride + i] = s;
+}
+
+__global__ void reduce_final_kernel(const float* slab, int S, long long stride, int count,
+                                    float* out, int accumulate, int C9) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   float s = 0.f;
   for (int k = 0; k < S; ++k) s += slab[(size_t)k * stride + i];
-  out[i] = accumulate ? out[i] + s : s;
+  int o = C9 ? (i % C9) * 9 + i / C9 : i;
+  out[o] = accumulate ? out[o] + s : s;
 }
 
-int reduce_slabs(const float* slab, int S, long long stride, long long count, float* out,
-                 int accumulate, hipStream_t st) {
-  reduce_slabs_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slab, S, stride, count, out,
-                                                                        accumulate);
+int reduce_slabs_ex(float* slab, int S, long long stride, long long count, float* out,
+                    int accumulate, int C9, hipStream_t st) {
+  if (count <= 0 || count > 0x7fffffff) { set_error("reduce_slabs: bad count"); return E_INVALID; }
+  int n = (int)count;
+  int S2 = S;
+  if (S > RED_Q) {
+    dim3 g1(cdiv(n, 256), RED_Q);
+    reduce_fold_kernel<<<g1, 256, 0, st>>>(slab, S, RED_Q, stride, n);
+    S2 = RED_Q;
+  }
+  reduce_final_kernel<<<cdiv(n, 256), 256, 0, st>>>(slab, S2, stride, n, out, accumulate, C9);
   return check_launch("reduce_slabs");
+}
+
+int reduce_slabs(float* slab, int S, long long stride, long long count, float* out,
+                 int accumulate, hipStream_t st) {
+  return reduce_slabs_ex(slab, S, stride, count, out, accumulate, 0, st);
 }
 
 // per-block column sums of D [M][N] (ld) -> part [P][N]  (bias gradients)

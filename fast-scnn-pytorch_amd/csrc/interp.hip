@@ -163,27 +163,37 @@ __host__ __device__ __forceinline__ int pp_start(int i, int in, int k) { return 
 __host__ __device__ __forceinline__ int pp_end(int i, int in, int k) { return ((i + 1) * in + k - 1) / k; }
 
 
+// one workgroup per (bin, image): 128 channel lanes x 4 row groups, fixed-order LDS combine
 template <typename T>
-__global__ __launch_bounds__(128) void pyramid_pool_kernel(PoolArgs a) {
+__global__ __launch_bounds__(512) void pyramid_pool_kernel(PoolArgs a) {
   const int b = blockIdx.x, n = blockIdx.y;
+  const int tx = threadIdx.x & 127, g = threadIdx.x >> 7;
+  __shared__ float red[4][128];
   int k, bi, bj;
   pp_bin(b, k, bi, bj);
-  int h0 = pp_start(bi, a.H, k), h1 = pp_end(bi, a.H, k);
-  int w0 = pp_start(bj, a.W, k), w1 = pp_end(bj, a.W, k);
-  float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+  const int h0 = pp_start(bi, a.H, k), h1 = pp_end(bi, a.H, k);
+  const int w0 = pp_start(bj, a.W, k), w1 = pp_end(bj, a.W, k);
+  const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
   const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.ldx;
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+  for (int c0 = 0; c0 < a.C; c0 += 128) {
+    const int c = c0 + tx;
     float s = 0.f;
-    for (int h = h0; h < h1; ++h)
-      for (int w = w0; w < w1; ++w) s += ld1(xb + ((size_t)h * a.W + w) * a.ldx + c);
-    st1((T*)a.pooled + ((size_t)b * a.N + n) * a.C + c, s * inv);
+    if (c < a.C)
+      for (int h = h0 + g; h < h1; h += 4)
+        for (int w = w0; w < w1; ++w) s += ld1(xb + ((size_t)h * a.W + w) * a.ldx + c);
+    red[g][tx] = s;
+    __syncthreads();
+    if (g == 0 && c < a.C)
+      st1((T*)a.pooled + ((size_t)b * a.N + n) * a.C + c,
+          (red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]) * inv);
+    __syncthreads();
   }
 }
 
 int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
   dim3 grid(50, a.N);
-  if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 128, 0, st>>>(a);
-  else pyramid_pool_kernel<bf16><<<grid, 128, 0, st>>>(a);
+  if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 512, 0, st>>>(a);
+  else pyramid_pool_kernel<bf16><<<grid, 512, 0, st>>>(a);
   return check_launch("pyramid_pool");
 }
 
@@ -268,39 +278,45 @@ int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
 }
 
 // backward: dfeats[bin][n][c] = sum_{h,w} wy(h,bi) wx(w,bj) dy[n,h,w,coff+lv*CF+c]  (gather)
+// one workgroup per (bin, image): CF channel lanes x (256/CF) row groups, fixed-order combine
 template <typename T>
 __global__ __launch_bounds__(256) void ppm_up_bwd_kernel(PpmUpArgs a, void* dfeats) {
-  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = 50LL * a.N * a.CF;
-  if (t >= total) return;
-  int c = (int)(t % a.CF);
-  long long r = t / a.CF;
-  int n = (int)(r % a.N);
-  int b = (int)(r / a.N);
+  const int b = blockIdx.x, n = blockIdx.y;
+  const int G = 256 / a.CF;
+  const int c = threadIdx.x % a.CF, g = threadIdx.x / a.CF;
+  __shared__ float red[256];
   int k, bi, bj;
   pp_bin(b, k, bi, bj);
   const int lv = k == 1 ? 0 : (k == 2 ? 1 : (k == 3 ? 2 : 3));
   const float sh = ac_scale(k, a.H), sw = ac_scale(k, a.W);
-  const T* g = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * a.CF + c;
+  const T* gp = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * a.CF + c;
   float s = 0.f;
-  for (int h = 0; h < a.H; ++h) {
-    Lerp lh = ac_lerp(h, k, a.H, sh);
-    float wy = (lh.i0 == bi ? lh.l0 : 0.f) + (lh.i1 == bi ? lh.l1 : 0.f);
-    if (wy == 0.f) continue;
-    float sr = 0.f;
-    for (int w = 0; w < a.W; ++w) {
-      Lerp lw = ac_lerp(w, k, a.W, sw);
-      float wx = (lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f);
-      if (wx != 0.f) sr += wx * ld1(g + ((size_t)h * a.W + w) * a.ldy);
+  if (g < G) {
+    for (int h = g; h < a.H; h += G) {
+      Lerp lh = ac_lerp(h, k, a.H, sh);
+      float wy = (lh.i0 == bi ? lh.l0 : 0.f) + (lh.i1 == bi ? lh.l1 : 0.f);
+      if (wy == 0.f) continue;
+      float sr = 0.f;
+      for (int w = 0; w < a.W; ++w) {
+        Lerp lw = ac_lerp(w, k, a.W, sw);
+        float wx = (lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f);
+        if (wx != 0.f) sr += wx * ld1(gp + ((size_t)h * a.W + w) * a.ldy);
+      }
+      s += wy * sr;
     }
-    s += wy * sr;
   }
-  st1((T*)dfeats + ((size_t)b * a.N + n) * a.CF + c, s);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (g == 0) {
+    float t = 0.f;
+    for (int q = 0; q < G; ++q) t += red[q * a.CF + c];
+    st1((T*)dfeats + ((size_t)b * a.N + n) * a.CF + c, t);
+  }
 }
 
 int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
-  long long total = 50LL * a.N * a.CF;
-  unsigned grid = (unsigned)((total + 255) / 256);
+  if (a.CF <= 0 || a.CF > 256 || 256 % a.CF) { set_error("ppm_up_bwd: CF=%d", a.CF); return E_INVALID; }
+  dim3 grid(50, a.N);
   if (dtype == DT_F32) ppm_up_bwd_kernel<float><<<grid, 256, 0, st>>>(a, dfeats);
   else ppm_up_bwd_kernel<bf16><<<grid, 256, 0, st>>>(a, dfeats);
   return check_launch("ppm_up_bwd");

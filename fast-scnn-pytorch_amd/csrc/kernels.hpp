@@ -212,14 +212,17 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
 int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype);
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
-int dw_wgrad_reduce(const float* slab, int P, int C, float* dw, hipStream_t st);
+int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st);
 
 int gemm_parts(int M);
 int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st);
 int gemm_tn_splits(int M, int N, int K);
 int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st);
-int reduce_slabs(const float* slab, int S, long long stride, long long count, float* out,
+// slab is consumed (folded in place)
+int reduce_slabs(float* slab, int S, long long stride, long long count, float* out,
                  int accumulate, hipStream_t st);
+int reduce_slabs_ex(float* slab, int S, long long stride, long long count, float* out,
+                    int accumulate, int C9, hipStream_t st);
 int colsum_parts(int M);
 int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStream_t st);
 

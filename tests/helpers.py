@@ -44,6 +44,23 @@ def golden_target(g):
         ignore_frac=float(g["ignore_frac"])))
 
 
+def oracle_bf16_emulated(sd, x, nc):
+    """Oracle forward with bf16 rounding of conv inputs / weights / outputs (autocast-like).
+
+    Its deviation from the fp32 oracle is the error budget bf16 arithmetic itself implies for a
+    given weight set; the HIP bf16 path is held to that budget (plus margin)."""
+    import torch.nn.functional as F
+    from oracle import fast_scnn_ref as ref
+    q = lambda v: v.to(torch.bfloat16).float()  # noqa: E731
+    oc = F.conv2d
+    F.conv2d = lambda a, w, b=None, *r, **k: q(oc(q(a), q(w), b, *r, **k))
+    try:
+        with torch.no_grad():
+            return ref.forward(sd, x, nc)[0][0]
+    finally:
+        F.conv2d = oc
+
+
 def argmax_agreement(logits, ref_argmax, ref_logits=None, margin_tol=1e-4):
     """Fraction of equal argmax pixels, and count of disagreements at margin > margin_tol.
 

@@ -216,17 +216,24 @@ def test_grads_are_arena_views():
 
 
 # ---------------------------------------------------------------------------------- bf16
-def test_bf16_forward_close_to_fp32():
-    g = load_golden("eval_c19_calib")
-    m = make_model(g, 19).eval()
-    x = golden_input(g).to(DEV)
+@pytest.mark.parametrize("case", ["eval_c19_calib", "eval_c2_calib", "eval_c19_default"])
+def test_bf16_forward_within_bf16_budget(case):
+    from helpers import oracle_bf16_emulated
+    g = load_golden(case)
+    nc = int(g["num_classes"])
+    m = make_model(g, nc).eval()
+    x = golden_input(g)
     with torch.no_grad():
-        o32 = m(x)[0].float()
-        o16 = m(x.to(torch.bfloat16))[0].float()
-    assert o16.dtype == torch.float32 and m(x.to(torch.bfloat16))[0].dtype == torch.bfloat16
-    rng = (o32.max() - o32.min()).item()
-    assert (o16 - o32).abs().max().item() < 0.05 * rng
-    assert (o16.argmax(1) == o32.argmax(1)).float().mean().item() > 0.98
+        out16 = m(x.to(DEV).to(torch.bfloat16))[0]
+    assert out16.dtype == torch.bfloat16
+    o16 = out16.float().cpu()
+    o32 = oracle_eval(golden_sd(g), x, nc)
+    oem = oracle_bf16_emulated(golden_sd(g), x, nc)
+    budget = (oem - o32).abs().max().item()
+    assert (o16 - o32).abs().max().item() <= 1.5 * budget + 1e-3 * (o32.abs().max().item()), budget
+    agree_em = (oem.argmax(1) == o32.argmax(1)).float().mean().item()
+    agree = (o16.argmax(1) == o32.argmax(1)).float().mean().item()
+    assert agree >= agree_em - 0.03, (agree, agree_em)
 
 
 def test_bf16_train_step_and_progress():
