@@ -43,11 +43,11 @@ struct ProfState {
 
 void prof_start(hipStream_t st) {
   if (g_prof.used + 2 > g_prof.ev.size()) { g_prof.overflow = true; return; }
-  hipEventRecord(g_prof.ev[g_prof.used], st);
+  (void)hipEventRecord(g_prof.ev[g_prof.used], st);
 }
 void prof_stop(hipStream_t st, double bytes, double flops) {
   if (g_prof.used + 2 > g_prof.ev.size()) return;
-  hipEventRecord(g_prof.ev[g_prof.used + 1], st);
+  (void)hipEventRecord(g_prof.ev[g_prof.used + 1], st);
   g_prof.used += 2;
   g_prof.bytes += bytes;
   g_prof.flops += flops;
@@ -225,6 +225,37 @@ int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int 
   }
   RunArgs r{};
   r.dout = dout; r.x = x; r.x_dtype = x_dtype; r.P = params; r.G = grads; r.ws = ws; r.bws = bws;
+  r.seed = seed; r.dropout_p = dropout_p; r.st = S(stream);
+  GUARD(net_backward(plan->plan, r, stage_from, stage_to));
+}
+
+int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
+                       long long ignore_index, float* loss2, const float* params, float* running,
+                       long long* nbt, void* ws, unsigned long long seed, float dropout_p,
+                       float momentum, void* stream) {
+  if (!plan || !x || !target || !loss2 || !params || !running || !ws) {
+    set_error("fscnn_forward_loss: null argument");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.x = x; r.x_dtype = x_dtype; r.out = nullptr; r.out_dtype = plan->plan.dtype;
+  r.P = params; r.R = running; r.NBT = nbt; r.ws = ws;
+  r.seed = seed; r.dropout_p = dropout_p; r.momentum = momentum; r.st = S(stream);
+  r.target = target; r.ignore_index = ignore_index; r.loss2 = loss2;
+  GUARD(net_forward(plan->plan, r));
+}
+
+int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const float* loss2,
+                        const void* x, int x_dtype, const float* params, float* grads, void* ws,
+                        void* bws, unsigned long long seed, float dropout_p, int stage_from,
+                        int stage_to, void* stream) {
+  if (!plan || !grad_loss || !loss2 || !x || !params || !grads || !ws || !bws) {
+    set_error("fscnn_backward_loss: null argument");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.gloss = grad_loss; r.loss2 = const_cast<float*>(loss2);
+  r.x = x; r.x_dtype = x_dtype; r.P = params; r.G = grads; r.ws = ws; r.bws = bws;
   r.seed = seed; r.dropout_p = dropout_p; r.st = S(stream);
   GUARD(net_backward(plan->plan, r, stage_from, stage_to));
 }

@@ -183,6 +183,20 @@ struct CeArgs {
   void* dlogits;          // [N][C][HW] or null
 };
 
+// Fused training head: bilinear(align_corners) upsample of the low-res logits to the input
+// resolution + cross-entropy(ignore_index) + its gradient back to the low-res logits, without
+// materialising full-resolution logits.  g_raw receives sum_pixels w * (softmax - onehot)
+// (unscaled); loss partials per workgroup.
+struct CeHeadArgs {
+  int N, C, Hl, Wl, H, W;
+  const void* logits;        // NHWC [N][Hl][Wl][ldl]
+  int ldl;
+  const long long* target;   // [N][H][W]
+  long long ignore_index;
+  float* g_raw;              // NHWC [N][Hl][Wl][ldl] fp32
+  float* part;               // [P][2]
+};
+
 struct DropArgs {
   int N, H, W, C;
   const void* x; int ldx;
@@ -246,6 +260,11 @@ int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st);
 int ce_parts(int N, long long HW);
 int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st);
 int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hipStream_t st);
+int ce_head_parts(int N, int Hl, int Wl);
+int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
+// g[m][c] = g_raw[m][c] * gout / count  (c < C; pad columns zeroed)
+int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const float* gout,
+                  const float* out2, int dtype, hipStream_t st);
 int dropout(const DropArgs& a, int dtype, hipStream_t st);
 int sgd(const SgdArgs& a, hipStream_t st);
 int cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st);

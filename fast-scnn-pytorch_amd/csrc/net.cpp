@@ -234,6 +234,10 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   unit(pl.c2pw, M2, 128, gemm_parts((int)M2));
   pl.drop = train ? A.get((size_t)M2 * 128 * E) : pl.c2pw.a;
   pl.logits = A.get((size_t)M2 * pl.Cp * E);
+  if (train) {
+    pl.g_raw = A.get((size_t)M2 * pl.Cp * 4);
+    pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
+  }
   pl.ws_bytes = A.top;
   auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
     pl.named.push_back({n, off, rows, cols, ld, bws});
@@ -586,6 +590,18 @@ struct Exec {
       g.C = W(pl.logits); g.ldc = pl.Cp;
       TRY(gemm_nt(g, dt, r.st));
     }
+    if (r.target) {
+      // ---- fused training head: upsample + CE + gradient at low resolution ----
+      if (!train) {
+        set_error("forward_loss needs a training plan");
+        return E_INVALID;
+      }
+      CeHeadArgs h{};
+      h.N = N; h.C = net.num_classes; h.Hl = pl.H3; h.Wl = pl.W3; h.H = pl.H; h.W = pl.W;
+      h.logits = W(pl.logits); h.ldl = pl.Cp; h.target = r.target; h.ignore_index = r.ignore_index;
+      h.g_raw = Wf(pl.g_raw); h.part = Wf(pl.head_part);
+      return ce_head(h, r.loss2, dt, r.st);
+    }
     // ---- final bilinear (align_corners) to NCHW ----
     UpArgs u{};
     u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
@@ -648,8 +664,12 @@ struct Exec {
   int backward_head() {
     const int N = pl.N, C = net.num_classes;
     void* dz = Bw(pl.dz);
-    // final upsample: W pass (NCHW rows) then H pass into NHWC low-res logits grad
-    {
+    if (r.gloss) {
+      // fused head: the low-res logits gradient was gathered in the forward; scale by dL/dloss / count
+      TRY(ce_head_scale(Wf(pl.g_raw), Bw(pl.g_logits), pl.c2pw.M, C, pl.Cp, r.gloss, r.loss2, dt,
+                        r.st));
+    } else {
+      // final upsample: W pass (NCHW rows) then H pass into NHWC low-res logits grad
       AxisBwdArgs a{};
       a.n_o1 = (long long)N * C * pl.H; a.n_o2 = 1; a.Lout = pl.W; a.Lin = pl.W3; a.n_in = 1;
       a.g = r.dout; a.g_s1 = pl.W; a.g_s2 = 0; a.g_idx = 1; a.g_in = 0;

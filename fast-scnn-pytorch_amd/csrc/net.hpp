@@ -79,6 +79,7 @@ struct Plan {
   Unit aux0;
   size_t concat = 0, pooled = 0, feats_a = 0, feats_z = 0, up_low = 0, f = 0, drop = 0,
          logits = 0, aux_drop = 0, aux_logits = 0, pbf = 0, fold_tmp = 0;
+  size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
@@ -106,6 +107,13 @@ struct RunArgs {
   float dropout_p;
   float momentum;
   hipStream_t st;
+  // fused loss head: forward with target != null computes the CE loss into loss2[0..1]
+  // (mean, count) instead of writing full-resolution logits; backward with gloss != null
+  // starts from d(loss) instead of d(logits).
+  const long long* target = nullptr;
+  long long ignore_index = -1;
+  float* loss2 = nullptr;
+  const float* gloss = nullptr;
 };
 
 int net_forward(const Plan& pl, const RunArgs& r);

@@ -218,6 +218,27 @@ class _FastSCNNFunction(torch.autograd.Function):
         return (None, None) + tuple(grads)
 
 
+class _FastSCNNLossFunction(torch.autograd.Function):
+    """Fused train step head: loss = CE(upsample(logits_lowres), target) at low resolution."""
+
+    @staticmethod
+    def forward(ctx, x, target, ignore_index, model, *params):
+        loss2, ws, seed, dt = model._run_forward_loss(x, target, ignore_index)
+        ctx.model = model
+        ctx.ws, ctx.seed, ctx.dt, ctx.loss2 = ws, seed, dt, loss2
+        ctx.save_for_backward(x)
+        return loss2[0].clone()
+
+    @staticmethod
+    def backward(ctx, gloss):
+        (x,) = ctx.saved_tensors
+        g = gloss.to(torch.float32).reshape(1).contiguous()
+        grads = ctx.model._run_backward(None, x, ctx.ws, ctx.seed, ctx.dt, gloss=g,
+                                        loss2=ctx.loss2)
+        ctx.ws = None
+        return (None, None, None, None) + tuple(grads)
+
+
 class FastSCNN(nn.Module):
     """Fast-SCNN (models/fast_scnn.py:16-46) on the MI355X HIP path."""
 
@@ -377,12 +398,56 @@ class FastSCNN(nn.Module):
         flat = base[off.value:off.value + n * esz].view(dt)
         return flat.as_strided((rows.value, cols.value), (ld.value, 1))
 
-    def _run_backward(self, gout, x, ws, seed, dt):
+    def _run_forward_loss(self, x, target, ignore_index):
+        if not x.is_cuda or not target.is_cuda:
+            raise RuntimeError("FastSCNN.forward_loss: the HIP path needs ROCm device tensors")
+        nat = self.native()
+        ar = self.arena()
+        N, _, H, W = x.shape
+        if tuple(target.shape) != (N, H, W):
+            raise RuntimeError("forward_loss: target %s does not match input %s"
+                               % (tuple(target.shape), tuple(x.shape)))
+        if N < 2:
+            raise ValueError("Expected more than 1 value per channel when training, got input "
+                             "size torch.Size([1, 32, 1, 1])")
+        dt = self._compute_dtype(x)
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        target = target.to(torch.int64).contiguous()
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), True)
+        ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
+        loss2 = torch.empty(2, dtype=torch.float32, device=x.device)
+        p = self._dropout_p()
+        seed = 0
+        if p > 0:
+            fixed = getattr(self, "_dropout_seed", None)
+            seed = int(fixed) if fixed is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
+        _lib.call("fscnn_forward_loss", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(target),
+                  int(ignore_index), _lib.ptr(loss2), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]),
+                  _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p),
+                  _lib.c_float(self._momentum()), _lib.stream_ptr(x.device))
+        if getattr(self, "_keep_ws", False):
+            self._debug = {"plan": plan, "ws": ws, "dt": dt}
+        return loss2, ws, seed, dt
+
+    def forward_loss(self, x, target, ignore_index=-1):
+        """Fused train-step head: ``criterion(self(x)[0], target)`` of train.py:270-271 for
+        ``nn.CrossEntropyLoss(ignore_index)`` (utils/loss.py:103-124), computed at the low-res
+        logit resolution without materialising full-resolution logits.  Same loss and gradients
+        as the unfused path (tests/test_gpu_model.py); requires train mode."""
+        if not self.training:
+            raise RuntimeError("forward_loss is the training step; call model.train() first")
+        ar = self.arena()
+        return _FastSCNNLossFunction.apply(x, target, ignore_index, self, *ar["params"])
+
+    def _run_backward(self, gout, x, ws, seed, dt, gloss=None, loss2=None):
         nat = self.native()
         ar = self.arena()
         N, _, H, W = x.shape
         plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), True)
-        gout = gout.to(dt).contiguous()
+        if gout is not None:
+            gout = gout.to(dt).contiguous()
         G = torch.zeros(nat.p_total, dtype=torch.float32, device=x.device)
         bws = torch.empty(max(bw, 1), dtype=torch.uint8, device=x.device)
         p = self._dropout_p()
@@ -390,9 +455,16 @@ class FastSCNN(nn.Module):
             self._debug["bws"] = bws
         hook = self.grad_stage_hook
         for s in range(4):
-            _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x), _lib.dtype_code(x.dtype),
-                      _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws), _lib.ptr(bws), _lib.c_ull(seed),
-                      _lib.c_float(p), s, s, _lib.stream_ptr(x.device))
+            if gloss is None:
+                _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x),
+                          _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                          _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                          _lib.stream_ptr(x.device))
+            else:
+                _lib.call("fscnn_backward_loss", plan, _lib.ptr(gloss), _lib.ptr(loss2), _lib.ptr(x),
+                          _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                          _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                          _lib.stream_ptr(x.device))
             if hook is not None:
                 b, e = nat.stage_ranges[s]
                 hook(s, G, b, e)

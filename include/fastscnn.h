@@ -74,6 +74,20 @@ int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int 
                    unsigned long long dropout_seed, float dropout_p, int stage_from,
                    int stage_to, void* stream);
 
+/* Fused training step head (train plans only): forward + bilinear upsample + CE(ignore_index)
+ * evaluated at low resolution; loss2[0] = mean loss, loss2[1] = valid pixel count.  Computes
+ * exactly criterion(model(x)[0], target) of train.py:270-271 without materialising the
+ * full-resolution logits.  backward_loss then takes d(loss) (device scalar) instead of
+ * d(logits). */
+int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
+                       long long ignore_index, float* loss2, const float* params, float* running,
+                       long long* nbt, void* ws, unsigned long long dropout_seed, float dropout_p,
+                       float momentum, void* stream);
+int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const float* loss2,
+                        const void* x, int x_dtype, const float* params, float* grads, void* ws,
+                        void* bws, unsigned long long dropout_seed, float dropout_p,
+                        int stage_from, int stage_to, void* stream);
+
 /* ---- launch profiler (bench.py roofline) --------------------------------------------------
  * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 9 upsample.
  * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own

@@ -215,6 +215,60 @@ def test_grads_are_arena_views():
     assert all(gg.untyped_storage().data_ptr() == st for gg in grads)
 
 
+# ---------------------------------------------------------------------------------- fused head
+@pytest.mark.parametrize("case", ["train_c19", "train_c2"])
+def test_fused_loss_head_vs_oracle(case):
+    g = load_golden(case)
+    nc = int(g["num_classes"])
+    m = make_model(g, nc).train()
+    m._dropout_seed = int(g["drop_seed"])
+    x, t = golden_input(g).to(DEV), golden_target(g).to(DEV)
+    loss = m.forward_loss(x, t, ignore_index=-1)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(g["loss"])) < 1e-5 * max(1.0, float(g["loss"]))
+    lref, gref, _ = oracle_train(golden_sd(g), golden_input(g), golden_target(g), nc,
+                                 int(g["drop_seed"]))
+    _check_grads(m, gref, nc)
+    sd = m.state_dict()
+    for k in g:
+        if k.startswith("stats."):
+            np.testing.assert_allclose(sd[k[6:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5,
+                                       err_msg=k)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fused_loss_head_matches_unfused(dt):
+    from fast_scnn_pytorch_amd.loss import cross_entropy
+    g = load_golden("train_c19")
+    x, t = golden_input(g).to(DEV).to(dt), golden_target(g).to(DEV)
+    t[:, :7, :] = -1  # whole rows ignored
+    m1 = make_model(g, 19).train()
+    m1._dropout_seed = 5
+    l1 = cross_entropy(m1(x)[0], t)
+    l1.backward()
+    m2 = make_model(g, 19).train()
+    m2._dropout_seed = 5
+    l2 = m2.forward_loss(x, t)
+    l2.backward()
+    torch.cuda.synchronize()
+    # bf16: the unfused path rounds full-res logits to bf16 before the CE, the fused one does not
+    tol = 1e-6 if dt == torch.float32 else 2e-3
+    assert abs(l1.item() - l2.item()) <= tol * abs(l1.item()), (l1.item(), l2.item())
+    n1, n2 = dict(m1.named_parameters()), dict(m2.named_parameters())
+    a = torch.cat([n1[k].grad.flatten() for k in n1]).double()
+    b = torch.cat([n2[k].grad.flatten() for k in n2]).double()
+    cos = (a @ b / (a.norm() * b.norm())).item()
+    assert cos > (0.99999 if dt == torch.float32 else 0.9), cos
+    for k in ("classifier.conv.1.weight", "classifier.conv.1.bias"):
+        ga, gb = n1[k].grad.double(), n2[k].grad.double()
+        assert (ga - gb).norm().item() <= (1e-5 if dt == torch.float32 else 2e-2) * ga.norm().item(), k
+    s1, s2 = m1.state_dict(), m2.state_dict()
+    for k in s1:
+        if "running" in k:
+            assert torch.equal(s1[k], s2[k]), k
+
+
 # ---------------------------------------------------------------------------------- bf16
 @pytest.mark.parametrize("case", ["eval_c19_calib", "eval_c2_calib", "eval_c19_default"])
 def test_bf16_forward_within_bf16_budget(case):
