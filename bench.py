@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--profile-kind", type=int, default=0, help="0 = dominant (census)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-forward", action="store_true")
+    ap.add_argument("--unfused-loss", action="store_true",
+                    help="materialise full-res logits and run the separate CE kernels")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
@@ -143,8 +145,12 @@ def main():
 
     def step():
         opt.zero_grad(set_to_none=True)
-        out = net(x)[0]
-        loss = cross_entropy(out, t)
+        if args.unfused_loss:
+            loss = cross_entropy(net(x)[0], t)
+        else:
+            # same loss and gradients as cross_entropy(net(x)[0], t) (tests/test_gpu_model.py
+            # test_fused_loss_head_*), evaluated at 1/8 resolution without full-res logits
+            loss = net.forward_loss(x, t)
         loss.backward()
         opt.step()
         return loss
@@ -217,7 +223,7 @@ def main():
         "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (portable counter-based generator; random-init weights, default law)",
-        "config": {"workload": "cfg3 train step: fwd + CE(ignore -1) + bwd + fused SGD",
+        "config": {"workload": ("cfg3 train step: fwd + CE(ignore -1) + bwd + fused SGD" + (" (unfused CE)" if args.unfused_loss else " (fused low-res upsample+CE head)")),
                    "model": "FastSCNN (19 classes)", "global_batch": world * B,
                    "per_gpu_batch": B, "resolution": [H, W], "parallelism": "dp%d" % world},
         "roofline": roof,

@@ -4,20 +4,21 @@
 // logits (8 x 19 x 1024 x 2048 would be 637 MB bf16 written, read, re-written and re-read by the
 // unfused path).
 //
-// Deterministic gather: workgroup (n, hb, wb) OWNS low-res cells [hb*TH, +TH) x [wb*TW, +TW) of
-// image n.  It walks every full-res pixel whose bilinear stencil touches one of its cells
-// (its support, a 1-cell halo), recomputes the interpolated logits and the softmax there, keeps
-// the per-pixel gradient (softmax - onehot) of a pass in LDS, and each (cell, class) accumulator
-// is owned by exactly one thread that sums its contributions in a fixed order.  A pixel's loss is
-// counted by the workgroup that owns its (i0(h), i0(w)) cell, so every pixel counts once.
+// Layout of the work: workgroup (hl, n) owns the full-resolution pixels whose bilinear row tap
+// i0(h) is low-res row hl, across the whole width; thread t owns the pixels whose column tap
+// i0(w) is low-res column t.  Every pixel is therefore computed exactly once (no halo).  A pixel
+// touches cells (i0h|i1h) x (i0w|i1w); its four contributions are accumulated in registers:
+// (hl, t) and (hl, t+1) belong to the workgroup's own row, (hl+1, *) is its row spill.  At the
+// end thread t adds its neighbour's (hl, t) share in a fixed order and writes the own-row plane;
+// the spill plane (row hl+1) is written separately and summed in ce_head_scale, so the result is
+// deterministic without atomics.  The two low-res logit rows the workgroup interpolates from are
+// staged in LDS (odd row stride: conflict-free per-thread class walks).
 #include "kernels.hpp"
 
 namespace fscnn {
 
-constexpr int HD_TH = 4;     // owned low-res rows per workgroup
-constexpr int HD_TW = 14;    // owned low-res cols per workgroup (row support <= 128 px at x8)
-constexpr int HD_CMAX = 32;  // max classes
-constexpr int HD_GS = HD_CMAX + 1;
+constexpr int HD_T = 256;
+constexpr int HD_CMAX = 32;
 
 __device__ __forceinline__ int hd_first_ge(int i, int Lin, int Lout, float sc) {
   int lo = 0, hi = Lout;
@@ -29,113 +30,145 @@ __device__ __forceinline__ int hd_first_ge(int i, int Lin, int Lout, float sc) {
   return lo;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void ce_head_kernel(CeHeadArgs a) {
-  __shared__ float s_g[256 * HD_GS];              // per-pixel gradients of the current pass
-  __shared__ float s_acc[HD_TH * HD_TW * HD_CMAX];  // owned (cell, class) accumulators
-  __shared__ int s_wi0[256];
-  __shared__ float s_wl0[256], s_wl1[256];
-  __shared__ int s_wlo[HD_TW], s_whi[HD_TW];
-  __shared__ float s_r1[256], s_r2[256];
+template <typename T, int CT, bool EXACT>
+__global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
+  constexpr int SL = (CT % 2 == 0) ? CT + 1 : CT;  // odd LDS stride per column
+  __shared__ float s_L[2 * (HD_T + 1) * SL];
+  __shared__ float s_carry[2 * CT];
+  __shared__ float s_r1[HD_T], s_r2[HD_T];
   const int tid = threadIdx.x;
-  const int n = blockIdx.z;
-  const int hi0 = blockIdx.y * HD_TH, wi0 = blockIdx.x * HD_TW;
-  const int nth = min(HD_TH, a.Hl - hi0), ntw = min(HD_TW, a.Wl - wi0);
-  const int C = a.C;
-  const float sh = ac_scale(a.Hl, a.H), sw = ac_scale(a.Wl, a.W);
-  const int h_lo = hd_first_ge(hi0 - 1, a.Hl, a.H, sh), h_hi = hd_first_ge(hi0 + nth, a.Hl, a.H, sh);
-  const int w_lo = hd_first_ge(wi0 - 1, a.Wl, a.W, sw), w_hi = hd_first_ge(wi0 + ntw, a.Wl, a.W, sw);
-  if (tid < ntw) {
-    s_wlo[tid] = hd_first_ge(wi0 + tid - 1, a.Wl, a.W, sw);
-    s_whi[tid] = hd_first_ge(wi0 + tid + 1, a.Wl, a.W, sw);
-  }
-  for (int i = tid; i < HD_TH * HD_TW * HD_CMAX; i += 256) s_acc[i] = 0.f;
-  const int npx_row = w_hi - w_lo;
-  const int cw = npx_row <= 256 ? npx_row : 256;  // pixels per row per pass
-  const int R = npx_row <= 256 ? max(1, 256 / max(1, npx_row)) : 1;
-  const T* lg = (const T*)a.logits + (size_t)n * a.Hl * a.Wl * a.ldl;
+  const int hl = blockIdx.x, n = blockIdx.y;
+  const int Hl = a.Hl, Wl = a.Wl, H = a.H, W = a.W, ldl = a.ldl;
+  const int Cm = EXACT ? CT : a.C;
+  const float sh = ac_scale(Hl, H), sw = ac_scale(Wl, W);
+  const int h_lo = hd_first_ge(hl, Hl, H, sh), h_hi = hd_first_ge(hl + 1, Hl, H, sh);
+  const int hl1 = min(hl + 1, Hl - 1);
+  const T* lg = (const T*)a.logits + (size_t)n * Hl * Wl * ldl;
+  float* g0 = a.g_raw;                              // own-row plane
+  float* g1 = a.g_raw + (size_t)a.N * Hl * Wl * ldl;  // spill plane (row hl+1)
+  const long long* tgt = a.target + (size_t)n * H * W;
   float loss = 0.f, cnt = 0.f;
-  __syncthreads();
-  for (int h0 = h_lo; h0 < h_hi; h0 += R) {
-    for (int wc = w_lo; wc < w_hi; wc += cw) {
-      const int ncw = min(cw, w_hi - wc);
-      // ---- pass 1: gradient of each pixel of R rows x ncw cols ----------------------------
-      {
-        const int r = tid / max(1, cw), px = tid - r * cw;
-        const int h = h0 + r, w = wc + px;
-        if (r < R && h < h_hi && px < ncw) {
-          Lerp lh = ac_lerp(h, a.Hl, a.H, sh);
-          Lerp lw = ac_lerp(w, a.Wl, a.W, sw);
-          if (r == 0) {
-            s_wi0[px] = lw.i0;
-            s_wl0[px] = lw.l0;
-            s_wl1[px] = lw.l1;
+  if (tid < 2 * CT) s_carry[tid] = 0.f;
+  if (hl == 0) {  // nothing spills into row 0
+    for (int i = tid; i < Wl * ldl; i += HD_T) g1[(size_t)n * Hl * Wl * ldl + i] = 0.f;
+  }
+  for (int cb = 0; cb < Wl; cb += HD_T) {
+    __syncthreads();
+    // ---- stage low-res rows hl, hl1 for columns [cb, cb + HD_T] (clamped) -----------------
+    for (int i = tid; i < 2 * (HD_T + 1) * CT; i += HD_T) {
+      const int c = i % CT, jr = i / CT;
+      const int j = jr % (HD_T + 1), r = jr / (HD_T + 1);
+      const int col = min(cb + j, Wl - 1);
+      const int row = r ? hl1 : hl;
+      s_L[(r * (HD_T + 1) + j) * SL + c] =
+          c < Cm ? ld1(lg + ((size_t)row * Wl + col) * ldl + c) : 0.f;
+    }
+    __syncthreads();
+    const int t = cb + tid;
+    const bool active = t < Wl;
+    float acc00[CT], acc01[CT], acc10[CT], acc11[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc00[c] = acc01[c] = acc10[c] = acc11[c] = 0.f;
+    if (active) {
+      const int w_lo = hd_first_ge(t, Wl, W, sw), w_hi = hd_first_ge(t + 1, Wl, W, sw);
+      const float* L0 = &s_L[tid * SL];
+      const float* L1 = &s_L[((HD_T + 1) + tid) * SL];
+      for (int h = h_lo; h < h_hi; ++h) {
+        const Lerp lh = ac_lerp(h, Hl, H, sh);
+        float v0[CT], v1[CT];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          v0[c] = lh.l0 * L0[c] + lh.l1 * L1[c];
+          v1[c] = lh.l0 * L0[SL + c] + lh.l1 * L1[SL + c];
+        }
+        const long long* trow = tgt + (size_t)h * W;
+        for (int w = w_lo; w < w_hi; ++w) {
+          const Lerp lw = ac_lerp(w, Wl, W, sw);
+          const long long tg = trow[w];
+          const bool valid = tg != a.ignore_index && tg >= 0 && tg < Cm;
+          const int ti = (int)tg;
+          float e[CT];
+          float mx = -INFINITY, lt = 0.f;
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            e[c] = lw.l0 * v0[c] + lw.l1 * v1[c];
+            if (c < Cm) mx = fmaxf(mx, e[c]);
+            lt = (c == ti) ? e[c] : lt;
           }
-          const T* q00 = lg + ((size_t)lh.i0 * a.Wl + lw.i0) * a.ldl;
-          const T* q01 = lg + ((size_t)lh.i0 * a.Wl + lw.i1) * a.ldl;
-          const T* q10 = lg + ((size_t)lh.i1 * a.Wl + lw.i0) * a.ldl;
-          const T* q11 = lg + ((size_t)lh.i1 * a.Wl + lw.i1) * a.ldl;
-          float* gp = &s_g[(r * cw + px) * HD_GS];
-          float mx = -INFINITY;
-          for (int c = 0; c < C; ++c) {
-            float l = lh.l0 * (lw.l0 * ld1(q00 + c) + lw.l1 * ld1(q01 + c)) +
-                      lh.l1 * (lw.l0 * ld1(q10 + c) + lw.l1 * ld1(q11 + c));
-            gp[c] = l;
-            mx = fmaxf(mx, l);
-          }
-          const long long t = a.target[((size_t)n * a.H + h) * a.W + w];
-          const bool valid = t != a.ignore_index && t >= 0 && t < C;
           float se = 0.f;
-          for (int c = 0; c < C; ++c) se += expf(gp[c] - mx);
-          const float inv = 1.f / se;
-          const bool own = lh.i0 >= hi0 && lh.i0 < hi0 + nth && lw.i0 >= wi0 && lw.i0 < wi0 + ntw;
-          if (valid && own) {
-            loss += mx + logf(se) - gp[(int)t];
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            e[c] = c < Cm ? expf(e[c] - mx) : 0.f;
+            se += e[c];
+          }
+          const float inv = valid ? 1.f / se : 0.f;
+          if (valid) {
+            loss += mx + logf(se) - lt;
             cnt += 1.f;
           }
-          for (int c = 0; c < C; ++c) {
-            float p = expf(gp[c] - mx) * inv;
-            gp[c] = valid ? p - (c == (int)t ? 1.f : 0.f) : 0.f;
+          const float k00 = lh.l0 * lw.l0, k01 = lh.l0 * lw.l1;
+          const float k10 = lh.l1 * lw.l0, k11 = lh.l1 * lw.l1;
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            const float g = e[c] * inv - ((valid && c == ti) ? 1.f : 0.f);
+            acc00[c] += k00 * g;
+            acc01[c] += k01 * g;
+            acc10[c] += k10 * g;
+            acc11[c] += k11 * g;
           }
         }
       }
-      __syncthreads();
-      // ---- pass 2: every owned (cell column j, class c) gathers its contributions ---------
-      for (int idx = tid; idx < ntw * C; idx += 256) {
-        const int j = idx / C, c = idx - j * C;
-        const int wi = wi0 + j;
-        const int a0 = max(s_wlo[j], wc), a1 = min(s_whi[j], wc + ncw);
-        for (int r = 0; r < R; ++r) {
-          const int h = h0 + r;
-          if (h >= h_hi) break;
-          float s = 0.f;
-          for (int w = a0; w < a1; ++w) {
-            const int p = w - wc;
-            const int i0 = s_wi0[p];
-            const int i1 = i0 + (i0 < a.Wl - 1 ? 1 : 0);
-            const float wx = (i0 == wi ? s_wl0[p] : 0.f) + (i1 == wi ? s_wl1[p] : 0.f);
-            s += wx * s_g[(r * cw + p) * HD_GS + c];
-          }
-          Lerp lh = ac_lerp(h, a.Hl, a.H, sh);
-          if (lh.i0 >= hi0 && lh.i0 < hi0 + nth)
-            s_acc[((lh.i0 - hi0) * HD_TW + j) * HD_CMAX + c] += lh.l0 * s;
-          if (lh.i1 != lh.i0 && lh.i1 >= hi0 && lh.i1 < hi0 + nth)
-            s_acc[((lh.i1 - hi0) * HD_TW + j) * HD_CMAX + c] += lh.l1 * s;
+      if (t == Wl - 1) {  // i1(w) == i0(w) on the last column: both taps are column t
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          acc00[c] += acc01[c];
+          acc10[c] += acc11[c];
+          acc01[c] = acc11[c] = 0.f;
         }
       }
-      __syncthreads();
+      if (hl1 == hl) {  // last row: both row taps are row hl
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          acc00[c] += acc10[c];
+          acc01[c] += acc11[c];
+          acc10[c] = acc11[c] = 0.f;
+        }
+      }
     }
-  }
-  for (int idx = tid; idx < nth * ntw * C; idx += 256) {
-    const int c = idx % C, rj = idx / C;
-    const int r = rj / ntw, j = rj - r * ntw;
-    a.g_raw[(((size_t)n * a.Hl + hi0 + r) * a.Wl + wi0 + j) * a.ldl + c] =
-        s_acc[(r * HD_TW + j) * HD_CMAX + c];
+    // ---- hand the (*, t+1) shares to thread t+1 through LDS -------------------------------
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      s_L[tid * SL + c] = acc01[c];
+      s_L[((HD_T + 1) + tid) * SL + c] = acc11[c];
+    }
+    __syncthreads();
+    if (active) {
+      float* o0 = g0 + (((size_t)n * Hl + hl) * Wl + t) * ldl;
+      float* o1 = g1 + (((size_t)n * Hl + hl + 1) * Wl + t) * ldl;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        if (c < Cm) {
+          const float left0 = tid > 0 ? s_L[(tid - 1) * SL + c] : s_carry[c];
+          const float left1 = tid > 0 ? s_L[((HD_T + 1) + tid - 1) * SL + c] : s_carry[CT + c];
+          o0[c] = acc00[c] + left0;
+          if (hl1 != hl) o1[c] = acc10[c] + left1;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == HD_T - 1) {  // column cb + HD_T starts the next chunk
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        s_carry[c] = acc01[c];
+        s_carry[CT + c] = acc11[c];
+      }
+    }
   }
   s_r1[tid] = loss;
   s_r2[tid] = cnt;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
+  for (int off = HD_T / 2; off > 0; off >>= 1) {
     if (tid < off) {
       s_r1[tid] += s_r1[tid + off];
       s_r2[tid] += s_r2[tid + off];
@@ -143,13 +176,13 @@ __global__ __launch_bounds__(256) void ce_head_kernel(CeHeadArgs a) {
     __syncthreads();
   }
   if (tid == 0) {
-    const size_t pi = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const size_t pi = (size_t)n * Hl + hl;
     a.part[2 * pi] = s_r1[0];
     a.part[2 * pi + 1] = s_r2[0];
   }
 }
 
-int ce_head_parts(int N, int Hl, int Wl) { return N * cdiv(Hl, HD_TH) * cdiv(Wl, HD_TW); }
+int ce_head_parts(int N, int Hl, int Wl) { return N * Hl; }
 
 __global__ __launch_bounds__(256) void ce_head_finalize_kernel(const float* part, int P, float* out) {
   __shared__ double r1[256], r2[256];
@@ -179,13 +212,25 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
     set_error("ce_head: %d classes (max %d)", a.C, HD_CMAX);
     return E_UNSUPPORTED;
   }
-  dim3 grid(cdiv(a.Wl, HD_TW), cdiv(a.Hl, HD_TH), a.N);
+  dim3 grid(a.Hl, a.N);
   {
-    ProfScope ps(PK_CE, st, (dtype == DT_F32 ? 4.0 : 2.0) * a.N * a.Hl * a.Wl * a.ldl * 1.3 +
-                                8.0 * a.N * a.H * a.W + 4.0 * a.N * a.Hl * a.Wl * a.ldl,
+    ProfScope ps(PK_CE, st, (dtype == DT_F32 ? 4.0 : 2.0) * a.N * a.Hl * a.Wl * a.C +
+                                8.0 * a.N * a.H * a.W + 2.0 * 4.0 * a.N * a.Hl * a.Wl * a.C,
                  0.0);
-    if (dtype == DT_F32) ce_head_kernel<float><<<grid, 256, 0, st>>>(a);
-    else ce_head_kernel<bf16><<<grid, 256, 0, st>>>(a);
+    const bool f32 = dtype == DT_F32;
+    if (a.C == 19) {
+      if (f32) ce_head_kernel<float, 19, true><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, 19, true><<<grid, HD_T, 0, st>>>(a);
+    } else if (a.C == 2) {
+      if (f32) ce_head_kernel<float, 2, true><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, 2, true><<<grid, HD_T, 0, st>>>(a);
+    } else if (a.C <= 8) {
+      if (f32) ce_head_kernel<float, 8, false><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, 8, false><<<grid, HD_T, 0, st>>>(a);
+    } else {
+      if (f32) ce_head_kernel<float, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
+    }
     int rc = check_launch("ce_head");
     if (rc) return rc;
   }
@@ -201,7 +246,8 @@ __global__ __launch_bounds__(256) void ce_head_scale_kernel(const float* g_raw, 
   if (i >= M * ld) return;
   const int c = i % ld;
   const float s = gout[0] / out2[1];
-  st1(g + i, c < C ? g_raw[i] * s : 0.f);
+  // own-row plane + the spill of the row above (fixed order)
+  st1(g + i, c < C ? (g_raw[i] + g_raw[(size_t)M * ld + i]) * s : 0.f);
 }
 
 int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const float* gout,

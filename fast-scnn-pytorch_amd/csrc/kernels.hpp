@@ -193,8 +193,8 @@ struct CeHeadArgs {
   int ldl;
   const long long* target;   // [N][H][W]
   long long ignore_index;
-  float* g_raw;              // NHWC [N][Hl][Wl][ldl] fp32
-  float* part;               // [P][2]
+  float* g_raw;              // 2 planes NHWC [N][Hl][Wl][ldl] fp32: own row, spill from row above
+  float* part;               // [N * Hl][2]
 };
 
 struct DropArgs {

@@ -235,7 +235,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   pl.drop = train ? A.get((size_t)M2 * 128 * E) : pl.c2pw.a;
   pl.logits = A.get((size_t)M2 * pl.Cp * E);
   if (train) {
-    pl.g_raw = A.get((size_t)M2 * pl.Cp * 4);
+    pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
   }
   pl.ws_bytes = A.top;

@@ -77,3 +77,7 @@ class DistributedFastSCNN(torch.nn.Module):
 
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)
+
+    def forward_loss(self, x, target, ignore_index=-1):
+        """Fused forward + CE of the local shard; backward all-reduces gradients per stage."""
+        return self.module.forward_loss(x, target, ignore_index=ignore_index)
