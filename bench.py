@@ -31,7 +31,8 @@ METRIC = "images/sec fwd+bwd @1024x2048 bs=8 per GPU; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0
 MFMA_PEAK_TFS = {"bf16": 2500.0, "fp32": 157.3}
 PROF_KINDS = {1: "conv0_fwd", 2: "dw_fwd", 3: "dw_dgrad", 4: "dw_wgrad", 5: "gemm_nt",
-              6: "gemm_tn", 9: "upsample"}
+              6: "gemm_tn", 9: "upsample", 11: "ce_head",
+              12: "conv0_wgrad"}
 
 
 def parse():

@@ -53,6 +53,8 @@ SIGNATURES = {
                           c_int, c_float, c_vp]),
     "fscnn_conv0_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
                                 c_int, c_vp]),
+    "fscnn_conv0_wgrad_slab_floats": (c_ll, [c_int, c_int, c_int]),
+    "fscnn_conv0_wgrad": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
     "fscnn_dw3x3_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                 c_int, c_vp, c_vp]),
     "fscnn_dw3x3_dgrad": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,

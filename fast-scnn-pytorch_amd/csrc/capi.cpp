@@ -100,7 +100,7 @@ extern "C" int fscnn_prof_end(double* total_ms, long long* launches, double* byt
 extern "C" const char* fscnn_prof_kind_name(int kind) {
   static const char* names[PK_COUNT] = {"none", "conv0_fwd", "dw_fwd", "dw_dgrad", "dw_wgrad",
                                         "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
-                                        "upsample_bwd", "cross_entropy"};
+                                        "upsample_bwd", "cross_entropy", "conv0_wgrad"};
   return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
 }
 
@@ -295,6 +295,19 @@ int fscnn_conv0_fwd(const void* x, int x_dtype, int N, int H, int W, const float
   a.Ho = (H - 3) / 2 + 1; a.Wo = (W - 3) / 2 + 1; a.w = w; a.scale = scale; a.shift = shift;
   a.relu = relu; a.y = y;
   return conv0_fwd(a, y_dtype, S(stream));
+}
+
+long long fscnn_conv0_wgrad_slab_floats(int N, int H, int W) {
+  return (long long)conv0_wgrad_parts(N, (H - 3) / 2 + 1, (W - 3) / 2 + 1, 0) * 864;
+}
+int fscnn_conv0_wgrad(const void* x, int x_dtype, int N, int H, int W, const void* dz,
+                      int dz_dtype, float* slab, float* dw, void* stream) {
+  Conv0WgradArgs a{};
+  a.x = x; a.x_bf16 = x_dtype == DT_BF16; a.N = N; a.H = H; a.W = W;
+  a.Ho = (H - 3) / 2 + 1; a.Wo = (W - 3) / 2 + 1; a.dz = dz; a.slab = slab;
+  int rc = conv0_wgrad(a, dz_dtype, S(stream));
+  if (rc) return rc;
+  return reduce_slabs(slab, conv0_wgrad_parts(N, a.Ho, a.Wo, 0), 864, 864, dw, 0, S(stream));
 }
 
 int fscnn_dw3x3_fwd(const void* x, int dtype, int N, int H, int W, int C, int stride,

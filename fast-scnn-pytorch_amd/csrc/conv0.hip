@@ -148,82 +148,179 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
 }
 
 // ---- weight gradient --------------------------------------------------------------------------
-// dW[co][ci][kh][kw] = sum_{n,ho,wo} dZ[n,ho,wo,co] * x[n,ci,2ho+kh,2wo+kw].
-// One workgroup per (row of output pixels, 256-wide segment), like the forward; each thread
-// owns one pixel, the 27 input taps and the 32 dZ values, and the block reduces the 864
-// products over its pixels through LDS.  Output: partial slab [part][864] (deterministic
-// reduction by reduce_slabs).
+// dW[co][ci][kh][kw] = sum_{n,ho,wo} dZ[n,ho,wo,co] * x[n,ci,2ho+kh,2wo+kw] is a GEMM with
+// M = 32 taps (27 used), N = 32 output channels and K = N*Ho*Wo pixels (4.2 M at cfg3):
+// dW^T[tap][co] = sum_p X[p][tap] dZ[p][co].  Each workgroup walks pixel tiles (256 pixels of one
+// output row) grid-stride; per tile it stages X^T[tap][p] (gathered from the NCHW image) and
+// dZ^T[co][p] (transposed from the NHWC gradient) in LDS, so every MFMA operand is one 16-B
+// ds_read per lane (8 consecutive pixels).  Wave w owns pixels [64w, 64w+64) of the tile and
+// keeps the full 32x32 accumulator (4 tiles of 16x16); the 4 waves are summed through LDS at the
+// end and one [864] partial per workgroup is written (reduced in fixed order by reduce_slabs).
+// HBM-bound: the x strip and the dZ tile are read once.
+constexpr int CW_TP = 256;  // pixels per tile
+constexpr int CW_MAXP = 1024;  // max workgroups (partials)
+
+template <typename T>
+struct CwOps;
+
+template <>
+struct CwOps<float> {
+  static constexpr int LD = CW_TP + 4;  // LDS row stride (elements)
+  static __device__ __forceinline__ void mma(const float* a, const float* b, f32x4& acc) {
+    // 8 consecutive pixels per lane group; 8 k-steps of 16x16x4 (k = 8*lq + m)
+    const float4 a0 = *reinterpret_cast<const float4*>(a), a1 = *reinterpret_cast<const float4*>(a + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(b), b1 = *reinterpret_cast<const float4*>(b + 4);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc, 0, 0, 0);
+  }
+};
+
+template <>
+struct CwOps<bf16> {
+  static constexpr int LD = CW_TP + 8;
+  static __device__ __forceinline__ void mma(const bf16* a, const bf16* b, f32x4& acc) {
+    i16x8 av, bv;
+    __builtin_memcpy(&av, a, 16);
+    __builtin_memcpy(&bv, b, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ T cw_cvt(float v);
+template <>
+__device__ __forceinline__ float cw_cvt<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ bf16 cw_cvt<bf16>(float v) {
+  bf16 r;
+  r.x = f2bf(v);
+  return r;
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
-  // Each thread accumulates 864/256 ~ 3.4 weights over all pixels of the block's rows: thread
-  // t owns outputs o = t, t+256, t+512, t+768 (<864).  Per pixel tile the inputs and dZ are
-  // staged in LDS.
-  __shared__ float s_in[3 * 3 * C0_IN_W];
-  __shared__ float s_dz[C0_TILE * 33];
-  const int tid = threadIdx.x;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  int oo[4], oco[4], otap[4];
+  constexpr int LD = CwOps<T>::LD;
+  constexpr int V = VecW<T>::V;
+  constexpr int SX = 32 * LD * sizeof(T);
+  constexpr int BYTES = 2 * SX > 4 * 1024 * 4 ? 2 * SX : 4 * 1024 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[BYTES];
+  T* sX = reinterpret_cast<T*>(s_raw);        // [32 taps][LD]
+  T* sD = reinterpret_cast<T*>(s_raw + SX);   // [32 co][LD]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int segs = cdiv(a.Wo, CW_TP);
+  const long long tiles = (long long)a.N * a.Ho * segs;
+  const size_t HW = (size_t)a.H * a.W;
+
+  // taps 27..31 of X^T stay zero
+  for (int i = tid; i < 5 * LD; i += 256) sX[27 * LD + i] = cw_cvt<T>(0.f);
+  f32x4 acc[2][2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    oo[j] = tid + 256 * j;
-    oco[j] = oo[j] / 27;
-    otap[j] = oo[j] - oco[j] * 27;
-  }
-  const int wo0 = blockIdx.x * C0_TILE;
-  const int npx = min(C0_TILE, a.Wo - wo0);
-  const int col0 = 2 * wo0;
-  const int ncol = min(C0_IN_W, a.W - col0);
-  const int nrows = a.N * a.Ho;
-  for (int rr = 0; rr < a.rows_per_block; ++rr) {
-    int row = blockIdx.y * a.rows_per_block + rr;
-    if (row >= nrows) break;
-    int n = row / a.Ho, ho = row - n * a.Ho;
-    __syncthreads();
-    for (int i = tid; i < 9 * C0_IN_W; i += 256) {
-      int cr = i / C0_IN_W, c = i - cr * C0_IN_W;
-      int ci = cr / 3, r = cr - ci * 3;
-      float v = 0.f;
-      if (c < ncol) {
-        size_t off = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c;
-        v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[off]) : ((const float*)a.x)[off];
-      }
-      s_in[i] = v;
-    }
-    const T* dz = (const T*)a.dz + ((size_t)row * a.Wo + wo0) * C0_OUT;
-    for (int i = tid; i < C0_TILE * C0_OUT; i += 256) {
-      int p = i >> 5, c = i & 31;
-      s_dz[p * 33 + c] = (p < npx) ? ld1(dz + i) : 0.f;
-    }
-    __syncthreads();
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (oo[j] < 27 * C0_OUT) {
-        int ci = otap[j] / 9, rc = otap[j] - ci * 9;
-        int r = rc / 3, c = rc - r * 3;
-        const float* xin = &s_in[(ci * 3 + r) * C0_IN_W + c];
-        float s = 0.f;
-        for (int p = 0; p < npx; ++p) s = fmaf(s_dz[p * 33 + oco[j]], xin[2 * p], s);
-        acc[j] += s;
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int seg = (int)(t % segs);
+    const long long row = t / segs;  // n * Ho + ho
+    const int n = (int)(row / a.Ho), ho = (int)(row - (long long)n * a.Ho);
+    const int wo0 = seg * CW_TP;
+    const int npx = min(CW_TP, a.Wo - wo0);
+    // ---- global loads first (registers), then one barrier, then LDS writes -----------------
+    // X^T: thread = pixel p, 27 taps
+    float xv[27];
+    {
+      const int p = tid;
+      const bool ok = p < npx;
+#pragma unroll
+      for (int cr = 0; cr < 9; ++cr) {
+        const int ci = cr / 3, kh = cr - ci * 3;
+        const size_t base = ((size_t)n * 3 + ci) * HW + (size_t)(2 * ho + kh) * a.W + 2 * (wo0 + p);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          float v = 0.f;
+          if (ok) v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[base + kw]) : ((const float*)a.x)[base + kw];
+          xv[cr * 3 + kw] = v;
+        }
       }
     }
-  }
-  size_t pi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    // dZ tile: npx*32 contiguous elements as 16-B vectors (V elements), transposed into sD
+    constexpr int NV = CW_TP * 32 / V / 256;  // vectors per thread (4 bf16 / 8 f32)
+    uint4 dv[NV];
+    const T* dz = (const T*)a.dz + ((size_t)row * a.Wo + wo0) * 32;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (oo[j] < 27 * C0_OUT) a.slab[pi * 864 + oo[j]] = acc[j];
+    for (int q = 0; q < NV; ++q) {
+      const int i = tid + 256 * q;
+      const int p = (i * V) >> 5;
+      dv[q] = p < npx ? *reinterpret_cast<const uint4*>(dz + (size_t)i * V) : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();  // previous tile's MFMA reads are done
+#pragma unroll
+    for (int k = 0; k < 27; ++k) sX[k * LD + tid] = cw_cvt<T>(xv[k]);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int i = tid + 256 * q;
+      const int p = (i * V) >> 5, c0 = (i * V) & 31;
+      const T* e = reinterpret_cast<const T*>(&dv[q]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) sD[(c0 + j) * LD + p] = e[j];
+    }
+    __syncthreads();
+    // ---- MFMA: wave's 64 pixels, 2 steps of 32 ------------------------------------------------
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kb = wave * 64 + ks * 32 + 8 * lq;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          CwOps<T>::mma(&sX[(16 * i + li) * LD + kb], &sD[(16 * j + li) * LD + kb], acc[i][j]);
+    }
+  }
+  // ---- sum the 4 waves' 32x32 accumulators; acc[i][j][r] = dW^T[16i + 4lq + r][16j + li] -----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(s_raw);  // [4 waves][32 tap][32 co]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave * 1024 + (16 * i + 4 * lq + r) * 32 + 16 * j + li] = acc[i][j][r];
+  __syncthreads();
+  float* out = a.slab + (size_t)blockIdx.x * 864;
+  for (int o = tid; o < 864; o += 256) {
+    const int co = o / 27, tap = o - co * 27;
+    const int k = tap * 32 + co;
+    out[o] = (red[k] + red[1024 + k]) + (red[2048 + k] + red[3072 + k]);
+  }
 }
 
-int conv0_wgrad_parts(int N, int Ho, int Wo, int rows_per_block) {
-  return cdiv(N * Ho, rows_per_block) * cdiv(Wo, C0_TILE);
+int conv0_wgrad_parts(int N, int Ho, int Wo, int) {
+  const long long tiles = (long long)N * Ho * cdiv(Wo, CW_TP);
+  return (int)(tiles < CW_MAXP ? tiles : CW_MAXP);
 }
 
 int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
-  dim3 grid(cdiv(a.Wo, C0_TILE), cdiv(a.N * a.Ho, a.rows_per_block));
+  const int P = conv0_wgrad_parts(a.N, a.Ho, a.Wo, 0);
+  if ((uintptr_t)a.dz % 16) {
+    set_error("conv0_wgrad: dZ must be 16-B aligned");
+    return E_INVALID;
+  }
+  const double px = (double)a.N * a.Ho * a.Wo;
+  ProfScope ps(PK_CONV0_WGRAD, st,
+               (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (dz_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
+               2.0 * 27 * 32 * px);
   if (dz_dtype == DT_F32)
-    conv0_wgrad_kernel<float><<<grid, 256, 0, st>>>(a);
+    conv0_wgrad_kernel<float><<<P, 256, 0, st>>>(a);
   else
-    conv0_wgrad_kernel<bf16><<<grid, 256, 0, st>>>(a);
+    conv0_wgrad_kernel<bf16><<<P, 256, 0, st>>>(a);
   return check_launch("conv0_wgrad");
 }
 

@@ -89,7 +89,8 @@ int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const fl
                         int stage_from, int stage_to, void* stream);
 
 /* ---- launch profiler (bench.py roofline) --------------------------------------------------
- * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 9 upsample.
+ * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 9 upsample,
+ * 11 cross_entropy / fused loss head, 12 conv0_wgrad.
  * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
  * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes
  * and flops of those launches (SURVEY.md §8(d) formulas). */
@@ -113,6 +114,11 @@ int fscnn_sgd(float* p, const float* g, float* buf, long long n, float lr, float
 int fscnn_conv0_fwd(const void* x, int x_dtype, int N, int H, int W, const float* w,
                     const float* scale, const float* shift, int relu, void* y, int y_dtype,
                     void* stream);
+/* dW [32][3][3][3] of the first conv from the NCHW image and NHWC dZ [N][Ho][Wo][32]
+ * (autograd of models/fast_scnn.py:153); slab: fscnn_conv0_wgrad_slab_floats floats */
+long long fscnn_conv0_wgrad_slab_floats(int N, int H, int W);
+int fscnn_conv0_wgrad(const void* x, int x_dtype, int N, int H, int W, const void* dz,
+                      int dz_dtype, float* slab, float* dw, void* stream);
 int fscnn_dw3x3_fwd(const void* x, int dtype, int N, int H, int W, int C, int stride,
                     const float* w, const float* scale, const float* shift, int relu, void* y,
                     void* stream);

@@ -64,6 +64,27 @@ def test_conv0_fwd(dt, shape):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 67, 131), (1, 128, 256), (3, 33, 1100), (2, 9, 8)])
+def test_conv0_wgrad(dt, shape):
+    """MFMA wgrad of the first conv (K = pixels, tiles of 256, tails and multi-segment rows)."""
+    N, H, W = shape
+    Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+    x = rnd(N, 3, H, W, seed=11).to(dt)
+    gz = rnd(N, 32, Ho, Wo, seed=12).to(dt)
+    xq = x.float().clone()
+    wq = torch.zeros(32, 3, 3, 3, requires_grad=True)
+    F.conv2d(xq, wq, stride=2).backward(gz.float())
+    xd, gzd = x.to(DEV).contiguous(), nhwc(gz).to(DEV)
+    slab = torch.empty(_lib.load().fscnn_conv0_wgrad_slab_floats(N, H, W), device=DEV)
+    dw = torch.empty(32, 3, 3, 3, device=DEV)
+    _lib.call("fscnn_conv0_wgrad", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, _lib.ptr(gzd),
+              _lib.dtype_code(dt), _lib.ptr(slab), _lib.ptr(dw), S())
+    sync()
+    # operands are exactly representable in dt; only the fp32 summation order differs
+    close(dw, wq.grad, 1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("N,H,W,C,s", [(2, 17, 23, 32, 1), (2, 17, 23, 48, 2), (1, 64, 128, 384, 2),
                                        (2, 32, 64, 576, 1), (1, 31, 63, 768, 1), (2, 16, 32, 128, 1)])
 def test_dw3x3_fwd_bwd(dt, N, H, W, C, s):
