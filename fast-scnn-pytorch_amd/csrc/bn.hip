@@ -37,52 +37,127 @@ int bn_fold(const FoldTable& t, hipStream_t st) {
 }
 
 // ---- train: merge partial records ------------------------------------------------------------
+// Two coalesced levels, in place (the records are consumed):
+//   fold : workgroup (64-channel chunk, q) — thread (c, ty) merges records p = q + Q*(ty + 4k),
+//          i.e. every record of residue class q mod Q, which no other thread touches; the 4 ty
+//          partials are merged in fixed order and the result overwrites record slot q.
+//   final: workgroup per 64-channel chunk merges slots 0..Q-1 (fixed order) and finishes.
+// Merges run in fp64 on (n, n*mean, M2 + n*mean^2) sums; lanes walk channels, so every record
+// row is read as contiguous 256-B segments.
+constexpr int BN_Q = 64;
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a) {
-  const int c = blockIdx.x;
-  __shared__ double sn[256], sm[256], s2[256];
-  Welford w = {0.0, 0.0, 0.0};
-  for (int p = threadIdx.x; p < a.P; p += 256) {
-    const float* rec = a.part + (size_t)p * 3 * a.C;
-    Welford b = {(double)rec[2 * a.C + c], (double)rec[c], (double)rec[a.C + c]};
-    if (b.n > 0) w = wf_merge(w, b);
-  }
-  sn[threadIdx.x] = w.n;
-  sm[threadIdx.x] = w.mean;
-  s2[threadIdx.x] = w.m2;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) {
-      Welford x = {sn[threadIdx.x], sm[threadIdx.x], s2[threadIdx.x]};
-      Welford y = {sn[threadIdx.x + off], sm[threadIdx.x + off], s2[threadIdx.x + off]};
-      Welford z = (y.n > 0) ? wf_merge(x, y) : x;
-      sn[threadIdx.x] = z.n;
-      sm[threadIdx.x] = z.mean;
-      s2[threadIdx.x] = z.m2;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    double n = sn[0], mean = sm[0] + (a.bias ? (double)a.bias[c] : 0.0);
-    double var = n > 0 ? s2[0] / n : 0.0;
-    float invstd = (float)(1.0 / sqrt(var + (double)BN_EPS));
-    float scale = a.gamma[c] * invstd;
-    a.mean[c] = (float)mean;
-    a.invstd[c] = invstd;
-    a.scale[c] = scale;
-    a.shift[c] = a.beta[c] - (float)mean * scale;
-    if (a.rmean) {
-      float m = a.momentum;
-      a.rmean[c] = (1.f - m) * a.rmean[c] + m * (float)mean;
-      float unb = n > 1 ? (float)(s2[0] / (n - 1.0)) : (float)var;
-      a.rvar[c] = (1.f - m) * a.rvar[c] + m * unb;
-    }
-    if (a.nbt && c == 0) a.nbt[0] += 1;
+__device__ __forceinline__ void bn_sum3(double& n, double& s1, double& s2, const float* rec, int C,
+                                        int c) {
+  const double cn = rec[2 * C + c];
+  if (cn > 0.0) {
+    const double m = rec[c];
+    n += cn;
+    s1 += cn * m;
+    s2 += (double)rec[C + c] + cn * m * m;
   }
 }
 
+__global__ __launch_bounds__(256) void bn_stats_fold_kernel(float* part, int P, int C, int Q) {
+  __shared__ double sh[3][4][64];
+  const int cx = threadIdx.x, ty = threadIdx.y;
+  const int c = blockIdx.x * 64 + cx, q = blockIdx.y;
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    // batches of 8 records: all loads issued before the fp64 accumulation (no serialized trips)
+    for (int p0 = q + Q * ty; p0 < P; p0 += 32 * Q) {
+      float rm[8], r2[8], rn[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + 4 * Q * u;
+        const float* rec = part + (size_t)(p < P ? p : p0) * 3 * C;  // clamped + select
+        const float t0 = rec[c], t1 = rec[C + c], t2 = rec[2 * C + c];
+        rm[u] = p < P ? t0 : 0.f;
+        r2[u] = p < P ? t1 : 0.f;
+        rn[u] = p < P ? t2 : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double cn = rn[u];
+        if (cn > 0.0) {
+          const double m = rm[u];
+          n += cn;
+          s1 += cn * m;
+          s2 += (double)r2[u] + cn * m * m;
+        }
+      }
+    }
+  }
+  sh[0][ty][cx] = n;
+  sh[1][ty][cx] = s1;
+  sh[2][ty][cx] = s2;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    n = (sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx]);
+    s1 = (sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx]);
+    s2 = (sh[2][0][cx] + sh[2][1][cx]) + (sh[2][2][cx] + sh[2][3][cx]);
+    float* rec = part + (size_t)q * 3 * C;
+    const double mean = n > 0.0 ? s1 / n : 0.0;
+    rec[c] = (float)mean;
+    rec[C + c] = n > 0.0 ? (float)fmax(s2 - n * mean * mean, 0.0) : 0.f;
+    rec[2 * C + c] = (float)n;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
+  __shared__ Welford sh[4][64];
+  const int cx = threadIdx.x, ty = threadIdx.y;
+  const int c = blockIdx.x * 64 + cx;
+  Welford w = {0.0, 0.0, 0.0};
+  if (c < a.C) {
+    // Q <= BN_Q = 64: the thread's <= 16 records are loaded at once, then merged in order
+    float rm[BN_Q / 4], r2[BN_Q / 4], rn[BN_Q / 4];
+#pragma unroll
+    for (int u = 0; u < BN_Q / 4; ++u) {
+      const int q = ty + 4 * u;
+      const float* rec = a.part + (size_t)(q < Q ? q : 0) * 3 * a.C;  // clamped + select
+      const float t0 = rec[2 * a.C + c], t1 = rec[c], t2 = rec[a.C + c];
+      rn[u] = q < Q ? t0 : 0.f;
+      rm[u] = q < Q ? t1 : 0.f;
+      r2[u] = q < Q ? t2 : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < BN_Q / 4; ++u) {
+      Welford b = {(double)rn[u], (double)rm[u], (double)r2[u]};
+      if (b.n > 0) w = wf_merge(w, b);
+    }
+  }
+  sh[ty][cx] = w;
+  __syncthreads();
+  if (ty != 0 || c >= a.C) return;
+  w = wf_merge(wf_merge(sh[0][cx], sh[1][cx]), wf_merge(sh[2][cx], sh[3][cx]));
+  const double n = w.n, mean = w.mean + (a.bias ? (double)a.bias[c] : 0.0);
+  const double var = n > 0 ? w.m2 / n : 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)BN_EPS));
+  const float scale = a.gamma[c] * invstd;
+  a.mean[c] = (float)mean;
+  a.invstd[c] = invstd;
+  a.scale[c] = scale;
+  a.shift[c] = a.beta[c] - (float)mean * scale;
+  if (a.rmean) {
+    const float m = a.momentum;
+    a.rmean[c] = (1.f - m) * a.rmean[c] + m * (float)mean;
+    const float unb = n > 1 ? (float)(w.m2 / (n - 1.0)) : (float)var;
+    a.rvar[c] = (1.f - m) * a.rvar[c] + m * unb;
+  }
+  if (a.nbt && c == 0) a.nbt[0] += 1;
+}
+
 int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
-  bn_finalize_kernel<<<a.C, 256, 0, st>>>(a);
+  if (a.P <= 0 || a.C <= 0) {
+    set_error("bn_finalize: P=%d C=%d", a.P, a.C);
+    return E_INVALID;
+  }
+  int Q = a.P;
+  if (a.P > BN_Q) {
+    Q = BN_Q;
+    bn_stats_fold_kernel<<<dim3(cdiv(a.C, 64), Q), dim3(64, 4), 0, st>>>(a.part, a.P, a.C, Q);
+  }
+  bn_finalize_kernel<<<cdiv(a.C, 64), dim3(64, 4), 0, st>>>(a, Q);
   return check_launch("bn_finalize");
 }
 
@@ -101,7 +176,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnApplyArgs a) {
   float z[V], o[V];
   ldv((const T*)a.z + m * a.ldz + c, z);
 #pragma unroll
-  for (int j = 0; j < V; ++j) o[j] = z[j] * a.scale[c + j] + a.shift[c + j];
+  for (int j = 0; j < V; ++j) o[j] = fmaf(z[j], a.scale[c + j], a.shift[c + j]);  // == relu_z mask
   if (a.z2) {
     ldv((const T*)a.z2 + m * a.ldz2 + c, z);
 #pragma unroll
@@ -133,7 +208,10 @@ int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st) {
 // dy_r = dy * [mask > 0] (mask = the saved post-activation output, if the BN is followed by a
 // ReLU or the FFM's ReLU), xhat = (z - mean) * invstd.
 
-template <typename T>
+// MODE: 0 = no ReLU, 1 = mask tensor (y > 0), 2 = relu_z (mask recomputed from z).  The mode is
+// a template parameter and rows past the end are clamped + zero-weighted, so a batch's loads are
+// issued back to back with no branch (a branch between loads and use forces vmcnt(0) waits).
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int CV = a.C / V;
@@ -146,26 +224,41 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
   if (cv < CV) {
     const int c = cv * V;
-    float mu[V], is[V];
+    float mu[V], is[V], fs[V], fb[V];
 #pragma unroll
-    for (int j = 0; j < V; ++j) { mu[j] = a.mean[c + j]; is[j] = a.invstd[c + j]; }
-    long long mb = (long long)blockIdx.y * a.rows_per_block;
-    long long me = min(a.M, mb + a.rows_per_block);
-    for (long long m = mb + threadIdx.y; m < me; m += BY) {
-      float g[V], z[V];
-      ldv((const T*)a.dy + m * a.lddy + c, g);
-      if (a.mask) {
-        float mk[V];
-        ldv((const T*)a.mask + m * a.ldmask + c, mk);
-#pragma unroll
-        for (int j = 0; j < V; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
+    for (int j = 0; j < V; ++j) {
+      mu[j] = a.mean[c + j];
+      is[j] = a.invstd[c + j];
+      if (MODE == 2) {
+        fs[j] = a.scale[c + j];
+        fb[j] = a.shift[c + j];
       }
-      ldv((const T*)a.z + m * a.ldz + c, z);
+    }
+    const long long mb = (long long)blockIdx.y * a.rows_per_block;
+    const long long me = min(a.M, mb + a.rows_per_block);
+    constexpr int U = 4;
+    for (long long m0 = mb + threadIdx.y; m0 < me; m0 += U * BY) {
+      float g[U][V], z[U][V], mk[U][V];
+      float ok[U];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        s1[j] += g[j];
-        s2[j] += g[j] * (z[j] - mu[j]) * is[j];
+      for (int u = 0; u < U; ++u) {
+        const long long mr = m0 + (long long)u * BY;
+        ok[u] = mr < me ? 1.f : 0.f;
+        const long long m = mr < me ? mr : me - 1;
+        ldv((const T*)a.dy + m * a.lddy + c, g[u]);
+        ldv((const T*)a.z + m * a.ldz + c, z[u]);
+        if (MODE == 1) ldv((const T*)a.mask + m * a.ldmask + c, mk[u]);
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          float gv = g[u][j] * ok[u];
+          if (MODE == 1) gv = mk[u][j] > 0.f ? gv : 0.f;
+          if (MODE == 2) gv = fmaf(z[u][j], fs[j], fb[j]) > 0.f ? gv : 0.f;
+          s1[j] += gv;
+          s2[j] += gv * (z[u][j] - mu[j]) * is[j];
+        }
     }
   }
 #pragma unroll
@@ -216,49 +309,99 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
   b.rows_per_block = rpb;
   dim3 grid(cdiv(a.C / V, bx), P), block(bx, by);
   size_t shm = (size_t)bx * by * V * 2 * sizeof(float);
-  if (dtype == DT_F32) bn_bwd_reduce_kernel<float><<<grid, block, shm, st>>>(b);
-  else bn_bwd_reduce_kernel<bf16><<<grid, block, shm, st>>>(b);
+  const int mode = b.relu_z ? 2 : (b.mask ? 1 : 0);
+#define BN_RED(T, M) bn_bwd_reduce_kernel<T, M><<<grid, block, shm, st>>>(b)
+  if (dtype == DT_F32) {
+    if (mode == 0) BN_RED(float, 0); else if (mode == 1) BN_RED(float, 1); else BN_RED(float, 2);
+  } else {
+    if (mode == 0) BN_RED(bf16, 0); else if (mode == 1) BN_RED(bf16, 1); else BN_RED(bf16, 2);
+  }
+#undef BN_RED
   return check_launch("bn_bwd_reduce");
 }
 
-// merge [P][2][C] -> dgamma, dbeta (written to the gradient arena) and coef [2][C];
-// one workgroup per channel, fixed-order strided partial sums + tree (deterministic)
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* part, int P, int C,
-                                                              double count, float* dgamma,
-                                                              float* dbeta, float* coef) {
-  const int c = blockIdx.x;
-  __shared__ double r1[256], r2[256];
+// merge [P][2][C] -> dgamma, dbeta (written to the gradient arena) and coef [2][C]; same
+// two-level in-place scheme as bn_finalize (fold residue classes mod Q, then fixed-order merge)
+__global__ __launch_bounds__(256) void bn_bwd_fold_kernel(float* part, int P, int C, int Q) {
+  __shared__ double sh[2][4][64];
+  const int cx = threadIdx.x, ty = threadIdx.y;
+  const int c = blockIdx.x * 64 + cx, q = blockIdx.y;
   double s1 = 0.0, s2 = 0.0;
-  for (int p = threadIdx.x; p < P; p += 256) {
-    s1 += part[(size_t)p * 2 * C + c];
-    s2 += part[(size_t)p * 2 * C + C + c];
-  }
-  r1[threadIdx.x] = s1;
-  r2[threadIdx.x] = s2;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) {
-      r1[threadIdx.x] += r1[threadIdx.x + off];
-      r2[threadIdx.x] += r2[threadIdx.x + off];
+  if (c < C)
+    for (int p0 = q + Q * ty; p0 < P; p0 += 32 * Q) {
+      float a1[8], a2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + 4 * Q * u;
+        const size_t pc = (size_t)(p < P ? p : p0) * 2 * C;  // clamped + select
+        const float t1 = part[pc + c], t2 = part[pc + C + c];
+        a1[u] = p < P ? t1 : 0.f;
+        a2[u] = p < P ? t2 : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s1 += a1[u];
+        s2 += a2[u];
+      }
     }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    if (dbeta) dbeta[c] = (float)r1[0];
-    if (dgamma) dgamma[c] = (float)r2[0];
-    coef[c] = (float)(r1[0] / count);
-    coef[C + c] = (float)(r2[0] / count);
+  sh[0][ty][cx] = s1;
+  sh[1][ty][cx] = s2;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    part[(size_t)q * 2 * C + c] = (float)((sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx]));
+    part[(size_t)q * 2 * C + C + c] =
+        (float)((sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx]));
   }
 }
 
-int bn_bwd_finalize(const float* part, int P, int C, double count, float* dgamma, float* dbeta,
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* part, int Q, int C,
+                                                              double count, float* dgamma,
+                                                              float* dbeta, float* coef) {
+  __shared__ double sh[2][4][64];
+  const int cx = threadIdx.x, ty = threadIdx.y;
+  const int c = blockIdx.x * 64 + cx;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    float a1[BN_Q / 4], a2[BN_Q / 4];
+#pragma unroll
+    for (int u = 0; u < BN_Q / 4; ++u) {
+      const int q = ty + 4 * u;
+      const size_t qc = (size_t)(q < Q ? q : 0) * 2 * C;  // clamped + select
+      const float t1 = part[qc + c], t2 = part[qc + C + c];
+      a1[u] = q < Q ? t1 : 0.f;
+      a2[u] = q < Q ? t2 : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < BN_Q / 4; ++u) {
+      s1 += a1[u];
+      s2 += a2[u];
+    }
+  }
+  sh[0][ty][cx] = s1;
+  sh[1][ty][cx] = s2;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  s1 = (sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx]);
+  s2 = (sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx]);
+  if (dbeta) dbeta[c] = (float)s1;
+  if (dgamma) dgamma[c] = (float)s2;
+  coef[c] = (float)(s1 / count);
+  coef[C + c] = (float)(s2 / count);
+}
+
+int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
                     float* coef, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<C, 256, 0, st>>>(part, P, C, count, dgamma, dbeta, coef);
+  int Q = P;
+  if (P > BN_Q) {
+    Q = BN_Q;
+    bn_bwd_fold_kernel<<<dim3(cdiv(C, 64), Q), dim3(64, 4), 0, st>>>(part, P, C, Q);
+  }
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), dim3(64, 4), 0, st>>>(part, Q, C, count, dgamma, dbeta, coef);
   return check_launch("bn_bwd_finalize");
 }
 
 // dz = scale * (dy_r - coef0 - xhat * coef1)   (train);  dz = scale * dy_r (eval: coef null)
-template <typename T>
+template <typename T, int MODE, bool TRAIN>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int CV = a.C / V;
@@ -268,34 +411,45 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const unsigned mu = i / (unsigned)CV;
   const int c = (int)(i - mu * (unsigned)CV) * V;
   const long long m = mu;
-  float g[V], z[V], o[V];
+  float g[V], z[V], mk[V], o[V];
   ldv((const T*)a.dy + m * a.lddy + c, g);
-  if (a.mask) {
-    float mk[V];
-    ldv((const T*)a.mask + m * a.ldmask + c, mk);
+  if (TRAIN || MODE == 2) ldv((const T*)a.z + m * a.ldz + c, z);
+  if (MODE == 1) ldv((const T*)a.mask + m * a.ldmask + c, mk);
 #pragma unroll
-    for (int j = 0; j < V; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
-  }
-  if (a.coef) {
-    ldv((const T*)a.z + m * a.ldz + c, z);
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      float xh = (z[j] - a.mean[c + j]) * a.invstd[c + j];
-      o[j] = a.scale[c + j] * (g[j] - a.coef[c + j] - xh * a.coef[a.C + c + j]);
+  for (int j = 0; j < V; ++j) {
+    float gv = g[j];
+    if (MODE == 1) gv = mk[j] > 0.f ? gv : 0.f;
+    if (MODE == 2) gv = fmaf(z[j], a.scale[c + j], a.shift[c + j]) > 0.f ? gv : 0.f;
+    if (TRAIN) {
+      const float xh = (z[j] - a.mean[c + j]) * a.invstd[c + j];
+      o[j] = a.scale[c + j] * (gv - a.coef[c + j] - xh * a.coef[a.C + c + j]);
+    } else {
+      o[j] = a.scale[c + j] * gv;
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = a.scale[c + j] * g[j];
   }
   stv((T*)a.dz + m * a.lddz + c, o);
+}
+
+template <typename T>
+static void bn_bwd_apply_launch(const BnBwdArgs& a, unsigned grid, hipStream_t st) {
+  const int mode = a.relu_z ? 2 : (a.mask ? 1 : 0);
+  if (a.coef) {
+    if (mode == 0) bn_bwd_apply_kernel<T, 0, true><<<grid, 256, 0, st>>>(a);
+    else if (mode == 1) bn_bwd_apply_kernel<T, 1, true><<<grid, 256, 0, st>>>(a);
+    else bn_bwd_apply_kernel<T, 2, true><<<grid, 256, 0, st>>>(a);
+  } else {
+    if (mode == 0) bn_bwd_apply_kernel<T, 0, false><<<grid, 256, 0, st>>>(a);
+    else if (mode == 1) bn_bwd_apply_kernel<T, 1, false><<<grid, 256, 0, st>>>(a);
+    else bn_bwd_apply_kernel<T, 2, false><<<grid, 256, 0, st>>>(a);
+  }
 }
 
 int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
   int V = dtype == DT_F32 ? 4 : 8;
   long long total = a.M * (a.C / V);
   unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) bn_bwd_apply_kernel<float><<<grid, 256, 0, st>>>(a);
-  else bn_bwd_apply_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) bn_bwd_apply_launch<float>(a, grid, st);
+  else bn_bwd_apply_launch<bf16>(a, grid, st);
   return check_launch("bn_bwd_apply");
 }
 

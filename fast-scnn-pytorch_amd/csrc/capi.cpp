@@ -364,7 +364,7 @@ int fscnn_pw_wgrad(int M, int N, int K, const void* D, int ldd, const void* X, i
   return reduce_slabs(slab, s, (long long)N * K, (long long)N * K, dW, 0, S(stream));
 }
 
-int fscnn_bn_finalize(const float* part, int P, int C, const float* gamma, const float* beta,
+int fscnn_bn_finalize(float* part, int P, int C, const float* gamma, const float* beta,
                       float* rmean, float* rvar, long long* nbt, float momentum, float* mean,
                       float* invstd, float* scale, float* shift, void* stream) {
   BnFinalizeArgs a{};

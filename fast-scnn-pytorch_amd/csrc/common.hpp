@@ -65,6 +65,23 @@ __device__ __forceinline__ void stv(bf16* p, const float (&v)[8]) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// raw 16-B vector in storage type -> floats (for code that keeps loads packed until use)
+__device__ __forceinline__ void unpackv(const uint4& t, float (&v)[4]) {
+  v[0] = __uint_as_float(t.x); v[1] = __uint_as_float(t.y);
+  v[2] = __uint_as_float(t.z); v[3] = __uint_as_float(t.w);
+}
+__device__ __forceinline__ void unpackv(const uint4& t, float (&v)[8]) {
+  const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+__device__ __forceinline__ uint4 sel4(bool ok, const uint4& t) {
+  return ok ? t : make_uint4(0u, 0u, 0u, 0u);
+}
+
 // ---- Chan parallel merge of (count, mean, M2) ------------------------------------------------
 struct Welford {
   double n, mean, m2;

@@ -39,12 +39,10 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   for (int i = tid; i < 9 * C0_IN_W; i += 256) {
     int cr = i / C0_IN_W, c = i - cr * C0_IN_W;  // cr = ci*3 + r
     int ci = cr / 3, r = cr - ci * 3;
-    float v = 0.f;
-    if (c < ncol) {
-      size_t off = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c;
-      v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[off]) : ((const float*)a.x)[off];
-    }
-    s_in[i] = v;
+    const bool ok = c < ncol;  // clamped load + select (branch-free)
+    const size_t off = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + (ok ? c : 0);
+    const float v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[off]) : ((const float*)a.x)[off];
+    s_in[i] = ok ? v : 0.f;
   }
   __syncthreads();
 
@@ -244,9 +242,9 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
         const size_t base = ((size_t)n * 3 + ci) * HW + (size_t)(2 * ho + kh) * a.W + 2 * (wo0 + p);
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
-          float v = 0.f;
-          if (ok) v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[base + kw]) : ((const float*)a.x)[base + kw];
-          xv[cr * 3 + kw] = v;
+          const size_t o = ok ? base + kw : 0;  // clamped load + select (branch-free)
+          const float v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[o]) : ((const float*)a.x)[o];
+          xv[cr * 3 + kw] = ok ? v : 0.f;
         }
       }
     }
@@ -258,7 +256,7 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
     for (int q = 0; q < NV; ++q) {
       const int i = tid + 256 * q;
       const int p = (i * V) >> 5;
-      dv[q] = p < npx ? *reinterpret_cast<const uint4*>(dz + (size_t)i * V) : make_uint4(0, 0, 0, 0);
+      dv[q] = sel4(p < npx, *reinterpret_cast<const uint4*>(dz + (size_t)(p < npx ? i : 0) * V));
     }
     __syncthreads();  // previous tile's MFMA reads are done
 #pragma unroll

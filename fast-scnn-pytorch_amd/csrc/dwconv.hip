@@ -32,6 +32,21 @@ __host__ __device__ inline void dw_block_shape(int C, int V, int& bx, int& by) {
 struct DwGeom {
   int gx, gy, gz;  // channel chunks, column tiles, row bands
 };
+
+// XCD-contiguous tile order (speed only): blocks L = x (mod 8) share an XCD, so residue class x
+// gets the contiguous logical range [x*T/8, (x+1)*T/8) of (chunk, column tile, band) in
+// chunk-fastest order — vertically adjacent bands then run on one XCD back to back and their
+// shared halo rows are served by its L2 instead of being fetched from HBM twice.
+__device__ __forceinline__ void dw_tile(int& cx, int& cy, int& cz) {
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const long long T = (long long)gx * gy * gz;
+  long long L = blockIdx.x + (long long)gx * (blockIdx.y + (long long)gy * blockIdx.z);
+  if ((T & 7) == 0) L = (L & 7) * (T >> 3) + (L >> 3);
+  cx = (int)(L % gx);
+  const long long r = L / gx;
+  cy = (int)(r % gy);
+  cz = (int)(r / gy);
+}
 static DwGeom dw_geom(int N, int Ho, int Wo, int C, int V) {
   int bx, by;
   dw_block_shape(C, V, bx, by);
@@ -51,12 +66,14 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   extern __shared__ float s_red[];         // [by][bx*V] (train statistics)
   __shared__ float s_cnt[256];
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
-  const int cv = blockIdx.x * BX + tx;
+  int bx, by, bz;
+  dw_tile(bx, by, bz);
+  const int cv = bx * BX + tx;
   const int CV = a.C / V;
   const int nb = (a.Ho + DW_HS - 1) / DW_HS;
-  const int n = blockIdx.z / nb;
-  const int ho0 = (blockIdx.z - n * nb) * DW_HS;
-  const int wo0 = (blockIdx.y * BY + ty) * DW_WS;
+  const int n = bz / nb;
+  const int ho0 = (bz - n * nb) * DW_HS;
+  const int wo0 = (by * BY + ty) * DW_WS;
   const int nrow = min(DW_HS, a.Ho - ho0);
   const int ncol = wo0 < a.Wo ? min(DW_WS, a.Wo - wo0) : 0;
   const bool active = cv < CV && ncol > 0;
@@ -77,17 +94,21 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
       for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = wp[j * 9 + t];
     const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.C + (size_t)cv * V;
     const int hi0 = ho0 * S - 1, wi0 = wo0 * S - 1;
+    // branch-free: out-of-image taps load a clamped in-bounds vector and are zeroed by select,
+    // so the loads issue back to back (a branch around a load forces vmcnt(0) at the join)
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
       const int hi = hi0 + rr;
-      if (hi < 0 || hi >= a.H) continue;
-      const T* xr = xb + (size_t)hi * a.W * a.C;
+      const bool rok = hi >= 0 && hi < a.H;
+      const T* xr = xb + (size_t)(rok ? hi : 0) * a.W * a.C;
 #pragma unroll
       for (int ci = 0; ci < NC; ++ci) {
         const int wi = wi0 + ci;
-        if (wi < 0 || wi >= a.W) continue;
+        const bool ok = rok && wi >= 0 && wi < a.W;
         float v[V];
-        ldv(xr + (size_t)wi * a.C, v);
+        ldv(xr + (size_t)(ok ? wi : 0) * a.C, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] = ok ? v[j] : 0.f;
 #pragma unroll
         for (int r = 0; r < DW_HS; ++r) {
           const int kh = rr - r * S;
@@ -165,7 +186,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   }
   __syncthreads();
   if (ty == 0 && cv < CV) {
-    float* rec = a.part + ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * 3 * a.C;
+    float* rec = a.part + ((size_t)bz * gridDim.y + by) * 3 * a.C;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       float m2 = 0.f;
@@ -226,12 +247,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
-  const int cv = blockIdx.x * BX + tx;
+  int bx, by, bz;
+  dw_tile(bx, by, bz);
+  const int cv = bx * BX + tx;
   const int CV = a.C / V;
   const int nb = (a.H + 1) / 2;
-  const int n = blockIdx.z / nb;
-  const int h0 = (blockIdx.z - n * nb) * 2;
-  const int w0 = (blockIdx.y * BY + ty) * 4;
+  const int n = bz / nb;
+  const int h0 = (bz - n * nb) * 2;
+  const int w0 = (by * BY + ty) * 4;
   if (cv >= CV || w0 >= a.W) return;
   float wt[9][V];
   const float* wp = a.w + (size_t)cv * V * 9;
@@ -251,13 +274,14 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
 #pragma unroll
   for (int dr = 0; dr < 2; ++dr) {       // dy rows hb, hb+1
     const int ho = hb + dr;
-    if (ho >= a.Ho) continue;
 #pragma unroll
     for (int dc = 0; dc < 3; ++dc) {     // dy cols wb, wb+1, wb+2
       const int wo = wb + dc;
-      if (wo >= a.Wo) continue;
+      const bool ok = ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
       float g[V];
-      ldv(gb + ((size_t)ho * a.Wo + wo) * a.C, g);
+      ldv(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * a.C, g);
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[j] = ok ? g[j] : 0.f;
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         // dx row h0+r reads dy row ho with kh = (h0 + r) + 1 - 2*ho
@@ -320,39 +344,58 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(DwBwdArgs a, int gy, int 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[t][j] = 0.f;
+  // part p walks the contiguous tile range [p*T/P, (p+1)*T/P): consecutive bands, so the halo
+  // rows it re-reads are its own recent loads (L1/L2 hits)
   const int ntiles = gy * gz;
-  for (int tile = blockIdx.y; cv < CV && tile < ntiles; tile += gridDim.y) {
+  const int t_lo = (int)((long long)ntiles * blockIdx.y / gridDim.y);
+  const int t_hi = (int)((long long)ntiles * (blockIdx.y + 1) / gridDim.y);
+  for (int tile = t_lo; cv < CV && tile < t_hi; ++tile) {
     const int tz = tile / gy, tyy = tile - tz * gy;
     const int n = tz / nb;
     const int ho0 = (tz - n * nb) * DW_HS;
     const int wo0 = (tyy * BY + ty) * DW_WS;
     if (wo0 >= a.Wo) continue;
     const int nrow = min(DW_HS, a.Ho - ho0), ncol = min(DW_WS, a.Wo - wo0);
+    // dy tile (unpacked once) and the input rows as raw 16-B vectors, double-buffered: row rr+1's
+    // loads are in flight while row rr is consumed.  Clamped addresses + selects, no branches.
     float g[DW_HS][DW_WS][V];
     const T* gb = (const T*)a.dy + (((size_t)n * a.Ho + ho0) * a.Wo + wo0) * a.C + (size_t)cv * V;
+    {
+      uint4 graw[DW_HS][DW_WS];
 #pragma unroll
-    for (int r = 0; r < DW_HS; ++r)
+      for (int r = 0; r < DW_HS; ++r)
 #pragma unroll
-      for (int p = 0; p < DW_WS; ++p) {
-        if (r < nrow && p < ncol) ldv(gb + ((size_t)r * a.Wo + p) * a.C, g[r][p]);
-        else {
-#pragma unroll
-          for (int j = 0; j < V; ++j) g[r][p][j] = 0.f;
+        for (int p = 0; p < DW_WS; ++p) {
+          const bool ok = r < nrow && p < ncol;
+          graw[r][p] = sel4(ok, *reinterpret_cast<const uint4*>(gb + (ok ? (size_t)r * a.Wo + p : 0) * a.C));
         }
-      }
+#pragma unroll
+      for (int r = 0; r < DW_HS; ++r)
+#pragma unroll
+        for (int p = 0; p < DW_WS; ++p) unpackv(graw[r][p], g[r][p]);
+    }
     const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.C + (size_t)cv * V;
     const int hi0 = ho0 * S - 1, wi0 = wo0 * S - 1;
-#pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
+    uint4 xrow[2][NC];
+    auto load_row = [&](int rr, uint4 (&dst)[NC]) {
       const int hi = hi0 + rr;
-      if (hi < 0 || hi >= a.H) continue;
-      const T* xr = xb + (size_t)hi * a.W * a.C;
+      const bool rok = hi >= 0 && hi < a.H;
+      const T* xr = xb + (size_t)(rok ? hi : 0) * a.W * a.C;
 #pragma unroll
       for (int ci = 0; ci < NC; ++ci) {
         const int wi = wi0 + ci;
-        if (wi < 0 || wi >= a.W) continue;
+        const bool ok = rok && wi >= 0 && wi < a.W;
+        dst[ci] = sel4(ok, *reinterpret_cast<const uint4*>(xr + (size_t)(ok ? wi : 0) * a.C));
+      }
+    };
+    load_row(0, xrow[0]);
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      if (rr + 1 < NR) load_row(rr + 1, xrow[(rr + 1) & 1]);
+#pragma unroll
+      for (int ci = 0; ci < NC; ++ci) {
         float v[V];
-        ldv(xr + (size_t)wi * a.C, v);
+        unpackv(xrow[rr & 1][ci], v);
 #pragma unroll
         for (int r = 0; r < DW_HS; ++r) {
           const int kh = rr - r * S;

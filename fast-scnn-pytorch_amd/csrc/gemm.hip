@@ -52,19 +52,37 @@ struct MfmaOp<bf16> {
 
 template <typename T>
 __device__ __forceinline__ uint4 zero_tail(uint4 v, int valid) {
-  // zero the elements >= valid (valid in [0, V)) of a 16-B vector
+  // zero the elements >= valid of a 16-B vector (valid <= 0: all, valid >= V: none); selects only
   constexpr int V = VecW<T>::V;
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
   if (V == 4) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j >= valid) w[j] = 0;
+    for (int j = 0; j < 4; ++j) w[j] = j < valid ? w[j] : 0u;
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j >= valid) w[j >> 1] &= (j & 1) ? 0x0000FFFFu : 0xFFFF0000u;
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = (2 * j < valid) ? 0x0000FFFFu : 0u;
+      const uint32_t hi = (2 * j + 1 < valid) ? 0xFFFF0000u : 0u;
+      w[j] &= lo | hi;
+    }
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// XCD-aware block -> (major, minor) tile map.  Blocks b = x (mod 8) run on one XCD (observed
+// round-robin placement; speed only, never correctness): give each residue class whole major
+// indices with all `minor` tiles consecutive, so the operand shared by the minor tiles (the A
+// row tile of gemm_nt, the D/X row split of gemm_tn) is fetched into that XCD's L2 once.
+__device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& major, int& minor) {
+  if (nminor > 1 && (nmajor & 7) == 0) {
+    const int x = b & 7, j = b >> 3;
+    const int q = j / nminor;
+    major = q * 8 + x;
+    minor = j - q * nminor;
+  } else {
+    major = b % nmajor;
+    minor = b / nmajor;
+  }
 }
 
 template <typename T, int NT, bool BT>
@@ -72,15 +90,23 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
   constexpr int KC = G_VROW * V;  // k elements per chunk
-  __shared__ uint4 sA[2][G_BM * G_VPAD];
-  __shared__ uint4 sB[2][BN * G_VPAD];
+  constexpr int SA_BYTES = 2 * G_BM * G_VPAD * 16, SB_BYTES = 2 * BN * G_VPAD * 16;
+  constexpr int CLD = BN + 4;                       // epilogue tile row stride (floats)
+  constexpr int SC_BYTES = G_BM * CLD * 4;
+  constexpr int RAW = SA_BYTES + SB_BYTES > SC_BYTES ? SA_BYTES + SB_BYTES : SC_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[RAW];
+  uint4 (*sA)[G_BM * G_VPAD] = reinterpret_cast<uint4 (*)[G_BM * G_VPAD]>(s_raw);
+  uint4 (*sB)[BN * G_VPAD] = reinterpret_cast<uint4 (*)[BN * G_VPAD]>(s_raw + SA_BYTES);
+  float* sC = reinterpret_cast<float*>(s_raw);      // after the main loop
   __shared__ float s_red[4][BN];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int m0 = blockIdx.x * G_BM;
-  const int n0 = blockIdx.y * BN;
+  int tm, tn;
+  xcd_tile(blockIdx.x, cdiv(a.M, G_BM), cdiv(a.N, BN), tm, tn);
+  const int m0 = tm * G_BM;
+  const int n0 = tn * BN;
   const T* A = (const T*)a.A;
   const T* B = (const T*)a.B;
   const int nchunks = (a.K + KC - 1) / KC;
@@ -95,6 +121,9 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   constexpr int BT_PER = (BT_VEC + 255) / 256;
   uint4 rbt[BT ? BT_PER : 1];
 
+  // Branch-free loads: every lane loads from an in-bounds (clamped) address and invalid or tail
+  // elements are zeroed with selects afterwards, so all loads of a chunk issue back to back
+  // (a branch around a load makes hipcc wait vmcnt(0) at the join).
   auto load_chunk = [&](int c) {
     const int k0 = c * KC;
 #pragma unroll
@@ -102,12 +131,9 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
       int id = tid + 256 * i;
       int row = id >> 3, vv = id & 7;
       int m = m0 + row, k = k0 + vv * V;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (m < a.M && k < a.K) {
-        v = *reinterpret_cast<const uint4*>(A + (size_t)m * a.lda + k);
-        if (k + V > a.K) v = zero_tail<T>(v, a.K - k);
-      }
-      ra[i] = v;
+      const bool ok = m < a.M && k < a.K;
+      const size_t off = ok ? (size_t)m * a.lda + k : 0;
+      ra[i] = *reinterpret_cast<const uint4*>(A + off);
     }
     if (!BT) {
 #pragma unroll
@@ -115,12 +141,9 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
         int id = tid + 256 * i;
         int row = id >> 3, vv = id & 7;
         int n = n0 + row, k = k0 + vv * V;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (id < BN * G_VROW && n < a.N && k < a.K) {
-          v = *reinterpret_cast<const uint4*>(B + (size_t)n * a.ldb + k);
-          if (k + V > a.K) v = zero_tail<T>(v, a.K - k);
-        }
-        rb[i] = v;
+        const bool ok = id < BN * G_VROW && n < a.N && k < a.K;
+        const size_t off = ok ? (size_t)n * a.ldb + k : 0;
+        rb[i] = *reinterpret_cast<const uint4*>(B + off);
       }
     } else {
 #pragma unroll
@@ -128,12 +151,34 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
         int id = tid + 256 * i;
         int kk = id / (BN / V), nv = id - kk * (BN / V);
         int k = k0 + kk, n = n0 + nv * V;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (id < BT_VEC && k < a.K && n < a.N) {
-          v = *reinterpret_cast<const uint4*>(B + (size_t)k * a.ldb + n);
-          if (n + V > a.N) v = zero_tail<T>(v, a.N - n);
-        }
-        rbt[i] = v;
+        const bool ok = id < BT_VEC && k < a.K && n < a.N;
+        const size_t off = ok ? (size_t)k * a.ldb + n : 0;
+        rbt[i] = *reinterpret_cast<const uint4*>(B + off);
+      }
+    }
+    // masks (after all loads are in flight)
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int id = tid + 256 * i;
+      int row = id >> 3, vv = id & 7;
+      int m = m0 + row, k = k0 + vv * V;
+      ra[i] = zero_tail<T>(ra[i], m < a.M ? a.K - k : 0);
+    }
+    if (!BT) {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        int id = tid + 256 * i;
+        int row = id >> 3, vv = id & 7;
+        int n = n0 + row, k = k0 + vv * V;
+        rb[i] = zero_tail<T>(rb[i], (id < BN * G_VROW && n < a.N) ? a.K - k : 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BT_PER; ++i) {
+        int id = tid + 256 * i;
+        int kk = id / (BN / V), nv = id - kk * (BN / V);
+        int k = k0 + kk, n = n0 + nv * V;
+        rbt[i] = zero_tail<T>(rbt[i], (id < BT_VEC && k < a.K) ? a.N - n : 0);
       }
     }
   };
@@ -194,26 +239,68 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   }
 
   // ---- epilogue -------------------------------------------------------------------------------
-  T* Cp = (T*)a.C;
-  const T* Rp = (const T*)a.R;
+  // v = acc*scale + shift (registers; also feeds the statistics), staged through LDS as fp32 so
+  // the stores (and the residual loads) are whole 16-B vectors: all residual loads are issued
+  // before any store, no branches between them.
+  float scv[NT], shv[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int n = n0 + nt * 16 + li;
-    const bool nok = n < a.N;
-    const float sc = (nok && a.scale) ? a.scale[n] : 1.f;
-    const float sh = (nok && a.shift) ? a.shift[n] : 0.f;
+    const int nc = n < a.N ? n : 0;
+    scv[nt] = a.scale ? a.scale[nc] : 1.f;
+    shv[nt] = a.shift ? a.shift[nc] : 0.f;
+  }
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
-        float v = acc[mt][nt][r] * sc + sh;
-        if (nok && m < a.M) {
-          if (Rp) v += ld1(Rp + (size_t)m * a.ldr + n);
-          if (a.relu) v = fmaxf(v, 0.f);
-          st1(Cp + (size_t)m * a.ldc + n, v);
-        }
+        const float v = acc[mt][nt][r] * scv[nt] + shv[nt];
         acc[mt][nt][r] = v;
+        sC[(wave * 32 + mt * 16 + lq * 4 + r) * CLD + nt * 16 + li] = v;
+      }
+  __syncthreads();
+  {
+    T* Cp = (T*)a.C;
+    const T* Rp = (const T*)a.R;
+    constexpr int VPRow = BN / V;
+    constexpr int ITER = (G_BM * VPRow + 255) / 256;
+    float rv[ITER][V];
+    if (Rp) {
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int i = tid + 256 * it;
+        const int row = i / VPRow, vc = i - row * VPRow;
+        const int m = m0 + row, n = n0 + vc * V;
+        const bool ok = i < G_BM * VPRow && m < a.M && n + V <= a.N;
+        float t[V];
+        ldv(Rp + (ok ? (size_t)m * a.ldr + n : 0), t);
+#pragma unroll
+        for (int j = 0; j < V; ++j) rv[it][j] = ok ? t[j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int i = tid + 256 * it;
+      const int row = i / VPRow, vc = i - row * VPRow;
+      const int m = m0 + row, n = n0 + vc * V;
+      if (i >= G_BM * VPRow || m >= a.M) continue;
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float v = sC[row * CLD + vc * V + j];
+        if (Rp) v += rv[it][j];
+        o[j] = a.relu ? fmaxf(v, 0.f) : v;
+      }
+      if (n + V <= a.N) {
+        stv(Cp + (size_t)m * a.ldc + n, o);
+      } else {
+        for (int j = 0; j < V && n + j < a.N; ++j) {
+          float v = o[j];
+          if (Rp) v = sC[row * CLD + vc * V + j] + ld1(Rp + (size_t)m * a.ldr + n + j);
+          st1(Cp + (size_t)m * a.ldc + n + j, a.relu ? fmaxf(v, 0.f) : v);
+        }
       }
     }
   }
@@ -260,7 +347,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   }
   __syncthreads();
   if (wave == 0 && lq == 0) {
-    float* rec = a.part + (size_t)blockIdx.x * 3 * a.N;
+    float* rec = a.part + (size_t)tm * 3 * a.N;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       int col = nt * 16 + li, n = n0 + col;
@@ -285,7 +372,7 @@ int gemm_parts(int M) { return cdiv(M, G_BM); }
 
 template <typename T, bool BT>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
-  dim3 grid(cdiv(a.M, G_BM), cdiv(a.N, 16 * nt));
+  dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   switch (nt) {
     case 2: gemm_nt_kernel<T, 2, BT><<<grid, 256, 0, st>>>(a); break;
     case 3: gemm_nt_kernel<T, 3, BT><<<grid, 256, 0, st>>>(a); break;
@@ -329,22 +416,57 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
 // =============================================================================================
 
 constexpr int TN_T = 64;    // output tile 64 (n) x 64 (k)
-constexpr int TN_MC = 32;   // rows per staged chunk
-constexpr int TN_PAD = 8;   // elements of row padding in LDS
+constexpr int TN_MC = 64;   // rows (m) per staged chunk
 
+// MFMA over 32 consecutive m held as 8 per lane group (k-index = 8*lq + e, same in A and B)
+template <typename T>
+struct TnOps;
+template <>
+struct TnOps<float> {
+  static constexpr int LD = TN_MC + 4;
+  static __device__ __forceinline__ void mma(const float* a, const float* b, f32x4& acc) {
+    const float4 a0 = *reinterpret_cast<const float4*>(a), a1 = *reinterpret_cast<const float4*>(a + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(b), b1 = *reinterpret_cast<const float4*>(b + 4);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc, 0, 0, 0);
+  }
+};
+template <>
+struct TnOps<bf16> {
+  static constexpr int LD = TN_MC + 8;
+  static __device__ __forceinline__ void mma(const bf16* a, const bf16* b, f32x4& acc) {
+    i16x8 av, bv;
+    __builtin_memcpy(&av, a, 16);
+    __builtin_memcpy(&bv, b, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  }
+};
+
+// dW[n][k] = sum_m D[m][n] X[m][k] over the block's row split.  Chunks of 64 rows are loaded as
+// 16-B vectors along n / k (coalesced), written TRANSPOSED into LDS (sDt[n][m], sXt[k][m]) so each
+// MFMA operand is one or two 16-B ds_reads; the next chunk's global loads are issued before the
+// current chunk's MFMAs.
 template <typename T>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int V = VecW<T>::V;
-  constexpr int LDS_LD = TN_T + TN_PAD;
-  __shared__ __attribute__((aligned(16))) T sD[TN_MC * LDS_LD];
-  __shared__ __attribute__((aligned(16))) T sX[TN_MC * LDS_LD];
+  constexpr int LD = TnOps<T>::LD;
+  __shared__ __attribute__((aligned(16))) T sDt[TN_T * LD];
+  __shared__ __attribute__((aligned(16))) T sXt[TN_T * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int tiles_k = cdiv(a.K, TN_T);
-  const int tn = blockIdx.x / tiles_k, tk = blockIdx.x - tn * tiles_k;
+  int split, tile;
+  xcd_tile(blockIdx.x, a.splits, cdiv(a.N, TN_T) * tiles_k, split, tile);
+  const int tn = tile / tiles_k, tk = tile - tn * tiles_k;
   const int n0 = tn * TN_T, k0 = tk * TN_T;
   const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;  // wave sub-tile
-  const int mb = blockIdx.y * a.rows_per_split;
+  const int mb = split * a.rows_per_split;
   const int me = min(a.M, mb + a.rows_per_split);
   const T* D = (const T*)a.D;
   const T* X = (const T*)a.X;
@@ -355,78 +477,80 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // LDS element (n, m) lives at n*LD + swz(n, m): the 8-element m-groups are XOR-swizzled by
+  // n>>3 so the transposed pair writes below hit distinct banks; reads stay 16-B contiguous.
+  auto swz = [](int n, int m) { return ((((m >> 3) ^ (n >> 3)) & 7) << 3) + (m & 7); };
   constexpr int VPR = TN_T / V;                 // vectors per staged row
-  constexpr int PER = TN_MC * VPR / 256;        // vectors per thread per operand (2 f32 / 1 bf16)
+  constexpr int PAIRS = TN_MC / 2 * VPR / 256;  // row pairs per thread (1 bf16 / 2 f32)
+  uint4 rd[PAIRS][2], rx[PAIRS][2];
+  auto load = [&](int mc) {
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      const int id = tid + 256 * i;
+      const int rp = id / VPR, vv = id - rp * VPR;
+      const int n = n0 + vv * V, k = k0 + vv * V;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = mc + 2 * rp + h;
+        const bool okd = m < me && n < a.N, okx = m < me && k < a.K;
+        rd[i][h] = *reinterpret_cast<const uint4*>(D + (okd ? (size_t)m * a.ldd + n : 0));
+        rx[i][h] = *reinterpret_cast<const uint4*>(X + (okx ? (size_t)m * a.ldx + k : 0));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      const int id = tid + 256 * i;
+      const int rp = id / VPR, vv = id - rp * VPR;
+      const int n = n0 + vv * V, k = k0 + vv * V;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool okm = mc + 2 * rp + h < me;
+        rd[i][h] = zero_tail<T>(rd[i][h], okm ? a.N - n : 0);
+        rx[i][h] = zero_tail<T>(rx[i][h], okm ? a.K - k : 0);
+      }
+    }
+  };
+  using Pair = typename std::conditional<sizeof(T) == 2, uint32_t, uint2>::type;
+  if (mb < me) load(mb);
   for (int mc = mb; mc < me; mc += TN_MC) {
-    uint4 rd[PER], rx[PER];
+    __syncthreads();  // previous chunk's MFMA reads done
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int id = tid + 256 * i;
-      int r = id / VPR, vv = id - r * VPR;
-      int m = mc + r;
-      int n = n0 + vv * V, k = k0 + vv * V;
-      uint4 d = make_uint4(0, 0, 0, 0), x = make_uint4(0, 0, 0, 0);
-      if (m < me) {
-        if (n < a.N) {
-          d = *reinterpret_cast<const uint4*>(D + (size_t)m * a.ldd + n);
-          if (n + V > a.N) d = zero_tail<T>(d, a.N - n);
-        }
-        if (k < a.K) {
-          x = *reinterpret_cast<const uint4*>(X + (size_t)m * a.ldx + k);
-          if (k + V > a.K) x = zero_tail<T>(x, a.K - k);
-        }
+    for (int i = 0; i < PAIRS; ++i) {
+      const int id = tid + 256 * i;
+      const int rp = id / VPR, vv = id - rp * VPR;
+      const T* d0 = reinterpret_cast<const T*>(&rd[i][0]);
+      const T* d1 = reinterpret_cast<const T*>(&rd[i][1]);
+      const T* x0 = reinterpret_cast<const T*>(&rx[i][0]);
+      const T* x1 = reinterpret_cast<const T*>(&rx[i][1]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int n = vv * V + j;
+        const int off = n * LD + swz(n, 2 * rp);
+        Pair pd, px;
+        __builtin_memcpy(reinterpret_cast<T*>(&pd), d0 + j, sizeof(T));
+        __builtin_memcpy(reinterpret_cast<T*>(&pd) + 1, d1 + j, sizeof(T));
+        __builtin_memcpy(reinterpret_cast<T*>(&px), x0 + j, sizeof(T));
+        __builtin_memcpy(reinterpret_cast<T*>(&px) + 1, x1 + j, sizeof(T));
+        *reinterpret_cast<Pair*>(&sDt[off]) = pd;
+        *reinterpret_cast<Pair*>(&sXt[off]) = px;
       }
-      rd[i] = d;
-      rx[i] = x;
     }
     __syncthreads();
+    if (mc + TN_MC < me) load(mc + TN_MC);
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int id = tid + 256 * i;
-      int r = id / VPR, vv = id - r * VPR;
-      *reinterpret_cast<uint4*>(&sD[r * LDS_LD + vv * V]) = rd[i];
-      *reinterpret_cast<uint4*>(&sX[r * LDS_LD + vv * V]) = rx[i];
-    }
-    __syncthreads();
-    if constexpr (V == 4) {
-      // fp32: 8 steps of 16x16x4, step s covers rows 4s..4s+3 (row 4s+lq for this lane)
-#pragma unroll
-      for (int s = 0; s < TN_MC / 4; ++s) {
-        const int r = 4 * s + lq;
-        float av[2], bv[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) av[i] = sD[r * LDS_LD + wn + i * 16 + li];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bv[j] = sX[r * LDS_LD + wk + j * 16 + li];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
-    } else {
-      // bf16: one 16x16x32 step; lane needs rows 8*lq .. 8*lq+7 of its column
-      i16x8 av[2], bv[2];
-      const short* sd = reinterpret_cast<const short*>(sD);
-      const short* sx = reinterpret_cast<const short*>(sX);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = 8 * lq + j;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          av[i][j] = sd[r * LDS_LD + wn + i * 16 + li];
-          bv[i][j] = sx[r * LDS_LD + wk + i * 16 + li];
-        }
-      }
+    for (int ks = 0; ks < TN_MC / 32; ++ks) {
+      const int kb = ks * 32 + 8 * lq;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          const int na = wn + i * 16 + li, nb = wk + j * 16 + li;
+          TnOps<T>::mma(&sDt[na * LD + swz(na, kb)], &sXt[nb * LD + swz(nb, kb)], acc[i][j]);
+        }
     }
   }
   // write the block's partial tile: slab[split][n][k]; acc[i][j][r]: n = wn+i*16+lq*4+r, k = wk+j*16+li
-  float* sl = a.slab + (size_t)blockIdx.y * a.N * a.K;
+  float* sl = a.slab + (size_t)split * a.N * a.K;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -439,10 +563,12 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
 }
 
 int gemm_tn_splits(int M, int N, int K) {
+  // ~1024 workgroups; a multiple of 8 splits so xcd_tile keeps a split's tiles on one XCD
   int tiles = cdiv(N, TN_T) * cdiv(K, TN_T);
-  int s = 2048 / tiles;
-  int smax = cdiv(M, 256);
+  int s = 1024 / tiles;
+  int smax = cdiv(M, 4 * TN_MC);
   if (s > smax) s = smax;
+  if (s >= 8) s &= ~7;
   if (s < 1) s = 1;
   return s;
 }
@@ -454,7 +580,8 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
     return E_INVALID;
   }
   a.rows_per_split = cdiv(cdiv(a.M, splits), TN_MC) * TN_MC;
-  dim3 grid(cdiv(a.N, TN_T) * cdiv(a.K, TN_T), splits);
+  a.splits = splits;
+  dim3 grid(cdiv(a.N, TN_T) * cdiv(a.K, TN_T) * splits);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   ProfScope ps(PK_GEMM_TN, st, E * (M * N + M * K) + 4.0 * N * K, 2.0 * M * N * K);
@@ -475,7 +602,17 @@ __global__ void reduce_fold_kernel(float* slab, int S, int Q, long long stride, 
   int q = blockIdx.y;
   if (i >= count) return;
   float s = 0.f;
-  for (int k = q; k < S; k += Q) s += slab[(size_t)k * stride + i];
+  for (int k0 = q; k0 < S; k0 += 8 * Q) {  // 8 independent loads in flight per batch
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u * Q;
+      const float t = slab[(size_t)(k < S ? k : q) * stride + i];  // clamped: branch-free
+      v[u] = k < S ? t : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
   slab[(size_t)q * stride + i] = s;
 }
 
@@ -484,7 +621,16 @@ __global__ void reduce_final_kernel(const float* slab, int S, long long stride, 
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   float s = 0.f;
-  for (int k = 0; k < S; ++k) s += slab[(size_t)k * stride + i];
+  for (int k0 = 0; k0 < S; k0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float t = slab[(size_t)(k0 + u < S ? k0 + u : 0) * stride + i];
+      v[u] = k0 + u < S ? t : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
   int o = C9 ? (i % C9) * 9 + i / C9 : i;
   out[o] = accumulate ? out[o] + s : s;
 }
@@ -518,7 +664,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* D, int M, int N, i
   float s = 0.f;
   if (n < N) {
     int mb = blockIdx.y * rows_per_block, me = min(M, mb + rows_per_block);
-    for (int m = mb + g; m < me; m += 4) s += ld1(D + (size_t)m * ld + n);
+    for (int m0 = mb + g; m0 < me; m0 += 32) {  // 8 rows per batch, loads first
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int m = m0 + 4 * u;
+        const float t = ld1(D + (size_t)(m < me ? m : mb) * ld + n);
+        v[u] = m < me ? t : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
   }
   red[g][threadIdx.x & 63] = s;
   __syncthreads();

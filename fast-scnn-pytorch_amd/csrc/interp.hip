@@ -112,35 +112,55 @@ __device__ __forceinline__ int first_out_with_i0_ge(int i, int Lin, int Lout, fl
   return lo;
 }
 
+// grid: x = 256-thread chunks of the (o, x) positions of one input index, y = input index i.
+// The contributing output range [p_lo, p_hi) of index i is found once per workgroup.
 template <typename TG, typename TD>
 __global__ __launch_bounds__(256) void axis_bwd_kernel(AxisBwdArgs a) {
-  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = a.n_o1 * a.n_o2 * a.Lin * a.n_in;
-  if (t >= total) return;
-  long long x = t % a.n_in;
-  long long r = t / a.n_in;
-  int i = (int)(r % a.Lin);
-  long long o = r / a.Lin;
-  long long o2 = o % a.n_o2, o1 = o / a.n_o2;
+  __shared__ int s_rng[2];
+  const int i = blockIdx.y;
   const float sc = ac_scale(a.Lin, a.Lout);
-  // contributors: outputs p with i0(p) in {i-1, i}  (i1 = i0 or i0+1)
-  int p_lo = first_out_with_i0_ge(i - 1, a.Lin, a.Lout, sc);
-  int p_hi = first_out_with_i0_ge(i + 1, a.Lin, a.Lout, sc);
-  const TG* gb = (const TG*)a.g + o1 * a.g_s1 + o2 * a.g_s2 + x * a.g_in;
-  float s = 0.f;
-  for (int p = p_lo; p < p_hi; ++p) {
-    Lerp l = ac_lerp(p, a.Lin, a.Lout, sc);
-    float w = (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
-    s += w * ld1(gb + (size_t)p * a.g_idx);
+  if (threadIdx.x == 0) {
+    // contributors: outputs p with i0(p) in {i-1, i}  (i1 = i0 or i0+1)
+    s_rng[0] = first_out_with_i0_ge(i - 1, a.Lin, a.Lout, sc);
+    s_rng[1] = first_out_with_i0_ge(i + 1, a.Lin, a.Lout, sc);
   }
-  TD* dp = (TD*)a.d + o1 * a.d_s1 + o2 * a.d_s2 + (long long)i * a.d_idx + x * a.d_in;
+  __syncthreads();
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned n_o = (unsigned)(a.n_o1 * a.n_o2), n_in = (unsigned)a.n_in;
+  if (t >= n_o * n_in) return;
+  const unsigned o = t / n_in, x = t - o * n_in;
+  const unsigned o1 = o / (unsigned)a.n_o2, o2 = o - o1 * (unsigned)a.n_o2;
+  const int p_lo = s_rng[0], p_hi = s_rng[1];
+  const TG* gb = (const TG*)a.g + (long long)o1 * a.g_s1 + (long long)o2 * a.g_s2 + (long long)x * a.g_in;
+  float s = 0.f;
+  for (int p0 = p_lo; p0 < p_hi; p0 += 4) {  // 4 independent loads per batch
+    float gv[4], wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + u;
+      const bool ok = p < p_hi;  // clamped load + select (branch-free)
+      const Lerp l = ac_lerp(ok ? p : p0, a.Lin, a.Lout, sc);
+      const float w = (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
+      const float gvv = ld1(gb + (size_t)(ok ? p : p0) * a.g_idx);
+      wv[u] = ok ? w : 0.f;
+      gv[u] = ok ? gvv : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += wv[u] * gv[u];
+  }
+  TD* dp = (TD*)a.d + (long long)o1 * a.d_s1 + (long long)o2 * a.d_s2 + (long long)i * a.d_idx +
+           (long long)x * a.d_in;
   if (a.accumulate) s += ld1(dp);
   st1(dp, s);
 }
 
 int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st) {
-  long long total = a.n_o1 * a.n_o2 * a.Lin * a.n_in;
-  unsigned grid = (unsigned)((total + 255) / 256);
+  const long long per_i = a.n_o1 * a.n_o2 * a.n_in;
+  if (per_i >= (1LL << 31) || a.Lin > 65535) {
+    set_error("axis_bwd: problem too large (%lld per index, Lin %d)", per_i, a.Lin);
+    return E_UNSUPPORTED;
+  }
+  dim3 grid((unsigned)((per_i + 255) / 256), a.Lin);
   if (g_dtype == DT_F32 && d_dtype == DT_F32) axis_bwd_kernel<float, float><<<grid, 256, 0, st>>>(a);
   else if (g_dtype == DT_BF16 && d_dtype == DT_BF16) axis_bwd_kernel<bf16, bf16><<<grid, 256, 0, st>>>(a);
   else if (g_dtype == DT_BF16 && d_dtype == DT_F32) axis_bwd_kernel<bf16, float><<<grid, 256, 0, st>>>(a);
@@ -163,37 +183,71 @@ __host__ __device__ __forceinline__ int pp_start(int i, int in, int k) { return 
 __host__ __device__ __forceinline__ int pp_end(int i, int in, int k) { return ((i + 1) * in + k - 1) / k; }
 
 
-// one workgroup per (bin, image): 128 channel lanes x 4 row groups, fixed-order LDS combine
+// one workgroup per (bin, image): CV = C/V channel vectors x PG = 256/CV pixel groups; every
+// thread walks its pixels of the window with 8 vector loads in flight per batch; the pixel
+// groups are combined in fixed order through LDS.
 template <typename T>
-__global__ __launch_bounds__(512) void pyramid_pool_kernel(PoolArgs a) {
+__global__ __launch_bounds__(256) void pyramid_pool_kernel(PoolArgs a) {
+  constexpr int V = VecW<T>::V;
+  __shared__ float red[256 * V];
   const int b = blockIdx.x, n = blockIdx.y;
-  const int tx = threadIdx.x & 127, g = threadIdx.x >> 7;
-  __shared__ float red[4][128];
+  const int CV = a.C / V;
+  const int PG = 256 / CV;
+  const int cv = threadIdx.x % CV, g = threadIdx.x / CV;
   int k, bi, bj;
   pp_bin(b, k, bi, bj);
   const int h0 = pp_start(bi, a.H, k), h1 = pp_end(bi, a.H, k);
   const int w0 = pp_start(bj, a.W, k), w1 = pp_end(bj, a.W, k);
-  const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
-  const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.ldx;
-  for (int c0 = 0; c0 < a.C; c0 += 128) {
-    const int c = c0 + tx;
-    float s = 0.f;
-    if (c < a.C)
-      for (int h = h0 + g; h < h1; h += 4)
-        for (int w = w0; w < w1; ++w) s += ld1(xb + ((size_t)h * a.W + w) * a.ldx + c);
-    red[g][tx] = s;
-    __syncthreads();
-    if (g == 0 && c < a.C)
-      st1((T*)a.pooled + ((size_t)b * a.N + n) * a.C + c,
-          (red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]) * inv);
-    __syncthreads();
+  const int ww = w1 - w0, npx = (h1 - h0) * ww;
+  const float inv = 1.f / (float)npx;
+  const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.ldx + cv * V;
+  float s[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) s[j] = 0.f;
+  if (g < PG) {
+    for (int q0 = g; q0 < npx; q0 += 8 * PG) {
+      float v[8][V];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + u * PG;
+        const bool ok = q < npx;  // clamped load + select (branch-free)
+        const int qq = ok ? q : q0;
+        const int hh = qq / ww, wq = qq - hh * ww;
+        ldv(xb + ((size_t)(h0 + hh) * a.W + w0 + wq) * a.ldx, v[u]);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[u][j] = ok ? v[u][j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < V; ++j) s[j] += v[u][j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[threadIdx.x * V + j] = s[j];
+  __syncthreads();
+  if (g == 0) {
+    float o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = 0.f;
+    for (int gg = 0; gg < PG; ++gg)
+#pragma unroll
+      for (int j = 0; j < V; ++j) o[j] += red[(gg * CV + cv) * V + j];
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] *= inv;
+    stv((T*)a.pooled + ((size_t)b * a.N + n) * a.C + cv * V, o);
   }
 }
 
 int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
+  const int V = dtype == DT_F32 ? 4 : 8;
+  if (a.C % V || a.C / V > 256 || a.ldx % V) {
+    set_error("pyramid_pool: C=%d ldx=%d", a.C, a.ldx);
+    return E_UNSUPPORTED;
+  }
   dim3 grid(50, a.N);
-  if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 512, 0, st>>>(a);
-  else pyramid_pool_kernel<bf16><<<grid, 512, 0, st>>>(a);
+  if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 256, 0, st>>>(a);
+  else pyramid_pool_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("pyramid_pool");
 }
 

@@ -74,6 +74,7 @@ struct GemmTnArgs {
   int ldx;
   float* slab;   // [splits][N][K]
   int rows_per_split;
+  int splits;
 };
 
 struct FoldEntry {
@@ -93,7 +94,7 @@ struct FoldTable {
 };
 
 struct BnFinalizeArgs {
-  const float* part;  // [P][3][C] (mean, M2, count)
+  float* part;        // [P][3][C] (mean, M2, count); consumed (folded in place)
   int P, C;
   const float* gamma;
   const float* beta;
@@ -124,9 +125,11 @@ struct BnBwdArgs {
   long long M;
   int C;
   const void* dy; int lddy;
-  const void* mask; int ldmask;   // null: no ReLU
+  const void* mask; int ldmask;   // null: no ReLU (unless relu_z)
   const void* z; int ldz;
   const float* mean; const float* invstd; const float* scale;
+  const float* shift;             // forward shift (relu_z)
+  int relu_z;                     // mask = fmaf(z, scale, shift) > 0, recomputed (no mask read)
   float* part;                    // [P][2][C]: sum dy_r, sum dy_r*xhat
   int rows_per_block;
   // apply
@@ -245,7 +248,7 @@ int bn_finalize(const BnFinalizeArgs& a, hipStream_t st);
 int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st);
 int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
 int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);
-int bn_bwd_finalize(const float* part, int P, int C, double count, float* dgamma, float* dbeta,
+int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
                     float* coef, hipStream_t st);
 int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st);
 

@@ -114,23 +114,34 @@ int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hi
 
 // ---- dropout on an NHWC activation, mask indexed in NCHW order (matches the oracle) ----------
 
+// thread = one 16-B channel vector of one pixel; 32-bit index math (pixels * C/V < 2^31)
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = (long long)a.N * a.H * a.W * a.C;
-  if (i >= total) return;
-  int c = (int)(i % a.C);
-  long long pix = i / a.C;
-  long long hw = pix % ((long long)a.H * a.W);
-  long long n = pix / ((long long)a.H * a.W);
-  uint64_t nchw = ((uint64_t)n * a.C + c) * (uint64_t)a.H * a.W + hw;
-  float v = ld1((const T*)a.x + pix * a.ldx + c);
-  float s = 1.f / (1.f - a.p);
-  st1((T*)a.y + pix * a.ldy + c, dropout_keep(a.seed, nchw, thr) ? v * s : 0.f);
+  constexpr int V = VecW<T>::V;
+  const unsigned CV = (unsigned)(a.C / V), HW = (unsigned)(a.H * a.W);
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned total = (unsigned)a.N * HW * CV;
+  if (t >= total) return;
+  const unsigned pix = t / CV, cv = t - pix * CV;
+  const unsigned n = pix / HW, hw = pix - n * HW;
+  float v[V];
+  ldv((const T*)a.x + (size_t)pix * a.ldx + cv * V, v);
+  const float s = 1.f / (1.f - a.p);
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const uint64_t nchw = ((uint64_t)n * a.C + cv * V + j) * HW + hw;
+    v[j] = dropout_keep(a.seed, nchw, thr) ? v[j] * s : 0.f;
+  }
+  stv((T*)a.y + (size_t)pix * a.ldy + cv * V, v);
 }
 
 int dropout(const DropArgs& a, int dtype, hipStream_t st) {
-  long long total = (long long)a.N * a.H * a.W * a.C;
+  const int V = dtype == DT_F32 ? 4 : 8;
+  const long long total = (long long)a.N * a.H * a.W * (a.C / V);
+  if (a.C % V || a.ldx % V || a.ldy % V || total >= (1LL << 31)) {
+    set_error("dropout: C=%d ldx=%d ldy=%d", a.C, a.ldx, a.ldy);
+    return E_UNSUPPORTED;
+  }
   unsigned grid = (unsigned)((total + 255) / 256);
   uint32_t thr = dropout_threshold(a.p);
   if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr);

@@ -612,12 +612,13 @@ struct Exec {
   // ================================ backward ===============================================
   // BN backward of unit u: dy = u.ga (ld u.ga_ld), mask = relu output (or null) → dz scratch
   int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
-             int ldmask, void* dz) {
+             int ldmask, void* dz, bool relu_z = false) {
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
     b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
     b.z = W(u.z); b.ldz = u.C;
     b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
+    b.shift = Wf(u.shift); b.relu_z = relu_z;
     b.part = (float*)Bw(pl.bnpart);
     TRY(bn_bwd_reduce(b, dt, r.st));
     int rpb;
@@ -627,6 +628,10 @@ struct Exec {
     b.coef = coef;
     b.dz = dz; b.lddz = u.C;
     return bn_bwd_apply(b, dt, r.st);
+  }
+  // BN whose output is relu(BN(z)) with no second branch: the ReLU mask is recomputed from z
+  int bn_bwd_relu(const Unit& u, const BnL& bn, const void* dy, int lddy, void* dz) {
+    return bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, true);
   }
   // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
   int pw_bwd(const ConvL& c, long long M, const void* dz, int lddz, const void* X, int ldx,
@@ -694,20 +699,20 @@ struct Exec {
       TRY(dropout(d, dt, r.st));
     }
     // classifier dsconv2, dsconv1
-    TRY(bn_bwd(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, W(pl.c2pw.a), 128, dz));
+    TRY(bn_bwd_relu(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, dz));
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, W(pl.c2dw.a), 128, Bw(pl.c2dw.ga), 128));
-    TRY(bn_bwd(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, W(pl.c2dw.a), 128, dz));
+    TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz));
     TRY(dw_bwd(net.cls2.dw, 128, dz, W(pl.c1pw.a), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
-    TRY(bn_bwd(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, W(pl.c1pw.a), 128, dz));
+    TRY(bn_bwd_relu(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, dz));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, W(pl.c1dw.a), 128, Bw(pl.c1dw.ga), 128));
-    TRY(bn_bwd(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, W(pl.c1dw.a), 128, dz));
+    TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz));
     TRY(dw_bwd(net.cls1.dw, 128, dz, W(pl.f), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, W(pl.fdw.a), 128, Bw(pl.fdw.ga), 128));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, W(pl.l2pw.a), 64, Bw(pl.l2pw.ga), 64));
-    TRY(bn_bwd(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, W(pl.fdw.a), 128, dz));
+    TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz));
     TRY(dw_bwd(net.ffm_dw, 128, dz, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_up)));
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     {
@@ -725,7 +730,7 @@ struct Exec {
       TRY(axis_bwd(b, DT_F32, dt, r.st));
     }
     // PPM out 1x1 (256→128) over the concat buffer
-    TRY(bn_bwd(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, W(pl.po.a), 128, dz));
+    TRY(bn_bwd_relu(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, dz));
     TRY(pw_bwd(net.ppm_o, pl.po.M, dz, 128, W(pl.concat), 256, Bw(pl.g_concat), 256));
     {
       PpmUpArgs u{};
@@ -764,9 +769,9 @@ struct Exec {
     const int e = l.cin * 6;
     TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz));
     TRY(pw_bwd(l.p, up.M, dz, l.cout, W(ud.a), e, Bw(ud.ga), e));
-    TRY(bn_bwd(ud, l.bd, Bw(ud.ga), e, W(ud.a), e, dz));
+    TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz));
     TRY(dw_bwd(l.d, e, dz, W(ue.a), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
-    TRY(bn_bwd(ue, l.be, Bw(ue.ga), e, W(ue.a), e, dz));
+    TRY(bn_bwd_relu(ue, l.be, Bw(ue.ga), e, dz));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
@@ -775,15 +780,15 @@ struct Exec {
 
   int backward_ltd() {
     void* dz = Bw(pl.dz);
-    TRY(bn_bwd(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, W(pl.l2pw.a), 64, dz));
+    TRY(bn_bwd_relu(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, dz));
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, W(pl.l2dw.a), 48, Bw(pl.l2dw.ga), 48));
-    TRY(bn_bwd(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, W(pl.l2dw.a), 48, dz));
+    TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz));
     TRY(dw_bwd(net.ltd2.dw, 48, dz, W(pl.l1pw.a), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
-    TRY(bn_bwd(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, W(pl.l1pw.a), 48, dz));
+    TRY(bn_bwd_relu(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, dz));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, W(pl.l1dw.a), 32, Bw(pl.l1dw.ga), 32));
-    TRY(bn_bwd(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, W(pl.l1dw.a), 32, dz));
+    TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz));
     TRY(dw_bwd(net.ltd1.dw, 32, dz, W(pl.c0.a), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
-    TRY(bn_bwd(pl.c0, net.b0, Bw(pl.c0.ga), 32, W(pl.c0.a), 32, dz));
+    TRY(bn_bwd_relu(pl.c0, net.b0, Bw(pl.c0.ga), 32, dz));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;

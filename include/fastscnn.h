@@ -135,7 +135,8 @@ long long fscnn_pw_wgrad_slab_floats(int M, int N, int K);
 /* dW[N][K] = sum_m D[m][n] X[m][k] */
 int fscnn_pw_wgrad(int M, int N, int K, const void* D, int ldd, const void* X, int ldx,
                    float* slab, float* dW, int dtype, void* stream);
-int fscnn_bn_finalize(const float* part, int P, int C, const float* gamma, const float* beta,
+/* part [P][3][C] is consumed (folded in place) */
+int fscnn_bn_finalize(float* part, int P, int C, const float* gamma, const float* beta,
                       float* rmean, float* rvar, long long* nbt, float momentum, float* mean,
                       float* invstd, float* scale, float* shift, void* stream);
 int fscnn_bilinear_ac_fwd(const void* x, int dtype, int N, int Hi, int Wi, int C, int Ho, int Wo,
