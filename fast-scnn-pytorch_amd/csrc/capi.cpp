@@ -329,7 +329,7 @@ int fscnn_dw3x3_dgrad(const void* dy, int dtype, int N, int H, int W, int C, int
 }
 long long fscnn_dw3x3_wgrad_slab_floats(int N, int H, int W, int C, int stride, int dtype) {
   int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  return (long long)dw_wgrad_parts(N, Ho, Wo, C, dtype) * 9 * C;
+  return (long long)dw_wgrad_parts(N, Ho, Wo, C, dtype, stride) * 9 * C;
 }
 int fscnn_dw3x3_wgrad(const void* x, const void* dy, int dtype, int N, int H, int W, int C,
                       int stride, float* slab, float* dw, void* stream) {
@@ -339,7 +339,7 @@ int fscnn_dw3x3_wgrad(const void* x, const void* dy, int dtype, int N, int H, in
   a.x = x; a.dy = dy; a.slab = slab;
   int rc = dw_wgrad(a, dtype, S(stream));
   if (rc) return rc;
-  return dw_wgrad_reduce(slab, dw_wgrad_parts(N, a.Ho, a.Wo, C, dtype), C, dw, S(stream));
+  return dw_wgrad_reduce(slab, dw_wgrad_parts(N, a.Ho, a.Wo, C, dtype, stride), C, dw, S(stream));
 }
 
 int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, int ldb,

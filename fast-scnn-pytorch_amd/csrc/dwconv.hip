@@ -2,16 +2,18 @@
 // :86 _DWConv; LTD.dsconv1/2, the 9 bottleneck expansions, FFM.dwconv, classifier dsconvs —
 // 14 layers).
 //
-// Workgroup = blockDim.x channel vectors (16 B: 4 fp32 / 8 bf16 channels) x blockDim.y column
-// tiles.  Each thread owns a register tile of HS=2 output rows x WS=4 output columns of its
-// channel vector: it streams the (HS-1)*s+3 input rows once, and every 16-B input vector it loads
-// feeds all the taps of the tile that read it (stride 1: 24 loads for 8 outputs instead of 72).
-// Lanes run along channels, so each wave-wide load is a run of contiguous 16-B vectors.
-// Grids are 3-D (channel chunk, column tile, row band) — no 64-bit index division.
+// LDS-tiled: a workgroup owns cbv <= 8 channel vectors (16 B: 4 fp32 / 8 bf16 channels) of a
+// spatial output tile (stride 1: 8 rows x 32 cols, stride 2: 4 x 16).  It loads the haloed input
+// tile ONCE, in one batch of branch-free 16-B loads (clamped addresses + selects: a branch
+// around a load makes hipcc wait vmcnt(0) at the join), into LDS; each thread then computes an
+// HS x WS block of outputs for its channel vector from LDS.  Row halo 10/8 (s1) instead of the
+// 2x of a per-thread register tile, one round trip per tile, ~150 VGPRs (occupancy 3).
+// Tiles are mapped XCD-contiguously (dw_tile) so neighbouring tiles share an XCD's L2.
 //
 // dgrad, stride 1 = the same kernel with the 3x3 taps flipped (correlation of dy);
 // dgrad, stride 2 = parity-aware gather (a 2x4 dx tile reads 2 dy rows x 3 dy columns).
-// wgrad = per-block partial [part][9][C] sums, reduced by the deterministic two-pass reducer.
+// wgrad = same tiles; a workgroup walks tpb tiles along a row band, accumulates 9 x V taps per
+// thread, reduces its 32 pixel groups in fixed order -> partial [part][9][C] (two-pass reducer).
 //
 // Roofline: HBM-bound.  Algorithmic bytes per layer = e*(N*C*Hi*Wi + N*C*Ho*Wo) + 9*C*4,
 // flops = 18*N*C*Ho*Wo.
@@ -19,24 +21,55 @@
 
 namespace fscnn {
 
-constexpr int DW_WS = 4;  // output columns per thread
-constexpr int DW_HS = 2;  // output rows per thread
+constexpr int DWL_CB = 8;  // max 16-B channel vectors per workgroup (128 B per pixel)
 
-__host__ __device__ inline void dw_block_shape(int C, int V, int& bx, int& by) {
-  int cv = C / V;
-  bx = cv < 64 ? cv : 64;
-  by = 256 / bx;
-  if (by < 1) by = 1;
+// A thread computes a channel QUAD (4 channels: 16 B fp32 / 8 B bf16 of LDS per read) for an
+// HS x WS block of outputs; G = 32 / (quads per vector) pixel groups of GX x GY cover the tile.
+template <typename T, int S> struct DwCfg;
+template <> struct DwCfg<float, 1> { static constexpr int HS = 2, WS = 4, GX = 8, GY = 4; };
+template <> struct DwCfg<float, 2> { static constexpr int HS = 1, WS = 2, GX = 8, GY = 4; };
+template <> struct DwCfg<bf16, 1> { static constexpr int HS = 2, WS = 4, GX = 4, GY = 4; };
+template <> struct DwCfg<bf16, 2> { static constexpr int HS = 2, WS = 2, GX = 4, GY = 4; };
+template <typename T, int S> struct DwTile {
+  static constexpr int HS = DwCfg<T, S>::HS, WS = DwCfg<T, S>::WS;
+  static constexpr int GX = DwCfg<T, S>::GX, GY = DwCfg<T, S>::GY, G = GX * GY;
+  static constexpr int QPV = VecW<T>::V / 4;                 // quads per 16-B vector
+  static constexpr int TH = GY * HS, TW = GX * WS;           // output tile
+  static constexpr int IR = (TH - 1) * S + 3, IC = (TW - 1) * S + 3;  // input tile
+  static constexpr int LPT = (IR * IC + QPV * G - 1) / (QPV * G);     // 16-B loads per thread
+  static constexpr int NR = (HS - 1) * S + 3, NC = (WS - 1) * S + 3;  // per-thread input window
+};
+
+// 4 channels (a quad) from LDS / registers
+__device__ __forceinline__ void quad_ld(const float* p, float (&v)[4]) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+__device__ __forceinline__ void quad_ld(const bf16* p, float (&v)[4]) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xFFFF0000u);
+  v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xFFFF0000u);
+}
+__device__ __forceinline__ void quad_st(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void quad_st(bf16* p, const float (&v)[4]) {
+  const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
 }
 
-struct DwGeom {
-  int gx, gy, gz;  // channel chunks, column tiles, row bands
-};
+// channel vectors per workgroup: the largest divisor of C/V that is <= 8
+static int dw_cbv(int CV) {
+  for (int b = DWL_CB; b > 1; --b)
+    if (CV % b == 0) return b;
+  return 1;
+}
 
 // XCD-contiguous tile order (speed only): blocks L = x (mod 8) share an XCD, so residue class x
 // gets the contiguous logical range [x*T/8, (x+1)*T/8) of (chunk, column tile, band) in
-// chunk-fastest order — vertically adjacent bands then run on one XCD back to back and their
-// shared halo rows are served by its L2 instead of being fetched from HBM twice.
+// chunk-fastest order — neighbouring tiles then run on one XCD back to back and their shared
+// halo rows are served by its L2.
 __device__ __forceinline__ void dw_tile(int& cx, int& cy, int& cz) {
   const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   const long long T = (long long)gx * gy * gz;
@@ -47,180 +80,197 @@ __device__ __forceinline__ void dw_tile(int& cx, int& cy, int& cz) {
   cy = (int)(r % gy);
   cz = (int)(r / gy);
 }
-static DwGeom dw_geom(int N, int Ho, int Wo, int C, int V) {
-  int bx, by;
-  dw_block_shape(C, V, bx, by);
-  DwGeom g;
-  g.gx = cdiv(C / V, bx);
-  g.gy = cdiv(Wo, by * DW_WS);
-  g.gz = N * cdiv(Ho, DW_HS);
-  return g;
+
+// stage the haloed input tile [IR][IC][cbv] (16-B vectors) of image n into LDS; out-of-image
+// positions are zero.  All loads of a thread are issued before any LDS store.
+template <typename T, int S>
+__device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, int C, int n,
+                                         int hi0, int wi0, int cvbase, int cbv, int tid, int nthr) {
+  using G = DwTile<T, S>;
+  constexpr int V = VecW<T>::V;
+  uint4 raw[G::LPT];
+#pragma unroll
+  for (int k = 0; k < G::LPT; ++k) {
+    const int i = tid + k * nthr;
+    const int pix = i / cbv, lv = i - pix * cbv;
+    const int r = pix / G::IC, col = pix - r * G::IC;
+    const int hi = hi0 + r, wi = wi0 + col;
+    const bool ok = pix < G::IR * G::IC && hi >= 0 && hi < H && wi >= 0 && wi < W;
+    const size_t off = ok ? (((size_t)n * H + hi) * W + wi) * C + (size_t)(cvbase + lv) * V : 0;
+    raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(x + off));
+  }
+#pragma unroll
+  for (int k = 0; k < G::LPT; ++k) {
+    const int i = tid + k * nthr;
+    if (i < G::IR * G::IC * cbv) s_in[i] = raw[k];
+  }
 }
 
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
 template <typename T, int S, bool FLIP>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
-  constexpr int V = VecW<T>::V;
-  constexpr int NR = (DW_HS - 1) * S + 3;  // input rows touched
-  constexpr int NC = (DW_WS - 1) * S + 3;  // input cols touched
-  extern __shared__ float s_red[];         // [by][bx*V] (train statistics)
-  __shared__ float s_cnt[256];
-  const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
+__global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
+  using G = DwTile<T, S>;
+  __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
+  __shared__ float s_red[256 * 4];
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int QB = cbv * G::QPV;                 // quads per workgroup
+  const int q = tid % QB, grp = tid / QB;
+  const int gx = grp % G::GX, gy = grp / G::GX;
   int bx, by, bz;
   dw_tile(bx, by, bz);
-  const int cv = bx * BX + tx;
-  const int CV = a.C / V;
-  const int nb = (a.Ho + DW_HS - 1) / DW_HS;
-  const int n = bz / nb;
-  const int ho0 = (bz - n * nb) * DW_HS;
-  const int wo0 = (by * BY + ty) * DW_WS;
-  const int nrow = min(DW_HS, a.Ho - ho0);
-  const int ncol = wo0 < a.Wo ? min(DW_WS, a.Wo - wo0) : 0;
-  const bool active = cv < CV && ncol > 0;
+  const int tiles_h = cdiv(a.Ho, G::TH);
+  const int n = bz / tiles_h;
+  const int th0 = (bz - n * tiles_h) * G::TH, tw0 = by * G::TW;
+  const int c0 = bx * cbv * VecW<T>::V + q * 4;  // first channel of the thread's quad
+  dw_stage<T, S>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv, cbv,
+                 tid, nthr);
+  float wt[9][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = a.w[(size_t)(c0 + j) * 9 + t];
+  __syncthreads();
 
-  float acc[DW_HS][DW_WS][V];
+  const T* sl = reinterpret_cast<const T*>(s_in);
+  const int pstride = cbv * VecW<T>::V;          // elements per staged pixel
+  float acc[G::HS][G::WS][4];
 #pragma unroll
-  for (int r = 0; r < DW_HS; ++r)
+  for (int r = 0; r < G::HS; ++r)
 #pragma unroll
-    for (int p = 0; p < DW_WS; ++p)
+    for (int p = 0; p < G::WS; ++p)
 #pragma unroll
-      for (int j = 0; j < V; ++j) acc[r][p][j] = 0.f;
-  if (active) {
-    float wt[9][V];
-    const float* wp = a.w + (size_t)cv * V * 9;
+      for (int j = 0; j < 4; ++j) acc[r][p][j] = 0.f;
+  const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
 #pragma unroll
-    for (int j = 0; j < V; ++j)
+  for (int rr = 0; rr < G::NR; ++rr)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = wp[j * 9 + t];
-    const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.C + (size_t)cv * V;
-    const int hi0 = ho0 * S - 1, wi0 = wo0 * S - 1;
-    // branch-free: out-of-image taps load a clamped in-bounds vector and are zeroed by select,
-    // so the loads issue back to back (a branch around a load forces vmcnt(0) at the join)
+    for (int ci = 0; ci < G::NC; ++ci) {
+      float v[4];
+      quad_ld(sl + ((lr0 + rr) * G::IC + lc0 + ci) * pstride + q * 4, v);
 #pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
-      const int hi = hi0 + rr;
-      const bool rok = hi >= 0 && hi < a.H;
-      const T* xr = xb + (size_t)(rok ? hi : 0) * a.W * a.C;
+      for (int r = 0; r < G::HS; ++r) {
+        const int kh = rr - r * S;
+        if (kh < 0 || kh > 2) continue;
 #pragma unroll
-      for (int ci = 0; ci < NC; ++ci) {
-        const int wi = wi0 + ci;
-        const bool ok = rok && wi >= 0 && wi < a.W;
-        float v[V];
-        ldv(xr + (size_t)(ok ? wi : 0) * a.C, v);
+        for (int p = 0; p < G::WS; ++p) {
+          const int kw = ci - p * S;
+          if (kw < 0 || kw > 2) continue;
 #pragma unroll
-        for (int j = 0; j < V; ++j) v[j] = ok ? v[j] : 0.f;
-#pragma unroll
-        for (int r = 0; r < DW_HS; ++r) {
-          const int kh = rr - r * S;
-          if (kh < 0 || kh > 2) continue;
-#pragma unroll
-          for (int p = 0; p < DW_WS; ++p) {
-            const int kw = ci - p * S;
-            if (kw < 0 || kw > 2) continue;
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[r][p][j] = fmaf(v[j], wt[kh * 3 + kw][j], acc[r][p][j]);
-          }
+          for (int j = 0; j < 4; ++j) acc[r][p][j] = fmaf(v[j], wt[kh * 3 + kw][j], acc[r][p][j]);
         }
       }
     }
-    float sc[V], sh[V];
+
+  const int ho0 = th0 + gy * G::HS, wo0 = tw0 + gx * G::WS;
+  const int nrow = max(0, min(G::HS, a.Ho - ho0)), ncol = max(0, min(G::WS, a.Wo - wo0));
+  {
+    float sc[4], sh[4];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      sc[j] = a.scale ? a.scale[cv * V + j] : 1.f;
-      sh[j] = a.scale ? a.shift[cv * V + j] : 0.f;
+    for (int j = 0; j < 4; ++j) {
+      sc[j] = a.scale ? a.scale[c0 + j] : 1.f;
+      sh[j] = a.scale ? a.shift[c0 + j] : 0.f;
     }
 #pragma unroll
-    for (int r = 0; r < DW_HS; ++r) {
+    for (int r = 0; r < G::HS; ++r) {
       if (r >= nrow) continue;
-      T* yb = (T*)a.y + (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0) * a.C + (size_t)cv * V;
+      T* yb = (T*)a.y + (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0) * a.C + c0;
 #pragma unroll
-      for (int p = 0; p < DW_WS; ++p) {
+      for (int p = 0; p < G::WS; ++p) {
         if (p >= ncol) continue;
-        float o[V];
+        float o[4];
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-          float t = acc[r][p][j] * sc[j] + sh[j];
+        for (int j = 0; j < 4; ++j) {
+          const float t = acc[r][p][j] * sc[j] + sh[j];
           o[j] = a.relu ? fmaxf(t, 0.f) : t;
           acc[r][p][j] = o[j];
         }
-        stv(yb + (size_t)p * a.C, o);
+        quad_st(yb + (size_t)p * a.C, o);
       }
     }
   }
   if (a.part == nullptr) return;
-  // ---- per-channel (mean, M2, count) over the block's outputs (train-mode BN statistics) -----
-  const int npx = nrow * ncol;  // identical for every tx of this ty
+  // ---- per-channel (mean, M2, count) over the tile (train-mode BN statistics) ---------------
+  const int trows = min(G::TH, a.Ho - th0), tcols = min(G::TW, a.Wo - tw0);
+  const float cnt = (float)(trows * tcols);
+  float mean[4];
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    float s = 0.f;
+  for (int j = 0; j < 4; ++j) {
+    float sum = 0.f;
 #pragma unroll
-    for (int r = 0; r < DW_HS; ++r)
+    for (int r = 0; r < G::HS; ++r)
 #pragma unroll
-      for (int p = 0; p < DW_WS; ++p) s += (r < nrow && p < ncol) ? acc[r][p][j] : 0.f;
-    s_red[ty * BX * V + tx * V + j] = s;
+      for (int p = 0; p < G::WS; ++p) sum += (r < nrow && p < ncol) ? acc[r][p][j] : 0.f;
+    s_red[(grp * QB + q) * 4 + j] = sum;
   }
-  s_cnt[ty] = (float)npx;
-  __syncthreads();
-  float cnt = 0.f, mean[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) mean[j] = 0.f;
-  for (int k = 0; k < BY; ++k) {
-    cnt += s_cnt[k];
-#pragma unroll
-    for (int j = 0; j < V; ++j) mean[j] += s_red[k * BX * V + tx * V + j];
-  }
-#pragma unroll
-  for (int j = 0; j < V; ++j) mean[j] = cnt > 0.f ? mean[j] / cnt : 0.f;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
+  for (int j = 0; j < 4; ++j) {
+    float sum = 0.f;
+    for (int g = 0; g < G::G; ++g) sum += s_red[(g * QB + q) * 4 + j];
+    mean[j] = sum / cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
     float m2 = 0.f;
 #pragma unroll
-    for (int r = 0; r < DW_HS; ++r)
+    for (int r = 0; r < G::HS; ++r)
 #pragma unroll
-      for (int p = 0; p < DW_WS; ++p) {
-        float d = acc[r][p][j] - mean[j];
+      for (int p = 0; p < G::WS; ++p) {
+        const float d = acc[r][p][j] - mean[j];
         m2 += (r < nrow && p < ncol) ? d * d : 0.f;
       }
-    s_red[ty * BX * V + tx * V + j] = m2;
+    s_red[(grp * QB + q) * 4 + j] = m2;
   }
   __syncthreads();
-  if (ty == 0 && cv < CV) {
+  if (grp == 0) {
     float* rec = a.part + ((size_t)bz * gridDim.y + by) * 3 * a.C;
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
+    for (int j = 0; j < 4; ++j) {
       float m2 = 0.f;
-      for (int k = 0; k < BY; ++k) m2 += s_red[k * BX * V + tx * V + j];
-      rec[cv * V + j] = mean[j];
-      rec[a.C + cv * V + j] = m2;
-      rec[2 * a.C + cv * V + j] = cnt;
+      for (int g = 0; g < G::G; ++g) m2 += s_red[(g * QB + q) * 4 + j];
+      rec[c0 + j] = mean[j];
+      rec[a.C + c0 + j] = m2;
+      rec[2 * a.C + c0 + j] = cnt;
     }
   }
 }
 
-int dw_parts(int N, int Ho, int Wo, int C, int dtype) {
-  DwGeom g = dw_geom(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8);
-  return g.gy * g.gz;
+static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv) {
+  cbv = dw_cbv(C / V);
+  int TH, TW;
+  if (V == 4) {
+    TH = S == 1 ? DwTile<float, 1>::TH : DwTile<float, 2>::TH;
+    TW = S == 1 ? DwTile<float, 1>::TW : DwTile<float, 2>::TW;
+  } else {
+    TH = S == 1 ? DwTile<bf16, 1>::TH : DwTile<bf16, 2>::TH;
+    TW = S == 1 ? DwTile<bf16, 1>::TW : DwTile<bf16, 2>::TW;
+  }
+  return dim3(C / V / cbv, cdiv(Wo, TW), N * cdiv(Ho, TH));
+}
+
+int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
+  int cbv;
+  dim3 g = dw_grid(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8, stride, cbv);
+  return (int)(g.y * g.z);
 }
 
 template <bool FLIP>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
-  int bx, by;
-  dw_block_shape(a.C, V, bx, by);
-  DwGeom g = dw_geom(a.N, a.Ho, a.Wo, a.C, V);
-  if (g.gz > 65535 || g.gy > 65535) {
-    set_error("dw: grid too large (N*Ho/2=%d)", g.gz);
+  int cbv;
+  dim3 grid = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
+  if (grid.z > 65535 || grid.y > 65535) {
+    set_error("dw: grid too large (%u x %u)", grid.y, grid.z);
     return E_UNSUPPORTED;
   }
-  dim3 grid(g.gx, g.gy, g.gz), block(bx, by);
-  size_t shm = a.part ? (size_t)bx * by * V * sizeof(float) : 0;
+  const int nthr = cbv * 32;  // = quads * groups for both dtypes
   if (dtype == DT_F32) {
-    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP><<<grid, block, shm, st>>>(a);
-    else dw_fwd_kernel<float, 2, FLIP><<<grid, block, shm, st>>>(a);
+    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<float, 2, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
   } else {
-    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP><<<grid, block, shm, st>>>(a);
-    else dw_fwd_kernel<bf16, 2, FLIP><<<grid, block, shm, st>>>(a);
+    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<bf16, 2, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
   }
   return check_launch("dw_fwd");
 }
@@ -236,6 +286,13 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_FWD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
   return dw_launch_fwd<false>(a, dtype, st);
+}
+
+static void dw_block_shape(int C, int V, int& bx, int& by) {
+  int cv = C / V;
+  bx = cv < 64 ? cv : 64;
+  by = 256 / bx;
+  if (by < 1) by = 1;
 }
 
 // ---- input gradient ---------------------------------------------------------------------------
@@ -327,133 +384,128 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   return check_launch("dw_dgrad");
 }
 
-// ---- weight gradient: per-block partial [part][9][C] -----------------------------------------
-// Blocks walk (row band, column tile) pairs grid-stride so the partial count stays bounded.
+// ---- weight gradient: per-workgroup partial [part][9][C] --------------------------------------
+// grid: x = channel chunk, y = groups of tpb column tiles, z = N * row bands; part = (z, y).
 template <typename T, int S>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(DwBwdArgs a, int gy, int gz) {
-  constexpr int V = VecW<T>::V;
-  constexpr int NR = (DW_HS - 1) * S + 3;
-  constexpr int NC = (DW_WS - 1) * S + 3;
-  extern __shared__ float s_red[];  // [BY][BX*V]
-  const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
-  const int cv = blockIdx.x * BX + tx;
-  const int CV = a.C / V;
-  const int nb = (a.Ho + DW_HS - 1) / DW_HS;
-  float acc[9][V];
+__global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, int tpb) {
+  using G = DwTile<T, S>;
+  __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int QB = cbv * G::QPV;
+  const int q = tid % QB, grp = tid / QB;
+  const int gx = grp % G::GX, gy = grp / G::GX;
+  int bx, by, bz;
+  dw_tile(bx, by, bz);
+  const int tiles_h = cdiv(a.Ho, G::TH), tiles_w = cdiv(a.Wo, G::TW);
+  const int n = bz / tiles_h;
+  const int th0 = (bz - n * tiles_h) * G::TH;
+  const int c0 = bx * cbv * VecW<T>::V + q * 4;
+  const int ho0 = th0 + gy * G::HS;
+  const int nrow = max(0, min(G::HS, a.Ho - ho0));
+  const T* sl = reinterpret_cast<const T*>(s_in);
+  const int pstride = cbv * VecW<T>::V;
+  float acc[9][4];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int j = 0; j < V; ++j) acc[t][j] = 0.f;
-  // part p walks the contiguous tile range [p*T/P, (p+1)*T/P): consecutive bands, so the halo
-  // rows it re-reads are its own recent loads (L1/L2 hits)
-  const int ntiles = gy * gz;
-  const int t_lo = (int)((long long)ntiles * blockIdx.y / gridDim.y);
-  const int t_hi = (int)((long long)ntiles * (blockIdx.y + 1) / gridDim.y);
-  for (int tile = t_lo; cv < CV && tile < t_hi; ++tile) {
-    const int tz = tile / gy, tyy = tile - tz * gy;
-    const int n = tz / nb;
-    const int ho0 = (tz - n * nb) * DW_HS;
-    const int wo0 = (tyy * BY + ty) * DW_WS;
-    if (wo0 >= a.Wo) continue;
-    const int nrow = min(DW_HS, a.Ho - ho0), ncol = min(DW_WS, a.Wo - wo0);
-    // dy tile (unpacked once) and the input rows as raw 16-B vectors, double-buffered: row rr+1's
-    // loads are in flight while row rr is consumed.  Clamped addresses + selects, no branches.
-    float g[DW_HS][DW_WS][V];
-    const T* gb = (const T*)a.dy + (((size_t)n * a.Ho + ho0) * a.Wo + wo0) * a.C + (size_t)cv * V;
-    {
-      uint4 graw[DW_HS][DW_WS];
+    for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
+  const int tw_lo = by * tpb, tw_hi = min(tiles_w, tw_lo + tpb);
+  for (int twi = tw_lo; twi < tw_hi; ++twi) {
+    const int tw0 = twi * G::TW;
+    const int wo0 = tw0 + gx * G::WS;
+    const int ncol = max(0, min(G::WS, a.Wo - wo0));
+    // dy of the thread's outputs (clamped + selected), issued with the tile loads
+    float g[G::HS][G::WS][4];
+    const T* gb = (const T*)a.dy + c0;
 #pragma unroll
-      for (int r = 0; r < DW_HS; ++r)
+    for (int r = 0; r < G::HS; ++r)
 #pragma unroll
-        for (int p = 0; p < DW_WS; ++p) {
-          const bool ok = r < nrow && p < ncol;
-          graw[r][p] = sel4(ok, *reinterpret_cast<const uint4*>(gb + (ok ? (size_t)r * a.Wo + p : 0) * a.C));
-        }
+      for (int p = 0; p < G::WS; ++p) {
+        const bool ok = r < nrow && p < ncol;
+        const size_t off = ok ? (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0 + p) * a.C : 0;
+        quad_ld(gb + off, g[r][p]);
 #pragma unroll
-      for (int r = 0; r < DW_HS; ++r)
-#pragma unroll
-        for (int p = 0; p < DW_WS; ++p) unpackv(graw[r][p], g[r][p]);
-    }
-    const T* xb = (const T*)a.x + (size_t)n * a.H * a.W * a.C + (size_t)cv * V;
-    const int hi0 = ho0 * S - 1, wi0 = wo0 * S - 1;
-    uint4 xrow[2][NC];
-    auto load_row = [&](int rr, uint4 (&dst)[NC]) {
-      const int hi = hi0 + rr;
-      const bool rok = hi >= 0 && hi < a.H;
-      const T* xr = xb + (size_t)(rok ? hi : 0) * a.W * a.C;
-#pragma unroll
-      for (int ci = 0; ci < NC; ++ci) {
-        const int wi = wi0 + ci;
-        const bool ok = rok && wi >= 0 && wi < a.W;
-        dst[ci] = sel4(ok, *reinterpret_cast<const uint4*>(xr + (size_t)(ok ? wi : 0) * a.C));
+        for (int j = 0; j < 4; ++j) g[r][p][j] = ok ? g[r][p][j] : 0.f;
       }
-    };
-    load_row(0, xrow[0]);
+    __syncthreads();  // previous tile's LDS reads are done
+    dw_stage<T, S>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv, cbv,
+                   tid, nthr);
+    __syncthreads();
+    const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
 #pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
-      if (rr + 1 < NR) load_row(rr + 1, xrow[(rr + 1) & 1]);
+    for (int rr = 0; rr < G::NR; ++rr)
 #pragma unroll
-      for (int ci = 0; ci < NC; ++ci) {
-        float v[V];
-        unpackv(xrow[rr & 1][ci], v);
+      for (int ci = 0; ci < G::NC; ++ci) {
+        float v[4];
+        quad_ld(sl + ((lr0 + rr) * G::IC + lc0 + ci) * pstride + q * 4, v);
 #pragma unroll
-        for (int r = 0; r < DW_HS; ++r) {
+        for (int r = 0; r < G::HS; ++r) {
           const int kh = rr - r * S;
           if (kh < 0 || kh > 2) continue;
 #pragma unroll
-          for (int p = 0; p < DW_WS; ++p) {
+          for (int p = 0; p < G::WS; ++p) {
             const int kw = ci - p * S;
             if (kw < 0 || kw > 2) continue;
 #pragma unroll
-            for (int j = 0; j < V; ++j)
+            for (int j = 0; j < 4; ++j)
               acc[kh * 3 + kw][j] = fmaf(v[j], g[r][p][j], acc[kh * 3 + kw][j]);
           }
         }
       }
-    }
   }
+  // ---- fixed-order reduction of the pixel groups, one tap at a time (LDS reused) ------------
+  float* red = reinterpret_cast<float*>(s_in);  // [G][QB*4]
+  const size_t part = (size_t)bz * gridDim.y + by;
   for (int t = 0; t < 9; ++t) {
-#pragma unroll
-    for (int j = 0; j < V; ++j) s_red[ty * BX * V + tx * V + j] = acc[t][j];
     __syncthreads();
-    if (ty == 0 && cv < CV) {
-      float* rec = a.slab + ((size_t)blockIdx.y * 9 + t) * a.C;
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float s = 0.f;
-        for (int k = 0; k < BY; ++k) s += s_red[k * BX * V + tx * V + j];
-        rec[cv * V + j] = s;
+    for (int j = 0; j < 4; ++j) red[(grp * QB + q) * 4 + j] = acc[t][j];
+    __syncthreads();
+    if (grp == 0) {
+      float* rec = a.slab + (part * 9 + t) * a.C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float sum = 0.f;
+        for (int g2 = 0; g2 < G::G; ++g2) sum += red[(g2 * QB + q) * 4 + j];
+        rec[c0 + j] = sum;
       }
     }
-    __syncthreads();
   }
 }
 
-int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype) {
-  DwGeom g = dw_geom(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8);
-  long long tiles = (long long)g.gy * g.gz;
-  long long cap = 2048 / g.gx;
-  if (cap < 1) cap = 1;
-  return (int)(tiles < cap ? tiles : cap);
+static int dw_wgrad_tpb(int N, int Ho, int Wo, int C, int V, int S, dim3& grid, int& cbv) {
+  grid = dw_grid(N, Ho, Wo, C, V, S, cbv);
+  const long long tiles_w = grid.y;
+  const long long blocks = (long long)grid.x * grid.y * grid.z;
+  long long tpb = blocks / 2048;  // ~2048 workgroups; bounded partial count
+  if (tpb < 1) tpb = 1;
+  if (tpb > tiles_w) tpb = tiles_w;
+  grid.y = (unsigned)cdiv((int)tiles_w, (int)tpb);
+  return (int)tpb;
+}
+
+int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
+  dim3 g;
+  int cbv;
+  dw_wgrad_tpb(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8, stride, g, cbv);
+  return (int)(g.y * g.z);
 }
 
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
-  int V = dtype == DT_F32 ? 4 : 8;
-  int bx, by;
-  dw_block_shape(a.C, V, bx, by);
-  DwGeom g = dw_geom(a.N, a.Ho, a.Wo, a.C, V);
-  dim3 grid(g.gx, dw_wgrad_parts(a.N, a.Ho, a.Wo, a.C, dtype));
-  dim3 block(bx, by);
-  size_t shm = (size_t)bx * by * V * sizeof(float);
+  const int V = dtype == DT_F32 ? 4 : 8;
+  dim3 grid;
+  int cbv;
+  const int tpb = dw_wgrad_tpb(a.N, a.Ho, a.Wo, a.C, V, a.stride, grid, cbv);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el), 18.0 * out_el);
+  const int nthr = cbv * 32;
   if (dtype == DT_F32) {
-    if (a.stride == 1) dw_wgrad_kernel<float, 1><<<grid, block, shm, st>>>(a, g.gy, g.gz);
-    else dw_wgrad_kernel<float, 2><<<grid, block, shm, st>>>(a, g.gy, g.gz);
+    if (a.stride == 1) dw_wgrad_kernel<float, 1><<<grid, nthr, 0, st>>>(a, cbv, tpb);
+    else dw_wgrad_kernel<float, 2><<<grid, nthr, 0, st>>>(a, cbv, tpb);
   } else {
-    if (a.stride == 1) dw_wgrad_kernel<bf16, 1><<<grid, block, shm, st>>>(a, g.gy, g.gz);
-    else dw_wgrad_kernel<bf16, 2><<<grid, block, shm, st>>>(a, g.gy, g.gz);
+    if (a.stride == 1) dw_wgrad_kernel<bf16, 1><<<grid, nthr, 0, st>>>(a, cbv, tpb);
+    else dw_wgrad_kernel<bf16, 2><<<grid, nthr, 0, st>>>(a, cbv, tpb);
   }
   return check_launch("dw_wgrad");
 }

@@ -224,10 +224,10 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st);
 int conv0_wgrad_parts(int N, int Ho, int Wo, int rows_per_block);
 int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
 
-int dw_parts(int N, int Ho, int Wo, int C, int dtype);
+int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
-int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype);
+int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
 int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st);
 

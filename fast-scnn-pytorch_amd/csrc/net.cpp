@@ -198,9 +198,9 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   }
   if (dtype == DT_BF16) pl.pbf = A.get((size_t)net.p_total * 2);
   unit(pl.c0, M0, 32, conv0_parts(N, pl.H1, pl.W1));
-  unit(pl.l1dw, M1, 32, dw_parts(N, pl.H2, pl.W2, 32, dtype));
+  unit(pl.l1dw, M1, 32, dw_parts(N, pl.H2, pl.W2, 32, dtype, 2));
   unit(pl.l1pw, M1, 48, gemm_parts((int)M1));
-  unit(pl.l2dw, M2, 48, dw_parts(N, pl.H3, pl.W3, 48, dtype));
+  unit(pl.l2dw, M2, 48, dw_parts(N, pl.H3, pl.W3, 48, dtype, 2));
   unit(pl.l2pw, M2, 64, gemm_parts((int)M2));
   pl.concat = A.get((size_t)M5 * 256 * E);
   for (int i = 0; i < 9; ++i) {
@@ -210,7 +210,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     int Ho = i < 3 ? pl.H4 : pl.H5, Wo = i < 3 ? pl.W4 : pl.W5;
     int e = l.cin * 6;
     unit(pl.lbe[i], Min, e, gemm_parts((int)Min));
-    unit(pl.lbd[i], Mout, e, dw_parts(N, Ho, Wo, e, dtype));
+    unit(pl.lbd[i], Mout, e, dw_parts(N, Ho, Wo, e, dtype, l.stride));
     if (i == 8) unit(pl.lbp[i], Mout, l.cout, gemm_parts((int)Mout), pl.concat, 256);
     else unit(pl.lbp[i], Mout, l.cout, gemm_parts((int)Mout));
   }
@@ -224,13 +224,13 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   }
   unit(pl.po, M5, 128, gemm_parts((int)M5));
   pl.up_low = A.get((size_t)M2 * 128 * E);
-  unit(pl.fdw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype));
+  unit(pl.fdw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype, 1));
   pl.f = A.get((size_t)M2 * 128 * E);
   unit(pl.flow, M2, 128, gemm_parts((int)M2), pl.f);    // a = f (combined), z own
   unit(pl.fhigh, M2, 128, gemm_parts((int)M2), pl.f);
-  unit(pl.c1dw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype));
+  unit(pl.c1dw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype, 1));
   unit(pl.c1pw, M2, 128, gemm_parts((int)M2));
-  unit(pl.c2dw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype));
+  unit(pl.c2dw, M2, 128, dw_parts(N, pl.H3, pl.W3, 128, dtype, 1));
   unit(pl.c2pw, M2, 128, gemm_parts((int)M2));
   pl.drop = train ? A.get((size_t)M2 * 128 * E) : pl.c2pw.a;
   pl.logits = A.get((size_t)M2 * pl.Cp * E);
@@ -308,23 +308,23 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
       size_t s = (size_t)gemm_tn_splits((int)M, n, k) * n * k;
       if (s > slab) slab = s;
     };
-    auto dw_slab = [&](int Ho, int Wo, int Cc) {
-      size_t s = (size_t)dw_wgrad_parts(N, Ho, Wo, Cc, dtype) * 9 * Cc;
+    auto dw_slab = [&](int Ho, int Wo, int Cc, int st) {
+      size_t s = (size_t)dw_wgrad_parts(N, Ho, Wo, Cc, dtype, st) * 9 * Cc;
       if (s > slab) slab = s;
     };
     pw_slab(M1, 48, 32); pw_slab(M2, 64, 48);
-    dw_slab(pl.H2, pl.W2, 32); dw_slab(pl.H3, pl.W3, 48);
+    dw_slab(pl.H2, pl.W2, 32, 2); dw_slab(pl.H3, pl.W3, 48, 2);
     for (int i = 0; i < 9; ++i) {
       const LbL& l = net.lb[i];
       long long Min = pl.lbe[i].M, Mout = pl.lbd[i].M;
       int Ho = i < 3 ? pl.H4 : pl.H5, Wo = i < 3 ? pl.W4 : pl.W5;
       pw_slab(Min, l.cin * 6, l.cin);
       pw_slab(Mout, l.cout, l.cin * 6);
-      dw_slab(Ho, Wo, l.cin * 6);
+      dw_slab(Ho, Wo, l.cin * 6, l.stride);
     }
     for (int i = 0; i < 4; ++i) pw_slab(pl.ppk[i].M, 32, 128);
     pw_slab(M5, 128, 256);
-    dw_slab(pl.H3, pl.W3, 128);
+    dw_slab(pl.H3, pl.W3, 128, 1);
     pw_slab(M2, 128, 128); pw_slab(M2, 128, 64); pw_slab(M2, C, 128);
     size_t c0s = (size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864;
     if (c0s > slab) slab = c0s;
@@ -662,7 +662,7 @@ struct Exec {
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
     d.x = X; d.dy = dz; d.w = P(c.w); d.dx = dX; d.slab = (float*)Bw(pl.slab);
     TRY(dw_wgrad(d, dt, r.st));
-    TRY(dw_wgrad_reduce(d.slab, dw_wgrad_parts(pl.N, Ho, Wo, C, dt), C, G(c.w), r.st));
+    TRY(dw_wgrad_reduce(d.slab, dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride), C, G(c.w), r.st));
     return dw_dgrad(d, dt, r.st);
   }
 
