@@ -183,6 +183,7 @@ int fscnn_plan_create(const fscnn_net* net, int N, int H, int W, int dtype, int 
   if (!p) { set_error("out of host memory"); return E_INVALID; }
   int rc = plan_build(net->net, N, H, W, dtype, train, p->plan);
   if (rc) { delete p; return rc; }
+  p->plan.graphs = make_graph_cache();
   *out = p;
   return OK;
 }

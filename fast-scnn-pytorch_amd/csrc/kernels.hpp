@@ -206,6 +206,7 @@ struct DropArgs {
   void* y; int ldy;
   uint64_t seed;
   float p;
+  const uint64_t* seed_ptr = nullptr;  // device slot holding the seed (graph-replayable), or null
 };
 
 struct SgdArgs {
@@ -269,6 +270,8 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
 int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const float* gout,
                   const float* out2, int dtype, hipStream_t st);
 int dropout(const DropArgs& a, int dtype, hipStream_t st);
+// *p = v (one thread): per-call scalars that captured graphs read from device memory
+int set_u64(uint64_t* p, uint64_t v, hipStream_t st);
 int sgd(const SgdArgs& a, hipStream_t st);
 int cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st);
 int fill_f32(float* x, long long n, float v, hipStream_t st);

@@ -124,13 +124,14 @@ __global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr) 
   if (t >= total) return;
   const unsigned pix = t / CV, cv = t - pix * CV;
   const unsigned n = pix / HW, hw = pix - n * HW;
+  const uint64_t seed = a.seed_ptr ? *a.seed_ptr : a.seed;
   float v[V];
   ldv((const T*)a.x + (size_t)pix * a.ldx + cv * V, v);
   const float s = 1.f / (1.f - a.p);
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const uint64_t nchw = ((uint64_t)n * a.C + cv * V + j) * HW + hw;
-    v[j] = dropout_keep(a.seed, nchw, thr) ? v[j] * s : 0.f;
+    v[j] = dropout_keep(seed, nchw, thr) ? v[j] * s : 0.f;
   }
   stv((T*)a.y + (size_t)pix * a.ldy + cv * V, v);
 }
@@ -147,6 +148,13 @@ int dropout(const DropArgs& a, int dtype, hipStream_t st) {
   if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr);
   else dropout_kernel<bf16><<<grid, 256, 0, st>>>(a, thr);
   return check_launch("dropout");
+}
+
+__global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
+
+int set_u64(uint64_t* p, uint64_t v, hipStream_t st) {
+  set_u64_kernel<<<1, 1, 0, st>>>(p, v);
+  return check_launch("set_u64");
 }
 
 // ---- fused SGD over a flat fp32 arena ------------------------------------------------------

@@ -11,6 +11,10 @@
 // train: producer writes raw z + per-block statistics → bn_finalize → bn_apply (+res / ReLU)
 #include "net.hpp"
 
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
 #include <cstdio>
 #include <cstring>
 
@@ -238,6 +242,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
   }
+  if (train) pl.seed_slot = A.get(64);
   pl.ws_bytes = A.top;
   auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
     pl.named.push_back({n, off, rows, cols, ld, bws});
@@ -580,6 +585,7 @@ struct Exec {
       DropArgs d{};
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = W(pl.c2pw.a); d.ldx = 128;
       d.y = W(pl.drop); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
+      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
       TRY(dropout(d, dt, r.st));
       cls_in = W(pl.drop);
     }
@@ -696,6 +702,7 @@ struct Exec {
       DropArgs d{};
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = Bw(pl.g_drop); d.ldx = 128;
       d.y = Bw(pl.c2pw.ga); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
+      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
       TRY(dropout(d, dt, r.st));
     }
     // classifier dsconv2, dsconv1
@@ -801,9 +808,136 @@ struct Exec {
 
 }  // namespace
 
+// ================================ hipGraph replay =============================================
+// A whole forward (~100 launches) or backward stage (~100-200 launches) is captured once into a
+// hipGraph on an internal stream and replayed with one hipGraphLaunch while its arguments (all
+// pointers and scalars; the dropout seed lives in device memory, written before each replay) are
+// unchanged.  The caller's stream is chained in and out with events, so ordering with the
+// caller's other work (and RCCL on other streams) is preserved.  Disabled with FSCNN_GRAPHS=0,
+// while the launch profiler is active, or when the caller's stream is itself being captured.
+struct GraphCache {
+  std::mutex mu;
+  int dev = -1;
+  hipStream_t gs = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  struct Entry {
+    std::vector<uint64_t> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<Entry> entries;  // least recently used first
+  ~GraphCache() {
+    for (auto& e : entries) (void)hipGraphExecDestroy(e.exec);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+    if (gs) (void)hipStreamDestroy(gs);
+  }
+};
+
+std::shared_ptr<GraphCache> make_graph_cache() { return std::make_shared<GraphCache>(); }
+
+namespace {
+
+bool graphs_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_GRAPHS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+uint64_t fbits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+
+std::vector<uint64_t> run_key(int kind, int s0, int s1, const RunArgs& r) {
+  auto P = [](const void* p) { return (uint64_t)(uintptr_t)p; };
+  return {(uint64_t)kind, (uint64_t)s0, (uint64_t)s1, P(r.x), (uint64_t)r.x_dtype, P(r.out),
+          (uint64_t)r.out_dtype, P(r.aux_out), P(r.P), P(r.R), P(r.NBT), P(r.G), P(r.ws),
+          P(r.bws), P(r.dout), P(r.daux), fbits(r.dropout_p), fbits(r.momentum), P(r.target),
+          (uint64_t)r.ignore_index, P(r.loss2), P(r.gloss)};
+}
+
+template <typename F>
+int run_graphed(const Plan& pl, std::vector<uint64_t> key, hipStream_t st, F&& body) {
+  if (!graphs_enabled() || g_prof_kind != PK_NONE || !pl.graphs) return body(st);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return body(st);
+  }
+  GraphCache& gc = *pl.graphs;
+  std::lock_guard<std::mutex> lock(gc.mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return body(st);
+  if (!gc.gs) {
+    if (hipStreamCreateWithFlags(&gc.gs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&gc.ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&gc.ev_out, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return body(st);
+    }
+    gc.dev = dev;
+  } else if (dev != gc.dev) {
+    return body(st);
+  }
+  hipGraphExec_t exec = nullptr;
+  for (size_t i = 0; i < gc.entries.size(); ++i) {
+    if (gc.entries[i].key == key) {
+      GraphCache::Entry e = gc.entries[i];
+      gc.entries.erase(gc.entries.begin() + i);
+      gc.entries.push_back(e);
+      exec = e.exec;
+      break;
+    }
+  }
+  // order: caller's prior work -> graph stream
+  if (hipEventRecord(gc.ev_in, st) != hipSuccess || hipStreamWaitEvent(gc.gs, gc.ev_in, 0) != hipSuccess) {
+    set_error("graph: event chaining failed");
+    return E_HIP;
+  }
+  if (!exec) {
+    if (hipStreamBeginCapture(gc.gs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      (void)hipGetLastError();
+      return body(st);
+    }
+    const int rc = body(gc.gs);
+    hipGraph_t g = nullptr;
+    const hipError_t e1 = hipStreamEndCapture(gc.gs, &g);
+    hipError_t e2 = hipErrorUnknown;
+    if (!rc && e1 == hipSuccess && g) e2 = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    if (e1 != hipSuccess || e2 != hipSuccess) {  // capture unsupported: run directly
+      (void)hipGetLastError();
+      return body(st);
+    }
+    gc.entries.push_back({std::move(key), exec});
+    if (gc.entries.size() > 16) {
+      (void)hipGraphExecDestroy(gc.entries.front().exec);
+      gc.entries.erase(gc.entries.begin());
+    }
+  }
+  if (hipGraphLaunch(exec, gc.gs) != hipSuccess || hipEventRecord(gc.ev_out, gc.gs) != hipSuccess ||
+      hipStreamWaitEvent(st, gc.ev_out, 0) != hipSuccess) {
+    set_error("graph: launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return E_HIP;
+  }
+  return OK;
+}
+
+}  // namespace
+
 int net_forward(const Plan& pl, const RunArgs& r) {
-  Exec ex(pl, r);
-  return ex.forward();
+  if (pl.train && r.dropout_p > 0.f)  // read by the dropout kernels (outside any graph)
+    TRY(set_u64(reinterpret_cast<uint64_t*>((char*)r.ws + pl.seed_slot), r.seed, r.st));
+  return run_graphed(pl, run_key(0, 0, 0, r), r.st, [&](hipStream_t st) -> int {
+    RunArgs rr = r;
+    rr.st = st;
+    Exec ex(pl, rr);
+    return ex.forward();
+  });
 }
 
 // stages: 0 = head (upsample, classifier, FFM, PPM), 1 = bottleneck3, 2 = bottleneck2,
@@ -813,20 +947,28 @@ int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to)
     set_error("net_backward: the plan was built for inference (train=0)");
     return E_INVALID;
   }
-  Exec ex(pl, r);
-  for (int s = stage_from; s <= stage_to; ++s) {
-    switch (s) {
-      case 0: TRY(ex.backward_head()); break;
-      case 1: for (int i = 8; i >= 6; --i) TRY(ex.backward_block(i)); break;
-      case 2: for (int i = 5; i >= 3; --i) TRY(ex.backward_block(i)); break;
-      case 3:
-        for (int i = 2; i >= 0; --i) TRY(ex.backward_block(i));
-        TRY(ex.backward_ltd());
-        break;
-      default: set_error("net_backward: bad stage %d", s); return E_INVALID;
+  for (int s = stage_from; s <= stage_to; ++s)
+    if (s < 0 || s > 3) {
+      set_error("net_backward: bad stage %d", s);
+      return E_INVALID;
     }
-  }
-  return OK;
+  return run_graphed(pl, run_key(1, stage_from, stage_to, r), r.st, [&](hipStream_t st) -> int {
+    RunArgs rr = r;
+    rr.st = st;
+    Exec ex(pl, rr);
+    for (int s = stage_from; s <= stage_to; ++s) {
+      switch (s) {
+        case 0: TRY(ex.backward_head()); break;
+        case 1: for (int i = 8; i >= 6; --i) TRY(ex.backward_block(i)); break;
+        case 2: for (int i = 5; i >= 3; --i) TRY(ex.backward_block(i)); break;
+        default:
+          for (int i = 2; i >= 0; --i) TRY(ex.backward_block(i));
+          TRY(ex.backward_ltd());
+          break;
+      }
+    }
+    return OK;
+  });
 }
 
 }  // namespace fscnn

@@ -4,6 +4,7 @@
 // and workspaces (see include/fastscnn.h).
 #pragma once
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "kernels.hpp"
@@ -64,6 +65,8 @@ struct Unit {
   int ga_ld = 0;
 };
 
+struct GraphCache;
+
 struct Plan {
   const Net* net = nullptr;
   int N = 0, H = 0, W = 0, dtype = DT_F32, train = 0;
@@ -80,6 +83,7 @@ struct Plan {
   size_t concat = 0, pooled = 0, feats_a = 0, feats_z = 0, up_low = 0, f = 0, drop = 0,
          logits = 0, aux_drop = 0, aux_logits = 0, pbf = 0, fold_tmp = 0;
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
+  size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
@@ -87,9 +91,12 @@ struct Plan {
   // named buffers for debugging / stage-level parity: name -> (offset, rows, cols, ld, in_bws)
   struct Named { std::string name; size_t off; long long rows; int cols, ld, bws; };
   std::vector<Named> named;
+  // captured hipGraphs of whole forward / backward-stage calls, keyed by their arguments
+  std::shared_ptr<GraphCache> graphs;
 };
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl);
+std::shared_ptr<GraphCache> make_graph_cache();
 
 struct RunArgs {
   const void* x; int x_dtype;     // NCHW input image

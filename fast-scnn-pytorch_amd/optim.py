@@ -32,6 +32,11 @@ class FusedSGD(torch.optim.Optimizer):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening,
                         weight_decay=weight_decay, nesterov=nesterov, grad_scale=grad_scale)
         super().__init__(params, defaults)
+        self._aux = {}  # group index -> {"flat": momentum arena, "plan": cached fused plan}
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._aux = {}  # momentum buffers were replaced: rebuild the flat view on the next step
 
     def _launch(self, p, g, buf, n, group, first):
         _lib.call("fscnn_sgd", _lib.c_vp(p), _lib.c_vp(g), _lib.c_vp(buf), n,
@@ -40,13 +45,43 @@ class FusedSGD(torch.optim.Optimizer):
                   int(group["nesterov"]), int(first), _lib.c_float(group["grad_scale"]),
                   _lib.stream_ptr())
 
+    def _fast_step(self, gi, group):
+        """Steady-state path: same parameter views as the cached fused plan and every grad a
+        view of one base at the parameters' offsets (what FastSCNN's backward returns) -> one
+        launch without re-deriving the plan.  Returns False when the plan does not apply."""
+        aux = self._aux.get(gi)
+        plan = aux.get("plan") if aux else None
+        params = group["params"]
+        if plan is None or len(params) != plan["n"]:
+            return False
+        if params[0].data_ptr() != plan["p0"] or params[-1].data_ptr() != plan["p1"]:
+            return False
+        g0 = params[0].grad
+        if g0 is None or g0.dtype != torch.float32:
+            return False
+        base = g0._base
+        if base is None:
+            return False
+        offs = plan["offs"]
+        for p, o in zip(params, offs):
+            g = p.grad
+            if g is None or g._base is not base or g.storage_offset() != o:
+                return False
+        gptr = base.untyped_storage().data_ptr()
+        self._launch(plan["pbase"], gptr + plan["lo"] * 4, aux["flat"].data_ptr(),
+                     plan["len"], group, False)
+        return True
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
+            if self._fast_step(gi, group):
+                continue
+            aux = self._aux.setdefault(gi, {})
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
                 continue
@@ -62,15 +97,22 @@ class FusedSGD(torch.optim.Optimizer):
             if fused:
                 lo = min(pb[1])
                 hi = max(o + p.numel() for o, p in zip(pb[1], params))
-                key = "_flat_buf"
-                flat = group.get(key)
+                flat = aux.get("flat")
                 if flat is None or flat.numel() != hi - lo or first:
                     flat = torch.zeros(hi - lo, dtype=torch.float32, device=params[0].device)
-                    group[key] = flat
+                    aux["flat"] = flat
                     for o, p in zip(pb[1], params):
-                        self.state[p]["momentum_buffer"] = flat[o - lo:o - lo + p.numel()].view_as(p)
+                        view = flat[o - lo:o - lo + p.numel()].view_as(p)
+                        old = self.state[p].get("momentum_buffer")
+                        if old is not None and not first:  # e.g. after load_state_dict
+                            view.copy_(old)
+                        self.state[p]["momentum_buffer"] = view
                 self._launch(pb[0] + lo * 4, gb[0] + lo * 4, flat.data_ptr(), hi - lo, group,
                              first)
+                if len(params) == len(group["params"]) and pb[1] == gb[1]:
+                    aux["plan"] = {"n": len(params), "p0": params[0].data_ptr(),
+                                            "p1": params[-1].data_ptr(), "offs": list(gb[1]),
+                                            "pbase": pb[0] + lo * 4, "lo": lo, "len": hi - lo}
             else:
                 for p in params:
                     st = self.state[p]

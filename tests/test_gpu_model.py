@@ -208,6 +208,35 @@ def test_sgd_step_matches_torch_semantics():
         np.testing.assert_allclose(v, g["sgd_val." + k], rtol=0, atol=2e-4, err_msg=k)
 
 
+def test_fused_sgd_fast_path_and_state_dict():
+    """Several real train steps: FusedSGD (cached single-launch path) == torch.optim.SGD on the
+    same gradients; state_dict() holds only torch's keys; load_state_dict() keeps momentum."""
+    g = load_golden("train_c2")
+    x, t = golden_input(g).to(DEV), golden_target(g).to(DEV)
+    from fast_scnn_pytorch_amd.optim import FusedSGD
+    m = make_model(g, 2).train()
+    m._dropout_seed = 3
+    ref = {k: p.detach().clone().requires_grad_(True) for k, p in m.named_parameters()}
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    topt = torch.optim.SGD(list(ref.values()), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    for it in range(4):
+        opt.zero_grad(set_to_none=True)
+        m.forward_loss(x, t).backward()
+        for k, p in m.named_parameters():
+            ref[k].grad = p.grad.detach().clone()
+        opt.step()
+        topt.step()
+        torch.cuda.synchronize()
+        for k, p in m.named_parameters():
+            assert torch.allclose(p.detach(), ref[k].detach(), rtol=1e-6, atol=1e-7), (it, k)
+        if it == 1:
+            sd = opt.state_dict()
+            assert set(sd["param_groups"][0]) == set(topt.state_dict()["param_groups"][0])
+            opt2 = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+            opt2.load_state_dict(sd)
+            opt = opt2
+
+
 def test_grads_are_arena_views():
     m, _ = _hip_train_step(load_golden("train_c2"))
     grads = [p.grad for p in m.parameters()]
