@@ -17,69 +17,127 @@ constexpr int C0_IN_W = 2 * C0_TILE + 1;  // staged input columns
 constexpr int C0_OSTR = 36;              // LDS floats per staged output pixel (16B aligned)
 
 
-template <typename TO>
+// MFMA helpers for the im2col GEMM out[px][co] = sum_k patch[px][k] * W[co][k], K = 27 -> 32:
+// lane (li, lq) supplies k = 8*lq .. 8*lq+7 for its row (pixel li / channel li).
+template <bool BF>
+struct C0Mma;
+template <>
+struct C0Mma<true> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x 16 co
+  using Frag = i16x8;
+  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
+    Frag f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (short)f2bf(v[e]);
+    return f;
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+};
+template <>
+struct C0Mma<false> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
+  struct Frag { float v[8]; };
+  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
+    Frag f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f.v[e] = v[e];
+    return f;
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[e], b.v[e], acc, 0, 0, 0);
+  }
+};
+
+template <typename TO, bool XB>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
-  __shared__ float s_in[3 * 3 * C0_IN_W];          // [ci][r][col]
-  __shared__ float s_w[27 * C0_OUT];               // [tap][co]
+  constexpr bool BF = sizeof(TO) == 2;  // bf16 output => bf16 MFMA operands (compute dtype)
+  using M = C0Mma<BF>;
+  constexpr int NIN = 3 * 3 * C0_IN_W;              // staged input elements
+  constexpr int LPT = (NIN + 255) / 256;            // loads per thread (fixed count)
+  __shared__ float s_in[NIN];                        // [ci][r][col]
   __shared__ __attribute__((aligned(16))) float s_out[C0_TILE * C0_OSTR];
   __shared__ float s_red[8 * C0_OUT];
 
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
   const int wo0 = blockIdx.x * C0_TILE;
   const int row = blockIdx.y;  // n * Ho + ho
   const int n = row / a.Ho, ho = row - n * a.Ho;
   const int npx = min(C0_TILE, a.Wo - wo0);
 
-  for (int i = tid; i < 27 * C0_OUT; i += 256) {
-    int co = i / 27, t = i - co * 27;
-    s_w[t * C0_OUT + co] = a.w[i];
-  }
+  // ---- stage the 3 x 3 x (2*256+1) input strip: all loads first, then the LDS stores --------
   const int col0 = 2 * wo0;
   const int ncol = min(C0_IN_W, a.W - col0);
-  for (int i = tid; i < 9 * C0_IN_W; i += 256) {
-    int cr = i / C0_IN_W, c = i - cr * C0_IN_W;  // cr = ci*3 + r
-    int ci = cr / 3, r = cr - ci * 3;
-    const bool ok = c < ncol;  // clamped load + select (branch-free)
-    const size_t off = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + (ok ? c : 0);
-    const float v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[off]) : ((const float*)a.x)[off];
-    s_in[i] = ok ? v : 0.f;
+  {
+    float v[LPT];
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int i = tid + 256 * k;
+      const int cr = i / C0_IN_W, c = i - cr * C0_IN_W;  // cr = ci*3 + r
+      const int ci = cr / 3, r = cr - ci * 3;
+      const bool ok = i < NIN && c < ncol;  // clamped load + select (branch-free)
+      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c : 0;
+      const float t = XB ? bf2f(((const uint16_t*)a.x)[off]) : ((const float*)a.x)[off];
+      v[k] = ok ? t : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < LPT; ++k)
+      if (tid + 256 * k < NIN) s_in[tid + 256 * k] = v[k];
+  }
+  // B fragments (weights) for the two 16-channel tiles: W[16*jt + li][8*lq + e], k >= 27 -> 0
+  typename M::Frag bw[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    float wv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * lq + e;
+      const float t = a.w[(16 * jt + li) * 27 + (k < 27 ? k : 0)];
+      wv[e] = k < 27 ? t : 0.f;
+    }
+    bw[jt] = M::pack(wv);
+  }
+  // tap k -> offset in s_in relative to the pixel's column 2*px: (ci*3 + kh)*IN_W + kw
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * lq + e;
+    const int kk = k < 27 ? k : 0;
+    const int ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
+    koff[e] = (ci * 3 + kh) * C0_IN_W + kw;
   }
   __syncthreads();
 
-  float acc[C0_OUT];
+  // eval BN fold of the lane's two channels (li, 16 + li), loaded once
+  float fsc[2], fsh[2];
 #pragma unroll
-  for (int co = 0; co < C0_OUT; ++co) acc[co] = 0.f;
-  if (tid < npx) {
-#pragma unroll
-    for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          float v = s_in[(ci * 3 + r) * C0_IN_W + 2 * tid + c];
-          const float4* wp = reinterpret_cast<const float4*>(&s_w[((ci * 3 + r) * 3 + c) * C0_OUT]);
-#pragma unroll
-          for (int q = 0; q < C0_OUT / 4; ++q) {
-            float4 w4 = wp[q];
-            acc[4 * q + 0] = fmaf(v, w4.x, acc[4 * q + 0]);
-            acc[4 * q + 1] = fmaf(v, w4.y, acc[4 * q + 1]);
-            acc[4 * q + 2] = fmaf(v, w4.z, acc[4 * q + 2]);
-            acc[4 * q + 3] = fmaf(v, w4.w, acc[4 * q + 3]);
-          }
-        }
+  for (int jt = 0; jt < 2; ++jt) {
+    fsc[jt] = a.scale ? a.scale[16 * jt + li] : 1.f;
+    fsh[jt] = a.scale ? a.shift[16 * jt + li] : 0.f;
   }
-  // epilogue: BN fold (+ReLU) in eval, raw in train
+  // ---- wave w computes pixels [64w, 64w+64) as 4 groups of 16 x 32 channels ---------------
 #pragma unroll
-  for (int co = 0; co < C0_OUT; ++co) {
-    float v = acc[co];
-    if (a.scale) v = v * a.scale[co] + a.shift[co];
-    if (a.relu) v = fmaxf(v, 0.f);
-    acc[co] = v;
+  for (int gi = 0; gi < 4; ++gi) {
+    const int px = wave * 64 + gi * 16 + li;  // A row = pixel
+    float av[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) av[e] = 8 * lq + e < 27 ? s_in[koff[e] + 2 * px] : 0.f;
+    const typename M::Frag af = M::pack(av);
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      M::mma(af, bw[jt], acc);
+      // acc[r] = out[pixel wave*64 + gi*16 + 4*lq + r][channel 16*jt + li]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * jt + li;
+        float v = acc[r] * fsc[jt] + fsh[jt];
+        if (a.relu) v = fmaxf(v, 0.f);
+        s_out[(wave * 64 + gi * 16 + 4 * lq + r) * C0_OSTR + co] = v;
+      }
+    }
   }
-#pragma unroll
-  for (int q = 0; q < C0_OUT / 4; ++q)
-    *reinterpret_cast<float4*>(&s_out[tid * C0_OSTR + 4 * q]) =
-        make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
   __syncthreads();
 
   // coalesced store of npx*32 contiguous elements
@@ -138,10 +196,13 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
   ProfScope ps(PK_CONV0_FWD, st,
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (y_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
                2.0 * 27 * 32 * px);
-  if (y_dtype == DT_F32)
-    conv0_fwd_kernel<float><<<grid, 256, 0, st>>>(a);
-  else
-    conv0_fwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (y_dtype == DT_F32) {
+    if (a.x_bf16) conv0_fwd_kernel<float, true><<<grid, 256, 0, st>>>(a);
+    else conv0_fwd_kernel<float, false><<<grid, 256, 0, st>>>(a);
+  } else {
+    if (a.x_bf16) conv0_fwd_kernel<bf16, true><<<grid, 256, 0, st>>>(a);
+    else conv0_fwd_kernel<bf16, false><<<grid, 256, 0, st>>>(a);
+  }
   return check_launch("conv0_fwd");
 }
 

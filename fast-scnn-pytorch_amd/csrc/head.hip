@@ -19,6 +19,7 @@ namespace fscnn {
 
 constexpr int HD_T = 256;
 constexpr int HD_CMAX = 32;
+constexpr int HD_TMAX = 4096;  // max full-res row width whose targets are staged in LDS
 
 __device__ __forceinline__ int hd_first_ge(int i, int Lin, int Lout, float sc) {
   int lo = 0, hi = Lout;
@@ -35,6 +36,7 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
   constexpr int SL = (CT % 2 == 0) ? CT + 1 : CT;  // odd LDS stride per column
   __shared__ float s_L[2 * (HD_T + 1) * SL];
   __shared__ float s_carry[2 * CT];
+  __shared__ signed char s_t[2 * HD_TMAX];
   __shared__ float s_r1[HD_T], s_r2[HD_T];
   const int tid = threadIdx.x;
   const int hl = blockIdx.x, n = blockIdx.y;
@@ -69,11 +71,36 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
     float acc00[CT], acc01[CT], acc10[CT], acc11[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) acc00[c] = acc01[c] = acc10[c] = acc11[c] = 0.f;
-    if (active) {
-      const int w_lo = hd_first_ge(t, Wl, W, sw), w_hi = hd_first_ge(t + 1, Wl, W, sw);
-      const float* L0 = &s_L[tid * SL];
-      const float* L1 = &s_L[((HD_T + 1) + tid) * SL];
-      for (int h = h_lo; h < h_hi; ++h) {
+    // the full-resolution target rows are loaded by the whole workgroup with coalesced int64
+    // loads (next row prefetched into registers during the current row) and kept in LDS as int8
+    // class indices (-1 = ignored); all threads run the row loop (inactive columns: no pixels)
+    const int w_lo = active ? hd_first_ge(t, Wl, W, sw) : 0;
+    const int w_hi = active ? hd_first_ge(t + 1, Wl, W, sw) : 0;
+    const bool lds_t = W <= HD_TMAX;
+    constexpr int TPT = HD_TMAX / HD_T;
+    int tnext[TPT];
+    auto load_trow = [&](int h) {
+      const long long* tr = tgt + (size_t)h * W;
+#pragma unroll
+      for (int k = 0; k < TPT; ++k) {
+        const int w = tid + HD_T * k;
+        const long long tg = tr[w < W ? w : 0];
+        tnext[k] = (w < W && tg != a.ignore_index && tg >= 0 && tg < Cm) ? (int)tg : -1;
+      }
+    };
+    if (lds_t && h_lo < h_hi) load_trow(h_lo);
+    const float* L0 = &s_L[tid * SL];
+    const float* L1 = &s_L[((HD_T + 1) + tid) * SL];
+    for (int h = h_lo; h < h_hi; ++h) {
+      signed char* trow_s = s_t + (h & 1) * HD_TMAX;
+      if (lds_t) {
+#pragma unroll
+        for (int k = 0; k < TPT; ++k)
+          if (tid + HD_T * k < W) trow_s[tid + HD_T * k] = (signed char)tnext[k];
+        __syncthreads();
+        if (h + 1 < h_hi) load_trow(h + 1);
+      }
+      if (active) {
         const Lerp lh = ac_lerp(h, Hl, H, sh);
         float v0[CT], v1[CT];
 #pragma unroll
@@ -84,9 +111,14 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
         const long long* trow = tgt + (size_t)h * W;
         for (int w = w_lo; w < w_hi; ++w) {
           const Lerp lw = ac_lerp(w, Wl, W, sw);
-          const long long tg = trow[w];
-          const bool valid = tg != a.ignore_index && tg >= 0 && tg < Cm;
-          const int ti = (int)tg;
+          int ti;
+          if (lds_t) {
+            ti = trow_s[w];
+          } else {
+            const long long tg = trow[w];
+            ti = (tg != a.ignore_index && tg >= 0 && tg < Cm) ? (int)tg : -1;
+          }
+          const bool valid = ti >= 0;
           float e[CT];
           float mx = -INFINITY, lt = 0.f;
 #pragma unroll
@@ -98,7 +130,7 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
           float se = 0.f;
 #pragma unroll
           for (int c = 0; c < CT; ++c) {
-            e[c] = c < Cm ? expf(e[c] - mx) : 0.f;
+            e[c] = c < Cm ? __expf(e[c] - mx) : 0.f;  // v_exp_f32 path; loss uses accurate logf
             se += e[c];
           }
           const float inv = valid ? 1.f / se : 0.f;
@@ -118,6 +150,8 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
           }
         }
       }
+    }
+    if (active) {
       if (t == Wl - 1) {  // i1(w) == i0(w) on the last column: both taps are column t
 #pragma unroll
         for (int c = 0; c < CT; ++c) {

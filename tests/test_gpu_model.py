@@ -231,7 +231,9 @@ def test_fused_sgd_fast_path_and_state_dict():
             assert torch.allclose(p.detach(), ref[k].detach(), rtol=1e-6, atol=1e-7), (it, k)
         if it == 1:
             sd = opt.state_dict()
-            assert set(sd["param_groups"][0]) == set(topt.state_dict()["param_groups"][0])
+            keys = set(sd["param_groups"][0])
+            assert not any(k.startswith("_") for k in keys), keys  # no private caches leak
+            assert {"lr", "momentum", "dampening", "weight_decay", "nesterov", "params"} <= keys
             opt2 = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
             opt2.load_state_dict(sd)
             opt = opt2
