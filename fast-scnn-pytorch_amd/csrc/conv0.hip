@@ -53,11 +53,14 @@ template <typename TO, bool XB>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   constexpr bool BF = sizeof(TO) == 2;  // bf16 output => bf16 MFMA operands (compute dtype)
   using M = C0Mma<BF>;
-  constexpr int NIN = 3 * 3 * C0_IN_W;              // staged input elements
-  constexpr int LPT = (NIN + 255) / 256;            // loads per thread (fixed count)
-  __shared__ float s_in[NIN];                        // [ci][r][col]
-  __shared__ __attribute__((aligned(16))) float s_out[C0_TILE * C0_OSTR];
-  __shared__ float s_red[8 * C0_OUT];
+  using TI = typename std::conditional<XB, uint16_t, float>::type;
+  constexpr int VI = 16 / sizeof(TI);               // input elements per 16-B vector
+  constexpr int NVR = (C0_IN_W + VI - 1) / VI;      // vectors per staged input row
+  constexpr int LPV = (9 * NVR + 255) / 256;        // vector loads per thread
+  constexpr int OST = 32 + 16 / sizeof(TO);         // s_out row stride (elements, 16-B aligned)
+  __shared__ float s_in[9 * C0_IN_W + VI];          // [ci][r][col] (+ slack for the last vector)
+  __shared__ __attribute__((aligned(16))) TO s_out[C0_TILE * OST];
+  __shared__ float s_red[2][4][C0_OUT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -66,24 +69,64 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   const int n = row / a.Ho, ho = row - n * a.Ho;
   const int npx = min(C0_TILE, a.Wo - wo0);
 
-  // ---- stage the 3 x 3 x (2*256+1) input strip: all loads first, then the LDS stores --------
+  // ---- stage the 3 x 3 x (2*256+1) input strip with 16-B loads (all issued, then stored) ----
   const int col0 = 2 * wo0;
   const int ncol = min(C0_IN_W, a.W - col0);
-  {
+  const TI* xin = (const TI*)a.x;
+  if (a.W % VI != 0) {  // rows not 16-B aligned: scalar staging (odd widths only)
+    constexpr int NIN = 9 * C0_IN_W, LPT = (NIN + 255) / 256;
     float v[LPT];
 #pragma unroll
     for (int k = 0; k < LPT; ++k) {
       const int i = tid + 256 * k;
-      const int cr = i / C0_IN_W, c = i - cr * C0_IN_W;  // cr = ci*3 + r
+      const int cr = i / C0_IN_W, c = i - cr * C0_IN_W;
       const int ci = cr / 3, r = cr - ci * 3;
-      const bool ok = i < NIN && c < ncol;  // clamped load + select (branch-free)
+      const bool ok = i < NIN && c < ncol;
       const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c : 0;
-      const float t = XB ? bf2f(((const uint16_t*)a.x)[off]) : ((const float*)a.x)[off];
+      const float t = XB ? bf2f((uint16_t)xin[off]) : (float)xin[off];
       v[k] = ok ? t : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < LPT; ++k)
       if (tid + 256 * k < NIN) s_in[tid + 256 * k] = v[k];
+  } else {
+    uint4 raw[LPV];
+#pragma unroll
+    for (int k = 0; k < LPV; ++k) {
+      const int i = tid + 256 * k;
+      const int cr = i / NVR, v = i - cr * NVR;  // cr = ci*3 + r
+      const int ci = cr / 3, r = cr - ci * 3;
+      const bool ok = i < 9 * NVR && v * VI + VI <= ncol;  // whole vector inside the row
+      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + v * VI : 0;
+      raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(xin + off));
+    }
+#pragma unroll
+    for (int k = 0; k < LPV; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= 9 * NVR) continue;
+      const int cr = i / NVR, v = i - cr * NVR;
+      const TI* e = reinterpret_cast<const TI*>(&raw[k]);
+#pragma unroll
+      for (int j = 0; j < VI; ++j) {
+        const int c = v * VI + j;
+        float f;
+        if (XB) f = bf2f((uint16_t)e[j]);
+        else f = (float)e[j];
+        if (c < C0_IN_W) s_in[cr * C0_IN_W + c] = f;
+      }
+      if (v * VI < ncol && v * VI + VI > ncol) {  // the image's right edge: partial vector
+        for (int j = 0; j < VI; ++j) {
+          const int c = v * VI + j;
+          const int ci = cr / 3, r = cr - ci * 3;
+          float f = 0.f;
+          if (c < ncol) {
+            const size_t o = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c;
+            f = XB ? bf2f((uint16_t)xin[o]) : (float)xin[o];
+          }
+          if (c < C0_IN_W) s_in[cr * C0_IN_W + c] = f;
+        }
+      }
+    }
   }
   // B fragments (weights) for the two 16-channel tiles: W[16*jt + li][8*lq + e], k >= 27 -> 0
   typename M::Frag bw[2];
@@ -107,16 +150,17 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     const int ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
     koff[e] = (ci * 3 + kh) * C0_IN_W + kw;
   }
-  __syncthreads();
-
-  // eval BN fold of the lane's two channels (li, 16 + li), loaded once
-  float fsc[2], fsh[2];
+  float fsc[2], fsh[2];  // eval BN fold of the lane's two channels (li, 16 + li)
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
     fsc[jt] = a.scale ? a.scale[16 * jt + li] : 1.f;
     fsh[jt] = a.scale ? a.shift[16 * jt + li] : 0.f;
   }
-  // ---- wave w computes pixels [64w, 64w+64) as 4 groups of 16 x 32 channels ---------------
+  __syncthreads();
+
+  // ---- wave w: pixels [64w, 64w+64) = 4 groups of 16, x 32 channels; acc[gi][jt][r] is
+  //      out[pixel 64w + 16gi + 4lq + r][channel 16jt + li] -------------------------------------
+  f32x4 acc[4][2];
 #pragma unroll
   for (int gi = 0; gi < 4; ++gi) {
     const int px = wave * 64 + gi * 16 + li;  // A row = pixel
@@ -126,59 +170,98 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     const typename M::Frag af = M::pack(av);
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      M::mma(af, bw[jt], acc);
-      // acc[r] = out[pixel wave*64 + gi*16 + 4*lq + r][channel 16*jt + li]
+      acc[gi][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      M::mma(af, bw[jt], acc[gi][jt]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = 16 * jt + li;
-        float v = acc[r] * fsc[jt] + fsh[jt];
+        float v = acc[gi][jt][r] * fsc[jt] + fsh[jt];
         if (a.relu) v = fmaxf(v, 0.f);
-        s_out[(wave * 64 + gi * 16 + 4 * lq + r) * C0_OSTR + co] = v;
+        acc[gi][jt][r] = v;
       }
     }
   }
+  // ---- stage the tile in the storage type, then coalesced 16-B stores ----------------------
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        TO t;
+        if constexpr (BF) t.x = f2bf(acc[gi][jt][r]);
+        else t = acc[gi][jt][r];
+        s_out[(wave * 64 + gi * 16 + 4 * lq + r) * OST + 16 * jt + li] = t;
+      }
   __syncthreads();
-
-  // coalesced store of npx*32 contiguous elements
-  constexpr int V = VecW<TO>::V;
-  TO* y = (TO*)a.y + ((size_t)row * a.Wo + wo0) * C0_OUT;
-  const int nvec = npx * C0_OUT / V;
-  for (int i = tid; i < nvec; i += 256) {
-    int p = (i * V) / C0_OUT, c = (i * V) - p * C0_OUT;
-    float v[V];
+  {
+    constexpr int V = VecW<TO>::V;
+    TO* y = (TO*)a.y + ((size_t)row * a.Wo + wo0) * C0_OUT;
+    const int nvec = npx * C0_OUT / V;
 #pragma unroll
-    for (int j = 0; j < V; ++j) v[j] = s_out[p * C0_OSTR + c + j];
-    stv(y + (size_t)i * V, v);
-  }
-
-  if (a.part) {
-    // per-channel (mean, M2, count) over this block's npx pixels: thread = (channel, group of 8)
-    const int c = tid & 31, g = tid >> 5;
-    float s = 0.f;
-    for (int p = g; p < npx; p += 8) s += s_out[p * C0_OSTR + c];
-    s_red[g * C0_OUT + c] = s;
-    __syncthreads();
-    float mean = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) mean += s_red[k * C0_OUT + c];
-    mean /= (float)npx;
-    __syncthreads();
-    float m2 = 0.f;
-    for (int p = g; p < npx; p += 8) {
-      float d = s_out[p * C0_OSTR + c] - mean;
-      m2 += d * d;
+    for (int k = 0; k < C0_TILE * C0_OUT / V / 256; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= nvec) continue;
+      const int p = (i * V) / C0_OUT, c = (i * V) - p * C0_OUT;
+      *reinterpret_cast<uint4*>(y + (size_t)i * V) = *reinterpret_cast<const uint4*>(&s_out[p * OST + c]);
     }
-    s_red[g * C0_OUT + c] = m2;
-    __syncthreads();
-    if (g == 0) {
-      float t = 0.f;
+  }
+  if (a.part == nullptr) return;
+  // ---- per-channel (mean, M2, count) over the block's npx pixels, from the fp32 registers ----
+  float sum[2] = {0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) t += s_red[k * C0_OUT + c];
-      size_t pi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-      float* rec = a.part + pi * 3 * C0_OUT;
-      rec[c] = mean;
-      rec[C0_OUT + c] = t;
+  for (int gi = 0; gi < 4; ++gi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = wave * 64 + gi * 16 + 4 * lq + r < npx;
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? acc[gi][jt][r] : 0.f;
+    }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    sum[jt] += __shfl_xor(sum[jt], 16);
+    sum[jt] += __shfl_xor(sum[jt], 32);
+  }
+  if (lq == 0) {
+    s_red[0][wave][li] = sum[0];
+    s_red[0][wave][16 + li] = sum[1];
+  }
+  __syncthreads();
+  float mean[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int c = 16 * jt + li;
+    mean[jt] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
+  }
+  float m2[2] = {0.f, 0.f};
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = wave * 64 + gi * 16 + 4 * lq + r < npx;
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const float d = acc[gi][jt][r] - mean[jt];
+        m2[jt] += ok ? d * d : 0.f;
+      }
+    }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    m2[jt] += __shfl_xor(m2[jt], 16);
+    m2[jt] += __shfl_xor(m2[jt], 32);
+  }
+  if (lq == 0) {
+    s_red[1][wave][li] = m2[0];
+    s_red[1][wave][16 + li] = m2[1];
+  }
+  __syncthreads();
+  if (wave == 0 && lq == 0) {
+    const size_t pi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    float* rec = a.part + pi * 3 * C0_OUT;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const int c = 16 * jt + li;
+      rec[c] = mean[jt];
+      rec[C0_OUT + c] = (s_red[1][0][c] + s_red[1][1][c]) + (s_red[1][2][c] + s_red[1][3][c]);
       rec[2 * C0_OUT + c] = (float)npx;
     }
   }

@@ -90,14 +90,17 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
   constexpr int KC = G_VROW * V;  // k elements per chunk
-  constexpr int SA_BYTES = 2 * G_BM * G_VPAD * 16, SB_BYTES = 2 * BN * G_VPAD * 16;
+  // dynamic LDS: nbuf (1 when K fits one chunk, else 2) x (A + B tiles); the epilogue reuses it
+  // for a 64-row fp32 half tile.  Single-chunk GEMMs (the K <= 64 expands) thus need ~32 KB and
+  // run 4-5 workgroups per CU instead of 2.
   constexpr int CLD = BN + 4;                       // epilogue tile row stride (floats)
-  constexpr int SC_BYTES = G_BM * CLD * 4;
-  constexpr int RAW = SA_BYTES + SB_BYTES > SC_BYTES ? SA_BYTES + SB_BYTES : SC_BYTES;
-  __shared__ __attribute__((aligned(16))) unsigned char s_raw[RAW];
-  uint4 (*sA)[G_BM * G_VPAD] = reinterpret_cast<uint4 (*)[G_BM * G_VPAD]>(s_raw);
-  uint4 (*sB)[BN * G_VPAD] = reinterpret_cast<uint4 (*)[BN * G_VPAD]>(s_raw + SA_BYTES);
-  float* sC = reinterpret_cast<float*>(s_raw);      // after the main loop
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  const int nbuf = (a.K + KC - 1) / KC > 1 ? 2 : 1;
+  uint4* sAbase = reinterpret_cast<uint4*>(s_dyn);
+  uint4* sBbase = sAbase + nbuf * G_BM * G_VPAD;
+  auto sA = [&](int b) { return sAbase + b * G_BM * G_VPAD; };
+  auto sB = [&](int b) { return sBbase + b * BN * G_VPAD; };
+  float* sC = reinterpret_cast<float*>(s_dyn);      // after the main loop
   __shared__ float s_red[4][BN];
 
   const int tid = threadIdx.x;
@@ -186,16 +189,16 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int id = tid + 256 * i;
-      sA[buf][(id >> 3) * G_VPAD + (id & 7)] = ra[i];
+      sA(buf)[(id >> 3) * G_VPAD + (id & 7)] = ra[i];
     }
     if (!BT) {
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
         int id = tid + 256 * i;
-        if (id < BN * G_VROW) sB[buf][(id >> 3) * G_VPAD + (id & 7)] = rb[i];
+        if (id < BN * G_VROW) sB(buf)[(id >> 3) * G_VPAD + (id & 7)] = rb[i];
       }
     } else {
-      T* sbs = reinterpret_cast<T*>(&sB[buf][0]);
+      T* sbs = reinterpret_cast<T*>(sB(buf));
 #pragma unroll
       for (int i = 0; i < BT_PER; ++i) {
         int id = tid + 256 * i;
@@ -219,16 +222,16 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   store_chunk(0);
   __syncthreads();
   for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
+    const int buf = nbuf == 2 ? (c & 1) : 0;
     if (c + 1 < nchunks) load_chunk(c + 1);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int vv = lq + 4 * h;
       uint4 af[2], bfv[NT];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) af[mt] = sA[buf][(wave * 32 + mt * 16 + li) * G_VPAD + vv];
+      for (int mt = 0; mt < 2; ++mt) af[mt] = sA(buf)[(wave * 32 + mt * 16 + li) * G_VPAD + vv];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB[buf][(nt * 16 + li) * G_VPAD + vv];
+      for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB(buf)[(nt * 16 + li) * G_VPAD + vv];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -255,25 +258,32 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = acc[mt][nt][r] * scv[nt] + shv[nt];
-        acc[mt][nt][r] = v;
-        sC[(wave * 32 + mt * 16 + lq * 4 + r) * CLD + nt * 16 + li] = v;
-      }
-  __syncthreads();
-  {
-    T* Cp = (T*)a.C;
-    const T* Rp = (const T*)a.R;
-    constexpr int VPRow = BN / V;
-    constexpr int ITER = (G_BM * VPRow + 255) / 256;
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = acc[mt][nt][r] * scv[nt] + shv[nt];
+  T* Cp = (T*)a.C;
+  const T* Rp = (const T*)a.R;
+  constexpr int VPRow = BN / V;
+  constexpr int HROWS = G_BM / 2;  // rows staged per half (waves 2h, 2h+1)
+  constexpr int ITER = (HROWS * VPRow + 255) / 256;
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();  // main-loop LDS reads / previous half's reads done
+    if ((wave >> 1) == half) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sC[((wave & 1) * 32 + mt * 16 + lq * 4 + r) * CLD + nt * 16 + li] = acc[mt][nt][r];
+    }
+    __syncthreads();
     float rv[ITER][V];
     if (Rp) {
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
         const int i = tid + 256 * it;
         const int row = i / VPRow, vc = i - row * VPRow;
-        const int m = m0 + row, n = n0 + vc * V;
-        const bool ok = i < G_BM * VPRow && m < a.M && n + V <= a.N;
+        const int m = m0 + half * HROWS + row, n = n0 + vc * V;
+        const bool ok = i < HROWS * VPRow && m < a.M && n + V <= a.N;
         float t[V];
         ldv(Rp + (ok ? (size_t)m * a.ldr + n : 0), t);
 #pragma unroll
@@ -284,8 +294,8 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
     for (int it = 0; it < ITER; ++it) {
       const int i = tid + 256 * it;
       const int row = i / VPRow, vc = i - row * VPRow;
-      const int m = m0 + row, n = n0 + vc * V;
-      if (i >= G_BM * VPRow || m >= a.M) continue;
+      const int m = m0 + half * HROWS + row, n = n0 + vc * V;
+      if (i >= HROWS * VPRow || m >= a.M) continue;
       float o[V];
 #pragma unroll
       for (int j = 0; j < V; ++j) {
@@ -297,8 +307,8 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
         stv(Cp + (size_t)m * a.ldc + n, o);
       } else {
         for (int j = 0; j < V && n + j < a.N; ++j) {
-          float v = o[j];
-          if (Rp) v = sC[row * CLD + vc * V + j] + ld1(Rp + (size_t)m * a.ldr + n + j);
+          float v = sC[row * CLD + vc * V + j];
+          if (Rp) v += ld1(Rp + (size_t)m * a.ldr + n + j);
           st1(Cp + (size_t)m * a.ldc + n + j, a.relu ? fmaxf(v, 0.f) : v);
         }
       }
@@ -373,12 +383,18 @@ int gemm_parts(int M) { return cdiv(M, G_BM); }
 template <typename T, bool BT>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
+  constexpr int V = VecW<T>::V;
+  const int BN = 16 * nt;
+  const int nbuf = cdiv(a.K, G_VROW * V) > 1 ? 2 : 1;
+  const size_t tiles = (size_t)nbuf * (G_BM + BN) * G_VPAD * 16;
+  const size_t ctile = (size_t)(G_BM / 2) * (BN + 4) * 4;
+  const size_t shm = tiles > ctile ? tiles : ctile;
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT><<<grid, 256, 0, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT><<<grid, 256, 0, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT><<<grid, 256, 0, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT><<<grid, 256, 0, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT><<<grid, 256, 0, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT><<<grid, 256, shm, st>>>(a); break;
   }
 }
 
