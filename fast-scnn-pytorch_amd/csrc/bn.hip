@@ -57,7 +57,7 @@ __device__ __forceinline__ void bn_sum3(double& n, double& s1, double& s2, const
   }
 }
 
-__global__ __launch_bounds__(256) void bn_stats_fold_kernel(float* part, int P, int C, int Q) {
+__device__ __forceinline__ void bn_stats_fold_body(float* part, int P, int C, int Q) {
   __shared__ double sh[3][4][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = blockIdx.x * 64 + cx, q = blockIdx.y;
@@ -103,10 +103,15 @@ __global__ __launch_bounds__(256) void bn_stats_fold_kernel(float* part, int P, 
   }
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
+__global__ __launch_bounds__(256) void bn_stats_fold_kernel(float* part, int P, int C, int Q) {
+  bn_stats_fold_body(part, P, C, Q);
+}
+
+// merge the Q folded records of channels [64*chunk, 64*chunk + 64) and finish (block 64 x 4)
+__device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q, int chunk) {
   __shared__ Welford sh[4][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
-  const int c = blockIdx.x * 64 + cx;
+  const int c = chunk * 64 + cx;
   Welford w = {0.0, 0.0, 0.0};
   if (c < a.C) {
     // Q <= BN_Q = 64: the thread's <= 16 records are loaded at once, then merged in order
@@ -147,6 +152,36 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int 
   if (a.nbt && c == 0) a.nbt[0] += 1;
 }
 
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
+  bn_finalize_chunk(a, Q, blockIdx.x);
+}
+
+// Fold + finalize in ONE launch: every (chunk, q) workgroup folds its residue class into slot q,
+// publishes it (agent-scope release, then a per-chunk arrival counter); the last workgroup of a
+// chunk to arrive acquires and finishes that chunk, then re-arms the counter for the next BN.
+// (Placement-independent release/acquire protocol; counters zeroed once per executor call.)
+__device__ __forceinline__ bool bn_last_arrival(unsigned* ctr) {
+  __shared__ int s_last;
+  __threadfence();  // release: this thread's slot writes are visible device-wide
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    const unsigned prev = atomicAdd(&ctr[blockIdx.x], 1u);
+    s_last = prev == gridDim.y - 1;
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  __threadfence();  // acquire: other workgroups' slots
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bn_stats_fold_fin_kernel(BnFinalizeArgs a, int Q,
+                                                                unsigned* ctr) {
+  bn_stats_fold_body(a.part, a.P, a.C, Q);
+  if (!bn_last_arrival(ctr)) return;
+  bn_finalize_chunk(a, Q, blockIdx.x);
+  if (threadIdx.x == 0 && threadIdx.y == 0) ctr[blockIdx.x] = 0;
+}
+
 int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
   if (a.P <= 0 || a.C <= 0) {
     set_error("bn_finalize: P=%d C=%d", a.P, a.C);
@@ -155,6 +190,10 @@ int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
   int Q = a.P;
   if (a.P > BN_Q) {
     Q = BN_Q;
+    if (a.counters) {
+      bn_stats_fold_fin_kernel<<<dim3(cdiv(a.C, 64), Q), dim3(64, 4), 0, st>>>(a, Q, a.counters);
+      return check_launch("bn_finalize");
+    }
     bn_stats_fold_kernel<<<dim3(cdiv(a.C, 64), Q), dim3(64, 4), 0, st>>>(a.part, a.P, a.C, Q);
   }
   bn_finalize_kernel<<<cdiv(a.C, 64), dim3(64, 4), 0, st>>>(a, Q);
@@ -236,7 +275,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
     }
     const long long mb = (long long)blockIdx.y * a.rows_per_block;
     const long long me = min(a.M, mb + a.rows_per_block);
-    constexpr int U = 4;
+    constexpr int U = 4;  // rows per batch (8 measured slower: 256 VGPRs, occupancy 2)
     for (long long m0 = mb + threadIdx.y; m0 < me; m0 += U * BY) {
       float g[U][V], z[U][V], mk[U][V];
       float ok[U];
@@ -322,7 +361,7 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
 
 // merge [P][2][C] -> dgamma, dbeta (written to the gradient arena) and coef [2][C]; same
 // two-level in-place scheme as bn_finalize (fold residue classes mod Q, then fixed-order merge)
-__global__ __launch_bounds__(256) void bn_bwd_fold_kernel(float* part, int P, int C, int Q) {
+__device__ __forceinline__ void bn_bwd_fold_body(float* part, int P, int C, int Q) {
   __shared__ double sh[2][4][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = blockIdx.x * 64 + cx, q = blockIdx.y;
@@ -354,12 +393,17 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_kernel(float* part, int P, in
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* part, int Q, int C,
-                                                              double count, float* dgamma,
-                                                              float* dbeta, float* coef) {
-  __shared__ double sh[2][4][64];
+__global__ __launch_bounds__(256) void bn_bwd_fold_kernel(float* part, int P, int C, int Q) {
+  bn_bwd_fold_body(part, P, C, Q);
+}
+
+__device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, int C, double count,
+                                                      float* dgamma, float* dbeta, float* coef,
+                                                      int chunk) {
+  __shared__ double shf[2][4][64];
+  double (*sh)[4][64] = shf;
   const int cx = threadIdx.x, ty = threadIdx.y;
-  const int c = blockIdx.x * 64 + cx;
+  const int c = chunk * 64 + cx;
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     float a1[BN_Q / 4], a2[BN_Q / 4];
@@ -389,11 +433,33 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* part,
   coef[C + c] = (float)(s2 / count);
 }
 
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* part, int Q, int C,
+                                                              double count, float* dgamma,
+                                                              float* dbeta, float* coef) {
+  bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_fold_fin_kernel(float* part, int P, int C, int Q,
+                                                              double count, float* dgamma,
+                                                              float* dbeta, float* coef,
+                                                              unsigned* ctr) {
+  bn_bwd_fold_body(part, P, C, Q);
+  if (!bn_last_arrival(ctr)) return;
+  bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
+  if (threadIdx.x == 0 && threadIdx.y == 0) ctr[blockIdx.x] = 0;
+}
+
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
-                    float* coef, hipStream_t st) {
+                    float* coef, hipStream_t st, unsigned* counters) {
   int Q = P;
   if (P > BN_Q) {
     Q = BN_Q;
+    if (counters) {
+      bn_bwd_fold_fin_kernel<<<dim3(cdiv(C, 64), Q), dim3(64, 4), 0, st>>>(part, P, C, Q, count,
+                                                                            dgamma, dbeta, coef,
+                                                                            counters);
+      return check_launch("bn_bwd_finalize");
+    }
     bn_bwd_fold_kernel<<<dim3(cdiv(C, 64), Q), dim3(64, 4), 0, st>>>(part, P, C, Q);
   }
   bn_bwd_finalize_kernel<<<cdiv(C, 64), dim3(64, 4), 0, st>>>(part, Q, C, count, dgamma, dbeta, coef);

@@ -345,7 +345,7 @@ __device__ __forceinline__ bf16 cw_cvt<bf16>(float v) {
   return r;
 }
 
-template <typename T>
+template <typename T, bool XB>
 __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
   constexpr int LD = CwOps<T>::LD;
   constexpr int V = VecW<T>::V;
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const size_t o = ok ? base + kw : 0;  // clamped load + select (branch-free)
-          const float v = a.x_bf16 ? bf2f(((const uint16_t*)a.x)[o]) : ((const float*)a.x)[o];
+          const float v = XB ? bf2f(((const uint16_t*)a.x)[o]) : ((const float*)a.x)[o];
           xv[cr * 3 + kw] = ok ? v : 0.f;
         }
       }
@@ -459,10 +459,13 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
   ProfScope ps(PK_CONV0_WGRAD, st,
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (dz_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
                2.0 * 27 * 32 * px);
-  if (dz_dtype == DT_F32)
-    conv0_wgrad_kernel<float><<<P, 256, 0, st>>>(a);
-  else
-    conv0_wgrad_kernel<bf16><<<P, 256, 0, st>>>(a);
+  if (dz_dtype == DT_F32) {
+    if (a.x_bf16) conv0_wgrad_kernel<float, true><<<P, 256, 0, st>>>(a);
+    else conv0_wgrad_kernel<float, false><<<P, 256, 0, st>>>(a);
+  } else {
+    if (a.x_bf16) conv0_wgrad_kernel<bf16, true><<<P, 256, 0, st>>>(a);
+    else conv0_wgrad_kernel<bf16, false><<<P, 256, 0, st>>>(a);
+  }
   return check_launch("conv0_wgrad");
 }
 

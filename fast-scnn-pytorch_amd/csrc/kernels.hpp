@@ -107,6 +107,7 @@ struct BnFinalizeArgs {
   float* invstd;      // [C]
   float* scale;       // [C] gamma*invstd
   float* shift;       // [C] beta - mean*scale
+  unsigned* counters = nullptr;  // >= cdiv(C,64) zeroed arrival counters: one-launch fold+finalize
 };
 
 struct BnApplyArgs {
@@ -250,7 +251,7 @@ int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st);
 int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
 int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
-                    float* coef, hipStream_t st);
+                    float* coef, hipStream_t st, unsigned* counters = nullptr);
 int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st);
 
 int up_nhwc(const UpArgs& a, int dtype, hipStream_t st);

@@ -242,7 +242,10 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
   }
-  if (train) pl.seed_slot = A.get(64);
+  if (train) {
+    pl.seed_slot = A.get(64);
+    pl.fcnt = A.get(64 * 4);
+  }
   pl.ws_bytes = A.top;
   auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
     pl.named.push_back({n, off, rows, cols, ld, bws});
@@ -334,6 +337,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     size_t c0s = (size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864;
     if (c0s > slab) slab = c0s;
     pl.slab = B.get(slab * 4);
+    pl.bcnt = B.get(64 * 4);
     // BN backward partials: max P*2*C
     size_t bnp = 0;
     auto bn_upd = [&](const Unit& u) {
@@ -414,7 +418,8 @@ struct Exec {
     f.momentum = r.momentum;
     f.bias = nullptr;
     f.mean = Wf(u.mean); f.invstd = Wf(u.invstd); f.scale = Wf(u.scale); f.shift = Wf(u.shift);
-    return bn_finalize(f, r.st);
+    return bn_finalize(f, r.st);  // two launches: the single-launch arrival-counter variant
+                                  // (f.counters) measured slower (agent-scope release per block)
   }
   int apply(const Unit& u, bool relu, const void* res = nullptr, int ldres = 0) {
     BnApplyArgs a{};

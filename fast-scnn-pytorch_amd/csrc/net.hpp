@@ -84,6 +84,7 @@ struct Plan {
          logits = 0, aux_drop = 0, aux_logits = 0, pbf = 0, fold_tmp = 0;
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
+  size_t fcnt = 0, bcnt = 0;        // BN fold+finalize arrival counters (ws / bws), 64 each
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
