@@ -85,8 +85,8 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
   }
 }
 
-template <typename T, int NT, bool BT>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
+template <typename T, int NT, bool BT, bool BS>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
   constexpr int KC = G_VROW * V;  // k elements per chunk
@@ -262,8 +262,33 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
   T* Cp = (T*)a.C;
   const T* Rp = (const T*)a.R;
   constexpr int VPRow = BN / V;
-  constexpr int HROWS = G_BM / 2;  // rows staged per half (waves 2h, 2h+1)
-  constexpr int ITER = (HROWS * VPRow + 255) / 256;
+  constexpr int HROWS = G_BM / 2;                // rows staged per half (waves 2h, 2h+1)
+  constexpr int RG = 256 / VPRow;                // row groups; a thread keeps ONE column vector
+  constexpr int NRT = (HROWS + RG - 1) / RG;     // rows per thread per half
+  const int vc = tid % VPRow, rg = tid / VPRow;
+  const bool tact = rg < RG;
+  const int n = n0 + vc * V;
+  const bool nfull = n + V <= a.N;
+  constexpr bool bst = BS;  // fused BN-backward partials (dgrad producing a BN's dy)
+  const T* Bz = (const T*)a.bz;
+  // ReLU mask of the BN output recomputed as fmaf(z, scale, shift) > 0 (mode 2); mode 0 (no
+  // ReLU) uses scale 0, shift 1 so both are the same select
+  float bmu[bst ? V : 1], bis[bst ? V : 1], bsc[bst ? V : 1], bsh[bst ? V : 1];
+  float s1[bst ? V : 1], s2[bst ? V : 1];
+  if constexpr (bst) {
+    const bool m2 = a.bmode == 2;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int nc = n + j < a.N ? n + j : 0;
+      bmu[j] = a.bmean[nc];
+      bis[j] = a.binvstd[nc];
+      const float sc = a.bscale[nc], sh = a.bshift[nc];
+      bsc[j] = m2 ? sc : 0.f;
+      bsh[j] = m2 ? sh : 1.f;
+      s1[j] = 0.f;
+      s2[j] = 0.f;
+    }
+  }
   for (int half = 0; half < 2; ++half) {
     __syncthreads();  // main-loop LDS reads / previous half's reads done
     if ((wave >> 1) == half) {
@@ -276,43 +301,85 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmArgs a) {
             sC[((wave & 1) * 32 + mt * 16 + lq * 4 + r) * CLD + nt * 16 + li] = acc[mt][nt][r];
     }
     __syncthreads();
-    float rv[ITER][V];
-    if (Rp) {
+    // all global loads of the half (residual, BN z / mask) first: clamped + selected, no branch
+    uint4 rr[NRT], zr[bst ? NRT : 1];
 #pragma unroll
-      for (int it = 0; it < ITER; ++it) {
-        const int i = tid + 256 * it;
-        const int row = i / VPRow, vc = i - row * VPRow;
-        const int m = m0 + half * HROWS + row, n = n0 + vc * V;
-        const bool ok = i < HROWS * VPRow && m < a.M && n + V <= a.N;
-        float t[V];
-        ldv(Rp + (ok ? (size_t)m * a.ldr + n : 0), t);
-#pragma unroll
-        for (int j = 0; j < V; ++j) rv[it][j] = ok ? t[j] : 0.f;
-      }
+    for (int k = 0; k < NRT; ++k) {
+      const int row = rg + k * RG;
+      const int m = m0 + half * HROWS + row;
+      const bool ok = tact && row < HROWS && m < a.M && nfull;
+      if (Rp) rr[k] = sel4(ok, *reinterpret_cast<const uint4*>(Rp + (ok ? (size_t)m * a.ldr + n : 0)));
+      if constexpr (bst)
+        zr[k] = sel4(ok, *reinterpret_cast<const uint4*>(Bz + (ok ? (size_t)m * a.ldbz + n : 0)));
     }
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      const int i = tid + 256 * it;
-      const int row = i / VPRow, vc = i - row * VPRow;
-      const int m = m0 + half * HROWS + row, n = n0 + vc * V;
-      if (i >= HROWS * VPRow || m >= a.M) continue;
-      float o[V];
+    for (int k = 0; k < NRT; ++k) {
+      const int row = rg + k * RG;
+      const int m = m0 + half * HROWS + row;
+      if (!tact || row >= HROWS || m >= a.M) continue;
+      float o[V], rv[V];
+      if (Rp) unpackv(rr[k], rv);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         float v = sC[row * CLD + vc * V + j];
-        if (Rp) v += rv[it][j];
+        if (Rp) v += rv[j];
         o[j] = a.relu ? fmaxf(v, 0.f) : v;
       }
-      if (n + V <= a.N) {
+      if (nfull) {
         stv(Cp + (size_t)m * a.ldc + n, o);
+        if constexpr (bst) {  // BN-backward partials of the value as stored (rounded to T)
+          float z[V];
+          unpackv(zr[k], z);
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            float gv;
+            if constexpr (V == 8) gv = bf2f(f2bf(o[j]));
+            else gv = o[j];
+            gv = fmaf(z[j], bsc[j], bsh[j]) > 0.f ? gv : 0.f;
+            s1[j] += gv;
+            s2[j] += gv * (z[j] - bmu[j]) * bis[j];
+          }
+        }
       } else {
         for (int j = 0; j < V && n + j < a.N; ++j) {
           float v = sC[row * CLD + vc * V + j];
           if (Rp) v += ld1(Rp + (size_t)m * a.ldr + n + j);
-          st1(Cp + (size_t)m * a.ldc + n + j, a.relu ? fmaxf(v, 0.f) : v);
+          v = a.relu ? fmaxf(v, 0.f) : v;
+          st1(Cp + (size_t)m * a.ldc + n + j, v);
+          if constexpr (bst) {
+            const float z = ld1(Bz + (size_t)m * a.ldbz + n + j);
+            float gv = ld1(Cp + (size_t)m * a.ldc + n + j);
+            gv = fmaf(z, bsc[j], bsh[j]) > 0.f ? gv : 0.f;
+            s1[j] += gv;
+            s2[j] += gv * (z - bmu[j]) * bis[j];
+          }
         }
       }
     }
+  }
+  if constexpr (bst) {
+    // fixed-order column reduction over the RG row groups -> one record per 128-row tile
+    __syncthreads();
+    float* red = sC;  // [2][RG][BN]
+    if (tact) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        red[rg * BN + vc * V + j] = s1[j];
+        red[RG * BN + rg * BN + vc * V + j] = s2[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int g2 = 0; g2 < RG; ++g2) {
+        t1 += red[g2 * BN + tid];
+        t2 += red[RG * BN + g2 * BN + tid];
+      }
+      float* rec = a.bpart + (size_t)tm * 2 * a.N;
+      rec[n0 + tid] = t1;
+      rec[a.N + n0 + tid] = t2;
+    }
+    return;  // a dgrad output never carries forward statistics (acc dies with the epilogue)
   }
   if (a.part == nullptr) return;
 
@@ -380,21 +447,23 @@ static int pick_nt(int N) {
 
 int gemm_parts(int M) { return cdiv(M, G_BM); }
 
-template <typename T, bool BT>
+template <typename T, bool BT, bool BS>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   constexpr int V = VecW<T>::V;
   const int BN = 16 * nt;
   const int nbuf = cdiv(a.K, G_VROW * V) > 1 ? 2 : 1;
   const size_t tiles = (size_t)nbuf * (G_BM + BN) * G_VPAD * 16;
-  const size_t ctile = (size_t)(G_BM / 2) * (BN + 4) * 4;
+  size_t ctile = (size_t)(G_BM / 2) * (BN + 4) * 4;
+  const size_t red = (size_t)2 * 256 * V * 4;  // bwd-BN column reduction (2 x RG x BN floats)
+  if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT><<<grid, 256, shm, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT, BS><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS><<<grid, 256, shm, st>>>(a); break;
   }
 }
 
@@ -417,12 +486,18 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   ProfScope ps(PK_GEMM_NT, st, E * (M * K + M * N * (a.R ? 2 : 1) + N * K), 2.0 * M * N * K);
+  const bool bs = a.bpart != nullptr;
+  if (bs && (a.part || !a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
+             (a.bmode != 0 && a.bmode != 2) || a.ldbz % V || !a.b_trans)) {
+    set_error("gemm_nt: inconsistent fused BN-backward arguments");
+    return E_INVALID;
+  }
   if (dtype == DT_F32) {
-    if (a.b_trans) launch_nt<float, true>(a, nt, st);
-    else launch_nt<float, false>(a, nt, st);
+    if (a.b_trans) { if (bs) launch_nt<float, true, true>(a, nt, st); else launch_nt<float, true, false>(a, nt, st); }
+    else launch_nt<float, false, false>(a, nt, st);
   } else {
-    if (a.b_trans) launch_nt<bf16, true>(a, nt, st);
-    else launch_nt<bf16, false>(a, nt, st);
+    if (a.b_trans) { if (bs) launch_nt<bf16, true, true>(a, nt, st); else launch_nt<bf16, true, false>(a, nt, st); }
+    else launch_nt<bf16, false, false>(a, nt, st);
   }
   return check_launch("gemm_nt");
 }

@@ -64,6 +64,14 @@ struct GemmArgs {
   void* C;
   int ldc;
   float* part;          // BN partial records [gridDim.x][3][N] or null
+  // Fused BatchNorm-backward partial sums of the OUTPUT, when this GEMM produces the dy of a BN
+  // (dgrad): per 128-row tile, s1[n] = sum g*mask, s2[n] = sum g*mask*(z-mean)*invstd with g the
+  // stored (rounded) output.  bpart [cdiv(M,128)][2][N] or null.
+  float* bpart = nullptr;
+  const void* bz = nullptr; int ldbz = 0;        // z of that BN (pre-BN forward tensor)
+  const float* bmean = nullptr; const float* binvstd = nullptr;
+  const float* bscale = nullptr; const float* bshift = nullptr;  // forward BN affine (mode 2)
+  int bmode = 0;        // 0 no ReLU, 2 relu_z: mask = fmaf(z, bscale, bshift) > 0
 };
 
 struct GemmTnArgs {

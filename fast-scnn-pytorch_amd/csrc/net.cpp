@@ -344,6 +344,8 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
       int rpb;
       size_t s = (size_t)bn_bwd_parts(u.M, u.C, dtype, &rpb) * 2 * u.C;
       if (s > bnp) bnp = s;
+      s = (size_t)gemm_parts((int)u.M) * 2 * u.C;  // fused dgrad-epilogue records
+      if (s > bnp) bnp = s;
     };
     bn_upd(pl.c0); bn_upd(pl.l1dw); bn_upd(pl.l1pw); bn_upd(pl.l2dw); bn_upd(pl.l2pw);
     for (int i = 0; i < 9; ++i) { bn_upd(pl.lbe[i]); bn_upd(pl.lbd[i]); bn_upd(pl.lbp[i]); }
@@ -383,6 +385,12 @@ namespace {
     int rc__ = (x);            \
     if (rc__) return rc__;     \
   } while (0)
+
+// fused BN-backward partials: the dgrad GEMM producing the dy of unit `u` emits its records
+struct BTarget {
+  const Unit* u = nullptr;
+  int mode = 0;  // 0 no ReLU, 2 relu_z (mask recomputed from z)
+};
 
 struct Exec {
   const Plan& pl;
@@ -622,8 +630,10 @@ struct Exec {
 
   // ================================ backward ===============================================
   // BN backward of unit u: dy = u.ga (ld u.ga_ld), mask = relu output (or null) → dz scratch
+  // P_pre > 0: the producer of dy (a dgrad GEMM with bpart set) already wrote P_pre partial
+  // records into bnpart, so the reduce pass is skipped.
   int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
-             int ldmask, void* dz, bool relu_z = false) {
+             int ldmask, void* dz, bool relu_z = false, int P_pre = 0) {
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
     b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
@@ -631,9 +641,12 @@ struct Exec {
     b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
     b.shift = Wf(u.shift); b.relu_z = relu_z;
     b.part = (float*)Bw(pl.bnpart);
-    TRY(bn_bwd_reduce(b, dt, r.st));
-    int rpb;
-    int P = bn_bwd_parts(u.M, u.C, dt, &rpb);
+    int P = P_pre;
+    if (!P) {
+      TRY(bn_bwd_reduce(b, dt, r.st));
+      int rpb;
+      P = bn_bwd_parts(u.M, u.C, dt, &rpb);
+    }
     float* coef = (float*)Bw(pl.coef);
     TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b), coef, r.st));
     b.coef = coef;
@@ -641,12 +654,19 @@ struct Exec {
     return bn_bwd_apply(b, dt, r.st);
   }
   // BN whose output is relu(BN(z)) with no second branch: the ReLU mask is recomputed from z
-  int bn_bwd_relu(const Unit& u, const BnL& bn, const void* dy, int lddy, void* dz) {
-    return bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, true);
+  int bn_bwd_relu(const Unit& u, const BnL& bn, const void* dy, int lddy, void* dz, int P_pre = 0) {
+    return bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, true, P_pre);
+  }
+  void set_btarget(GemmArgs& g, const BTarget& t) {
+    const Unit& u = *t.u;
+    g.bpart = (float*)Bw(pl.bnpart);
+    g.bz = W(u.z); g.ldbz = u.C;
+    g.bmean = Wf(u.mean); g.binvstd = Wf(u.invstd); g.bscale = Wf(u.scale); g.bshift = Wf(u.shift);
+    g.bmode = t.mode;
   }
   // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
   int pw_bwd(const ConvL& c, long long M, const void* dz, int lddz, const void* X, int ldx,
-             void* dX, int lddx, const void* R = nullptr, int ldr = 0) {
+             void* dX, int lddx, const void* R = nullptr, int ldr = 0, BTarget bt = BTarget()) {
     GemmTnArgs t{};
     t.M = (int)M; t.N = c.cout; t.K = c.cin; t.D = dz; t.ldd = lddz; t.X = X; t.ldx = ldx;
     t.slab = (float*)Bw(pl.slab);
@@ -664,8 +684,12 @@ struct Exec {
     g.B = Wg(c); g.ldb = c.cin; g.b_trans = 1;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
+    if (bt.u && train) set_btarget(g, bt);
     return gemm_nt(g, dt, r.st);
   }
+  BTarget relu_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 2; return t; }
+  BTarget plain_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 0; return t; }
+  static int pre(const Unit& u) { return gemm_parts((int)u.M); }
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
   int dw_bwd(const ConvL& c, int C, const void* dz, const void* X, int H, int Wd, int Ho, int Wo,
              int stride, void* dX) {
@@ -712,20 +736,25 @@ struct Exec {
     }
     // classifier dsconv2, dsconv1
     TRY(bn_bwd_relu(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, dz));
-    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, W(pl.c2dw.a), 128, Bw(pl.c2dw.ga), 128));
-    TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz));
+    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, W(pl.c2dw.a), 128, Bw(pl.c2dw.ga), 128, nullptr, 0,
+               relu_target(pl.c2dw)));
+    TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz, pre(pl.c2dw)));
     TRY(dw_bwd(net.cls2.dw, 128, dz, W(pl.c1pw.a), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
     TRY(bn_bwd_relu(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, dz));
-    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, W(pl.c1dw.a), 128, Bw(pl.c1dw.ga), 128));
-    TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz));
+    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, W(pl.c1dw.a), 128, Bw(pl.c1dw.ga), 128, nullptr, 0,
+               relu_target(pl.c1dw)));
+    TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz, pre(pl.c1dw)));
     TRY(dw_bwd(net.cls1.dw, 128, dz, W(pl.f), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
+    // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
+    //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, W(pl.fdw.a), 128, Bw(pl.fdw.ga), 128));
+    TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, W(pl.fdw.a), 128, Bw(pl.fdw.ga), 128, nullptr, 0,
+               relu_target(pl.fdw)));
+    TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz, pre(pl.fdw)));
+    TRY(dw_bwd(net.ffm_dw, 128, dz, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_up)));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, W(pl.l2pw.a), 64, Bw(pl.l2pw.ga), 64));
-    TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz));
-    TRY(dw_bwd(net.ffm_dw, 128, dz, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_up)));
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     {
       AxisBwdArgs a{};
@@ -779,26 +808,32 @@ struct Exec {
     int gxld = i == 0 ? 64 : pl.lbp[i - 1].ga_ld;
     bool shortcut = l.stride == 1 && l.cin == l.cout;
     const int e = l.cin * 6;
-    TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz));
-    TRY(pw_bwd(l.p, up.M, dz, l.cout, W(ud.a), e, Bw(ud.ga), e));
-    TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz));
+    // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
+    // block: its dy is the PPM concat gradient)
+    TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz, false, i < 8 ? pre(up) : 0));
+    TRY(pw_bwd(l.p, up.M, dz, l.cout, W(ud.a), e, Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
+    TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz, pre(ud)));
     TRY(dw_bwd(l.d, e, dz, W(ue.a), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
     TRY(bn_bwd_relu(ue, l.be, Bw(ue.ga), e, dz));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
-    return pw_bwd(l.e, ue.M, dz, e, x, xld, gx, gxld, R, ldr);
+    // the dgrad is the dy of the previous block's project BN (or of LTD.dsconv2's pw BN)
+    const BTarget bt = i == 0 ? relu_target(pl.l2pw) : plain_target(pl.lbp[i - 1]);
+    return pw_bwd(l.e, ue.M, dz, e, x, xld, gx, gxld, R, ldr, bt);
   }
 
   int backward_ltd() {
     void* dz = Bw(pl.dz);
-    TRY(bn_bwd_relu(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, dz));
-    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, W(pl.l2dw.a), 48, Bw(pl.l2dw.ga), 48));
-    TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz));
+    TRY(bn_bwd_relu(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, dz, pre(pl.l2pw)));
+    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, W(pl.l2dw.a), 48, Bw(pl.l2dw.ga), 48, nullptr, 0,
+               relu_target(pl.l2dw)));
+    TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz, pre(pl.l2dw)));
     TRY(dw_bwd(net.ltd2.dw, 48, dz, W(pl.l1pw.a), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
     TRY(bn_bwd_relu(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, dz));
-    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, W(pl.l1dw.a), 32, Bw(pl.l1dw.ga), 32));
-    TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz));
+    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, W(pl.l1dw.a), 32, Bw(pl.l1dw.ga), 32, nullptr, 0,
+               relu_target(pl.l1dw)));
+    TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz, pre(pl.l1dw)));
     TRY(dw_bwd(net.ltd1.dw, 32, dz, W(pl.c0.a), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
     TRY(bn_bwd_relu(pl.c0, net.b0, Bw(pl.c0.ga), 32, dz));
     Conv0WgradArgs c{};
