@@ -58,8 +58,11 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   constexpr int NVR = (C0_IN_W + VI - 1) / VI;      // vectors per staged input row
   constexpr int LPV = (9 * NVR + 255) / 256;        // vector loads per thread
   constexpr int OST = 32 + 16 / sizeof(TO);         // s_out row stride (elements, 16-B aligned)
-  __shared__ float s_in[9 * C0_IN_W + VI];          // [ci][r][col] (+ slack for the last vector)
-  __shared__ __attribute__((aligned(16))) TO s_out[C0_TILE * OST];
+  // the input strip and the output tile are live in disjoint phases: one LDS region (occupancy)
+  constexpr int IN_BYTES = (9 * C0_IN_W + VI) * 4, OUT_BYTES = C0_TILE * OST * (int)sizeof(TO);
+  __shared__ __attribute__((aligned(16))) char s_raw[IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES];
+  float* s_in = reinterpret_cast<float*>(s_raw);   // [ci][r][col] (+ slack for the last vector)
+  TO* s_out = reinterpret_cast<TO*>(s_raw);        // [px][OST]
   __shared__ float s_red[2][4][C0_OUT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -181,6 +184,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     }
   }
   // ---- stage the tile in the storage type, then coalesced 16-B stores ----------------------
+  __syncthreads();  // every wave is done reading s_in (aliased by s_out)
 #pragma unroll
   for (int gi = 0; gi < 4; ++gi)
 #pragma unroll

@@ -486,6 +486,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   ProfScope ps(PK_GEMM_NT, st, E * (M * K + M * N * (a.R ? 2 : 1) + N * K), 2.0 * M * N * K);
+  static const bool stream_on = [] {
+    const char* e = getenv("FSCNN_GEMM_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  if (stream_on && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
   const bool bs = a.bpart != nullptr;
   if (bs && (a.part || !a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
              (a.bmode != 0 && a.bmode != 2) || a.ldbz % V || !a.b_trans)) {

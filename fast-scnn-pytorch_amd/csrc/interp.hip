@@ -81,6 +81,72 @@ __global__ __launch_bounds__(256) void up_nchw_kernel(UpArgs a) {
   }
 }
 
+// Row-staged form (the 1.27 GB fp32 write of cfg2 is the whole cost, so stores are what matter):
+// a workgroup owns one output row (n, ho) and UPR_COLS consecutive columns.  The two source rows
+// i0(ho), i1(ho) are staged once in LDS, class-major [2][C][Wi] in fp32, then every thread
+// produces 4 consecutive columns of each class plane and writes them with one 16-B (fp32) /
+// 8-B (bf16) non-temporal store.  Same weights and the same W-then-H expression as aten, so the
+// fp32 result is bit-identical to the per-pixel kernel above.
+constexpr int UPR_THREADS = 256;
+constexpr int UPR_COLS = 4 * UPR_THREADS;
+
+typedef float upr_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int upr_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st4_nt(float* p, const float (&v)[4]) {
+  upr_f4 t = {v[0], v[1], v[2], v[3]};
+  __builtin_nontemporal_store(t, (upr_f4*)p);
+}
+__device__ __forceinline__ void st4_nt(bf16* p, const float (&v)[4]) {
+  upr_u2 t = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+  __builtin_nontemporal_store(t, (upr_u2*)p);
+}
+
+template <typename TI, typename TO, bool VEC>
+__global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
+  extern __shared__ float s_rows[];  // [2][C][Wi + 1] (padded: the staging stores walk c)
+  const int ho = blockIdx.y, n = blockIdx.z;
+  const Lerp lh = ac_lerp(ho, a.Hi, a.Ho, ac_scale(a.Hi, a.Ho));
+  const int CW = a.C * a.Wi, WP = a.Wi + 1, CWP = a.C * WP;
+  const TI* xb = (const TI*)a.x + (size_t)n * a.Hi * a.Wi * a.ldx;
+  // stage: element e = (r, wi, c) with c fastest in global memory (NHWC), class-major in LDS
+  for (int e = threadIdx.x; e < 2 * CW; e += UPR_THREADS) {
+    const int r = e >= CW;
+    const int rem = e - r * CW;
+    const int wi = rem / a.C, c = rem - wi * a.C;
+    const int hi = r ? lh.i1 : lh.i0;
+    s_rows[r * CWP + c * WP + wi] = ld1(xb + ((size_t)hi * a.Wi + wi) * a.ldx + c);
+  }
+  __syncthreads();
+  const int wo0 = blockIdx.x * UPR_COLS + threadIdx.x * 4;
+  if (wo0 >= a.Wo) return;
+  const float sw = ac_scale(a.Wi, a.Wo);
+  Lerp lw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lw[j] = ac_lerp(min(wo0 + j, a.Wo - 1), a.Wi, a.Wo, sw);
+  const size_t plane = (size_t)a.Ho * a.Wo;
+  TO* yb = (TO*)a.y + (size_t)n * a.C * plane + (size_t)ho * a.Wo + wo0;
+  const float* s0 = s_rows;
+  const float* s1 = s_rows + CWP;
+  for (int c = 0; c < a.C; ++c) {
+    const float* r0 = s0 + c * WP;
+    const float* r1 = s1 + c * WP;
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = lh.l0 * (lw[j].l0 * r0[lw[j].i0] + lw[j].l1 * r0[lw[j].i1]) +
+             lh.l1 * (lw[j].l0 * r1[lw[j].i0] + lw[j].l1 * r1[lw[j].i1]);
+    TO* yp = yb + c * plane;
+    if (VEC && wo0 + 4 <= a.Wo) {
+      st4_nt(yp, o);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (wo0 + j < a.Wo) st1(yp + j, o[j]);
+    }
+  }
+}
+
 int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
   long long total = (long long)a.N * a.Ho * a.Wo;
   unsigned grid = (unsigned)((total + 255) / 256);
@@ -88,6 +154,22 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
                (in_dtype == DT_F32 ? 4.0 : 2.0) * a.N * a.C * a.Hi * a.Wi +
                    (out_dtype == DT_F32 ? 4.0 : 2.0) * (double)a.N * a.C * a.Ho * a.Wo,
                7.0 * a.N * a.C * a.Ho * a.Wo);
+  const size_t lds = (size_t)2 * a.C * (a.Wi + 1) * sizeof(float);
+  if (lds <= 64 * 1024 && a.Ho <= 65535 && a.N <= 65535) {
+    dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)a.Ho, (unsigned)a.N);
+    const bool vec = a.Wo % 4 == 0;
+#define UPR_LAUNCH(TI, TO)                                                              \
+  do {                                                                                  \
+    if (vec) up_nchw_rows_kernel<TI, TO, true><<<g, UPR_THREADS, lds, st>>>(a);         \
+    else up_nchw_rows_kernel<TI, TO, false><<<g, UPR_THREADS, lds, st>>>(a);            \
+  } while (0)
+    if (in_dtype == DT_F32 && out_dtype == DT_F32) UPR_LAUNCH(float, float);
+    else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) UPR_LAUNCH(bf16, bf16);
+    else if (in_dtype == DT_BF16 && out_dtype == DT_F32) UPR_LAUNCH(bf16, float);
+    else UPR_LAUNCH(float, bf16);
+#undef UPR_LAUNCH
+    return check_launch("up_nchw");
+  }
   if (in_dtype == DT_F32 && out_dtype == DT_F32) up_nchw_kernel<float, float, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) up_nchw_kernel<bf16, bf16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_F32) up_nchw_kernel<bf16, float, 0><<<grid, 256, 0, st>>>(a);

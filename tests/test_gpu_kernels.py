@@ -124,7 +124,8 @@ def test_dw3x3_fwd_bwd(dt, N, H, W, C, s):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(1000, 48, 32), (4096, 384, 64), (777, 64, 384), (300, 96, 576),
                                    (513, 128, 768), (129, 19, 128), (40, 32, 128), (2048, 128, 256),
-                                   (999, 2, 128)])
+                                   (999, 2, 128), (3000, 128, 48), (5000, 576, 96), (2500, 768, 128),
+                                   (70001, 128, 128)])
 def test_pw_gemm(dt, M, N, K):
     A = rnd(M, K, seed=10)
     B = rnd(N, K, seed=11, scale=1 / math.sqrt(K))
@@ -167,6 +168,27 @@ def test_pw_gemm(dt, M, N, K):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(4099, 128, 128), (300, 128, 64)])
+def test_pw_gemm_residual_in_place(dt, M, N, K):
+    # FFM eval form (models/fast_scnn.py:217-218): C = relu(A.W^T * sc + sh + C), C read and
+    # overwritten in place by the same launch
+    A = rnd(M, K, seed=20)
+    B = rnd(N, K, seed=21, scale=1 / math.sqrt(K))
+    R = rnd(M, N, seed=22)
+    sc, sh = rnd(N, seed=23).abs() + 0.5, rnd(N, seed=24)
+    Aq, Bq, Rq = A.to(dt).float(), B.to(dt).float(), R.to(dt).float()
+    ref = F.relu((Aq @ Bq.t()) * sc + sh + Rq)
+    C = R.to(dt).to(DEV).contiguous()
+    Ad, Bd = A.to(dt).to(DEV), B.to(dt).to(DEV)
+    scd, shd = sc.to(DEV), sh.to(DEV)  # held: raw pointers do not keep tensors alive
+    _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(Ad), K, _lib.ptr(Bd), K, 0, _lib.ptr(scd),
+              _lib.ptr(shd), _lib.ptr(C), N, 1, _lib.ptr(C), N, None,
+              _lib.dtype_code(dt), S())
+    sync()
+    close(C, ref, TOL[dt] * (10 if dt == torch.float32 else 1))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_bn_statistics(dt):
     M, N, K = 3001, 96, 64
     A = rnd(M, K, seed=20) + 3.0  # large mean: catches E[x^2]-E[x]^2 cancellation
@@ -197,22 +219,33 @@ def test_gemm_bn_statistics(dt):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("Hi,Wi,Ho,Wo,C", [(4, 8, 32, 64, 32), (1, 1, 15, 20, 32),
                                            (32, 64, 128, 256, 128), (16, 32, 128, 256, 24),
-                                           (15, 20, 60, 80, 8), (6, 6, 32, 64, 32)])
+                                           (15, 20, 60, 80, 8), (6, 6, 32, 64, 32),
+                                           (5, 7, 33, 63, 19), (16, 32, 1023, 2046, 19)])
 def test_bilinear_ac(dt, Hi, Wi, Ho, Wo, C):
     N = 2
     x = rnd(N, C, Hi, Wi, seed=30)
     xq = x.to(dt).float().clone().requires_grad_(True)
     ref = F.interpolate(xq, (Ho, Wo), mode="bilinear", align_corners=True)
     xd = nhwc(x.to(dt)).to(DEV)
+    nhwc_ok = C % 8 == 0  # the NHWC form needs whole 16-B channel vectors
     y = torch.empty(N, Ho, Wo, C, dtype=dt, device=DEV)
-    _lib.call("fscnn_bilinear_ac_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, Hi, Wi, C, Ho, Wo,
-              _lib.ptr(y), 0, _lib.dtype_code(dt), S())
+    if nhwc_ok:
+        _lib.call("fscnn_bilinear_ac_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, Hi, Wi, C, Ho,
+                  Wo, _lib.ptr(y), 0, _lib.dtype_code(dt), S())
     y2 = torch.empty(N, C, Ho, Wo, dtype=torch.float32, device=DEV)
     _lib.call("fscnn_bilinear_ac_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, Hi, Wi, C, Ho, Wo,
               _lib.ptr(y2), 1, _lib.DT_F32, S())
     sync()
-    close(nchw(y), ref.detach(), TOL[dt])
+    if nhwc_ok:
+        close(nchw(y), ref.detach(), TOL[dt])
     close(y2, ref.detach(), 1e-5)  # fp32 out: only FMA-contraction / order differences
+    y3 = torch.empty(N, C, Ho, Wo, dtype=torch.bfloat16, device=DEV)
+    _lib.call("fscnn_bilinear_ac_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, Hi, Wi, C, Ho, Wo,
+              _lib.ptr(y3), 1, _lib.DT_BF16, S())
+    sync()
+    close(y3.float(), ref.detach(), TOL[torch.bfloat16])
+    if not nhwc_ok:
+        return
     g = rnd(N, C, Ho, Wo, seed=31).to(dt)
     ref.backward(g.float())
     tmp = torch.empty(N * Ho * Wi * C, dtype=torch.float32, device=DEV)
