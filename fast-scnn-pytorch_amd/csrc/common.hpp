@@ -98,6 +98,26 @@ __device__ __forceinline__ Welford wf_merge(Welford a, Welford b) {
   return r;
 }
 
+// ---- 4-element vectors (16 B fp32 / 8 B bf16) ------------------------------------------------
+__device__ __forceinline__ void st4v(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st4v(bf16* p, const float (&v)[4]) {
+  uint2 t;
+  t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
+__device__ __forceinline__ void ld4v(const float* p, float (&v)[4]) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+__device__ __forceinline__ void ld4v(const bf16* p, float (&v)[4]) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xFFFF0000u);
+  v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xFFFF0000u);
+}
+
 // ---- dropout keep-mask: a pure function of (seed, NCHW linear index) -------------------------
 // Must match oracle/fast_scnn_ref.py:dropout_mask bit for bit.
 // keep iff (hash >> 40) >= thr, thr = ceil(p * 2^24)  (<=> 24-bit uniform u >= p)

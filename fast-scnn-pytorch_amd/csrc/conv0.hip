@@ -59,7 +59,11 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   constexpr int LPV = (9 * NVR + 255) / 256;        // vector loads per thread
   constexpr int OST = 32 + 16 / sizeof(TO);         // s_out row stride (elements, 16-B aligned)
   // the input strip and the output tile are live in disjoint phases: one LDS region (occupancy)
-  constexpr int IN_BYTES = (9 * C0_IN_W + VI) * 4, OUT_BYTES = C0_TILE * OST * (int)sizeof(TO);
+  // fp32 output (SW): swapped MFMA operands put 4 consecutive channels of one pixel in each lane,
+  // stored straight from registers as 16-B vectors, so no output tile in LDS
+  constexpr bool SW = !BF;
+  constexpr int IN_BYTES = (9 * C0_IN_W + VI) * 4;
+  constexpr int OUT_BYTES = SW ? 0 : C0_TILE * OST * (int)sizeof(TO);
   __shared__ __attribute__((aligned(16))) char s_raw[IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES];
   float* s_in = reinterpret_cast<float*>(s_raw);   // [ci][r][col] (+ slack for the last vector)
   TO* s_out = reinterpret_cast<TO*>(s_raw);        // [px][OST]
@@ -153,6 +157,110 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     const int ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
     koff[e] = (ci * 3 + kh) * C0_IN_W + kw;
   }
+  if constexpr (SW) {
+    __syncthreads();
+    // acc[gi][jt][r] = out[pixel 64w + 16gi + li][channel 16jt + 4lq + r]
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) {
+      const int px = wave * 64 + gi * 16 + li;
+      float av[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = 8 * lq + e < 27 ? s_in[koff[e] + 2 * px] : 0.f;
+      const typename M::Frag af = M::pack(av);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        acc[gi][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        M::mma(bw[jt], af, acc[gi][jt]);
+      }
+    }
+    float* y = (float*)a.y + ((size_t)row * a.Wo + wo0) * C0_OUT;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      float sc[4], sh[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * jt + 4 * lq + r;
+        sc[r] = a.scale ? a.scale[c] : 1.f;
+        sh[r] = a.scale ? a.shift[c] : 0.f;
+      }
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        const int px = wave * 64 + gi * 16 + li;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[gi][jt][r] * sc[r] + sh[r];
+          if (a.relu) v[r] = fmaxf(v[r], 0.f);
+          acc[gi][jt][r] = v[r];
+        }
+        if (px < npx)
+          *reinterpret_cast<float4*>(y + (size_t)px * C0_OUT + 16 * jt + 4 * lq) =
+              make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    if (a.part == nullptr) return;
+    // per-channel (mean, M2, count) over the block's npx pixels: lanes li hold pixels
+    float sum[2][4];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) t += (wave * 64 + gi * 16 + li < npx) ? acc[gi][jt][r] : 0.f;
+        t += __shfl_xor(t, 1);
+        t += __shfl_xor(t, 2);
+        t += __shfl_xor(t, 4);
+        t += __shfl_xor(t, 8);
+        sum[jt][r] = t;
+      }
+    if (li == 0)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s_red[0][wave][16 * jt + 4 * lq + r] = sum[jt][r];
+    __syncthreads();
+    float mean[2][4];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * jt + 4 * lq + r;
+        mean[jt][r] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
+      }
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) {
+          const float d = acc[gi][jt][r] - mean[jt][r];
+          t += (wave * 64 + gi * 16 + li < npx) ? d * d : 0.f;
+        }
+        t += __shfl_xor(t, 1);
+        t += __shfl_xor(t, 2);
+        t += __shfl_xor(t, 4);
+        t += __shfl_xor(t, 8);
+        sum[jt][r] = t;
+      }
+    if (li == 0)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s_red[1][wave][16 * jt + 4 * lq + r] = sum[jt][r];
+    __syncthreads();
+    if (tid < C0_OUT) {
+      const size_t pi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+      float* rec = a.part + pi * 3 * C0_OUT;
+      const int c = tid;
+      rec[c] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
+      rec[C0_OUT + c] = (s_red[1][0][c] + s_red[1][1][c]) + (s_red[1][2][c] + s_red[1][3][c]);
+      rec[2 * C0_OUT + c] = (float)npx;
+    }
+    return;
+  } else {
   float fsc[2], fsh[2];  // eval BN fold of the lane's two channels (li, 16 + li)
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
@@ -269,6 +377,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       rec[2 * C0_OUT + c] = (float)npx;
     }
   }
+  }  // SW
 }
 
 int conv0_parts(int N, int Ho, int Wo) { return N * Ho * cdiv(Wo, C0_TILE); }

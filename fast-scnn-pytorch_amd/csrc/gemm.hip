@@ -483,6 +483,10 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   int nt = pick_nt(a.N);
+  // small-M problems (the 16 K-row bottleneck3 / bottleneck2 projects): split the columns
+  // further so the grid covers the 256 CUs (the A tile is then read twice, from L2)
+  if ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < 256 && (nt == 8 || nt == 6 || nt == 4))
+    nt /= 2;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   ProfScope ps(PK_GEMM_NT, st, E * (M * K + M * N * (a.R ? 2 : 1) + N * K), 2.0 * M * N * K);

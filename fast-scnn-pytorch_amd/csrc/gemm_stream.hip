@@ -43,25 +43,6 @@ struct GsMma<bf16> {
   }
 };
 
-__device__ __forceinline__ void st4v(float* p, const float (&v)[4]) {
-  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-}
-__device__ __forceinline__ void st4v(bf16* p, const float (&v)[4]) {
-  uint2 t;
-  t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  *reinterpret_cast<uint2*>(p) = t;
-}
-__device__ __forceinline__ void ld4v(const float* p, float (&v)[4]) {
-  const float4 t = *reinterpret_cast<const float4*>(p);
-  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-}
-__device__ __forceinline__ void ld4v(const bf16* p, float (&v)[4]) {
-  const uint2 t = *reinterpret_cast<const uint2*>(p);
-  v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xFFFF0000u);
-  v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xFFFF0000u);
-}
-
 // zero the elements >= valid of a 16-B vector with selects only (no dynamic register indexing)
 template <typename T>
 __device__ __forceinline__ uint4 gs_tail(uint4 v, int valid) {
@@ -245,6 +226,7 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   if (lds > 72 * 1024) return false;
   return a.M >= 4096;  // tiny GEMMs (PPM bins): loading a weight slice per block does not pay
 }
+
 
 template <typename T, int NT, bool TAIL>
 static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int bpg,

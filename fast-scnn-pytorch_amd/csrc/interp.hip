@@ -81,14 +81,17 @@ __global__ __launch_bounds__(256) void up_nchw_kernel(UpArgs a) {
   }
 }
 
-// Row-staged form (the 1.27 GB fp32 write of cfg2 is the whole cost, so stores are what matter):
-// a workgroup owns one output row (n, ho) and UPR_COLS consecutive columns.  The two source rows
-// i0(ho), i1(ho) are staged once in LDS, class-major [2][C][Wi] in fp32, then every thread
-// produces 4 consecutive columns of each class plane and writes them with one 16-B (fp32) /
-// 8-B (bf16) non-temporal store.  Same weights and the same W-then-H expression as aten, so the
-// fp32 result is bit-identical to the per-pixel kernel above.
-constexpr int UPR_THREADS = 256;
+// Row-group form (the 1.27 GB fp32 write of cfg2 is the whole cost, so stores are what matter):
+// a workgroup owns UPR_R consecutive output rows of image n and UPR_COLS columns.  The source
+// rows they read, [i0(first row), i1(last row)] (at most `rows` of them, bounded on the host), are
+// staged once in LDS class-major [row][C][Wi+1] in fp32; then every thread produces 4
+// consecutive columns of each class plane of each of the UPR_R rows and writes them with 16-B
+// (fp32) / 8-B (bf16) non-temporal stores.  Same weights and the same W-then-H expression as aten,
+// so the fp32 result is bit-identical to the per-pixel kernel above.
+constexpr int UPR_THREADS = 512;
 constexpr int UPR_COLS = 4 * UPR_THREADS;
+constexpr int UPR_R = 8;
+constexpr int UPR_MAXROWS = 4;  // staged source rows per group (host-checked)
 
 typedef float upr_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int upr_u2 __attribute__((ext_vector_type(2)));
@@ -104,18 +107,20 @@ __device__ __forceinline__ void st4_nt(bf16* p, const float (&v)[4]) {
 
 template <typename TI, typename TO, bool VEC>
 __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
-  extern __shared__ float s_rows[];  // [2][C][Wi + 1] (padded: the staging stores walk c)
-  const int ho = blockIdx.y, n = blockIdx.z;
-  const Lerp lh = ac_lerp(ho, a.Hi, a.Ho, ac_scale(a.Hi, a.Ho));
-  const int CW = a.C * a.Wi, WP = a.Wi + 1, CWP = a.C * WP;
-  const TI* xb = (const TI*)a.x + (size_t)n * a.Hi * a.Wi * a.ldx;
+  extern __shared__ float s_rows[];  // [rows][C][Wi + 1] (padded: the staging stores walk c)
+  const int ho0 = blockIdx.y * UPR_R, n = blockIdx.z;
+  const int ho1 = min(ho0 + UPR_R, a.Ho) - 1;
+  const float sh = ac_scale(a.Hi, a.Ho);
+  const int lo = ac_lerp(ho0, a.Hi, a.Ho, sh).i0;
+  const int nrows = ac_lerp(ho1, a.Hi, a.Ho, sh).i1 - lo + 1;  // <= host bound
+  const int WP = a.Wi + 1, CWP = a.C * WP, CW = a.C * a.Wi;
+  const TI* xb = (const TI*)a.x + ((size_t)n * a.Hi + lo) * a.Wi * a.ldx;
   // stage: element e = (r, wi, c) with c fastest in global memory (NHWC), class-major in LDS
-  for (int e = threadIdx.x; e < 2 * CW; e += UPR_THREADS) {
-    const int r = e >= CW;
+  for (int e = threadIdx.x; e < nrows * CW; e += UPR_THREADS) {
+    const int r = e / CW;
     const int rem = e - r * CW;
     const int wi = rem / a.C, c = rem - wi * a.C;
-    const int hi = r ? lh.i1 : lh.i0;
-    s_rows[r * CWP + c * WP + wi] = ld1(xb + ((size_t)hi * a.Wi + wi) * a.ldx + c);
+    s_rows[r * CWP + c * WP + wi] = ld1(xb + ((size_t)r * a.Wi + wi) * a.ldx + c);
   }
   __syncthreads();
   const int wo0 = blockIdx.x * UPR_COLS + threadIdx.x * 4;
@@ -125,26 +130,53 @@ __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) lw[j] = ac_lerp(min(wo0 + j, a.Wo - 1), a.Wi, a.Wo, sw);
   const size_t plane = (size_t)a.Ho * a.Wo;
-  TO* yb = (TO*)a.y + (size_t)n * a.C * plane + (size_t)ho * a.Wo + wo0;
-  const float* s0 = s_rows;
-  const float* s1 = s_rows + CWP;
+  TO* yb = (TO*)a.y + (size_t)n * a.C * plane + wo0;
   for (int c = 0; c < a.C; ++c) {
-    const float* r0 = s0 + c * WP;
-    const float* r1 = s1 + c * WP;
-    float o[4];
+    // W-interpolation of each staged source row for this thread's 4 columns (aten's inner
+    // bracket), computed once and shared by the UPR_R output rows
+    float wr[UPR_MAXROWS][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      o[j] = lh.l0 * (lw[j].l0 * r0[lw[j].i0] + lw[j].l1 * r0[lw[j].i1]) +
-             lh.l1 * (lw[j].l0 * r1[lw[j].i0] + lw[j].l1 * r1[lw[j].i1]);
-    TO* yp = yb + c * plane;
-    if (VEC && wo0 + 4 <= a.Wo) {
-      st4_nt(yp, o);
-    } else {
+    for (int r = 0; r < UPR_MAXROWS; ++r) {
+      const float* row = s_rows + min(r, nrows - 1) * CWP + c * WP;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (wo0 + j < a.Wo) st1(yp + j, o[j]);
+      for (int j = 0; j < 4; ++j) wr[r][j] = lw[j].l0 * row[lw[j].i0] + lw[j].l1 * row[lw[j].i1];
+    }
+    for (int ho = ho0; ho <= ho1; ++ho) {
+      const Lerp lh = ac_lerp(ho, a.Hi, a.Ho, sh);
+      const int d0 = lh.i0 - lo, d1 = lh.i1 - lo;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x0 = wr[0][j], x1 = wr[0][j];
+#pragma unroll
+        for (int r = 1; r < UPR_MAXROWS; ++r) {  // register selects, no dynamic indexing
+          x0 = d0 == r ? wr[r][j] : x0;
+          x1 = d1 == r ? wr[r][j] : x1;
+        }
+        o[j] = lh.l0 * x0 + lh.l1 * x1;
+      }
+      TO* yp = yb + c * plane + (size_t)ho * a.Wo;
+      if (VEC && wo0 + 4 <= a.Wo) {
+        st4_nt(yp, o);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (wo0 + j < a.Wo) st1(yp + j, o[j]);
+      }
     }
   }
+}
+
+// largest number of source rows any UPR_R-row group reads (host copy of the kernel's bound)
+static int upr_max_rows(int Hi, int Ho) {
+  const float sh = ac_scale(Hi, Ho);
+  int mx = 0;
+  for (int g0 = 0; g0 < Ho; g0 += UPR_R) {
+    const int g1 = (g0 + UPR_R < Ho ? g0 + UPR_R : Ho) - 1;
+    const int r = ac_lerp(g1, Hi, Ho, sh).i1 - ac_lerp(g0, Hi, Ho, sh).i0 + 1;
+    mx = r > mx ? r : mx;
+  }
+  return mx;
 }
 
 int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
@@ -154,9 +186,9 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
                (in_dtype == DT_F32 ? 4.0 : 2.0) * a.N * a.C * a.Hi * a.Wi +
                    (out_dtype == DT_F32 ? 4.0 : 2.0) * (double)a.N * a.C * a.Ho * a.Wo,
                7.0 * a.N * a.C * a.Ho * a.Wo);
-  const size_t lds = (size_t)2 * a.C * (a.Wi + 1) * sizeof(float);
-  if (lds <= 64 * 1024 && a.Ho <= 65535 && a.N <= 65535) {
-    dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)a.Ho, (unsigned)a.N);
+  const size_t lds = (size_t)upr_max_rows(a.Hi, a.Ho) * a.C * (a.Wi + 1) * sizeof(float);
+  if (lds <= 64 * 1024 && a.N <= 65535 && upr_max_rows(a.Hi, a.Ho) <= UPR_MAXROWS) {
+    dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)cdiv(a.Ho, UPR_R), (unsigned)a.N);
     const bool vec = a.Wo % 4 == 0;
 #define UPR_LAUNCH(TI, TO)                                                              \
   do {                                                                                  \
@@ -196,7 +228,9 @@ __device__ __forceinline__ int first_out_with_i0_ge(int i, int Lin, int Lout, fl
 
 // grid: x = 256-thread chunks of the (o, x) positions of one input index, y = input index i.
 // The contributing output range [p_lo, p_hi) of index i is found once per workgroup.
-template <typename TG, typename TD>
+// VX = 4: the innermost coordinate is contiguous on both sides (channels of an NHWC tensor), so a
+// thread owns 4 consecutive x and every load / store is one 8-B (bf16) or 16-B (fp32) vector.
+template <typename TG, typename TD, int VX>
 __global__ __launch_bounds__(256) void axis_bwd_kernel(AxisBwdArgs a) {
   __shared__ int s_rng[2];
   const int i = blockIdx.y;
@@ -208,32 +242,46 @@ __global__ __launch_bounds__(256) void axis_bwd_kernel(AxisBwdArgs a) {
   }
   __syncthreads();
   const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned n_o = (unsigned)(a.n_o1 * a.n_o2), n_in = (unsigned)a.n_in;
+  const unsigned n_o = (unsigned)(a.n_o1 * a.n_o2), n_in = (unsigned)(a.n_in / VX);
   if (t >= n_o * n_in) return;
-  const unsigned o = t / n_in, x = t - o * n_in;
+  const unsigned o = t / n_in, x = (t - o * n_in) * VX;
   const unsigned o1 = o / (unsigned)a.n_o2, o2 = o - o1 * (unsigned)a.n_o2;
   const int p_lo = s_rng[0], p_hi = s_rng[1];
   const TG* gb = (const TG*)a.g + (long long)o1 * a.g_s1 + (long long)o2 * a.g_s2 + (long long)x * a.g_in;
-  float s = 0.f;
+  float s[VX];
+#pragma unroll
+  for (int j = 0; j < VX; ++j) s[j] = 0.f;
   for (int p0 = p_lo; p0 < p_hi; p0 += 4) {  // 4 independent loads per batch
-    float gv[4], wv[4];
+    float gv[4][VX], wv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int p = p0 + u;
       const bool ok = p < p_hi;  // clamped load + select (branch-free)
       const Lerp l = ac_lerp(ok ? p : p0, a.Lin, a.Lout, sc);
       const float w = (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
-      const float gvv = ld1(gb + (size_t)(ok ? p : p0) * a.g_idx);
+      if constexpr (VX == 4) ld4v(gb + (size_t)(ok ? p : p0) * a.g_idx, gv[u]);
+      else gv[u][0] = ld1(gb + (size_t)(ok ? p : p0) * a.g_idx);
       wv[u] = ok ? w : 0.f;
-      gv[u] = ok ? gvv : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s += wv[u] * gv[u];
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < VX; ++j) s[j] += wv[u] * gv[u][j];
   }
   TD* dp = (TD*)a.d + (long long)o1 * a.d_s1 + (long long)o2 * a.d_s2 + (long long)i * a.d_idx +
            (long long)x * a.d_in;
-  if (a.accumulate) s += ld1(dp);
-  st1(dp, s);
+  if constexpr (VX == 4) {
+    if (a.accumulate) {
+      float prev[4];
+      ld4v(dp, prev);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += prev[j];
+    }
+    st4v(dp, s);
+  } else {
+    if (a.accumulate) s[0] += ld1(dp);
+    st1(dp, s[0]);
+  }
 }
 
 int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st) {
@@ -242,11 +290,22 @@ int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st) {
     set_error("axis_bwd: problem too large (%lld per index, Lin %d)", per_i, a.Lin);
     return E_UNSUPPORTED;
   }
-  dim3 grid((unsigned)((per_i + 255) / 256), a.Lin);
-  if (g_dtype == DT_F32 && d_dtype == DT_F32) axis_bwd_kernel<float, float><<<grid, 256, 0, st>>>(a);
-  else if (g_dtype == DT_BF16 && d_dtype == DT_BF16) axis_bwd_kernel<bf16, bf16><<<grid, 256, 0, st>>>(a);
-  else if (g_dtype == DT_BF16 && d_dtype == DT_F32) axis_bwd_kernel<bf16, float><<<grid, 256, 0, st>>>(a);
-  else axis_bwd_kernel<float, bf16><<<grid, 256, 0, st>>>(a);
+  // vector form: x contiguous and every other stride / base a whole number of 4-element vectors
+  const bool vec = a.g_in == 1 && a.d_in == 1 && a.n_in % 4 == 0 && a.g_s1 % 4 == 0 &&
+                   a.g_s2 % 4 == 0 && a.g_idx % 4 == 0 && a.d_s1 % 4 == 0 && a.d_s2 % 4 == 0 &&
+                   a.d_idx % 4 == 0 && (uintptr_t)a.g % 16 == 0 && (uintptr_t)a.d % 16 == 0;
+  const int vx = vec ? 4 : 1;
+  dim3 grid((unsigned)((per_i / vx + 255) / 256), a.Lin);
+#define AXB(TG, TD)                                                          \
+  do {                                                                       \
+    if (vec) axis_bwd_kernel<TG, TD, 4><<<grid, 256, 0, st>>>(a);            \
+    else axis_bwd_kernel<TG, TD, 1><<<grid, 256, 0, st>>>(a);                \
+  } while (0)
+  if (g_dtype == DT_F32 && d_dtype == DT_F32) AXB(float, float);
+  else if (g_dtype == DT_BF16 && d_dtype == DT_BF16) AXB(bf16, bf16);
+  else if (g_dtype == DT_BF16 && d_dtype == DT_F32) AXB(bf16, float);
+  else AXB(float, bf16);
+#undef AXB
   return check_launch("axis_bwd");
 }
 
@@ -414,47 +473,63 @@ int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
 }
 
 // backward: dfeats[bin][n][c] = sum_{h,w} wy(h,bi) wx(w,bj) dy[n,h,w,coff+lv*CF+c]  (gather)
-// one workgroup per (bin, image): CF channel lanes x (256/CF) row groups, fixed-order combine
+// Separable, one workgroup per (level, image): phase 1 reduces every row of the level's dy slice
+// onto the k column bins (rows[h][bj][c] = sum_w wx(w,bj) dy[h,w,c], one thread per (c, row)),
+// phase 2 folds the rows onto the k row bins (one thread per (c, bin)), fixed order throughout.
+constexpr int PPB_THREADS = 1024;
+constexpr int PPB_MAXH = 80;  // LDS rows[H][6][CF<=32] fp32
+
 template <typename T>
-__global__ __launch_bounds__(256) void ppm_up_bwd_kernel(PpmUpArgs a, void* dfeats) {
-  const int b = blockIdx.x, n = blockIdx.y;
-  const int G = 256 / a.CF;
-  const int c = threadIdx.x % a.CF, g = threadIdx.x / a.CF;
-  __shared__ float red[256];
-  int k, bi, bj;
-  pp_bin(b, k, bi, bj);
-  const int lv = k == 1 ? 0 : (k == 2 ? 1 : (k == 3 ? 2 : 3));
+__global__ __launch_bounds__(PPB_THREADS) void ppm_up_bwd_kernel(PpmUpArgs a, void* dfeats) {
+  __shared__ float rows[PPB_MAXH * 6 * 32];
+  const int lv = blockIdx.x, n = blockIdx.y;
+  const int k = PP_LEVELS[lv];
+  const int base = lv == 0 ? 0 : (lv == 1 ? 1 : (lv == 2 ? 5 : 14));
   const float sh = ac_scale(k, a.H), sw = ac_scale(k, a.W);
-  const T* gp = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * a.CF + c;
-  float s = 0.f;
-  if (g < G) {
-    for (int h = g; h < a.H; h += G) {
-      Lerp lh = ac_lerp(h, k, a.H, sh);
-      float wy = (lh.i0 == bi ? lh.l0 : 0.f) + (lh.i1 == bi ? lh.l1 : 0.f);
-      if (wy == 0.f) continue;
-      float sr = 0.f;
-      for (int w = 0; w < a.W; ++w) {
-        Lerp lw = ac_lerp(w, k, a.W, sw);
-        float wx = (lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f);
-        if (wx != 0.f) sr += wx * ld1(gp + ((size_t)h * a.W + w) * a.ldy);
+  const int CF = a.CF, G = PPB_THREADS / CF;
+  const int c = threadIdx.x % CF, g = threadIdx.x / CF;
+  const T* gp = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * CF + c;
+  for (int h = g; h < a.H; h += G) {
+    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const T* gr = gp + (size_t)h * a.W * a.ldy;
+    for (int w0 = 0; w0 < a.W; w0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // 8 independent loads per batch (clamped + selected)
+        const int w = w0 + u < a.W ? w0 + u : a.W - 1;
+        v[u] = w0 + u < a.W ? ld1(gr + (size_t)w * a.ldy) : 0.f;
       }
-      s += wy * sr;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const Lerp lw = ac_lerp(w0 + u < a.W ? w0 + u : a.W - 1, k, a.W, sw);
+#pragma unroll
+        for (int bj = 0; bj < 6; ++bj)
+          acc[bj] += ((lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f)) * v[u];
+      }
     }
+    for (int bj = 0; bj < k; ++bj) rows[(h * 6 + bj) * 32 + c] = acc[bj];
   }
-  red[threadIdx.x] = s;
   __syncthreads();
-  if (g == 0) {
-    float t = 0.f;
-    for (int q = 0; q < G; ++q) t += red[q * a.CF + c];
-    st1((T*)dfeats + ((size_t)b * a.N + n) * a.CF + c, t);
+  for (int t = threadIdx.x; t < k * k * CF; t += PPB_THREADS) {
+    const int cc = t % CF, bin = t / CF, bi = bin / k, bj = bin - bi * k;
+    float s = 0.f;
+    for (int h = 0; h < a.H; ++h) {
+      const Lerp lh = ac_lerp(h, k, a.H, sh);
+      const float wy = (lh.i0 == bi ? lh.l0 : 0.f) + (lh.i1 == bi ? lh.l1 : 0.f);
+      s += wy * rows[(h * 6 + bj) * 32 + cc];
+    }
+    st1((T*)dfeats + ((size_t)(base + bin) * a.N + n) * CF + cc, s);
   }
 }
 
 int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
-  if (a.CF <= 0 || a.CF > 256 || 256 % a.CF) { set_error("ppm_up_bwd: CF=%d", a.CF); return E_INVALID; }
-  dim3 grid(50, a.N);
-  if (dtype == DT_F32) ppm_up_bwd_kernel<float><<<grid, 256, 0, st>>>(a, dfeats);
-  else ppm_up_bwd_kernel<bf16><<<grid, 256, 0, st>>>(a, dfeats);
+  if (a.CF <= 0 || a.CF > 32 || PPB_THREADS % a.CF || a.H > PPB_MAXH || a.N > 65535) {
+    set_error("ppm_up_bwd: CF=%d H=%d unsupported", a.CF, a.H);
+    return E_UNSUPPORTED;
+  }
+  dim3 grid(4, a.N);
+  if (dtype == DT_F32) ppm_up_bwd_kernel<float><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
+  else ppm_up_bwd_kernel<bf16><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
   return check_launch("ppm_up_bwd");
 }
 

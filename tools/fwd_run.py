@@ -27,11 +27,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", type=int, default=2)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--bf16", action="store_true", help="bf16 input (bf16 compute)")
     a = ap.parse_args()
     if a.cfg == 5:
         C, shape, dt = 2, (32, 3, 480, 640), torch.float16
     else:
         C, shape, dt = 19, (8, 3, 1024, 2048), torch.float32
+    if a.bf16:
+        dt = torch.bfloat16
     dev = torch.device("cuda", 0)
     m = FastSCNN(C)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
