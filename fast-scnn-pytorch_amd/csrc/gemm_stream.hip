@@ -129,11 +129,16 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 
   T* Cp = (T*)a.C;
   const T* Rp = (const T*)a.R;
-  // No register double-buffering of the next chunk (it would double the A registers and push
-  // the big tiles past 256 VGPRs): the two to three co-resident waves per SIMD alternate their
-  // load and MFMA phases, and within a chunk the MFMAs of step s wait only for step s's loads.
+  // Small chunks (KS <= 4: 32 A registers or fewer) double-buffer the next chunk in registers;
+  // the big fp32 tiles do not (it would push them past 256 VGPRs): there the co-resident waves
+  // of a SIMD alternate their load and MFMA phases, and the MFMAs of step s wait only for step
+  // s's loads.
+  constexpr bool PF = KS <= 4;
+  uint4 xn[2][PF ? KS : 1];
+  if constexpr (PF) loadx(c, xa);
   for (; c < nchunks; c += wstride) {
-    loadx(c, xa);
+    if constexpr (PF) loadx(c + wstride, xn);  // clamped / zeroed past the end
+    else loadx(c, xa);
     f32x4 acc[2][NT];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -200,6 +205,12 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
         }
       }
     }
+    if constexpr (PF) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) xa[mt][s] = xn[mt][s];
+    }
   }
 }
 
@@ -249,7 +260,7 @@ static void gs_launch(const GemmArgs& a, hipStream_t st) {
   const int groups = cdiv(a.N, 16 * nt);
   const size_t lds = (size_t)16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4;
   const int nchunks = cdiv(a.M, GS_MW);
-  // resident workgroups: LDS-limited (160 KB / CU) and at most 2 per CU by launch bounds
+  // resident workgroups: LDS-limited (160 KB / CU), at most 2 per CU (measured: 3-4 slower)
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
   int bpg = cdiv(256 * per_cu, groups);
