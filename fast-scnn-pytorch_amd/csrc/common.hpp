@@ -118,6 +118,33 @@ __device__ __forceinline__ void ld4v(const bf16* p, float (&v)[4]) {
   v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xFFFF0000u);
 }
 
+// ---- lazily applied BatchNorm + ReLU of a producer whose activation is never stored ---------
+// relu(fmaf(x, sc[j], sh[j])) on one raw 16-B vector of the storage type: exactly bn_apply's
+// arithmetic (fp32 fma, ReLU, RNE back to the storage type), so a consumer that applies it while
+// staging its operand sees the same bits bn_apply would have written.
+template <typename T>
+__device__ __forceinline__ uint4 bnrelu_vec(const uint4& t, const float* sc, const float* sh) {
+  if constexpr (sizeof(T) == 4) {
+    float v[4];
+    unpackv(t, v);
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = __float_as_uint(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    float v[8];
+    unpackv(t, v);
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = fmaxf(fmaf(v[2 * i], sc[2 * i], sh[2 * i]), 0.f);
+      const float b = fmaxf(fmaf(v[2 * i + 1], sc[2 * i + 1], sh[2 * i + 1]), 0.f);
+      w[i] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // ---- dropout keep-mask: a pure function of (seed, NCHW linear index) -------------------------
 // Must match oracle/fast_scnn_ref.py:dropout_mask bit for bit.
 // keep iff (hash >> 40) >= thr, thr = ceil(p * 2^24)  (<=> 24-bit uniform u >= p)

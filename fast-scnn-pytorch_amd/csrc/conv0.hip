@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   // the input strip and the output tile are live in disjoint phases: one LDS region (occupancy)
   // fp32 output (SW): swapped MFMA operands put 4 consecutive channels of one pixel in each lane,
   // stored straight from registers as 16-B vectors, so no output tile in LDS
-  constexpr bool SW = !BF;
+  constexpr bool SW = false;  // measured slower than the LDS-staged tile (256 vs 230 us, cfg2)
   constexpr int IN_BYTES = (9 * C0_IN_W + VI) * 4;
   constexpr int OUT_BYTES = SW ? 0 : C0_TILE * OST * (int)sizeof(TO);
   __shared__ __attribute__((aligned(16))) char s_raw[IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES];

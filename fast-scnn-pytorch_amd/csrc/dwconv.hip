@@ -83,11 +83,24 @@ __device__ __forceinline__ void dw_tile(int& cx, int& cy, int& cz) {
 
 // stage the haloed input tile [IR][IC][cbv] (16-B vectors) of image n into LDS; out-of-image
 // positions are zero.  All loads of a thread are issued before any LDS store.
-template <typename T, int S>
+// IT: x is the raw conv output z of a BatchNorm+ReLU that is never stored (train); the staged
+// value is relu(fmaf(z, isc[c], ish[c])) (bn_apply's arithmetic), padding stays zero.  A thread's
+// vectors all belong to one channel vector (lv = tid % cbv), so its V pairs are loaded once.
+template <typename T, int S, bool IT>
 __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, int C, int n,
-                                         int hi0, int wi0, int cvbase, int cbv, int tid, int nthr) {
+                                         int hi0, int wi0, int cvbase, int cbv, int tid, int nthr,
+                                         const float* isc, const float* ish) {
   using G = DwTile<T, S>;
   constexpr int V = VecW<T>::V;
+  float sc[IT ? V : 1], sh[IT ? V : 1];
+  if constexpr (IT) {
+    const int cb = (cvbase + tid % cbv) * V;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      sc[j] = isc[cb + j];
+      sh[j] = ish[cb + j];
+    }
+  }
   uint4 raw[G::LPT];
 #pragma unroll
   for (int k = 0; k < G::LPT; ++k) {
@@ -102,12 +115,22 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
 #pragma unroll
   for (int k = 0; k < G::LPT; ++k) {
     const int i = tid + k * nthr;
-    if (i < G::IR * G::IC * cbv) s_in[i] = raw[k];
+    if (i < G::IR * G::IC * cbv) {
+      uint4 v = raw[k];
+      if constexpr (IT) {
+        const int pix = i / cbv;
+        const int r = pix / G::IC, col = pix - r * G::IC;
+        const int hi = hi0 + r, wi = wi0 + col;
+        const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
+        v = sel4(ok, bnrelu_vec<T>(v, sc, sh));
+      }
+      s_in[i] = v;
+    }
   }
 }
 
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
-template <typename T, int S, bool FLIP>
+template <typename T, int S, bool FLIP, bool IT>
 __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
   __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
@@ -122,8 +145,8 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   const int n = bz / tiles_h;
   const int th0 = (bz - n * tiles_h) * G::TH, tw0 = by * G::TW;
   const int c0 = bx * cbv * VecW<T>::V + q * 4;  // first channel of the thread's quad
-  dw_stage<T, S>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv, cbv,
-                 tid, nthr);
+  dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv,
+                     cbv, tid, nthr, a.in_scale, a.in_shift);
   float wt[9][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -255,7 +278,7 @@ int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
   return (int)(g.y * g.z);
 }
 
-template <bool FLIP>
+template <bool FLIP, bool IT>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   int cbv;
@@ -266,11 +289,11 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   }
   const int nthr = cbv * 32;  // = quads * groups for both dtypes
   if (dtype == DT_F32) {
-    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<float, 2, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
+    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<float, 2, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
   } else {
-    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<bf16, 2, FLIP><<<grid, nthr, 0, st>>>(a, cbv);
+    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<bf16, 2, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
   }
   return check_launch("dw_fwd");
 }
@@ -285,7 +308,11 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_FWD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
-  return dw_launch_fwd<false>(a, dtype, st);
+  if (a.in_scale && !a.in_shift) {
+    set_error("dw_fwd: in_scale without in_shift");
+    return E_INVALID;
+  }
+  return a.in_scale ? dw_launch_fwd<false, true>(a, dtype, st) : dw_launch_fwd<false, false>(a, dtype, st);
 }
 
 static void dw_block_shape(int C, int V, int& bx, int& by) {
@@ -374,7 +401,7 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     DwArgs f{};
     f.N = a.N; f.H = a.Ho; f.W = a.Wo; f.C = a.C; f.Ho = a.H; f.Wo = a.W; f.stride = 1;
     f.x = a.dy; f.w = a.w; f.y = a.dx;
-    return dw_launch_fwd<true>(f, dtype, st);
+    return dw_launch_fwd<true, false>(f, dtype, st);
   }
   int bx, by;
   dw_block_shape(a.C, V, bx, by);
@@ -386,7 +413,7 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
 
 // ---- weight gradient: per-workgroup partial [part][9][C] --------------------------------------
 // grid: x = channel chunk, y = groups of tpb column tiles, z = N * row bands; part = (z, y).
-template <typename T, int S>
+template <typename T, int S, bool IT>
 __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, int tpb) {
   using G = DwTile<T, S>;
   __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
@@ -428,8 +455,8 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
         for (int j = 0; j < 4; ++j) g[r][p][j] = ok ? g[r][p][j] : 0.f;
       }
     __syncthreads();  // previous tile's LDS reads are done
-    dw_stage<T, S>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv, cbv,
-                   tid, nthr);
+    dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv,
+                       cbv, tid, nthr, a.x_scale, a.x_shift);
     __syncthreads();
     const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
 #pragma unroll
@@ -500,13 +527,19 @@ int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el), 18.0 * out_el);
   const int nthr = cbv * 32;
+#define DWW_LAUNCH(T, S)                                                              \
+  do {                                                                                \
+    if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, 0, st>>>(a, cbv, tpb);   \
+    else dw_wgrad_kernel<T, S, false><<<grid, nthr, 0, st>>>(a, cbv, tpb);            \
+  } while (0)
   if (dtype == DT_F32) {
-    if (a.stride == 1) dw_wgrad_kernel<float, 1><<<grid, nthr, 0, st>>>(a, cbv, tpb);
-    else dw_wgrad_kernel<float, 2><<<grid, nthr, 0, st>>>(a, cbv, tpb);
+    if (a.stride == 1) DWW_LAUNCH(float, 1);
+    else DWW_LAUNCH(float, 2);
   } else {
-    if (a.stride == 1) dw_wgrad_kernel<bf16, 1><<<grid, nthr, 0, st>>>(a, cbv, tpb);
-    else dw_wgrad_kernel<bf16, 2><<<grid, nthr, 0, st>>>(a, cbv, tpb);
+    if (a.stride == 1) DWW_LAUNCH(bf16, 1);
+    else DWW_LAUNCH(bf16, 2);
   }
+#undef DWW_LAUNCH
   return check_launch("dw_wgrad");
 }
 

@@ -25,6 +25,7 @@ namespace fscnn {
 constexpr int G_BM = 128;
 constexpr int G_VROW = 8;   // 16-B vectors per row per K chunk (128 B)
 constexpr int G_VPAD = 9;   // LDS row stride in vectors
+constexpr int G_ATMAX = 768;  // max K of a lazily normalised A operand (AT)
 
 template <typename T>
 struct MfmaOp;
@@ -85,7 +86,7 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
   }
 }
 
-template <typename T, int NT, bool BT, bool BS>
+template <typename T, int NT, bool BT, bool BS, bool AT>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -102,6 +103,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   auto sB = [&](int b) { return sBbase + b * BN * G_VPAD; };
   float* sC = reinterpret_cast<float*>(s_dyn);      // after the main loop
   __shared__ float s_red[4][BN];
+  // AT: A is the raw conv output z of a BatchNorm+ReLU whose activation is never stored (train
+  // forward); the GEMM consumes relu(fmaf(z, a_scale[k], a_shift[k])), bn_apply's arithmetic
+  __shared__ float s_at[AT ? 2 * G_ATMAX : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -159,13 +163,23 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         rbt[i] = *reinterpret_cast<const uint4*>(B + off);
       }
     }
-    // masks (after all loads are in flight)
+  };
+  // Tail masks (and the lazy BN+ReLU of A) are applied when a chunk is written to LDS, i.e. after
+  // the current chunk's MFMAs: applying them right after issuing the loads made every wave wait
+  // for the next chunk's loads before computing (no fetch/compute overlap).
+  auto store_chunk = [&](int buf, int c) {
+    const int k0 = c * KC;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int id = tid + 256 * i;
       int row = id >> 3, vv = id & 7;
       int m = m0 + row, k = k0 + vv * V;
-      ra[i] = zero_tail<T>(ra[i], m < a.M ? a.K - k : 0);
+      uint4 v = ra[i];
+      if constexpr (AT) {
+        const int kc = k < a.K ? k : 0;
+        v = bnrelu_vec<T>(v, s_at + kc, s_at + G_ATMAX + kc);
+      }
+      sA(buf)[row * G_VPAD + vv] = zero_tail<T>(v, m < a.M ? a.K - k : 0);
     }
     if (!BT) {
 #pragma unroll
@@ -173,29 +187,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         int id = tid + 256 * i;
         int row = id >> 3, vv = id & 7;
         int n = n0 + row, k = k0 + vv * V;
-        rb[i] = zero_tail<T>(rb[i], (id < BN * G_VROW && n < a.N) ? a.K - k : 0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < BT_PER; ++i) {
-        int id = tid + 256 * i;
-        int kk = id / (BN / V), nv = id - kk * (BN / V);
-        int k = k0 + kk, n = n0 + nv * V;
-        rbt[i] = zero_tail<T>(rbt[i], (id < BT_VEC && k < a.K) ? a.N - n : 0);
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int id = tid + 256 * i;
-      sA(buf)[(id >> 3) * G_VPAD + (id & 7)] = ra[i];
-    }
-    if (!BT) {
-#pragma unroll
-      for (int i = 0; i < B_PER; ++i) {
-        int id = tid + 256 * i;
-        if (id < BN * G_VROW) sB(buf)[(id >> 3) * G_VPAD + (id & 7)] = rb[i];
+        if (id < BN * G_VROW)
+          sB(buf)[row * G_VPAD + vv] = zero_tail<T>(rb[i], n < a.N ? a.K - k : 0);
       }
     } else {
       T* sbs = reinterpret_cast<T*>(sB(buf));
@@ -204,7 +197,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         int id = tid + 256 * i;
         if (id < BT_VEC) {
           int kk = id / (BN / V), nv = id - kk * (BN / V);
-          const T* e = reinterpret_cast<const T*>(&rbt[i]);
+          int k = k0 + kk, n = n0 + nv * V;
+          const uint4 v = zero_tail<T>(rbt[i], k < a.K ? a.N - n : 0);
+          const T* e = reinterpret_cast<const T*>(&v);
 #pragma unroll
           for (int j = 0; j < V; ++j) sbs[(nv * V + j) * G_VPAD * V + kk] = e[j];
         }
@@ -218,8 +213,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (AT) {
+    for (int k = tid; k < G_ATMAX; k += 256) {
+      s_at[k] = k < a.K ? a.a_scale[k] : 0.f;
+      s_at[G_ATMAX + k] = k < a.K ? a.a_shift[k] : 0.f;
+    }
+  }
   load_chunk(0);
-  store_chunk(0);
+  if constexpr (AT) __syncthreads();
+  store_chunk(0, 0);
   __syncthreads();
   for (int c = 0; c < nchunks; ++c) {
     const int buf = nbuf == 2 ? (c & 1) : 0;
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
     }
-    if (c + 1 < nchunks) store_chunk(buf ^ 1);
+    if (c + 1 < nchunks) store_chunk(buf ^ 1, c + 1);
     __syncthreads();
   }
 
@@ -447,7 +449,7 @@ static int pick_nt(int N) {
 
 int gemm_parts(int M) { return cdiv(M, G_BM); }
 
-template <typename T, bool BT, bool BS>
+template <typename T, bool BT, bool BS, bool AT = false>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   constexpr int V = VecW<T>::V;
@@ -459,11 +461,11 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS><<<grid, 256, shm, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
   }
 }
 
@@ -494,7 +496,12 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     const char* e = getenv("FSCNN_GEMM_STREAM");
     return !(e && e[0] == '0');
   }();
-  if (stream_on && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
+  const bool at = a.a_scale != nullptr;
+  if (at && (!a.a_shift || a.b_trans || a.bpart || a.K > G_ATMAX || a.K % V)) {
+    set_error("gemm_nt: lazy BN on A needs a plain GEMM with K <= %d, K %% %d == 0", G_ATMAX, V);
+    return E_UNSUPPORTED;
+  }
+  if (stream_on && !at && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
   const bool bs = a.bpart != nullptr;
   if (bs && (a.part || !a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
              (a.bmode != 0 && a.bmode != 2) || a.ldbz % V || !a.b_trans)) {
@@ -503,9 +510,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   }
   if (dtype == DT_F32) {
     if (a.b_trans) { if (bs) launch_nt<float, true, true>(a, nt, st); else launch_nt<float, true, false>(a, nt, st); }
+    else if (at) launch_nt<float, false, false, true>(a, nt, st);
     else launch_nt<float, false, false>(a, nt, st);
   } else {
     if (a.b_trans) { if (bs) launch_nt<bf16, true, true>(a, nt, st); else launch_nt<bf16, true, false>(a, nt, st); }
+    else if (at) launch_nt<bf16, false, false, true>(a, nt, st);
     else launch_nt<bf16, false, false>(a, nt, st);
   }
   return check_launch("gemm_nt");
@@ -552,7 +561,7 @@ struct TnOps<bf16> {
 // 16-B vectors along n / k (coalesced), written TRANSPOSED into LDS (sDt[n][m], sXt[k][m]) so each
 // MFMA operand is one or two 16-B ds_reads; the next chunk's global loads are issued before the
 // current chunk's MFMAs.
-template <typename T>
+template <typename T, bool XT>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int LD = TnOps<T>::LD;
@@ -597,6 +606,23 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
         rx[i][h] = *reinterpret_cast<const uint4*>(X + (okx ? (size_t)m * a.ldx + k : 0));
       }
     }
+  };
+  // XT: X is the raw conv output z of a BatchNorm+ReLU that is never stored (train); the operand
+  // is relu(fmaf(z, x_scale[k], x_shift[k])).  A thread's X vectors all cover one k range
+  // (vv = tid % VPR), so its V (scale, shift) pairs are loaded once.
+  float xsc[XT ? V : 1], xsh[XT ? V : 1];
+  if constexpr (XT) {
+    const int kb = k0 + (tid % VPR) * V;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int k = kb + j < a.K ? kb + j : 0;
+      xsc[j] = a.x_scale[k];
+      xsh[j] = a.x_shift[k];
+    }
+  }
+  // tail masks (and XT) right before the LDS stores, not right after issuing the loads (which
+  // would make the wave wait for them before the current chunk's MFMAs)
+  auto mask = [&](int mc) {
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
       const int id = tid + 256 * i;
@@ -606,13 +632,16 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
       for (int h = 0; h < 2; ++h) {
         const bool okm = mc + 2 * rp + h < me;
         rd[i][h] = zero_tail<T>(rd[i][h], okm ? a.N - n : 0);
-        rx[i][h] = zero_tail<T>(rx[i][h], okm ? a.K - k : 0);
+        uint4 xv = rx[i][h];
+        if constexpr (XT) xv = bnrelu_vec<T>(xv, xsc, xsh);
+        rx[i][h] = zero_tail<T>(xv, okm ? a.K - k : 0);
       }
     }
   };
   using Pair = typename std::conditional<sizeof(T) == 2, uint32_t, uint2>::type;
   if (mb < me) load(mb);
   for (int mc = mb; mc < me; mc += TN_MC) {
+    mask(mc);
     __syncthreads();  // previous chunk's MFMA reads done
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
@@ -685,8 +714,18 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   ProfScope ps(PK_GEMM_TN, st, E * (M * N + M * K) + 4.0 * N * K, 2.0 * M * N * K);
-  if (dtype == DT_F32) gemm_tn_kernel<float><<<grid, 256, 0, st>>>(a);
-  else gemm_tn_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  const bool xt = a.x_scale != nullptr;
+  if (xt && (!a.x_shift || a.K % V)) {
+    set_error("gemm_tn: lazy BN on X needs x_shift and K %% %d == 0", V);
+    return E_UNSUPPORTED;
+  }
+  if (dtype == DT_F32) {
+    if (xt) gemm_tn_kernel<float, true><<<grid, 256, 0, st>>>(a);
+    else gemm_tn_kernel<float, false><<<grid, 256, 0, st>>>(a);
+  } else {
+    if (xt) gemm_tn_kernel<bf16, true><<<grid, 256, 0, st>>>(a);
+    else gemm_tn_kernel<bf16, false><<<grid, 256, 0, st>>>(a);
+  }
   return check_launch("gemm_tn");
 }
 

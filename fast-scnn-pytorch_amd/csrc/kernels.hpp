@@ -38,6 +38,9 @@ struct DwArgs {
   int relu;
   void* y;         // NHWC [N,Ho,Wo,C]
   float* part;     // BN partial records [parts][3][C] or null
+  // lazily applied BN+ReLU of x (train: x is the producer's raw conv output z) or null
+  const float* in_scale = nullptr;
+  const float* in_shift = nullptr;
 };
 
 struct DwBwdArgs {
@@ -47,6 +50,8 @@ struct DwBwdArgs {
   const float* w;   // [C][9]
   void* dx;         // NHWC [N,H,W,C] (dgrad)
   float* slab;      // [parts][9][C] (wgrad)
+  const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
+  const float* x_shift = nullptr;
 };
 
 struct GemmArgs {
@@ -72,6 +77,10 @@ struct GemmArgs {
   const float* bmean = nullptr; const float* binvstd = nullptr;
   const float* bscale = nullptr; const float* bshift = nullptr;  // forward BN affine (mode 2)
   int bmode = 0;        // 0 no ReLU, 2 relu_z: mask = fmaf(z, bscale, bshift) > 0
+  // lazily applied BN+ReLU of the A operand (train forward: A is the producer's raw conv output
+  // z, the GEMM consumes relu(fmaf(z, a_scale[k], a_shift[k]))) or null
+  const float* a_scale = nullptr;
+  const float* a_shift = nullptr;
 };
 
 struct GemmTnArgs {
@@ -83,6 +92,8 @@ struct GemmTnArgs {
   float* slab;   // [splits][N][K]
   int rows_per_split;
   int splits;
+  const float* x_scale = nullptr;  // lazily applied BN+ReLU of X (see GemmArgs::a_scale) or null
+  const float* x_shift = nullptr;
 };
 
 struct FoldEntry {

@@ -152,6 +152,14 @@ struct Alloc {
 };
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
+
+bool lazy_bn_enabled() {  // FSCNN_LAZY_BN=0 materialises every BN output (A/B measurements)
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_LAZY_BN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 }  // namespace
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl) {
@@ -245,6 +253,14 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   if (train) {
     pl.seed_slot = A.get(64);
     pl.fcnt = A.get(64 * 4);
+  }
+  if (train && lazy_bn_enabled()) {
+    // BN+ReLU outputs whose only consumers are GEMM / depthwise operands (and the wgrads reading
+    // them again in the backward) are never stored: bn_apply is skipped and the consumers apply
+    // relu(fmaf(z, scale, shift)) while staging.  Saves a read + write of each tensor per step.
+    pl.c0.lazy = pl.l1dw.lazy = pl.l1pw.lazy = pl.l2dw.lazy = true;
+    for (int i = 0; i < 9; ++i) pl.lbe[i].lazy = pl.lbd[i].lazy = true;
+    pl.fdw.lazy = pl.c1dw.lazy = pl.c1pw.lazy = pl.c2dw.lazy = true;
   }
   pl.ws_bytes = A.top;
   auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
@@ -416,6 +432,19 @@ struct Exec {
     return ws + pl.pbf + (size_t)c.w * 2;
   }
 
+  // ---- operands: an activation buffer, or a lazy unit's z with its BN+ReLU applied on load --
+  struct In {
+    const void* p;
+    int ld;
+    const float* sc;
+    const float* sh;
+  };
+  In act(const Unit& u) const {
+    if (u.lazy) return {W(u.z), u.C, Wf(u.scale), Wf(u.shift)};
+    return {W(u.a), u.ld, nullptr, nullptr};
+  }
+  static In raw(const void* p, int ld) { return {p, ld, nullptr, nullptr}; }
+
   // ---- BN glue -----------------------------------------------------------------------
   int finalize(const Unit& u, const BnL& bn) {
     BnFinalizeArgs f{};
@@ -442,12 +471,13 @@ struct Exec {
 
   // ---- conv + BN (+ReLU) producers -------------------------------------------------------
   // pointwise conv on X [M][K] (ld ldx); eval: fused BN(+res,+relu); train: stats → apply
-  int pw(const Unit& u, const ConvL& c, const BnL* bn, const void* X, int ldx, bool relu,
+  int pw(const Unit& u, const ConvL& c, const BnL* bn, In x, bool relu,
          const void* res = nullptr, int ldres = 0) {
     GemmArgs g{};
-    g.M = (int)u.M; g.N = c.cout; g.K = c.cin;
-    g.A = X; g.lda = ldx;
-    g.B = Wg(c); g.ldb = c.cin; g.b_trans = 0;
+    const int K = c.cin * c.k * c.k;  // 1x1 convs; the aux 3x3 runs on its im2col columns
+    g.M = (int)u.M; g.N = c.cout; g.K = K;
+    g.A = x.p; g.lda = x.ld; g.a_scale = x.sc; g.a_shift = x.sh;
+    g.B = Wg(c); g.ldb = K; g.b_trans = 0;
     if (!train || !bn) {
       g.scale = bn ? Wf(u.scale) : nullptr;
       g.shift = bn ? Wf(u.shift) : P(c.b);
@@ -461,13 +491,17 @@ struct Exec {
     g.part = Wf(u.part);
     TRY(gemm_nt(g, dt, r.st));
     TRY(finalize(u, *bn));
-    return apply(u, relu, res, ldres);
+    return u.lazy ? OK : apply(u, relu, res, ldres);
   }
-  int dw(const Unit& u, const ConvL& c, const BnL& bn, const void* X, int H, int Wd, int Ho, int Wo,
+  int dw(const Unit& u, const ConvL& c, const BnL& bn, In x, int H, int Wd, int Ho, int Wo,
          int stride) {
     DwArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = u.C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
-    d.x = X; d.w = P(c.w);
+    d.x = x.p; d.w = P(c.w); d.in_scale = x.sc; d.in_shift = x.sh;
+    if (x.ld != u.C) {
+      set_error("dw: strided input (ld %d, C %d) not supported", x.ld, u.C);
+      return E_UNSUPPORTED;
+    }
     if (!train) {
       d.scale = Wf(u.scale); d.shift = Wf(u.shift); d.relu = 1; d.y = W(u.a);
       return dw_fwd(d, dt, r.st);
@@ -475,7 +509,7 @@ struct Exec {
     d.relu = 0; d.y = W(u.z); d.part = Wf(u.part);
     TRY(dw_fwd(d, dt, r.st));
     TRY(finalize(u, bn));
-    return apply(u, true);
+    return u.lazy ? OK : apply(u, true);
   }
 
   int fold_all() {
@@ -518,12 +552,15 @@ struct Exec {
       if (!train) { c.scale = Wf(pl.c0.scale); c.shift = Wf(pl.c0.shift); c.relu = 1; c.y = W(pl.c0.a); }
       else { c.relu = 0; c.y = W(pl.c0.z); c.part = Wf(pl.c0.part); }
       TRY(conv0_fwd(c, dt, r.st));
-      if (train) { TRY(finalize(pl.c0, net.b0)); TRY(apply(pl.c0, true)); }
+      if (train) {
+        TRY(finalize(pl.c0, net.b0));
+        if (!pl.c0.lazy) TRY(apply(pl.c0, true));
+      }
     }
-    TRY(dw(pl.l1dw, net.ltd1.dw, net.ltd1.bdw, W(pl.c0.a), pl.H1, pl.W1, pl.H2, pl.W2, 2));
-    TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, W(pl.l1dw.a), 32, true));
-    TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, W(pl.l1pw.a), pl.H2, pl.W2, pl.H3, pl.W3, 2));
-    TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, W(pl.l2dw.a), 48, true));
+    TRY(dw(pl.l1dw, net.ltd1.dw, net.ltd1.bdw, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2));
+    TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, act(pl.l1dw), true));
+    TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2));
+    TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, act(pl.l2dw), true));
     // ---- bottlenecks ----
     const void* x = W(pl.l2pw.a);
     int xld = 64;
@@ -531,11 +568,11 @@ struct Exec {
     for (int i = 0; i < 9; ++i) {
       const LbL& l = net.lb[i];
       int Ho = dwout(Hc, l.stride), Wo = dwout(Wc, l.stride);
-      TRY(pw(pl.lbe[i], l.e, &l.be, x, xld, true));
-      TRY(dw(pl.lbd[i], l.d, l.bd, W(pl.lbe[i].a), Hc, Wc, Ho, Wo, l.stride));
+      TRY(pw(pl.lbe[i], l.e, &l.be, raw(x, xld), true));
+      TRY(dw(pl.lbd[i], l.d, l.bd, act(pl.lbe[i]), Hc, Wc, Ho, Wo, l.stride));
       bool shortcut = l.stride == 1 && l.cin == l.cout;
-      TRY(pw(pl.lbp[i], l.p, &l.bp, W(pl.lbd[i].a), l.cin * 6, false,
-             shortcut ? x : nullptr, shortcut ? xld : 0));
+      TRY(pw(pl.lbp[i], l.p, &l.bp, act(pl.lbd[i]), false, shortcut ? x : nullptr,
+             shortcut ? xld : 0));
       x = W(pl.lbp[i].a);
       xld = pl.lbp[i].ld;
       Hc = Ho; Wc = Wo;
@@ -549,13 +586,13 @@ struct Exec {
       static const int base[4] = {0, 1, 5, 14};
       for (int i = 0; i < 4; ++i) {
         const void* xin = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
-        TRY(pw(pl.ppk[i], net.ppm_c[i], &net.ppm_b[i], xin, 128, true));
+        TRY(pw(pl.ppk[i], net.ppm_c[i], &net.ppm_b[i], raw(xin, 128), true));
       }
       PpmUpArgs u{};
       u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = W(pl.feats_a);
       u.y = W(pl.concat); u.ldy = 256; u.coff = 128;
       TRY(ppm_up_fwd(u, dt, r.st));
-      TRY(pw(pl.po, net.ppm_o, &net.ppm_ob, W(pl.concat), 256, true));
+      TRY(pw(pl.po, net.ppm_o, &net.ppm_ob, raw(W(pl.concat), 256), true));
     }
     // ---- FFM ----
     {
@@ -563,20 +600,22 @@ struct Exec {
       u.N = N; u.Hi = pl.H5; u.Wi = pl.W5; u.C = 128; u.Ho = pl.H3; u.Wo = pl.W3;
       u.x = W(pl.po.a); u.ldx = 128; u.y = W(pl.up_low); u.ldy = 128;
       TRY(up_nhwc(u, dt, r.st));
-      TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+      TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
       if (!train) {
         // f = BN_h(conv_h(hr)) ; f = relu(BN_l(conv_l(dw)) + f)
-        TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, W(pl.l2pw.a), 64, false));
-        TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, W(pl.fdw.a), 128, true,
-               W(pl.f), 128));
+        TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, raw(W(pl.l2pw.a), 64), false));
+        TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, act(pl.fdw), true, W(pl.f), 128));
       } else {
         GemmArgs g{};
-        g.M = (int)pl.flow.M; g.N = 128; g.K = 128; g.A = W(pl.fdw.a); g.lda = 128;
+        const In fin = act(pl.fdw);
+        g.M = (int)pl.flow.M; g.N = 128; g.K = 128; g.A = fin.p; g.lda = fin.ld;
+        g.a_scale = fin.sc; g.a_shift = fin.sh;
         g.B = Wg(net.ffm_low); g.ldb = 128; g.shift = P(net.ffm_low.b);
         g.C = W(pl.flow.z); g.ldc = 128; g.part = Wf(pl.flow.part);
         TRY(gemm_nt(g, dt, r.st));
         TRY(finalize(pl.flow, net.ffm_blow));
         g.K = 64; g.A = W(pl.l2pw.a); g.lda = 64; g.B = Wg(net.ffm_high); g.ldb = 64;
+        g.a_scale = g.a_shift = nullptr;
         g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z); g.part = Wf(pl.fhigh.part);
         TRY(gemm_nt(g, dt, r.st));
         TRY(finalize(pl.fhigh, net.ffm_bhigh));
@@ -589,10 +628,10 @@ struct Exec {
       }
     }
     // ---- Classifier ----
-    TRY(dw(pl.c1dw, net.cls1.dw, net.cls1.bdw, W(pl.f), pl.H3, pl.W3, pl.H3, pl.W3, 1));
-    TRY(pw(pl.c1pw, net.cls1.pw, &net.cls1.bpw, W(pl.c1dw.a), 128, true));
-    TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, W(pl.c1pw.a), pl.H3, pl.W3, pl.H3, pl.W3, 1));
-    TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, W(pl.c2dw.a), 128, true));
+    TRY(dw(pl.c1dw, net.cls1.dw, net.cls1.bdw, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+    TRY(pw(pl.c1pw, net.cls1.pw, &net.cls1.bpw, act(pl.c1dw), true));
+    TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+    TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, act(pl.c2dw), true));
     const void* cls_in = W(pl.c2pw.a);
     if (train && r.dropout_p > 0.f) {
       DropArgs d{};
@@ -665,14 +704,16 @@ struct Exec {
     g.bmode = t.mode;
   }
   // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
-  int pw_bwd(const ConvL& c, long long M, const void* dz, int lddz, const void* X, int ldx,
-             void* dX, int lddx, const void* R = nullptr, int ldr = 0, BTarget bt = BTarget()) {
+  int pw_bwd(const ConvL& c, long long M, const void* dz, int lddz, In X, void* dX, int lddx,
+             const void* R = nullptr, int ldr = 0, BTarget bt = BTarget()) {
+    const int K = c.cin * c.k * c.k;
     GemmTnArgs t{};
-    t.M = (int)M; t.N = c.cout; t.K = c.cin; t.D = dz; t.ldd = lddz; t.X = X; t.ldx = ldx;
+    t.M = (int)M; t.N = c.cout; t.K = K; t.D = dz; t.ldd = lddz; t.X = X.p; t.ldx = X.ld;
+    t.x_scale = X.sc; t.x_shift = X.sh;
     t.slab = (float*)Bw(pl.slab);
-    int S = gemm_tn_splits((int)M, c.cout, c.cin);
+    int S = gemm_tn_splits((int)M, c.cout, K);
     TRY(gemm_tn(t, S, dt, r.st));
-    TRY(reduce_slabs(t.slab, S, (long long)c.cout * c.cin, (long long)c.cout * c.cin, G(c.w), 0, r.st));
+    TRY(reduce_slabs(t.slab, S, (long long)c.cout * K, (long long)c.cout * K, G(c.w), 0, r.st));
     if (c.b >= 0) {
       float* part = (float*)Bw(pl.cspart);
       TRY(colsum(dz, (int)M, c.cout, lddz, part, dt, r.st));
@@ -680,8 +721,8 @@ struct Exec {
     }
     if (!dX) return OK;
     GemmArgs g{};
-    g.M = (int)M; g.N = c.cin; g.K = c.cout; g.A = dz; g.lda = lddz;
-    g.B = Wg(c); g.ldb = c.cin; g.b_trans = 1;
+    g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz; g.lda = lddz;
+    g.B = Wg(c); g.ldb = K; g.b_trans = 1;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
     if (bt.u && train) set_btarget(g, bt);
@@ -691,11 +732,11 @@ struct Exec {
   BTarget plain_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 0; return t; }
   static int pre(const Unit& u) { return gemm_parts((int)u.M); }
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
-  int dw_bwd(const ConvL& c, int C, const void* dz, const void* X, int H, int Wd, int Ho, int Wo,
+  int dw_bwd(const ConvL& c, int C, const void* dz, In X, int H, int Wd, int Ho, int Wo,
              int stride, void* dX) {
     DwBwdArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
-    d.x = X; d.dy = dz; d.w = P(c.w); d.dx = dX; d.slab = (float*)Bw(pl.slab);
+    d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz; d.w = P(c.w); d.dx = dX; d.slab = (float*)Bw(pl.slab);
     TRY(dw_wgrad(d, dt, r.st));
     TRY(dw_wgrad_reduce(d.slab, dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride), C, G(c.w), r.st));
     return dw_dgrad(d, dt, r.st);
@@ -725,8 +766,9 @@ struct Exec {
     }
     // classifier 1x1 (+bias), dropout
     const bool drop = r.dropout_p > 0.f;
-    TRY(pw_bwd(net.cls_out, pl.c2pw.M, Bw(pl.g_logits), pl.Cp, drop ? W(pl.drop) : W(pl.c2pw.a), 128,
-               drop ? Bw(pl.g_drop) : Bw(pl.c2pw.ga), 128));
+    TRY(pw_bwd(net.cls_out, pl.c2pw.M, Bw(pl.g_logits), pl.Cp,
+               raw(drop ? W(pl.drop) : W(pl.c2pw.a), 128), drop ? Bw(pl.g_drop) : Bw(pl.c2pw.ga),
+               128));
     if (drop) {
       DropArgs d{};
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = Bw(pl.g_drop); d.ldx = 128;
@@ -736,25 +778,26 @@ struct Exec {
     }
     // classifier dsconv2, dsconv1
     TRY(bn_bwd_relu(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, dz));
-    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, W(pl.c2dw.a), 128, Bw(pl.c2dw.ga), 128, nullptr, 0,
+    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw)));
     TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz, pre(pl.c2dw)));
-    TRY(dw_bwd(net.cls2.dw, 128, dz, W(pl.c1pw.a), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
+    TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
     TRY(bn_bwd_relu(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, dz));
-    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, W(pl.c1dw.a), 128, Bw(pl.c1dw.ga), 128, nullptr, 0,
+    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw)));
     TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz, pre(pl.c1dw)));
-    TRY(dw_bwd(net.cls1.dw, 128, dz, W(pl.f), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
+    TRY(dw_bwd(net.cls1.dw, 128, dz, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, W(pl.fdw.a), 128, Bw(pl.fdw.ga), 128, nullptr, 0,
+    TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw)));
     TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz, pre(pl.fdw)));
-    TRY(dw_bwd(net.ffm_dw, 128, dz, W(pl.up_low), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_up)));
+    TRY(dw_bwd(net.ffm_dw, 128, dz, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
+               Bw(pl.g_up)));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, W(pl.l2pw.a), 64, Bw(pl.l2pw.ga), 64));
+    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     {
       AxisBwdArgs a{};
@@ -772,7 +815,7 @@ struct Exec {
     }
     // PPM out 1x1 (256→128) over the concat buffer
     TRY(bn_bwd_relu(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, dz));
-    TRY(pw_bwd(net.ppm_o, pl.po.M, dz, 128, W(pl.concat), 256, Bw(pl.g_concat), 256));
+    TRY(pw_bwd(net.ppm_o, pl.po.M, dz, 128, raw(W(pl.concat), 256), Bw(pl.g_concat), 256));
     {
       PpmUpArgs u{};
       u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = nullptr;
@@ -784,7 +827,7 @@ struct Exec {
         size_t off = (size_t)base[i] * N;
         TRY(bn_bwd(u4, net.ppm_b[i], (char*)Bw(pl.g_feats) + off * 32 * E, 32,
                    (char*)W(pl.feats_a) + off * 32 * E, 32, dz));
-        TRY(pw_bwd(net.ppm_c[i], u4.M, dz, 32, (char*)W(pl.pooled) + off * 128 * E, 128,
+        TRY(pw_bwd(net.ppm_c[i], u4.M, dz, 32, raw((char*)W(pl.pooled) + off * 128 * E, 128),
                    (char*)Bw(pl.g_pooled) + off * 128 * E, 128));
       }
       PoolBwdArgs p{};
@@ -811,30 +854,30 @@ struct Exec {
     // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
     // block: its dy is the PPM concat gradient)
     TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz, false, i < 8 ? pre(up) : 0));
-    TRY(pw_bwd(l.p, up.M, dz, l.cout, W(ud.a), e, Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
+    TRY(pw_bwd(l.p, up.M, dz, l.cout, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
     TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz, pre(ud)));
-    TRY(dw_bwd(l.d, e, dz, W(ue.a), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
+    TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
     TRY(bn_bwd_relu(ue, l.be, Bw(ue.ga), e, dz));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
     // the dgrad is the dy of the previous block's project BN (or of LTD.dsconv2's pw BN)
     const BTarget bt = i == 0 ? relu_target(pl.l2pw) : plain_target(pl.lbp[i - 1]);
-    return pw_bwd(l.e, ue.M, dz, e, x, xld, gx, gxld, R, ldr, bt);
+    return pw_bwd(l.e, ue.M, dz, e, raw(x, xld), gx, gxld, R, ldr, bt);
   }
 
   int backward_ltd() {
     void* dz = Bw(pl.dz);
     TRY(bn_bwd_relu(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, dz, pre(pl.l2pw)));
-    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, W(pl.l2dw.a), 48, Bw(pl.l2dw.ga), 48, nullptr, 0,
+    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw)));
     TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz, pre(pl.l2dw)));
-    TRY(dw_bwd(net.ltd2.dw, 48, dz, W(pl.l1pw.a), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
+    TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
     TRY(bn_bwd_relu(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, dz));
-    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, W(pl.l1dw.a), 32, Bw(pl.l1dw.ga), 32, nullptr, 0,
+    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw)));
     TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz, pre(pl.l1dw)));
-    TRY(dw_bwd(net.ltd1.dw, 32, dz, W(pl.c0.a), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
+    TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
     TRY(bn_bwd_relu(pl.c0, net.b0, Bw(pl.c0.ga), 32, dz));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;

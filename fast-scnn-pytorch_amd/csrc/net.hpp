@@ -63,6 +63,9 @@ struct Unit {
   size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
   size_t ga = 0;            // backward: grad wrt a (bwd workspace)
   int ga_ld = 0;
+  // train: the BN+ReLU output is never stored; every consumer (forward GEMM / depthwise and the
+  // backward wgrads) applies relu(fmaf(z, scale, shift)) to z while staging its operand
+  bool lazy = false;
 };
 
 struct GraphCache;
