@@ -230,6 +230,35 @@ int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int 
   GUARD(net_backward(plan->plan, r, stage_from, stage_to));
 }
 
+int fscnn_forward_aux(const fscnn_plan* plan, const void* x, int x_dtype, void* out, void* aux_out,
+                      int out_dtype, const float* params, float* running, long long* nbt,
+                      void* ws, unsigned long long seed, float dropout_p, float momentum,
+                      void* stream) {
+  if (!plan || !x || !out || !aux_out || !params || !running || !ws) {
+    set_error("fscnn_forward_aux: null argument");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.x = x; r.x_dtype = x_dtype; r.out = out; r.aux_out = aux_out; r.out_dtype = out_dtype;
+  r.P = params; r.R = running; r.NBT = nbt; r.ws = ws;
+  r.seed = seed; r.dropout_p = dropout_p; r.momentum = momentum; r.st = S(stream);
+  GUARD(net_forward(plan->plan, r));
+}
+
+int fscnn_backward_aux(const fscnn_plan* plan, const void* dout, const void* daux, const void* x,
+                       int x_dtype, const float* params, float* grads, void* ws, void* bws,
+                       unsigned long long seed, float dropout_p, int stage_from, int stage_to,
+                       void* stream) {
+  if (!plan || !dout || !daux || !x || !params || !grads || !ws || !bws) {
+    set_error("fscnn_backward_aux: null argument");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.dout = dout; r.daux = daux; r.x = x; r.x_dtype = x_dtype; r.P = params; r.G = grads;
+  r.ws = ws; r.bws = bws; r.seed = seed; r.dropout_p = dropout_p; r.st = S(stream);
+  GUARD(net_backward(plan->plan, r, stage_from, stage_to));
+}
+
 int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
                        long long ignore_index, float* loss2, const float* params, float* running,
                        long long* nbt, void* ws, unsigned long long seed, float dropout_p,

@@ -17,7 +17,7 @@
 
 namespace fscnn {
 
-constexpr int HD_T = 256;        // low-res columns per chunk
+constexpr int HD_T = 128;        // low-res columns per chunk
 constexpr int HD_TH = 2 * HD_T;  // threads: a lane pair per column, each lane owning half the classes
 constexpr int HD_CMAX = 32;
 constexpr int HD_TMAX = 2048;  // max full-res row width whose targets are staged in LDS

@@ -227,6 +227,20 @@ struct DropArgs {
   uint64_t seed;
   float p;
   const uint64_t* seed_ptr = nullptr;  // device slot holding the seed (graph-replayable), or null
+  uint64_t seed_add = 0;               // mask seed = seed + seed_add (aux head Dropout: +1)
+};
+
+// aux head 3x3 conv as im2col + GEMM (aux.hip): col[m][c*9 + kh*3 + kw], pad 1, stride 1
+struct Im2ColArgs {
+  int N, H, W, C;
+  const void* x; int ldx;    // NHWC [N][H][W][ldx]
+  void* col; int ldcol;      // [N*H*W][ldcol], ldcol >= 9*C
+};
+struct Col2ImArgs {
+  int N, H, W, C;
+  const void* dcol; int ldcol;
+  void* dx; int lddx;
+  int accumulate;            // dx += (else dx =)
 };
 
 struct SgdArgs {
@@ -292,6 +306,8 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
 int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const float* gout,
                   const float* out2, int dtype, hipStream_t st);
 int dropout(const DropArgs& a, int dtype, hipStream_t st);
+int im2col3(const Im2ColArgs& a, int dtype, hipStream_t st);
+int col2im3(const Col2ImArgs& a, int dtype, hipStream_t st);
 // *p = v (one thread): per-call scalars that captured graphs read from device memory
 int set_u64(uint64_t* p, uint64_t v, hipStream_t st);
 int sgd(const SgdArgs& a, hipStream_t st);

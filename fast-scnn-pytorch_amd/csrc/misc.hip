@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr) 
   if (t >= total) return;
   const unsigned pix = t / CV, cv = t - pix * CV;
   const unsigned n = pix / HW, hw = pix - n * HW;
-  const uint64_t seed = a.seed_ptr ? *a.seed_ptr : a.seed;
+  const uint64_t seed = (a.seed_ptr ? *a.seed_ptr : a.seed) + a.seed_add;
   float v[V];
   ldv((const T*)a.x + (size_t)pix * a.ldx + cv * V, v);
   const float s = 1.f / (1.f - a.p);

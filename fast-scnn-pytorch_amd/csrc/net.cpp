@@ -163,10 +163,6 @@ bool lazy_bn_enabled() {  // FSCNN_LAZY_BN=0 materialises every BN output (A/B m
 }  // namespace
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl) {
-  if (net.aux) {
-    set_error("plan_build: aux head is not implemented on the HIP path yet");
-    return E_UNSUPPORTED;
-  }
   if (N < 1 || H < 3 || W < 3) {
     set_error("plan_build: bad input shape N=%d H=%d W=%d", N, H, W);
     return E_INVALID;
@@ -246,6 +242,12 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   unit(pl.c2pw, M2, 128, gemm_parts((int)M2));
   pl.drop = train ? A.get((size_t)M2 * 128 * E) : pl.c2pw.a;
   pl.logits = A.get((size_t)M2 * pl.Cp * E);
+  if (net.aux) {  // models/fast_scnn.py:24-31: 3x3 conv on im2col columns, BN, ReLU, Dropout, 1x1
+    unit(pl.aux0, M2, 32, gemm_parts((int)M2));
+    pl.aux_col = A.get((size_t)M2 * 576 * E);
+    pl.aux_drop = train ? A.get((size_t)M2 * 32 * E) : pl.aux0.a;
+    pl.aux_logits = A.get((size_t)M2 * pl.Cp * E);
+  }
   if (train) {
     pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
@@ -319,12 +321,19 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     gunit(pl.l1pw);
     gunit(pl.l1dw);
     gunit(pl.c0);
+    if (net.aux) {
+      gunit(pl.aux0);
+      pl.g_auxlog = B.get((size_t)M2 * pl.Cp * E);
+      pl.g_aux = B.get((size_t)M2 * 32 * E);
+      pl.aux_dcol = B.get((size_t)M2 * 576 * E);
+    }
     // scratch sized for the largest consumer
     long long max_mc = 0;
     auto upd = [&](const Unit& u) { if (u.M * u.C > max_mc) max_mc = u.M * u.C; };
     upd(pl.c0); upd(pl.l1dw); upd(pl.l1pw); upd(pl.l2dw); upd(pl.l2pw);
     for (int i = 0; i < 9; ++i) { upd(pl.lbe[i]); upd(pl.lbd[i]); upd(pl.lbp[i]); }
     upd(pl.po); upd(pl.fdw); upd(pl.flow); upd(pl.c1dw); upd(pl.c1pw);
+    if (net.aux) upd(pl.aux0);
     pl.dz = B.get((size_t)max_mc * E);
     // weight-gradient slabs: max over pw convs of splits*N*K, dw parts*9*C, conv0 parts*864
     size_t slab = 0;
@@ -350,6 +359,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pw_slab(M5, 128, 256);
     dw_slab(pl.H3, pl.W3, 128, 1);
     pw_slab(M2, 128, 128); pw_slab(M2, 128, 64); pw_slab(M2, C, 128);
+    if (net.aux) { pw_slab(M2, 32, 576); pw_slab(M2, C, 32); }
     size_t c0s = (size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864;
     if (c0s > slab) slab = c0s;
     pl.slab = B.get(slab * 4);
@@ -367,6 +377,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     for (int i = 0; i < 9; ++i) { bn_upd(pl.lbe[i]); bn_upd(pl.lbd[i]); bn_upd(pl.lbp[i]); }
     for (int i = 0; i < 4; ++i) bn_upd(pl.ppk[i]);
     bn_upd(pl.po); bn_upd(pl.fdw); bn_upd(pl.flow); bn_upd(pl.c1dw); bn_upd(pl.c1pw);
+    if (net.aux) bn_upd(pl.aux0);
     pl.bnpart = B.get(bnp * 4);
     pl.coef = B.get(2 * 1024 * 4);
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
@@ -535,6 +546,7 @@ struct Exec {
     add(net.ffm_bhigh, pl.fhigh, &net.ffm_high);
     add(net.cls1.bdw, pl.c1dw, nullptr); add(net.cls1.bpw, pl.c1pw, nullptr);
     add(net.cls2.bdw, pl.c2dw, nullptr); add(net.cls2.bpw, pl.c2pw, nullptr);
+    if (net.aux) add(net.aux1, pl.aux0, nullptr);
     return bn_fold(t, r.st);
   }
 
@@ -648,6 +660,7 @@ struct Exec {
       g.C = W(pl.logits); g.ldc = pl.Cp;
       TRY(gemm_nt(g, dt, r.st));
     }
+    if (net.aux && r.aux_out) TRY(forward_aux());
     if (r.target) {
       // ---- fused training head: upsample + CE + gradient at low resolution ----
       if (!train) {
@@ -665,6 +678,70 @@ struct Exec {
     u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
     u.x = W(pl.logits); u.ldx = pl.Cp; u.y = r.out; u.ldy = 0;
     return up_nchw(u, dt, r.out_dtype, r.st);
+  }
+
+  // aux head (models/fast_scnn.py:24-31,42-45) on the LearningToDownsample output l2pw.a
+  int forward_aux() {
+    const Unit& u = pl.aux0;
+    Im2ColArgs ic{};
+    ic.N = pl.N; ic.H = pl.H3; ic.W = pl.W3; ic.C = 64; ic.x = W(pl.l2pw.a); ic.ldx = 64;
+    ic.col = W(pl.aux_col); ic.ldcol = 576;
+    TRY(im2col3(ic, dt, r.st));
+    TRY(pw(u, net.aux0, &net.aux1, raw(W(pl.aux_col), 576), true));
+    const void* ain = W(u.a);
+    if (train && r.dropout_p > 0.f) {  // Dropout(0.1): the classifier's mask law with seed + 1
+      DropArgs d{};
+      d.N = pl.N; d.H = pl.H3; d.W = pl.W3; d.C = 32; d.x = W(u.a); d.ldx = 32;
+      d.y = W(pl.aux_drop); d.ldy = 32; d.seed = r.seed; d.p = r.dropout_p; d.seed_add = 1;
+      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
+      TRY(dropout(d, dt, r.st));
+      ain = W(pl.aux_drop);
+    }
+    GemmArgs g{};
+    g.M = (int)u.M; g.N = net.num_classes; g.K = 32; g.A = ain; g.lda = 32;
+    g.B = Wg(net.aux4); g.ldb = 32; g.shift = P(net.aux4.b);
+    g.C = W(pl.aux_logits); g.ldc = pl.Cp;
+    TRY(gemm_nt(g, dt, r.st));
+    UpArgs up{};
+    up.N = pl.N; up.Hi = pl.H3; up.Wi = pl.W3; up.C = net.num_classes; up.Ho = pl.H; up.Wo = pl.W;
+    up.x = W(pl.aux_logits); up.ldx = pl.Cp; up.y = r.aux_out; up.ldy = 0;
+    return up_nchw(up, dt, r.out_dtype, r.st);
+  }
+
+  // aux head backward from d(aux_out); its input gradient is added into l2pw.ga (which the FFM
+  // high-res dgrad has written and bottleneck 1's expand dgrad later accumulates into)
+  int backward_aux() {
+    const int N = pl.N, C = net.num_classes;
+    const Unit& u = pl.aux0;
+    void* dz = Bw(pl.dz);
+    AxisBwdArgs a{};
+    a.n_o1 = (long long)N * C * pl.H; a.n_o2 = 1; a.Lout = pl.W; a.Lin = pl.W3; a.n_in = 1;
+    a.g = r.daux; a.g_s1 = pl.W; a.g_s2 = 0; a.g_idx = 1; a.g_in = 0;
+    a.d = Bw(pl.t_up); a.d_s1 = pl.W3; a.d_s2 = 0; a.d_idx = 1; a.d_in = 0;
+    TRY(axis_bwd(a, dt, DT_F32, r.st));
+    AxisBwdArgs b{};
+    b.n_o1 = N; b.n_o2 = C; b.Lout = pl.H; b.Lin = pl.H3; b.n_in = pl.W3;
+    b.g = Bw(pl.t_up); b.g_s1 = (long long)C * pl.H * pl.W3; b.g_s2 = (long long)pl.H * pl.W3;
+    b.g_idx = pl.W3; b.g_in = 1;
+    b.d = Bw(pl.g_auxlog); b.d_s1 = (long long)pl.H3 * pl.W3 * pl.Cp; b.d_s2 = 1;
+    b.d_idx = (long long)pl.W3 * pl.Cp; b.d_in = pl.Cp;
+    TRY(axis_bwd(b, DT_F32, dt, r.st));
+    const bool drop = r.dropout_p > 0.f;
+    TRY(pw_bwd(net.aux4, u.M, Bw(pl.g_auxlog), pl.Cp, raw(drop ? W(pl.aux_drop) : W(u.a), 32),
+               drop ? Bw(pl.g_aux) : Bw(u.ga), 32));
+    if (drop) {
+      DropArgs d{};
+      d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 32; d.x = Bw(pl.g_aux); d.ldx = 32;
+      d.y = Bw(u.ga); d.ldy = 32; d.seed = r.seed; d.p = r.dropout_p; d.seed_add = 1;
+      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
+      TRY(dropout(d, dt, r.st));
+    }
+    TRY(bn_bwd_relu(u, net.aux1, Bw(u.ga), 32, dz));
+    TRY(pw_bwd(net.aux0, u.M, dz, 32, raw(W(pl.aux_col), 576), Bw(pl.aux_dcol), 576));
+    Col2ImArgs cc{};
+    cc.N = N; cc.H = pl.H3; cc.W = pl.W3; cc.C = 64; cc.dcol = Bw(pl.aux_dcol); cc.ldcol = 576;
+    cc.dx = Bw(pl.l2pw.ga); cc.lddx = 64; cc.accumulate = 1;
+    return col2im3(cc, dt, r.st);
   }
 
   // ================================ backward ===============================================
@@ -798,6 +875,7 @@ struct Exec {
                Bw(pl.g_up)));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
+    if (net.aux) TRY(backward_aux());
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     {
       AxisBwdArgs a{};
@@ -1016,6 +1094,14 @@ int run_graphed(const Plan& pl, std::vector<uint64_t> key, hipStream_t st, F&& b
 }  // namespace
 
 int net_forward(const Plan& pl, const RunArgs& r) {
+  if (pl.net->aux && r.target) {
+    set_error("forward_loss: the fused loss head covers the main output only (aux net)");
+    return E_UNSUPPORTED;
+  }
+  if (pl.net->aux && !r.aux_out) {
+    set_error("fscnn_forward: this net has the aux head; use fscnn_forward_aux");
+    return E_INVALID;
+  }
   if (pl.train && r.dropout_p > 0.f)  // read by the dropout kernels (outside any graph)
     TRY(set_u64(reinterpret_cast<uint64_t*>((char*)r.ws + pl.seed_slot), r.seed, r.st));
   return run_graphed(pl, run_key(0, 0, 0, r), r.st, [&](hipStream_t st) -> int {
@@ -1031,6 +1117,10 @@ int net_forward(const Plan& pl, const RunArgs& r) {
 int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to) {
   if (!pl.train) {
     set_error("net_backward: the plan was built for inference (train=0)");
+    return E_INVALID;
+  }
+  if (pl.net->aux && !r.daux) {
+    set_error("fscnn_backward: this net has the aux head; use fscnn_backward_aux");
     return E_INVALID;
   }
   for (int s = stage_from; s <= stage_to; ++s)

@@ -84,14 +84,14 @@ struct Plan {
   Unit c1dw, c1pw, c2dw, c2pw;
   Unit aux0;
   size_t concat = 0, pooled = 0, feats_a = 0, feats_z = 0, up_low = 0, f = 0, drop = 0,
-         logits = 0, aux_drop = 0, aux_logits = 0, pbf = 0, fold_tmp = 0;
+         logits = 0, aux_drop = 0, aux_logits = 0, aux_col = 0, pbf = 0, fold_tmp = 0;
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   size_t fcnt = 0, bcnt = 0;        // BN fold+finalize arrival counters (ws / bws), 64 each
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
-         g_aux = 0, g_auxlog = 0;
+         g_aux = 0, g_auxlog = 0, aux_dcol = 0;
   // named buffers for debugging / stage-level parity: name -> (offset, rows, cols, ld, in_bws)
   struct Named { std::string name; size_t off; long long rows; int cols, ld, bws; };
   std::vector<Named> named;

@@ -204,16 +204,17 @@ class _FastSCNNFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, model, *params):
-        out, ws, seed, dt = model._run_forward(x, train=True)
+        outs, ws, seed, dt = model._run_forward(x, train=True)
         ctx.model = model
         ctx.ws, ctx.seed, ctx.dt = ws, seed, dt
         ctx.save_for_backward(x)
-        return out
+        return outs if len(outs) > 1 else outs[0]
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, *gouts):
         (x,) = ctx.saved_tensors
-        grads = ctx.model._run_backward(gout, x, ctx.ws, ctx.seed, ctx.dt)
+        gaux = gouts[1] if len(gouts) > 1 else None
+        grads = ctx.model._run_backward(gouts[0], x, ctx.ws, ctx.seed, ctx.dt, gaux=gaux)
         ctx.ws = None
         return (None, None) + tuple(grads)
 
@@ -367,18 +368,24 @@ class FastSCNN(nn.Module):
         plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), train)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         out = torch.empty((N, self.num_classes, H, W), dtype=dt, device=x.device)
+        aux_out = torch.empty_like(out) if self.aux else None
         p = self._dropout_p() if train else 0.0
         seed = 0
         if train and p > 0:
             fixed = getattr(self, "_dropout_seed", None)  # tests pin the mask (oracle parity)
             seed = int(fixed) if fixed is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
-        _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(out),
-                  _lib.dtype_code(dt), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]),
-                  _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p), _lib.c_float(self._momentum()),
-                  _lib.stream_ptr(x.device))
+        rest = (_lib.dtype_code(dt), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]),
+                _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p), _lib.c_float(self._momentum()),
+                _lib.stream_ptr(x.device))
+        if self.aux:  # models/fast_scnn.py:42-45
+            _lib.call("fscnn_forward_aux", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
+                      _lib.ptr(out), _lib.ptr(aux_out), *rest)
+        else:
+            _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(out),
+                      *rest)
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
-        return out, ws, seed, dt
+        return ((out, aux_out) if self.aux else (out,)), ws, seed, dt
 
     def debug_buffer(self, name):
         """Tensor view of a named plan buffer of the last forward/backward (set ``_keep_ws``).
@@ -399,6 +406,10 @@ class FastSCNN(nn.Module):
         return flat.as_strided((rows.value, cols.value), (ld.value, 1))
 
     def _run_forward_loss(self, x, target, ignore_index):
+        if self.aux:
+            raise RuntimeError("forward_loss: the fused loss head covers the main output only; "
+                               "with aux=True use MixSoftmaxCrossEntropyLoss(aux=True)"
+                               "(model(x), target)")
         if not x.is_cuda or not target.is_cuda:
             raise RuntimeError("FastSCNN.forward_loss: the HIP path needs ROCm device tensors")
         nat = self.native()
@@ -441,13 +452,15 @@ class FastSCNN(nn.Module):
         ar = self.arena()
         return _FastSCNNLossFunction.apply(x, target, ignore_index, self, *ar["params"])
 
-    def _run_backward(self, gout, x, ws, seed, dt, gloss=None, loss2=None):
+    def _run_backward(self, gout, x, ws, seed, dt, gloss=None, loss2=None, gaux=None):
         nat = self.native()
         ar = self.arena()
         N, _, H, W = x.shape
         plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), True)
         if gout is not None:
             gout = gout.to(dt).contiguous()
+        if self.aux and gloss is None:
+            gaux = torch.zeros_like(gout) if gaux is None else gaux.to(dt).contiguous()
         G = torch.zeros(nat.p_total, dtype=torch.float32, device=x.device)
         bws = torch.empty(max(bw, 1), dtype=torch.uint8, device=x.device)
         p = self._dropout_p()
@@ -455,7 +468,12 @@ class FastSCNN(nn.Module):
             self._debug["bws"] = bws
         hook = self.grad_stage_hook
         for s in range(4):
-            if gloss is None:
+            if gloss is None and self.aux:
+                _lib.call("fscnn_backward_aux", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(x),
+                          _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                          _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                          _lib.stream_ptr(x.device))
+            elif gloss is None:
                 _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x),
                           _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
                           _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
@@ -479,9 +497,8 @@ class FastSCNN(nn.Module):
             if ar is None:
                 self._run_forward(x, train)  # raises the device error
             out = _FastSCNNFunction.apply(x, self, *ar["params"])
-        else:
-            out = self._run_forward(x, train)[0]
-        return (out,)
+            return tuple(out) if self.aux else (out,)
+        return self._run_forward(x, train)[0]
 
 
 def get_fast_scnn(dataset="citys", pretrained=False, root="./weights", map_cpu=False, **kwargs):

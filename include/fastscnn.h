@@ -74,6 +74,20 @@ int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int 
                    unsigned long long dropout_seed, float dropout_p, int stage_from,
                    int stage_to, void* stream);
 
+/* FastSCNN(aux=True) (models/fast_scnn.py:24-31, 42-45): the same forward / backward plus the
+ * auxiliary head (3x3 conv 64->32 + BN + ReLU + Dropout + 1x1 on the LearningToDownsample output,
+ * upsampled like the main logits).  aux_out / daux: NCHW [N][C][H][W] in out_dtype.  Plans of an
+ * aux net must use these entry points (fscnn_forward / fscnn_backward return -1;
+ * fscnn_forward_loss covers the main output only and returns -2). */
+int fscnn_forward_aux(const fscnn_plan* plan, const void* x, int x_dtype, void* out, void* aux_out,
+                      int out_dtype, const float* params, float* running, long long* nbt,
+                      void* ws, unsigned long long dropout_seed, float dropout_p, float momentum,
+                      void* stream);
+int fscnn_backward_aux(const fscnn_plan* plan, const void* dout, const void* daux, const void* x,
+                       int x_dtype, const float* params, float* grads, void* ws, void* bws,
+                       unsigned long long dropout_seed, float dropout_p, int stage_from,
+                       int stage_to, void* stream);
+
 /* Fused training step head (train plans only): forward + bilinear upsample + CE(ignore_index)
  * evaluated at low resolution; loss2[0] = mean loss, loss2[1] = valid pixel count.  Computes
  * exactly criterion(model(x)[0], target) of train.py:270-271 without materialising the

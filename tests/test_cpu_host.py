@@ -78,10 +78,11 @@ def test_plans_and_workspace_sizes():
     dims2 = (_lib.c_int * 10)()
     _lib.check(nat.lib.fscnn_plan_shapes(p2, dims2))
     assert list(dims2) == [383, 383, 192, 192, 96, 96, 48, 48, 24, 24]
-    # aux head is reported as unsupported on the HIP path (not silently wrong)
+    # the aux head (models/fast_scnn.py:24-31) plans its im2col columns and buffers on top
     nat_aux = _Native(19, True)
-    with pytest.raises(RuntimeError):
-        nat_aux.plan(2, 128, 256, _lib.DT_F32, False)
+    _, fwa, bwa = nat_aux.plan(2, 128, 256, _lib.DT_F32, True)
+    _, fw0, bw0 = nat.plan(2, 128, 256, _lib.DT_F32, True)
+    assert fwa > fw0 and bwa > bw0
     with pytest.raises(RuntimeError):
         nat.plan(0, 128, 256, _lib.DT_F32, False)
 
