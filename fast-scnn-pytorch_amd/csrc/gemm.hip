@@ -793,6 +793,71 @@ int reduce_slabs(float* slab, int S, long long stride, long long count, float* o
   return reduce_slabs_ex(slab, S, stride, count, out, accumulate, 0, st);
 }
 
+// Multi-job form: block b of the flattened job table belongs to the job whose [blk0, blk0')
+// range holds b; every job is folded / summed exactly as reduce_slabs_ex does it (same
+// assignment and order, so the result is bit-identical).
+__device__ __forceinline__ int red_job(const RedTable& t, int b) {
+  int lo = 0, hi = t.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.blk0[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void reduce_fold_multi_kernel(RedTable t) {
+  const int jb = red_job(t, blockIdx.x);
+  const RedJob& J = t.j[jb];
+  if (J.S <= RED_Q) return;
+  const int i = (blockIdx.x - t.blk0[jb]) * blockDim.x + threadIdx.x;
+  const int q = blockIdx.y;
+  if (i >= J.count) return;
+  float s = 0.f;
+  for (int k0 = q; k0 < J.S; k0 += 8 * RED_Q) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u * RED_Q;
+      const float x = J.slab[(size_t)(k < J.S ? k : q) * J.stride + i];
+      v[u] = k < J.S ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  J.slab[(size_t)q * J.stride + i] = s;
+}
+
+__global__ void reduce_final_multi_kernel(RedTable t) {
+  const int jb = red_job(t, blockIdx.x);
+  const RedJob& J = t.j[jb];
+  const int i = (blockIdx.x - t.blk0[jb]) * blockDim.x + threadIdx.x;
+  if (i >= J.count) return;
+  const int S = J.S > RED_Q ? RED_Q : J.S;
+  float s = 0.f;
+  for (int k0 = 0; k0 < S; k0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float x = J.slab[(size_t)(k0 + u < S ? k0 + u : 0) * J.stride + i];
+      v[u] = k0 + u < S ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  const int o = J.C9 ? (i % J.C9) * 9 + i / J.C9 : i;
+  J.out[o] = J.accumulate ? J.out[o] + s : s;
+}
+
+int reduce_slabs_multi(const RedTable& t, hipStream_t st) {
+  if (t.n <= 0) return OK;
+  bool fold = false;
+  for (int k = 0; k < t.n; ++k) fold = fold || t.j[k].S > RED_Q;
+  if (fold) reduce_fold_multi_kernel<<<dim3(t.blocks, RED_Q), 256, 0, st>>>(t);
+  reduce_final_multi_kernel<<<t.blocks, 256, 0, st>>>(t);
+  return check_launch("reduce_slabs_multi");
+}
+
 // per-block column sums of D [M][N] (ld) -> part [P][N]  (bias gradients)
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* D, int M, int N, int ld,

@@ -17,8 +17,7 @@
 
 namespace fscnn {
 
-constexpr int HD_T = 128;        // low-res columns per chunk
-constexpr int HD_TH = 2 * HD_T;  // threads: a lane pair per column, each lane owning half the classes
+constexpr int HD_T = 256;
 constexpr int HD_CMAX = 32;
 constexpr int HD_TMAX = 2048;  // max full-res row width whose targets are staged in LDS
 
@@ -32,25 +31,17 @@ __device__ __forceinline__ int hd_first_ge(int i, int Lin, int Lout, float sc) {
   return lo;
 }
 
-// Lane pair (2p, 2p+1) owns low-res column p; lane `half` holds classes [half*CH, half*CH + CH).
-// Softmax max / sum and the target logit are combined across the pair with one xor-1 shuffle
-// each, so per-thread state (4 accumulators + 2 interpolated rows per class) is halved: ~100
-// VGPRs instead of ~240 for 19 classes, i.e. twice the waves in flight.
 template <typename T, int CT, bool EXACT>
-__global__ __launch_bounds__(HD_TH) void ce_head_kernel(CeHeadArgs a) {
-  constexpr int CH = (CT + 1) / 2;  // classes per lane
-  constexpr int CS = 2 * CH;        // staged classes per column (zero padded)
-  constexpr int SL = CS + 1;        // odd LDS stride per column
+__global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
+  constexpr int SL = (CT % 2 == 0) ? CT + 1 : CT;  // odd LDS stride per column
   __shared__ float s_L[2 * (HD_T + 1) * SL];
-  __shared__ float s_carry[2 * CS];
+  __shared__ float s_carry[2 * CT];
   __shared__ signed char s_t[2 * HD_TMAX];
-  __shared__ float s_r1[HD_TH], s_r2[HD_TH];
+  __shared__ float s_r1[HD_T], s_r2[HD_T];
   const int tid = threadIdx.x;
-  const int pc = tid >> 1, half = tid & 1, cb0 = half * CH;
   const int hl = blockIdx.x, n = blockIdx.y;
   const int Hl = a.Hl, Wl = a.Wl, H = a.H, W = a.W, ldl = a.ldl;
   const int Cm = EXACT ? CT : a.C;
-  const int cval = Cm - cb0;  // this lane's class c is real iff c < cval
   const float sh = ac_scale(Hl, H), sw = ac_scale(Wl, W);
   const int h_lo = hd_first_ge(hl, Hl, H, sh), h_hi = hd_first_ge(hl + 1, Hl, H, sh);
   const int hl1 = min(hl + 1, Hl - 1);
@@ -59,15 +50,15 @@ __global__ __launch_bounds__(HD_TH) void ce_head_kernel(CeHeadArgs a) {
   float* g1 = a.g_raw + (size_t)a.N * Hl * Wl * ldl;  // spill plane (row hl+1)
   const long long* tgt = a.target + (size_t)n * H * W;
   float loss = 0.f, cnt = 0.f;
-  if (tid < 2 * CS) s_carry[tid] = 0.f;
+  if (tid < 2 * CT) s_carry[tid] = 0.f;
   if (hl == 0) {  // nothing spills into row 0
-    for (int i = tid; i < Wl * ldl; i += HD_TH) g1[(size_t)n * Hl * Wl * ldl + i] = 0.f;
+    for (int i = tid; i < Wl * ldl; i += HD_T) g1[(size_t)n * Hl * Wl * ldl + i] = 0.f;
   }
   for (int cb = 0; cb < Wl; cb += HD_T) {
     __syncthreads();
     // ---- stage low-res rows hl, hl1 for columns [cb, cb + HD_T] (clamped) -----------------
-    for (int i = tid; i < 2 * (HD_T + 1) * CS; i += HD_TH) {
-      const int c = i % CS, jr = i / CS;
+    for (int i = tid; i < 2 * (HD_T + 1) * CT; i += HD_T) {
+      const int c = i % CT, jr = i / CT;
       const int j = jr % (HD_T + 1), r = jr / (HD_T + 1);
       const int col = min(cb + j, Wl - 1);
       const int row = r ? hl1 : hl;
@@ -75,45 +66,45 @@ __global__ __launch_bounds__(HD_TH) void ce_head_kernel(CeHeadArgs a) {
           c < Cm ? ld1(lg + ((size_t)row * Wl + col) * ldl + c) : 0.f;
     }
     __syncthreads();
-    const int t = cb + pc;
+    const int t = cb + tid;
     const bool active = t < Wl;
-    float acc00[CH], acc01[CH], acc10[CH], acc11[CH];
+    float acc00[CT], acc01[CT], acc10[CT], acc11[CT];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) acc00[c] = acc01[c] = acc10[c] = acc11[c] = 0.f;
+    for (int c = 0; c < CT; ++c) acc00[c] = acc01[c] = acc10[c] = acc11[c] = 0.f;
     // the full-resolution target rows are loaded by the whole workgroup with coalesced int64
     // loads (next row prefetched into registers during the current row) and kept in LDS as int8
     // class indices (-1 = ignored); all threads run the row loop (inactive columns: no pixels)
     const int w_lo = active ? hd_first_ge(t, Wl, W, sw) : 0;
     const int w_hi = active ? hd_first_ge(t + 1, Wl, W, sw) : 0;
     const bool lds_t = W <= HD_TMAX;
-    constexpr int TPT = HD_TMAX / HD_TH;
+    constexpr int TPT = HD_TMAX / HD_T;
     int tnext[TPT];
     auto load_trow = [&](int h) {
       const long long* tr = tgt + (size_t)h * W;
 #pragma unroll
       for (int k = 0; k < TPT; ++k) {
-        const int w = tid + HD_TH * k;
+        const int w = tid + HD_T * k;
         const long long tg = tr[w < W ? w : 0];
         tnext[k] = (w < W && tg != a.ignore_index && tg >= 0 && tg < Cm) ? (int)tg : -1;
       }
     };
     if (lds_t && h_lo < h_hi) load_trow(h_lo);
-    const float* L0 = &s_L[pc * SL + cb0];
-    const float* L1 = &s_L[((HD_T + 1) + pc) * SL + cb0];
+    const float* L0 = &s_L[tid * SL];
+    const float* L1 = &s_L[((HD_T + 1) + tid) * SL];
     for (int h = h_lo; h < h_hi; ++h) {
       signed char* trow_s = s_t + (h & 1) * HD_TMAX;
       if (lds_t) {
 #pragma unroll
         for (int k = 0; k < TPT; ++k)
-          if (tid + HD_TH * k < W) trow_s[tid + HD_TH * k] = (signed char)tnext[k];
+          if (tid + HD_T * k < W) trow_s[tid + HD_T * k] = (signed char)tnext[k];
         __syncthreads();
         if (h + 1 < h_hi) load_trow(h + 1);
       }
       if (active) {
         const Lerp lh = ac_lerp(h, Hl, H, sh);
-        float v0[CH], v1[CH];
+        float v0[CT], v1[CT];
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
+        for (int c = 0; c < CT; ++c) {
           v0[c] = lh.l0 * L0[c] + lh.l1 * L1[c];
           v1[c] = lh.l0 * L0[SL + c] + lh.l1 * L1[SL + c];
         }
@@ -128,34 +119,30 @@ __global__ __launch_bounds__(HD_TH) void ce_head_kernel(CeHeadArgs a) {
             ti = (tg != a.ignore_index && tg >= 0 && tg < Cm) ? (int)tg : -1;
           }
           const bool valid = ti >= 0;
-          const int tl = ti - cb0;  // target class index in this lane's half (may be outside)
-          float e[CH];
+          float e[CT];
           float mx = -INFINITY, lt = 0.f;
 #pragma unroll
-          for (int c = 0; c < CH; ++c) {
+          for (int c = 0; c < CT; ++c) {
             e[c] = lw.l0 * v0[c] + lw.l1 * v1[c];
-            if (c < cval) mx = fmaxf(mx, e[c]);
-            lt = (c == tl) ? e[c] : lt;
+            if (c < Cm) mx = fmaxf(mx, e[c]);
+            lt = (c == ti) ? e[c] : lt;
           }
-          mx = fmaxf(mx, __shfl_xor(mx, 1));
-          lt += __shfl_xor(lt, 1);
           float se = 0.f;
 #pragma unroll
-          for (int c = 0; c < CH; ++c) {
-            e[c] = c < cval ? __expf(e[c] - mx) : 0.f;  // v_exp_f32 path; loss uses accurate logf
+          for (int c = 0; c < CT; ++c) {
+            e[c] = c < Cm ? __expf(e[c] - mx) : 0.f;  // v_exp_f32 path; loss uses accurate logf
             se += e[c];
           }
-          se += __shfl_xor(se, 1);
           const float inv = valid ? __builtin_amdgcn_rcpf(se) : 0.f;  // v_rcp_f32 (1 ulp)
-          if (valid && half == 0) {
+          if (valid) {
             loss += mx + logf(se) - lt;
             cnt += 1.f;
           }
           const float k00 = lh.l0 * lw.l0, k01 = lh.l0 * lw.l1;
           const float k10 = lh.l1 * lw.l0, k11 = lh.l1 * lw.l1;
 #pragma unroll
-          for (int c = 0; c < CH; ++c) {
-            const float g = e[c] * inv - ((valid && c == tl) ? 1.f : 0.f);
+          for (int c = 0; c < CT; ++c) {
+            const float g = e[c] * inv - ((valid && c == ti) ? 1.f : 0.f);
             acc00[c] += k00 * g;
             acc01[c] += k01 * g;
             acc10[c] += k10 * g;
@@ -167,7 +154,7 @@ __global__ __launch_bounds__(HD_TH) void ce_head_kernel(CeHeadArgs a) {
     if (active) {
       if (t == Wl - 1) {  // i1(w) == i0(w) on the last column: both taps are column t
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
+        for (int c = 0; c < CT; ++c) {
           acc00[c] += acc01[c];
           acc10[c] += acc11[c];
           acc01[c] = acc11[c] = 0.f;
@@ -175,48 +162,47 @@ __global__ __launch_bounds__(HD_TH) void ce_head_kernel(CeHeadArgs a) {
       }
       if (hl1 == hl) {  // last row: both row taps are row hl
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
+        for (int c = 0; c < CT; ++c) {
           acc00[c] += acc10[c];
           acc01[c] += acc11[c];
           acc10[c] = acc11[c] = 0.f;
         }
       }
     }
-    // ---- hand the (*, t+1) shares to column t+1 through LDS -------------------------------
+    // ---- hand the (*, t+1) shares to thread t+1 through LDS -------------------------------
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      s_L[pc * SL + cb0 + c] = acc01[c];
-      s_L[((HD_T + 1) + pc) * SL + cb0 + c] = acc11[c];
+    for (int c = 0; c < CT; ++c) {
+      s_L[tid * SL + c] = acc01[c];
+      s_L[((HD_T + 1) + tid) * SL + c] = acc11[c];
     }
     __syncthreads();
     if (active) {
       float* o0 = g0 + (((size_t)n * Hl + hl) * Wl + t) * ldl;
       float* o1 = g1 + (((size_t)n * Hl + hl + 1) * Wl + t) * ldl;
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        if (c < cval) {
-          const int cg = cb0 + c;
-          const float left0 = pc > 0 ? s_L[(pc - 1) * SL + cg] : s_carry[cg];
-          const float left1 = pc > 0 ? s_L[((HD_T + 1) + pc - 1) * SL + cg] : s_carry[CS + cg];
-          o0[cg] = acc00[c] + left0;
-          if (hl1 != hl) o1[cg] = acc10[c] + left1;
+      for (int c = 0; c < CT; ++c) {
+        if (c < Cm) {
+          const float left0 = tid > 0 ? s_L[(tid - 1) * SL + c] : s_carry[c];
+          const float left1 = tid > 0 ? s_L[((HD_T + 1) + tid - 1) * SL + c] : s_carry[CT + c];
+          o0[c] = acc00[c] + left0;
+          if (hl1 != hl) o1[c] = acc10[c] + left1;
         }
       }
     }
     __syncthreads();
-    if (pc == HD_T - 1) {  // column cb + HD_T starts the next chunk
+    if (tid == HD_T - 1) {  // column cb + HD_T starts the next chunk
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        s_carry[cb0 + c] = acc01[c];
-        s_carry[CS + cb0 + c] = acc11[c];
+      for (int c = 0; c < CT; ++c) {
+        s_carry[c] = acc01[c];
+        s_carry[CT + c] = acc11[c];
       }
     }
   }
   s_r1[tid] = loss;
   s_r2[tid] = cnt;
   __syncthreads();
-  for (int off = HD_TH / 2; off > 0; off >>= 1) {
+  for (int off = HD_T / 2; off > 0; off >>= 1) {
     if (tid < off) {
       s_r1[tid] += s_r1[tid + off];
       s_r2[tid] += s_r2[tid + off];
@@ -267,17 +253,17 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
                  0.0);
     const bool f32 = dtype == DT_F32;
     if (a.C == 19) {
-      if (f32) ce_head_kernel<float, 19, true><<<grid, HD_TH, 0, st>>>(a);
-      else ce_head_kernel<bf16, 19, true><<<grid, HD_TH, 0, st>>>(a);
+      if (f32) ce_head_kernel<float, 19, true><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, 19, true><<<grid, HD_T, 0, st>>>(a);
     } else if (a.C == 2) {
-      if (f32) ce_head_kernel<float, 2, true><<<grid, HD_TH, 0, st>>>(a);
-      else ce_head_kernel<bf16, 2, true><<<grid, HD_TH, 0, st>>>(a);
+      if (f32) ce_head_kernel<float, 2, true><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, 2, true><<<grid, HD_T, 0, st>>>(a);
     } else if (a.C <= 8) {
-      if (f32) ce_head_kernel<float, 8, false><<<grid, HD_TH, 0, st>>>(a);
-      else ce_head_kernel<bf16, 8, false><<<grid, HD_TH, 0, st>>>(a);
+      if (f32) ce_head_kernel<float, 8, false><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, 8, false><<<grid, HD_T, 0, st>>>(a);
     } else {
-      if (f32) ce_head_kernel<float, HD_CMAX, false><<<grid, HD_TH, 0, st>>>(a);
-      else ce_head_kernel<bf16, HD_CMAX, false><<<grid, HD_TH, 0, st>>>(a);
+      if (f32) ce_head_kernel<float, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
+      else ce_head_kernel<bf16, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
     }
     int rc = check_launch("ce_head");
     if (rc) return rc;

@@ -277,6 +277,22 @@ int reduce_slabs(float* slab, int S, long long stride, long long count, float* o
                  int accumulate, hipStream_t st);
 int reduce_slabs_ex(float* slab, int S, long long stride, long long count, float* out,
                     int accumulate, int C9, hipStream_t st);
+// Deferred weight-gradient reductions: the slab reductions of a backward stage are queued and run
+// by two launches (fold + final) over the whole job table instead of two per weight tensor.
+constexpr int RED_MAXJOBS = 48;
+struct RedJob {
+  float* slab;   // [S][stride] partials (consumed)
+  float* out;
+  long long stride;
+  int S, count, accumulate, C9;
+};
+struct RedTable {
+  int n = 0;
+  int blocks = 0;                 // 256-element blocks over all jobs
+  int blk0[RED_MAXJOBS + 1] = {};  // first block of each job
+  RedJob j[RED_MAXJOBS];
+};
+int reduce_slabs_multi(const RedTable& t, hipStream_t st);
 int colsum_parts(int M);
 int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStream_t st);
 

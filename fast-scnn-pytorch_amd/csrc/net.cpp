@@ -335,15 +335,17 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     upd(pl.po); upd(pl.fdw); upd(pl.flow); upd(pl.c1dw); upd(pl.c1pw);
     if (net.aux) upd(pl.aux0);
     pl.dz = B.get((size_t)max_mc * E);
-    // weight-gradient slabs: max over pw convs of splits*N*K, dw parts*9*C, conv0 parts*864
+    // weight-gradient partial slabs: the reductions of a backward stage are deferred to one
+    // multi-job launch pair (Exec::flush_reduce), so every job keeps its own slab until then;
+    // the arena holds the whole step's (sum over jobs, 64-float aligned each)
     size_t slab = 0;
-    auto pw_slab = [&](long long M, int n, int k) {
-      size_t s = (size_t)gemm_tn_splits((int)M, n, k) * n * k;
-      if (s > slab) slab = s;
+    auto add_slab = [&](size_t floats) { slab += (floats + 63) / 64 * 64; };
+    auto pw_slab = [&](long long M, int n, int k, bool bias = false) {
+      add_slab((size_t)gemm_tn_splits((int)M, n, k) * n * k);
+      if (bias) add_slab((size_t)colsum_parts((int)M) * n);
     };
     auto dw_slab = [&](int Ho, int Wo, int Cc, int st) {
-      size_t s = (size_t)dw_wgrad_parts(N, Ho, Wo, Cc, dtype, st) * 9 * Cc;
-      if (s > slab) slab = s;
+      add_slab((size_t)dw_wgrad_parts(N, Ho, Wo, Cc, dtype, st) * 9 * Cc);
     };
     pw_slab(M1, 48, 32); pw_slab(M2, 64, 48);
     dw_slab(pl.H2, pl.W2, 32, 2); dw_slab(pl.H3, pl.W3, 48, 2);
@@ -357,11 +359,13 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     }
     for (int i = 0; i < 4; ++i) pw_slab(pl.ppk[i].M, 32, 128);
     pw_slab(M5, 128, 256);
-    dw_slab(pl.H3, pl.W3, 128, 1);
-    pw_slab(M2, 128, 128); pw_slab(M2, 128, 64); pw_slab(M2, C, 128);
-    if (net.aux) { pw_slab(M2, 32, 576); pw_slab(M2, C, 32); }
-    size_t c0s = (size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864;
-    if (c0s > slab) slab = c0s;
+    for (int i = 0; i < 3; ++i) dw_slab(pl.H3, pl.W3, 128, 1);  // FFM dw, classifier dw x2
+    pw_slab(M2, 128, 128, true); pw_slab(M2, 128, 64, true);   // FFM low / high (bias)
+    pw_slab(M2, 128, 128); pw_slab(M2, 128, 128);              // classifier dsconv pw x2
+    pw_slab(M2, C, 128, true);                                 // classifier 1x1 (bias)
+    if (net.aux) { pw_slab(M2, 32, 576); pw_slab(M2, C, 32, true); }
+    add_slab((size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864);
+    pl.slab_floats = slab;
     pl.slab = B.get(slab * 4);
     pl.bcnt = B.get(64 * 4);
     // BN backward partials: max P*2*C
@@ -441,6 +445,43 @@ struct Exec {
   const void* Wg(const ConvL& c) const {
     if (dt == DT_F32) return r.P + c.w;
     return ws + pl.pbf + (size_t)c.w * 2;
+  }
+
+  // ---- deferred weight-gradient reductions ----------------------------------------------
+  RedTable red;
+  size_t slab_top = 0;  // floats of the plan's slab arena in use
+  float* slab_alloc(size_t floats) {
+    const size_t n = (floats + 63) / 64 * 64;
+    if (slab_top + n > pl.slab_floats) return nullptr;
+    float* p = (float*)Bw(pl.slab) + slab_top;
+    slab_top += n;
+    return p;
+  }
+  int defer_reduce(float* slab, int S, long long count, float* out, int C9) {
+    if (red.n == RED_MAXJOBS) TRY(flush_reduce());
+    if (count <= 0 || count > 0x7fffffff) {
+      set_error("defer_reduce: bad count %lld", count);
+      return E_INVALID;
+    }
+    RedJob& J = red.j[red.n];
+    J.slab = slab; J.out = out; J.stride = count; J.S = S; J.count = (int)count;
+    J.accumulate = 0; J.C9 = C9;
+    red.blk0[red.n] = red.blocks;
+    red.blocks += cdiv(count, 256);
+    red.n++;
+    red.blk0[red.n] = red.blocks;
+    return OK;
+  }
+  // slabs are reused only by kernels enqueued after these launches (same stream)
+  int flush_reduce() {
+    const int rc = reduce_slabs_multi(red, r.st);
+    red = RedTable();
+    slab_top = 0;
+    return rc;
+  }
+  int slab_oom() {
+    set_error("backward: weight-gradient slab arena exhausted");
+    return E_INVALID;
   }
 
   // ---- operands: an activation buffer, or a lazy unit's z with its BN+ReLU applied on load --
@@ -787,14 +828,16 @@ struct Exec {
     GemmTnArgs t{};
     t.M = (int)M; t.N = c.cout; t.K = K; t.D = dz; t.ldd = lddz; t.X = X.p; t.ldx = X.ld;
     t.x_scale = X.sc; t.x_shift = X.sh;
-    t.slab = (float*)Bw(pl.slab);
     int S = gemm_tn_splits((int)M, c.cout, K);
+    t.slab = slab_alloc((size_t)S * c.cout * K);
+    if (!t.slab) return slab_oom();
     TRY(gemm_tn(t, S, dt, r.st));
-    TRY(reduce_slabs(t.slab, S, (long long)c.cout * K, (long long)c.cout * K, G(c.w), 0, r.st));
+    TRY(defer_reduce(t.slab, S, (long long)c.cout * K, G(c.w), 0));
     if (c.b >= 0) {
-      float* part = (float*)Bw(pl.cspart);
+      float* part = slab_alloc((size_t)colsum_parts((int)M) * c.cout);
+      if (!part) return slab_oom();
       TRY(colsum(dz, (int)M, c.cout, lddz, part, dt, r.st));
-      TRY(reduce_slabs(part, colsum_parts((int)M), c.cout, c.cout, G(c.b), 0, r.st));
+      TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
     if (!dX) return OK;
     GemmArgs g{};
@@ -813,9 +856,12 @@ struct Exec {
              int stride, void* dX) {
     DwBwdArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
-    d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz; d.w = P(c.w); d.dx = dX; d.slab = (float*)Bw(pl.slab);
+    d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz; d.w = P(c.w); d.dx = dX;
+    const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
+    d.slab = slab_alloc((size_t)S * 9 * C);
+    if (!d.slab) return slab_oom();
     TRY(dw_wgrad(d, dt, r.st));
-    TRY(dw_wgrad_reduce(d.slab, dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride), C, G(c.w), r.st));
+    TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
     return dw_dgrad(d, dt, r.st);
   }
 
@@ -960,10 +1006,11 @@ struct Exec {
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
-    c.dz = dz; c.slab = (float*)Bw(pl.slab); c.rows_per_block = 8;
+    const int S = conv0_wgrad_parts(pl.N, pl.H1, pl.W1, 8);
+    c.dz = dz; c.slab = slab_alloc((size_t)S * 864); c.rows_per_block = 8;
+    if (!c.slab) return slab_oom();
     TRY(conv0_wgrad(c, dt, r.st));
-    int S = conv0_wgrad_parts(pl.N, pl.H1, pl.W1, 8);
-    return reduce_slabs(c.slab, S, 864, 864, G(net.c0.w), 0, r.st);
+    return defer_reduce(c.slab, S, 864, G(net.c0.w), 0);
   }
 };
 
@@ -1142,6 +1189,7 @@ int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to)
           TRY(ex.backward_ltd());
           break;
       }
+      TRY(ex.flush_reduce());  // the stage's gradient bucket is complete after this
     }
     return OK;
   });

@@ -76,6 +76,7 @@ struct Plan {
   int H1, W1, H2, W2, H3, W3, H4, W4, H5, W5;
   int Cp = 0;   // padded class count (row stride of the low-res logits)
   size_t ws_bytes = 0, bws_bytes = 0;
+  size_t slab_floats = 0;  // weight-gradient partial arena (every job of a step has its own slab)
   // forward units
   Unit c0, l1dw, l1pw, l2dw, l2pw;
   Unit lbe[9], lbd[9], lbp[9];
