@@ -259,6 +259,41 @@ int fscnn_backward_aux(const fscnn_plan* plan, const void* dout, const void* dau
   GUARD(net_backward(plan->plan, r, stage_from, stage_to));
 }
 
+int fscnn_predict(const fscnn_plan* plan, const void* x, int x_dtype, void* labels,
+                  int label_dtype, const float* params, float* running, long long* nbt, void* ws,
+                  void* stream) {
+  if (!plan || !x || !labels || !params || !running || !ws) {
+    set_error("fscnn_predict: null argument");
+    return E_INVALID;
+  }
+  if (plan->plan.train) {
+    set_error("fscnn_predict: needs an inference plan (train=0)");
+    return E_INVALID;
+  }
+  if (label_dtype != 0 && label_dtype != 1) {
+    set_error("fscnn_predict: label_dtype %d (0 int64, 1 uint8)", label_dtype);
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.x = x; r.x_dtype = x_dtype; r.out = nullptr; r.out_dtype = plan->plan.dtype;
+  r.labels = labels; r.label_u8 = label_dtype;
+  r.P = params; r.R = running; r.NBT = nbt; r.ws = ws; r.momentum = 0.1f; r.st = S(stream);
+  GUARD(net_forward(plan->plan, r));
+}
+
+int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, long long n,
+                     int nclass, long long* counts, void* stream) {
+  if ((!pred || !target || !counts) && n > 0) {
+    set_error("fscnn_seg_metric: null argument");
+    return E_INVALID;
+  }
+  if (pred_dtype != 0 && pred_dtype != 1) {
+    set_error("fscnn_seg_metric: pred_dtype %d (0 int64, 1 uint8)", pred_dtype);
+    return E_INVALID;
+  }
+  return seg_metric(pred, pred_dtype, target, n, nclass, counts, S(stream));
+}
+
 int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
                        long long ignore_index, float* loss2, const float* params, float* running,
                        long long* nbt, void* ws, unsigned long long seed, float dropout_p,

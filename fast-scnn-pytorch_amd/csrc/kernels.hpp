@@ -307,6 +307,11 @@ int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st);
 
 int up_nhwc(const UpArgs& a, int dtype, hipStream_t st);
 int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st);
+// final upsample + argmax over classes -> labels [N][Ho][Wo] (int64, or uint8 when label_u8)
+int up_argmax(const UpArgs& a, int in_dtype, void* labels, int label_u8, hipStream_t st);
+// SegmentationMetric counters [2 + 3C] (int64, accumulated); see misc.hip
+int seg_metric(const void* pred, int pred_u8, const long long* target, long long n, int C,
+               long long* counts, hipStream_t st);
 int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st);
 int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st);
 int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st);

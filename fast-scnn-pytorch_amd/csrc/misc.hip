@@ -150,6 +150,64 @@ int dropout(const DropArgs& a, int dtype, hipStream_t st) {
   return check_launch("dropout");
 }
 
+// ---- SegmentationMetric counters (utils/metric.py:73-105) -------------------------------------
+// counts[0] = correct = #(p == t, t >= 0), counts[1] = labeled = #(t >= 0) (batch_pix_accuracy:
+// labels >= C, e.g. 255, count as labeled), then per class c < C: inter = #(p == t == c),
+// area_pred = #(p == c, t >= 0), area_lab = #(t == c) (batch_intersection_union's histograms over
+// [1, C] of the +1-shifted values).  Integer counts: LDS histograms, one global integer add per
+// non-zero bin and workgroup, so the result is exact and order independent.  Accumulates.
+constexpr int SM_CMAX = 1024;
+
+template <typename TP>
+__global__ __launch_bounds__(256) void seg_metric_kernel(const TP* pred, const long long* tgt,
+                                                         long long n, int C,
+                                                         unsigned long long* counts) {
+  __shared__ unsigned s_h[3 * SM_CMAX];
+  __shared__ unsigned s_cl[2];
+  for (int j = threadIdx.x; j < 3 * C; j += blockDim.x) s_h[j] = 0u;
+  if (threadIdx.x < 2) s_cl[threadIdx.x] = 0u;
+  __syncthreads();
+  unsigned correct = 0, labeled = 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long t = tgt[i];
+    const long long p = (long long)pred[i];
+    if (t >= 0) {
+      ++labeled;
+      correct += p == t ? 1u : 0u;
+      if (p >= 0 && p < C) atomicAdd(&s_h[C + (int)p], 1u);
+    }
+    if (t >= 0 && t < C) {
+      atomicAdd(&s_h[2 * C + (int)t], 1u);
+      if (p == t) atomicAdd(&s_h[(int)t], 1u);
+    }
+  }
+  atomicAdd(&s_cl[0], correct);
+  atomicAdd(&s_cl[1], labeled);
+  __syncthreads();
+  for (int j = threadIdx.x; j < 3 * C; j += blockDim.x)
+    if (s_h[j]) atomicAdd(&counts[2 + j], (unsigned long long)s_h[j]);
+  if (threadIdx.x == 0) {
+    atomicAdd(&counts[0], (unsigned long long)s_cl[0]);
+    atomicAdd(&counts[1], (unsigned long long)s_cl[1]);
+  }
+}
+
+int seg_metric(const void* pred, int pred_u8, const long long* target, long long n, int C,
+               long long* counts, hipStream_t st) {
+  if (C < 1 || C > SM_CMAX || n < 0) {
+    set_error("seg_metric: nclass %d (1..%d), n %lld", C, SM_CMAX, n);
+    return E_INVALID;
+  }
+  if (n == 0) return OK;
+  const long long blocks = (n + 255) / 256;
+  const unsigned grid = (unsigned)(blocks < 1024 ? blocks : 1024);
+  unsigned long long* c = reinterpret_cast<unsigned long long*>(counts);
+  if (pred_u8) seg_metric_kernel<uint8_t><<<grid, 256, 0, st>>>((const uint8_t*)pred, target, n, C, c);
+  else seg_metric_kernel<long long><<<grid, 256, 0, st>>>((const long long*)pred, target, n, C, c);
+  return check_launch("seg_metric");
+}
+
 __global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
 
 int set_u64(uint64_t* p, uint64_t v, hipStream_t st) {

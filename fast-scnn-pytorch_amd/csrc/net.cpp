@@ -716,6 +716,11 @@ struct Exec {
     }
     // ---- final bilinear (align_corners) to NCHW ----
     UpArgs u{};
+    if (r.labels) {  // eval.py:45 / demo.py:48: only torch.argmax(outputs[0], 1) is consumed
+      u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
+      u.x = W(pl.logits); u.ldx = pl.Cp;
+      return up_argmax(u, dt, r.labels, r.label_u8, r.st);
+    }
     u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
     u.x = W(pl.logits); u.ldx = pl.Cp; u.y = r.out; u.ldy = 0;
     return up_nchw(u, dt, r.out_dtype, r.st);
@@ -1065,7 +1070,7 @@ uint64_t fbits(float f) {
 std::vector<uint64_t> run_key(int kind, int s0, int s1, const RunArgs& r) {
   auto P = [](const void* p) { return (uint64_t)(uintptr_t)p; };
   return {(uint64_t)kind, (uint64_t)s0, (uint64_t)s1, P(r.x), (uint64_t)r.x_dtype, P(r.out),
-          (uint64_t)r.out_dtype, P(r.aux_out), P(r.P), P(r.R), P(r.NBT), P(r.G), P(r.ws),
+          (uint64_t)r.out_dtype, P(r.aux_out), P(r.labels), (uint64_t)r.label_u8, P(r.P), P(r.R), P(r.NBT), P(r.G), P(r.ws),
           P(r.bws), P(r.dout), P(r.daux), fbits(r.dropout_p), fbits(r.momentum), P(r.target),
           (uint64_t)r.ignore_index, P(r.loss2), P(r.gloss)};
 }
@@ -1145,7 +1150,7 @@ int net_forward(const Plan& pl, const RunArgs& r) {
     set_error("forward_loss: the fused loss head covers the main output only (aux net)");
     return E_UNSUPPORTED;
   }
-  if (pl.net->aux && !r.aux_out) {
+  if (pl.net->aux && !r.aux_out && !r.labels) {
     set_error("fscnn_forward: this net has the aux head; use fscnn_forward_aux");
     return E_INVALID;
   }

@@ -126,6 +126,9 @@ struct RunArgs {
   long long ignore_index = -1;
   float* loss2 = nullptr;
   const float* gloss = nullptr;
+  // eval prediction: forward with labels != null writes argmax(upsampled logits) instead of out
+  void* labels = nullptr;
+  int label_u8 = 0;
 };
 
 int net_forward(const Plan& pl, const RunArgs& r);

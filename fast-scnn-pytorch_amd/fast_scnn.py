@@ -387,6 +387,35 @@ class FastSCNN(nn.Module):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return ((out, aux_out) if self.aux else (out,)), ws, seed, dt
 
+    def predict(self, x, dtype=torch.int64):
+        """``torch.argmax(self(x)[0], 1)`` of an eval-mode model (eval.py:43-45, demo.py:43-48)
+        without the upsampled logits: the final bilinear upsample and the argmax over classes run
+        as one kernel that writes only the labels (int64 like torch.argmax, or uint8)."""
+        if self.training:
+            raise RuntimeError("predict is the inference path; call model.eval() first")
+        if dtype not in (torch.int64, torch.uint8):
+            raise RuntimeError("predict: labels are int64 or uint8, not %s" % (dtype,))
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise RuntimeError("FastSCNN: expected input [N, 3, H, W], got %s" % (tuple(x.shape),))
+        if not x.is_cuda:
+            raise RuntimeError("FastSCNN.predict: the HIP path needs a ROCm device tensor")
+        nat = self.native()
+        ar = self.arena()
+        N, _, H, W = x.shape
+        if H < 32 or W < 32:
+            raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
+        dt = self._compute_dtype(x)
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), False)
+        ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
+        labels = torch.empty((N, H, W), dtype=dtype, device=x.device)
+        _lib.call("fscnn_predict", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(labels),
+                  1 if dtype == torch.uint8 else 0, _lib.ptr(ar["P"]), _lib.ptr(ar["R"]),
+                  _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.stream_ptr(x.device))
+        return labels
+
     def debug_buffer(self, name):
         """Tensor view of a named plan buffer of the last forward/backward (set ``_keep_ws``).
 

@@ -88,6 +88,19 @@ int fscnn_backward_aux(const fscnn_plan* plan, const void* dout, const void* dau
                        unsigned long long dropout_seed, float dropout_p, int stage_from,
                        int stage_to, void* stream);
 
+/* Eval prediction (eval.py:43-45, demo.py:43-48 consume only torch.argmax(outputs[0], 1)):
+ * forward of an inference plan whose final bilinear upsample is fused with the argmax over classes;
+ * labels [N][H][W] (label_dtype 0: int64 like torch.argmax, 1: uint8).  No logits are written. */
+int fscnn_predict(const fscnn_plan* plan, const void* x, int x_dtype, void* labels,
+                  int label_dtype, const float* params, float* running, long long* nbt, void* ws,
+                  void* stream);
+/* SegmentationMetric counters (utils/metric.py:73-105, batch_pix_accuracy +
+ * batch_intersection_union) of n predictions (pred_dtype 0 int64, 1 uint8) against int64 labels,
+ * ACCUMULATED into counts[2 + 3*nclass] (int64): [correct, labeled, inter[C], area_pred[C],
+ * area_lab[C]]; union = area_pred + area_lab - inter.  Exact integer counts. */
+int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, long long n,
+                     int nclass, long long* counts, void* stream);
+
 /* Fused training step head (train plans only): forward + bilinear upsample + CE(ignore_index)
  * evaluated at low resolution; loss2[0] = mean loss, loss2[1] = valid pixel count.  Computes
  * exactly criterion(model(x)[0], target) of train.py:270-271 without materialising the

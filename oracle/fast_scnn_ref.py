@@ -212,6 +212,30 @@ def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
     return tuple(outs), ctx.new_stats, ctx.acts
 
 
+def seg_counts(pred, label, nclass):
+    """SegmentationMetric counters of one batch (utils/metric.py:73-105): numpy int64
+    [correct, labeled, inter[C], area_pred[C], area_lab[C]] exactly as batch_pix_accuracy and
+    batch_intersection_union compute them (+1 shift, histograms over [1, nclass])."""
+    p = np.asarray(pred).astype(np.int64) + 1
+    t = np.asarray(label).astype(np.int64) + 1
+    labeled = int(np.sum(t > 0))
+    correct = int(np.sum((p == t) * (t > 0)))
+    p = p * (t > 0).astype(p.dtype)
+    inter = p * (p == t)
+    hist = lambda v: np.histogram(v, bins=nclass, range=(1, nclass))[0]  # noqa: E731
+    return np.concatenate([[correct, labeled], hist(inter), hist(p), hist(t)]).astype(np.int64)
+
+
+def seg_scores(counts, nclass):
+    """SegmentationMetric.get (utils/metric.py:42-54) from accumulated counters."""
+    c = np.asarray(counts)
+    inter, area_pred, area_lab = c[2:2 + nclass], c[2 + nclass:2 + 2 * nclass], c[2 + 2 * nclass:]
+    union = area_pred + area_lab - inter
+    pix_acc = 1.0 * c[0] / (np.spacing(1) + c[1])
+    iou = 1.0 * inter / (np.spacing(1) + union)
+    return pix_acc, iou.mean()
+
+
 def cross_entropy(logits, target, ignore_index=-1):
     """nn.CrossEntropyLoss(ignore_index=-1), mean over valid pixels (utils/loss.py:103-124)."""
     return F.cross_entropy(logits, target, ignore_index=ignore_index)

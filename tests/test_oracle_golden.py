@@ -78,3 +78,16 @@ def test_oracle_train_matches_reference(case):
     for k in g:
         if k.startswith("stats."):
             np.testing.assert_allclose(stats[k[6:]].numpy(), g[k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("nc", [19, 2])
+def test_oracle_metric_matches_reference(nc):
+    """oracle.seg_counts against the reference's own batch_pix_accuracy /
+    batch_intersection_union outputs (tools/gen_metric_golden.py), incl. -1 and 255 labels."""
+    g = load_golden("metric_c%d" % nc)
+    c = ref.seg_counts(g["pred"], g["label"], nc)
+    assert c[0] == int(g["correct"]) and c[1] == int(g["labeled"])
+    inter = c[2:2 + nc]
+    union = c[2 + nc:2 + 2 * nc] + c[2 + 2 * nc:] - inter
+    np.testing.assert_array_equal(inter, g["inter"])
+    np.testing.assert_array_equal(union, g["union"])
