@@ -177,15 +177,22 @@ def main():
         kind = max(PROF_KINDS, key=lambda k: census[PROF_KINDS[k]])
     barrier()
 
-    # ---- timed region: K steps, events on the dominant family's launches -------------------
-    _lib.check(lib.fscnn_prof_begin(kind, 512 * max(1, args.steps)), "fscnn_prof_begin")
+    # ---- timed region: K steps; HIP events bracket the dominant family's launches in the last
+    # quarter of the timed steps (timing events on every launch of every step would add ~0.4 ms
+    # of event packets to a 60-launch family; the events are created before the region)
+    nprof = max(1, args.steps // 4)
+    _lib.check(lib.fscnn_prof_begin(kind, 512 * nprof), "fscnn_prof_begin")
+    ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
+    _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
+                                  ctypes.byref(f)), "fscnn_prof_end")
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i == args.steps - nprof:
+            lib.fscnn_prof_begin(kind, 512 * nprof)
         loss = step()
     barrier()
     elapsed = time.perf_counter() - t0
-    ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
     _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
                                   ctypes.byref(f)), "fscnn_prof_end")
     last_loss = float(loss.item())

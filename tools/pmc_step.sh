@@ -19,5 +19,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
       > "$OUT/p$i.log" 2>&1
   echo "pass $i ($grp) done"
 done
-python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.txt"
+python3 tools/pmc_summary.py "$OUT" --json-dir "$OUT" --tag "$TAG" --dtype bf16 > "$OUT/summary.txt"
 cat "$OUT/summary.txt" | head -80
