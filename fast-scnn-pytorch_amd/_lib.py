@@ -37,6 +37,8 @@ SIGNATURES = {
                               c_float, c_float, c_vp]),
     "fscnn_backward": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_ull, c_float,
                                c_int, c_int, c_vp]),
+    "fscnn_normalize_u8": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "fscnn_remap_labels": (c_int, [c_vp, c_ll, c_vp, c_int, c_int, c_ll, c_vp, c_vp]),
     "fscnn_predict": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fscnn_seg_metric": (c_int, [c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_vp]),
     "fscnn_forward_aux": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,

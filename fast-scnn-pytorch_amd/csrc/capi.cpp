@@ -294,6 +294,28 @@ int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, 
   return seg_metric(pred, pred_dtype, target, n, nclass, counts, S(stream));
 }
 
+int fscnn_normalize_u8(const unsigned char* images, int N, int H, int W, const float* mean,
+                       const float* std, void* out, int out_dtype, void* stream) {
+  if (!images || !mean || !std || !out) {
+    set_error("fscnn_normalize_u8: null argument");
+    return E_INVALID;
+  }
+  if (out_dtype != DT_F32 && out_dtype != DT_BF16) {
+    set_error("fscnn_normalize_u8: out_dtype %d", out_dtype);
+    return E_INVALID;
+  }
+  return normalize_u8(images, N, H, W, mean, std, out, out_dtype, S(stream));
+}
+
+int fscnn_remap_labels(const unsigned char* labels, long long n, const long long* lut, int lut_size,
+                       int offset, long long invalid, long long* out, void* stream) {
+  if ((!labels || !out || !lut) && n > 0) {
+    set_error("fscnn_remap_labels: null argument");
+    return E_INVALID;
+  }
+  return remap_labels(labels, n, lut, lut_size, offset, invalid, out, S(stream));
+}
+
 int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
                        long long ignore_index, float* loss2, const float* params, float* running,
                        long long* nbt, void* ws, unsigned long long seed, float dropout_p,

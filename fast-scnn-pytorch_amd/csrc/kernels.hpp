@@ -327,6 +327,12 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
 int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const float* gout,
                   const float* out2, int dtype, hipStream_t st);
 int dropout(const DropArgs& a, int dtype, hipStream_t st);
+// GPU input path: ToTensor + Normalize of uint8 HWC images into NCHW (fp32 / bf16)
+int normalize_u8(const uint8_t* x, int N, int H, int W, const float* mean, const float* std,
+                 void* y, int out_dtype, hipStream_t st);
+// label-id -> train-id lookup (out-of-table ids -> invalid)
+int remap_labels(const uint8_t* in, long long n, const long long* lut, int lut_size, int offset,
+                 long long invalid, long long* out, hipStream_t st);
 int im2col3(const Im2ColArgs& a, int dtype, hipStream_t st);
 int col2im3(const Col2ImArgs& a, int dtype, hipStream_t st);
 // *p = v (one thread): per-call scalars that captured graphs read from device memory

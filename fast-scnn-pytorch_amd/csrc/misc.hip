@@ -208,6 +208,84 @@ int seg_metric(const void* pred, int pred_u8, const long long* target, long long
   return check_launch("seg_metric");
 }
 
+// ---- GPU input path ---------------------------------------------------
+// transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107, eval.py:22-25,
+// demo.py:37-40) on a batch of uint8 HWC RGB images, written as the NCHW network input:
+//     y[n][c][h][w] = (x[n][h][w][c] / 255 - mean[c]) / std[c]
+// with torchvision's fp32 operation order (div, sub, div), so the fp32 result is bit-identical.
+// Thread = 4 consecutive pixels of one row: 12 input bytes, 4-wide stores per channel plane.
+template <typename TO>
+__global__ __launch_bounds__(256) void normalize_u8_kernel(const uint8_t* x, long long npix4,
+                                                           long long HW, float m0, float m1,
+                                                           float m2, float s0, float s1, float s2,
+                                                           TO* y) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= npix4) return;
+  const long long p0 = t * 4;            // first pixel (flat over N*H*W; HW % 4 == 0 host-checked)
+  const long long n = p0 / HW, hw = p0 - n * HW;
+  const uint8_t* src = x + p0 * 3;
+  const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ((float)src[3 * j + c] / 255.f - mean[c]) / sd[c];
+    TO* dst = y + ((size_t)n * 3 + c) * HW + hw;
+    if constexpr (sizeof(TO) == 4) {
+      *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint2 u;
+      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(dst) = u;
+    }
+  }
+}
+
+int normalize_u8(const uint8_t* x, int N, int H, int W, const float* mean, const float* std,
+                 void* y, int out_dtype, hipStream_t st) {
+  const long long HW = (long long)H * W;
+  if (N < 1 || H < 1 || W < 1 || HW % 4 || (uintptr_t)y % 16) {
+    set_error("normalize_u8: N=%d H=%d W=%d (H*W must be a multiple of 4, y 16-B aligned)", N, H, W);
+    return E_INVALID;
+  }
+  const long long npix4 = (long long)N * HW / 4;
+  const unsigned grid = (unsigned)((npix4 + 255) / 256);
+  if (out_dtype == DT_F32)
+    normalize_u8_kernel<float><<<grid, 256, 0, st>>>(x, npix4, HW, mean[0], mean[1], mean[2],
+                                                     std[0], std[1], std[2], (float*)y);
+  else
+    normalize_u8_kernel<bf16><<<grid, 256, 0, st>>>(x, npix4, HW, mean[0], mean[1], mean[2],
+                                                    std[0], std[1], std[2], (bf16*)y);
+  return check_launch("normalize_u8");
+}
+
+// Dataset label-id -> train-id remap (data_loader/cityscapes.py:56-71 `_class_to_index`:
+// key[digitize(v, mapping=range(-1, K-1), right=True)] == key[v + 1] for v in [-1, K-2]) as a
+// lookup table on the device: out[i] = lut[in[i] + offset], and `invalid` (the reference
+// asserts instead) for ids outside the table.
+__global__ __launch_bounds__(256) void remap_labels_kernel(const uint8_t* in, long long n,
+                                                           const long long* lut, int lut_size,
+                                                           int offset, long long invalid,
+                                                           long long* out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = (int)in[i] + offset;
+  out[i] = (k >= 0 && k < lut_size) ? lut[k] : invalid;
+}
+
+int remap_labels(const uint8_t* in, long long n, const long long* lut, int lut_size, int offset,
+                 long long invalid, long long* out, hipStream_t st) {
+  if (n < 0 || lut_size < 1) {
+    set_error("remap_labels: n=%lld lut_size=%d", n, lut_size);
+    return E_INVALID;
+  }
+  if (n == 0) return OK;
+  remap_labels_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(in, n, lut, lut_size, offset,
+                                                                    invalid, out);
+  return check_launch("remap_labels");
+}
+
 __global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
 
 int set_u64(uint64_t* p, uint64_t v, hipStream_t st) {

@@ -101,6 +101,19 @@ int fscnn_predict(const fscnn_plan* plan, const void* x, int x_dtype, void* labe
 int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, long long n,
                      int nclass, long long* counts, void* stream);
 
+/* GPU input path.
+ * fscnn_normalize_u8: transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107,
+ *   eval.py:22-25, demo.py:37-40) of N uint8 HWC RGB images into the NCHW network input
+ *   ((x / 255 - mean[c]) / std[c], torchvision's fp32 operation order); mean/std are HOST arrays
+ *   of 3 floats; H*W must be a multiple of 4; out_dtype 0 fp32, 1 bf16.
+ * fscnn_remap_labels: dataset label ids -> train ids through a device lookup table
+ *   (data_loader/cityscapes.py:56-71 `_class_to_index` is lut = _key, offset = 1); ids outside
+ *   the table become `invalid`. */
+int fscnn_normalize_u8(const unsigned char* images, int N, int H, int W, const float* mean,
+                       const float* std, void* out, int out_dtype, void* stream);
+int fscnn_remap_labels(const unsigned char* labels, long long n, const long long* lut, int lut_size,
+                       int offset, long long invalid, long long* out, void* stream);
+
 /* Fused training step head (train plans only): forward + bilinear upsample + CE(ignore_index)
  * evaluated at low resolution; loss2[0] = mean loss, loss2[1] = valid pixel count.  Computes
  * exactly criterion(model(x)[0], target) of train.py:270-271 without materialising the

@@ -212,6 +212,27 @@ def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
     return tuple(outs), ctx.new_stats, ctx.acts
 
 
+def to_tensor_normalize(img_hwc_u8, mean, std):
+    """transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107): uint8 HWC ->
+    fp32 CHW, torchvision's operation order (float().div(255), sub_(mean), div_(std))."""
+    t = torch.from_numpy(np.ascontiguousarray(img_hwc_u8)).permute(2, 0, 1).contiguous()
+    t = t.float().div(255)
+    m = torch.as_tensor(mean, dtype=torch.float32)[:, None, None]
+    s = torch.as_tensor(std, dtype=torch.float32)[:, None, None]
+    return t.sub(m).div(s)
+
+
+def cityscapes_class_to_index(mask):
+    """CitySegmentation._class_to_index (data_loader/cityscapes.py:56-71), the same key / mapping
+    tables and np.digitize(right=True) lookup (restated: the reference module imports
+    torchvision, which is absent here)."""
+    key = np.array([-1, -1, -1, -1, -1, -1, -1, -1, 0, 1, -1, -1, 2, 3, 4, -1, -1, -1, 5, -1, 6,
+                    7, 8, 9, 10, 11, 12, 13, 14, 15, -1, -1, 16, 17, 18])
+    mapping = np.array(range(-1, len(key) - 1)).astype('int32')
+    index = np.digitize(np.asarray(mask).ravel(), mapping, right=True)
+    return key[index].reshape(np.asarray(mask).shape)
+
+
 def seg_counts(pred, label, nclass):
     """SegmentationMetric counters of one batch (utils/metric.py:73-105): numpy int64
     [correct, labeled, inter[C], area_pred[C], area_lab[C]] exactly as batch_pix_accuracy and

@@ -91,3 +91,12 @@ def test_oracle_metric_matches_reference(nc):
     union = c[2 + nc:2 + 2 * nc] + c[2 + 2 * nc:] - inter
     np.testing.assert_array_equal(inter, g["inter"])
     np.testing.assert_array_equal(union, g["union"])
+
+
+def test_oracle_label_map_known_answers():
+    """_class_to_index (data_loader/cityscapes.py:56-71): the reference's valid_classes list maps
+    to train ids 0..18 in order and every other id in [-1, 33] to -1."""
+    valid = [7, 8, 11, 12, 13, 17, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 31, 32, 33]
+    out = ref.cityscapes_class_to_index(np.arange(-1, 34))
+    assert [int(out[v + 1]) for v in valid] == list(range(19))
+    assert (np.delete(out, [v + 1 for v in valid]) == -1).all()
