@@ -39,6 +39,13 @@ SIGNATURES = {
                                c_int, c_int, c_vp]),
     "fscnn_normalize_u8": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "fscnn_remap_labels": (c_int, [c_vp, c_ll, c_vp, c_int, c_int, c_ll, c_vp, c_vp]),
+    "fscnn_ohem_prob": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_float, c_vp, c_vp,
+                                c_vp]),
+    "fscnn_kth_smallest": (c_int, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp]),
+    "fscnn_ce_weighted_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
+                                      c_float, c_vp, c_vp, c_vp]),
+    "fscnn_ce_weighted_bwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
+                                      c_float, c_vp, c_vp, c_vp, c_vp]),
     "fscnn_predict": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fscnn_seg_metric": (c_int, [c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_vp]),
     "fscnn_forward_aux": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,

@@ -316,6 +316,46 @@ int fscnn_remap_labels(const unsigned char* labels, long long n, const long long
   return remap_labels(labels, n, lut, lut_size, offset, invalid, out, S(stream));
 }
 
+int fscnn_ohem_prob(const void* logits, int dtype, const long long* target, int N, int C,
+                    long long HW, long long ignore_index, float thresh, float* prob,
+                    unsigned long long* counts, void* stream) {
+  if (!logits || !target || !prob || !counts) {
+    set_error("fscnn_ohem_prob: null argument");
+    return E_INVALID;
+  }
+  CeArgs a{};
+  a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target; a.ignore_index = ignore_index;
+  return ohem_prob(a, thresh, prob, counts, dtype, S(stream));
+}
+
+int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* hist, float* out,
+                       void* stream) {
+  if (!values || !hist || !out) {
+    set_error("fscnn_kth_smallest: null argument");
+    return E_INVALID;
+  }
+  return kth_smallest(values, n, k, hist, out, S(stream));
+}
+
+int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
+                          long long HW, long long ignore_index, const float* weight,
+                          const float* prob, float thr, float* part, float* out2, void* stream) {
+  CeArgs a{};
+  a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target;
+  a.ignore_index = ignore_index; a.part = part; a.weight = weight; a.prob = prob; a.thr = thr;
+  return ce_fwd(a, out2, dtype, S(stream));
+}
+
+int fscnn_ce_weighted_bwd(const void* logits, int dtype, const long long* target, int N, int C,
+                          long long HW, long long ignore_index, const float* weight,
+                          const float* prob, float thr, const float* grad_out, const float* out2,
+                          void* dlogits, void* stream) {
+  CeArgs a{};
+  a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target;
+  a.ignore_index = ignore_index; a.dlogits = dlogits; a.weight = weight; a.prob = prob; a.thr = thr;
+  return ce_bwd(a, grad_out, out2, dtype, S(stream));
+}
+
 int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
                        long long ignore_index, float* loss2, const float* params, float* running,
                        long long* nbt, void* ws, unsigned long long seed, float dropout_p,

@@ -204,6 +204,11 @@ struct CeArgs {
   // backward
   const float* scale;     // device scalar: grad_out / count (computed by ce_finalize)
   void* dlogits;          // [N][C][HW] or null
+  // OHEM (utils/loss.py:127-176): class weights [C] (weighted mean: sum w*nll / sum w) and the
+  // kept mask prob[i] <= thr (prob from ohem_prob); null = plain CE
+  const float* weight = nullptr;
+  const float* prob = nullptr;
+  float thr = 0.f;
 };
 
 // Fused training head: bilinear(align_corners) upsample of the low-res logits to the input
@@ -321,6 +326,12 @@ int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st);
 int ce_parts(int N, long long HW);
 int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st);
 int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hipStream_t st);
+// OHEM: label probabilities + counters [#labelled, #(prob <= thresh)] (accumulated), and the
+// k-th smallest of n non-negative floats (host-synchronising radix select; hist: 2048 uint32)
+int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* counts, int dtype,
+              hipStream_t st);
+int kth_smallest(const float* key, long long n, long long k, unsigned* hist, float* out,
+                 hipStream_t st);
 int ce_head_parts(int N, int Hl, int Wl);
 int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
 // g[m][c] = g_raw[m][c] * gout / count  (c < C; pad columns zeroed)

@@ -4,6 +4,9 @@
 // (torch.optim.SGD momentum 0.9 / wd 1e-4, train.py:195-198) and fp32 -> bf16 weight casts.
 #include "kernels.hpp"
 
+#include <algorithm>
+#include <cstring>
+
 namespace fscnn {
 
 // ---- cross entropy over NCHW logits, ignore_index --------------------------------------------
@@ -17,14 +20,15 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeArgs a) {
   if (i < total) {
     long long n = i / a.HW, p = i - n * a.HW;
     long long t = a.target[i];
-    if (t != a.ignore_index && t >= 0 && t < a.C) {
+    if (t != a.ignore_index && t >= 0 && t < a.C && (!a.prob || a.prob[i] <= a.thr)) {
       const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
       float mx = -INFINITY;
       for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
       float se = 0.f;
       for (int c = 0; c < a.C; ++c) se += expf(ld1(lb + (size_t)c * a.HW) - mx);
-      loss = mx + logf(se) - ld1(lb + (size_t)t * a.HW);
-      cnt = 1.f;
+      const float w = a.weight ? a.weight[t] : 1.f;
+      loss = w * (mx + logf(se) - ld1(lb + (size_t)t * a.HW));
+      cnt = w;
     }
   }
   r1[threadIdx.x] = loss;
@@ -89,11 +93,11 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(CeArgs a, const float* gout
   long long t = a.target[i];
   const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
   T* db = (T*)a.dlogits + (size_t)n * a.C * a.HW + p;
-  if (t == a.ignore_index || t < 0 || t >= a.C) {
+  if (t == a.ignore_index || t < 0 || t >= a.C || (a.prob && !(a.prob[i] <= a.thr))) {
     for (int c = 0; c < a.C; ++c) st1(db + (size_t)c * a.HW, 0.f);
     return;
   }
-  float g = gout[0] / stats[1];
+  float g = gout[0] / stats[1] * (a.weight ? a.weight[t] : 1.f);
   float mx = -INFINITY;
   for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
   float se = 0.f;
@@ -110,6 +114,108 @@ int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hi
   if (dtype == DT_F32) ce_bwd_kernel<float><<<P, 256, 0, st>>>(a, gout, stats);
   else ce_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, gout, stats);
   return check_launch("ce_bwd");
+}
+
+// ---- OHEM selection (SoftmaxCrossEntropyOHEMLoss.forward, utils/loss.py:143-176) -------------
+// prob[i] = softmax probability of the label (exp(x - max) / sum, the reference's numpy order in
+// fp32) for labelled pixels, 2.0 (sorts after every probability) for ignored ones; counts[0] +=
+// #labelled, counts[1] += #(prob <= thresh).  Integer counters: exact.
+template <typename T>
+__global__ __launch_bounds__(256) void ohem_prob_kernel(CeArgs a, float thresh, float* prob,
+                                                        unsigned long long* counts) {
+  __shared__ unsigned s_c[2];
+  if (threadIdx.x < 2) s_c[threadIdx.x] = 0u;
+  __syncthreads();
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)a.N * a.HW;
+  if (i < total) {
+    const long long n = i / a.HW, p = i - n * a.HW;
+    const long long t = a.target[i];
+    float pr = 2.f;
+    if (t != a.ignore_index && t >= 0 && t < a.C) {
+      const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
+      float mx = -INFINITY;
+      for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
+      float se = 0.f;
+      for (int c = 0; c < a.C; ++c) se += expf(ld1(lb + (size_t)c * a.HW) - mx);
+      pr = expf(ld1(lb + (size_t)t * a.HW) - mx) / se;
+      atomicAdd(&s_c[0], 1u);
+      if (pr <= thresh) atomicAdd(&s_c[1], 1u);
+    }
+    prob[i] = pr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_c[0]) atomicAdd(&counts[0], (unsigned long long)s_c[0]);
+    if (s_c[1]) atomicAdd(&counts[1], (unsigned long long)s_c[1]);
+  }
+}
+
+int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* counts, int dtype,
+              hipStream_t st) {
+  const int P = ce_parts(a.N, a.HW);
+  if (dtype == DT_F32) ohem_prob_kernel<float><<<P, 256, 0, st>>>(a, thresh, prob, counts);
+  else ohem_prob_kernel<bf16><<<P, 256, 0, st>>>(a, thresh, prob, counts);
+  return check_launch("ohem_prob");
+}
+
+// k-th smallest of n non-negative floats (the OHEM threshold pred[argsort(pred)[k-1]]): radix
+// select on the IEEE bit patterns (monotone for non-negative floats), 11 + 11 + 10 bits, one
+// histogram launch per digit and a host pick of the digit (the reference does this step on the
+// host in numpy too).
+__global__ __launch_bounds__(256) void radix_hist_kernel(const float* key, long long n, int shift,
+                                                         unsigned bins, int pshift,
+                                                         unsigned prefix, unsigned* hist) {
+  __shared__ unsigned s_h[2048];
+  for (unsigned j = threadIdx.x; j < bins; j += blockDim.x) s_h[j] = 0u;
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const unsigned u = __float_as_uint(key[i]);
+    const bool in = pshift >= 32 || (u >> pshift) == prefix;
+    if (in) atomicAdd(&s_h[(u >> shift) & (bins - 1)], 1u);
+  }
+  __syncthreads();
+  for (unsigned j = threadIdx.x; j < bins; j += blockDim.x)
+    if (s_h[j]) atomicAdd(&hist[j], s_h[j]);
+}
+
+int kth_smallest(const float* key, long long n, long long k, unsigned* hist, float* out,
+                 hipStream_t st) {
+  if (n <= 0 || k < 1 || k > n) {
+    set_error("kth_smallest: n=%lld k=%lld", n, k);
+    return E_INVALID;
+  }
+  static const int shifts[3] = {21, 10, 0}, widths[3] = {11, 11, 10};
+  unsigned prefix = 0;
+  int pshift = 32;
+  unsigned h[2048];
+  const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 2048);
+  for (int d = 0; d < 3; ++d) {
+    const unsigned bins = 1u << widths[d];
+    if (hipMemsetAsync(hist, 0, bins * sizeof(unsigned), st) != hipSuccess) return E_HIP;
+    radix_hist_kernel<<<grid, 256, 0, st>>>(key, n, shifts[d], bins, pshift, prefix, hist);
+    if (int rc = check_launch("radix_hist")) return rc;
+    if (hipMemcpyAsync(h, hist, bins * sizeof(unsigned), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      set_error("kth_smallest: copy failed");
+      return E_HIP;
+    }
+    unsigned b = 0;
+    for (; b < bins; ++b) {
+      if ((long long)h[b] >= k) break;
+      k -= h[b];
+    }
+    if (b == bins) {
+      set_error("kth_smallest: selection ran past the histogram");
+      return E_HIP;
+    }
+    prefix = (prefix << widths[d]) | b;
+    pshift = shifts[d];
+  }
+  uint32_t bits = prefix;
+  memcpy(out, &bits, 4);
+  return OK;
 }
 
 // ---- dropout on an NHWC activation, mask indexed in NCHW order (matches the oracle) ----------

@@ -1,10 +1,20 @@
 """Cross-entropy criterion on the HIP path (the consumer of the logits in train.py:270-271).
 
+``SoftmaxCrossEntropyOHEMLoss`` / ``MixSoftmaxCrossEntropyOHEMLoss`` mirror utils/loss.py:127-206
+(the default criterion of train.py:190-191): the label probabilities, the OHEM threshold (k-th
+smallest label probability by a radix select when fewer than ``min_kept`` pixels fall under
+``thresh``) and the class-weighted CE over the kept pixels all run on the device; only the two
+selection counters (and, rarely, the radix digits) come back to the host, where the reference
+copies the whole logits tensor.
+
 ``MixSoftmaxCrossEntropyLoss`` mirrors utils/loss.py:103-124 (``nn.CrossEntropyLoss`` with
 ``ignore_index=-1`` over a tuple of predictions, aux terms weighted by ``aux_weight``).  One
 fused kernel computes log-softmax + NLL per pixel with fixed-order partial sums; the backward
 recomputes the softmax and writes ``(softmax - onehot) * grad / count`` in one pass.
 """
+import ctypes
+
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -65,4 +75,124 @@ class MixSoftmaxCrossEntropyLoss(nn.Module):
         if self.aux:
             for p in preds[1:]:
                 loss = loss + self.aux_weight * cross_entropy(p, target, self.ignore_index)
+        return loss
+
+
+# utils/loss.py:134-136 (use_weight=True)
+OHEM_CLASS_WEIGHT = (0.8373, 0.918, 0.866, 1.0345, 1.0166, 0.9969, 0.9754, 1.0489, 0.8786, 1.0023,
+                     0.9539, 0.9843, 1.1116, 0.9037, 1.0865, 1.0955, 1.0865, 1.1529, 1.0507)
+
+
+def ohem_threshold(logits, target, ignore_index, thresh, min_kept):
+    """(prob, threshold) of SoftmaxCrossEntropyOHEMLoss.forward (utils/loss.py:151-170): prob of
+    the label per pixel (device) and the float32 threshold a pixel's prob must not exceed to be
+    kept (inf: every labelled pixel)."""
+    N, C, H, W = logits.shape
+    HW = H * W
+    dev = logits.device
+    st = _lib.stream_ptr(dev)
+    prob = torch.empty(N * HW, dtype=torch.float32, device=dev)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    thr32 = float(np.float32(thresh))
+    _lib.call("fscnn_ohem_prob", _lib.ptr(logits), _lib.dtype_code(logits.dtype), _lib.ptr(target),
+              N, C, HW, int(ignore_index), ctypes.c_float(thr32), _lib.ptr(prob), _lib.ptr(counts),
+              st)
+    num_valid, n_le = (int(v) for v in counts.tolist())
+    threshold = float("inf")
+    if min_kept >= num_valid:
+        print('Labels: {}'.format(num_valid))
+    elif num_valid > 0:
+        threshold = thr32
+        if min_kept > 0:
+            k = min(num_valid, min_kept)
+            if n_le < k:  # the k-th smallest label probability exceeds thresh
+                hist = torch.empty(2048, dtype=torch.int32, device=dev)
+                out = ctypes.c_float()
+                _lib.call("fscnn_kth_smallest", _lib.ptr(prob), prob.numel(), k, _lib.ptr(hist),
+                          ctypes.cast(ctypes.pointer(out), ctypes.c_void_p), st)
+                threshold = out.value
+    return prob, threshold
+
+
+class _OhemCrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index, thresh, min_kept, weight):
+        if not logits.is_cuda:
+            raise RuntimeError("OHEM cross entropy needs ROCm device tensors")
+        logits = logits.contiguous()
+        target = target.to(device=logits.device, dtype=torch.int64).contiguous()
+        N, C, H, W = logits.shape
+        if weight is not None and weight.numel() != C:
+            raise RuntimeError("weight tensor should be defined either for all %d classes or no "
+                               "classes but got weight tensor of shape: [%d]" % (C, weight.numel()))
+        prob, thr = ohem_threshold(logits, target, ignore_index, thresh, min_kept)
+        parts = int(_lib.load().fscnn_ce_parts(N, H * W))
+        part = torch.empty(parts * 2, dtype=torch.float32, device=logits.device)
+        out2 = torch.empty(2, dtype=torch.float32, device=logits.device)
+        wp = _lib.ptr(weight) if weight is not None else None
+        _lib.call("fscnn_ce_weighted_fwd", _lib.ptr(logits), _lib.dtype_code(logits.dtype),
+                  _lib.ptr(target), N, C, H * W, int(ignore_index), wp, _lib.ptr(prob),
+                  ctypes.c_float(thr), _lib.ptr(part), _lib.ptr(out2),
+                  _lib.stream_ptr(logits.device))
+        ctx.save_for_backward(logits, target, prob, out2)
+        ctx.weight, ctx.thr, ctx.ignore_index = weight, thr, int(ignore_index)
+        return out2[0].clone()
+
+    @staticmethod
+    def backward(ctx, grad):
+        logits, target, prob, out2 = ctx.saved_tensors
+        N, C, H, W = logits.shape
+        g = grad.to(torch.float32).reshape(1).contiguous()
+        dlogits = torch.empty_like(logits)
+        wp = _lib.ptr(ctx.weight) if ctx.weight is not None else None
+        _lib.call("fscnn_ce_weighted_bwd", _lib.ptr(logits), _lib.dtype_code(logits.dtype),
+                  _lib.ptr(target), N, C, H * W, ctx.ignore_index, wp, _lib.ptr(prob),
+                  ctypes.c_float(ctx.thr), _lib.ptr(g), _lib.ptr(out2), _lib.ptr(dlogits),
+                  _lib.stream_ptr(logits.device))
+        return dlogits, None, None, None, None, None
+
+
+class SoftmaxCrossEntropyOHEMLoss(nn.Module):
+    """utils/loss.py:127-176 on the HIP path."""
+
+    def __init__(self, ignore_label=-1, thresh=0.7, min_kept=256, use_weight=True, **kwargs):
+        super().__init__()
+        self.ignore_label = ignore_label
+        self.thresh = float(thresh)
+        self.min_kept = int(min_kept)
+        if use_weight:
+            print("w/ class balance")
+            self.weight = torch.tensor(OHEM_CLASS_WEIGHT, dtype=torch.float32)
+        else:
+            print("w/o class balance")
+            self.weight = None
+
+    def forward(self, predict, target, weight=None):
+        assert not target.requires_grad
+        assert predict.dim() == 4
+        assert target.dim() == 3
+        assert predict.size(0) == target.size(0)
+        assert predict.size(2) == target.size(1)
+        assert predict.size(3) == target.size(2)
+        w = self.weight.to(predict.device) if self.weight is not None else None
+        return _OhemCrossEntropyFn.apply(predict, target, self.ignore_label, self.thresh,
+                                         self.min_kept, w)
+
+
+class MixSoftmaxCrossEntropyOHEMLoss(SoftmaxCrossEntropyOHEMLoss):
+    """utils/loss.py:179-206 on the HIP path."""
+
+    def __init__(self, aux=False, aux_weight=0.2, ignore_index=-1, **kwargs):
+        super().__init__(ignore_label=ignore_index, **kwargs)
+        self.aux = aux
+        self.aux_weight = aux_weight
+
+    def forward(self, *inputs, **kwargs):
+        preds, target = tuple(inputs)
+        if isinstance(preds, torch.Tensor):
+            preds = (preds,)
+        loss = super().forward(preds[0], target)
+        if self.aux:
+            for p in preds[1:]:
+                loss = loss + self.aux_weight * super().forward(p, target)
         return loss

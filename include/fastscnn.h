@@ -101,6 +101,28 @@ int fscnn_predict(const fscnn_plan* plan, const void* x, int x_dtype, void* labe
 int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, long long n,
                      int nclass, long long* counts, void* stream);
 
+/* OHEM cross entropy (SoftmaxCrossEntropyOHEMLoss, utils/loss.py:127-176, the criterion of
+ * train.py:190-191):
+ * fscnn_ohem_prob: prob[i] = softmax probability of the label of pixel i (2.0 for ignored
+ *   pixels); counts[0] += #labelled, counts[1] += #(prob <= thresh)  (device uint64 x 2).
+ * fscnn_kth_smallest: k-th smallest of n non-negative floats (the OHEM threshold); writes the
+ *   HOST float *out; hist is device scratch of 2048 uint32; synchronises the stream.
+ * fscnn_ce_weighted_fwd / _bwd: nn.CrossEntropyLoss(weight, ignore_index) over the pixels with
+ *   prob <= thr (prob null: all labelled pixels; weight null: unweighted); out2 = (weighted mean
+ *   loss, sum of weights); part as for fscnn_ce_fwd. */
+int fscnn_ohem_prob(const void* logits, int dtype, const long long* target, int N, int C,
+                    long long HW, long long ignore_index, float thresh, float* prob,
+                    unsigned long long* counts, void* stream);
+int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* hist, float* out,
+                       void* stream);
+int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
+                          long long HW, long long ignore_index, const float* weight,
+                          const float* prob, float thr, float* part, float* out2, void* stream);
+int fscnn_ce_weighted_bwd(const void* logits, int dtype, const long long* target, int N, int C,
+                          long long HW, long long ignore_index, const float* weight,
+                          const float* prob, float thr, const float* grad_out, const float* out2,
+                          void* dlogits, void* stream);
+
 /* GPU input path.
  * fscnn_normalize_u8: transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107,
  *   eval.py:22-25, demo.py:37-40) of N uint8 HWC RGB images into the NCHW network input

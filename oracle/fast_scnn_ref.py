@@ -212,6 +212,48 @@ def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
     return tuple(outs), ctx.new_stats, ctx.acts
 
 
+OHEM_CLASS_WEIGHT = [0.8373, 0.918, 0.866, 1.0345, 1.0166, 0.9969, 0.9754, 1.0489, 0.8786, 1.0023,
+                     0.9539, 0.9843, 1.1116, 0.9037, 1.0865, 1.0955, 1.0865, 1.1529, 1.0507]
+
+
+def ohem_target(predict, target, ignore_label=-1, thresh=0.7, min_kept=256):
+    """SoftmaxCrossEntropyOHEMLoss.forward's target rebuild (utils/loss.py:151-172) in numpy:
+    label probabilities, threshold (k-th smallest when it exceeds thresh), pixels above it set to
+    ignore.  Returns (new_target, threshold or None)."""
+    n, c, h, w = predict.shape
+    input_label = target.numpy().ravel().astype(np.int32)
+    x = np.rollaxis(predict.detach().numpy(), 1).reshape((c, -1))
+    input_prob = np.exp(x - x.max(axis=0).reshape((1, -1)))
+    input_prob /= input_prob.sum(axis=0).reshape((1, -1))
+    valid_flag = input_label != ignore_label
+    valid_inds = np.where(valid_flag)[0]
+    label = input_label[valid_flag]
+    num_valid = valid_flag.sum()
+    threshold = None
+    if min_kept < num_valid and num_valid > 0:
+        prob = input_prob[:, valid_flag]
+        pred = prob[label, np.arange(len(label), dtype=np.int32)]
+        threshold = thresh
+        if min_kept > 0:
+            index = pred.argsort()
+            threshold_index = index[min(len(index), min_kept) - 1]
+            if pred[threshold_index] > thresh:
+                threshold = pred[threshold_index]
+        valid_inds = valid_inds[pred <= threshold]
+    label = input_label[valid_inds].copy()
+    input_label.fill(ignore_label)
+    input_label[valid_inds] = label
+    return torch.from_numpy(input_label.reshape(target.shape)).long(), threshold
+
+
+def ohem_cross_entropy(predict, target, ignore_label=-1, thresh=0.7, min_kept=256,
+                       use_weight=True):
+    """SoftmaxCrossEntropyOHEMLoss (utils/loss.py:127-176): weighted CE over the rebuilt target."""
+    t, _ = ohem_target(predict, target, ignore_label, thresh, min_kept)
+    weight = torch.tensor(OHEM_CLASS_WEIGHT, dtype=predict.dtype) if use_weight else None
+    return F.cross_entropy(predict, t, weight=weight, ignore_index=ignore_label)
+
+
 def to_tensor_normalize(img_hwc_u8, mean, std):
     """transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107): uint8 HWC ->
     fp32 CHW, torchvision's operation order (float().div(255), sub_(mean), div_(std))."""

@@ -100,3 +100,20 @@ def test_oracle_label_map_known_answers():
     out = ref.cityscapes_class_to_index(np.arange(-1, 34))
     assert [int(out[v + 1]) for v in valid] == list(range(19))
     assert (np.delete(out, [v + 1 for v in valid]) == -1).all()
+
+
+@pytest.mark.parametrize("case", ["default", "kth", "keepall", "c2"])
+def test_oracle_ohem_matches_reference(case):
+    """oracle.ohem_cross_entropy against the reference SoftmaxCrossEntropyOHEMLoss run on CPU
+    (tools/gen_ohem_golden.py): loss and d(loss)/d(logits)."""
+    g = load_golden("ohem")
+    x = torch.from_numpy(g[case + ".logits"]).requires_grad_(True)
+    t = torch.from_numpy(g[case + ".target"])
+    loss = ref.ohem_cross_entropy(x, t, -1, 0.7, int(g[case + ".min_kept"]),
+                                  bool(g[case + ".use_weight"]))
+    loss.backward()
+    assert abs(loss.item() - float(g[case + ".loss"])) <= 1e-6 * abs(float(g[case + ".loss"]))
+    np.testing.assert_allclose(x.grad.numpy(), g[case + ".grad"], rtol=0, atol=1e-7)
+    if case == "kth":  # the k-th smallest threshold branch is what this case exercises
+        _, thr = ref.ohem_target(x, t, -1, 0.7, int(g[case + ".min_kept"]))
+        assert thr > 0.7
