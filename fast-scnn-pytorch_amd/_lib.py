@@ -46,6 +46,10 @@ SIGNATURES = {
                                       c_float, c_vp, c_vp, c_vp]),
     "fscnn_ce_weighted_bwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
                                       c_float, c_vp, c_vp, c_vp, c_vp]),
+    "fscnn_dice_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_float, c_float, c_int,
+                               c_vp, c_vp, c_vp]),
+    "fscnn_dice_bwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_float, c_float, c_int,
+                               c_vp, c_vp, c_float, c_float, c_float, c_vp, c_vp]),
     "fscnn_predict": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fscnn_seg_metric": (c_int, [c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_vp]),
     "fscnn_forward_aux": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,

@@ -356,6 +356,28 @@ int fscnn_ce_weighted_bwd(const void* logits, int dtype, const long long* target
   return ce_bwd(a, grad_out, out2, dtype, S(stream));
 }
 
+int fscnn_dice_fwd(const void* logits, int dtype, const long long* target, int N, int C,
+                   long long HW, float alpha, float gamma, int focal, float* part, double* stats,
+                   void* stream) {
+  if (!logits || !target || !part || !stats) {
+    set_error("fscnn_dice_fwd: null argument");
+    return E_INVALID;
+  }
+  return dice_loss_fwd(logits, dtype, target, N, C, HW, alpha, gamma, focal, part, stats, S(stream));
+}
+
+int fscnn_dice_bwd(const void* logits, int dtype, const long long* target, int N, int C,
+                   long long HW, float alpha, float gamma, int focal, const double* stats,
+                   const float* grad_out, float smooth, float dice_weight, float focal_weight,
+                   void* dlogits, void* stream) {
+  if (!logits || !target || !stats || !grad_out || !dlogits) {
+    set_error("fscnn_dice_bwd: null argument");
+    return E_INVALID;
+  }
+  return dice_loss_bwd(logits, dtype, target, N, C, HW, alpha, gamma, focal, stats, grad_out,
+                       smooth, dice_weight, focal_weight, dlogits, S(stream));
+}
+
 int fscnn_forward_loss(const fscnn_plan* plan, const void* x, int x_dtype, const long long* target,
                        long long ignore_index, float* loss2, const float* params, float* running,
                        long long* nbt, void* ws, unsigned long long seed, float dropout_p,

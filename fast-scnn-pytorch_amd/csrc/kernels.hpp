@@ -332,6 +332,12 @@ int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* co
               hipStream_t st);
 int kth_smallest(const float* key, long long n, long long k, unsigned* hist, float* out,
                  hipStream_t st);
+// Dice / Focal+Dice criteria (misc.hip): stats = (sum p1 t, sum p1, sum t, sum focal) in fp64
+int dice_loss_fwd(const void* logits, int dtype, const long long* target, int N, int C, long long HW,
+                  float alpha, float gamma, int focal, float* part, double* stats, hipStream_t st);
+int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N, int C, long long HW,
+                  float alpha, float gamma, int focal, const double* stats, const float* gout,
+                  float smooth, float wd, float wf, void* dlogits, hipStream_t st);
 int ce_head_parts(int N, int Hl, int Wl);
 int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
 // g[m][c] = g_raw[m][c] * gout / count  (c < C; pad columns zeroed)

@@ -218,6 +218,152 @@ int kth_smallest(const float* key, long long n, long long k, unsigned* hist, flo
   return OK;
 }
 
+// ---- Dice / Focal+Dice (utils/loss.py:12-100; train.py:183-188 for binary lane segmentation) ----
+// p1 = softmax(logits)[:, 1] (C > 1) or sigmoid(logits[:, 0]) (C == 1), t = float(target):
+//   dice = (2 sum(p1 t) + s) / (sum p1 + sum t + s), DiceLoss = 1 - dice;
+//   focal (C > 1) = mean_i alpha (1 - pt_i)^gamma ce_i, ce_i = lse_i - x_{t_i}, pt_i = exp(-ce_i).
+// Forward: per-block partials of (sum p1 t, sum p1, sum t, sum focal), merged in fixed order in
+// fp64.  Backward: dL/dx_c = wd * dDice/dp1 * dp1/dx_c + wf/n * dfocal/dce * (p_c - [c == t]).
+struct DiceArgs {
+  const void* logits;
+  const long long* target;
+  long long N, HW;
+  int C;
+  float alpha, gamma;
+  int focal;  // compute the focal term (C > 1)
+};
+
+template <typename T>
+__device__ __forceinline__ void dice_pixel(const DiceArgs& a, long long i, float& p1, float& tf,
+                                           float& ce, float& pt, float* pc, int cmax) {
+  const long long n = i / a.HW, p = i - n * a.HW;
+  const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
+  const long long t = a.target[i];
+  tf = (float)t;
+  if (a.C == 1) {
+    p1 = 1.f / (1.f + expf(-ld1(lb)));
+    ce = 0.f;
+    pt = 0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
+  float se = 0.f;
+  for (int c = 0; c < a.C; ++c) se += expf(ld1(lb + (size_t)c * a.HW) - mx);
+  p1 = expf(ld1(lb + a.HW) - mx) / se;
+  const long long tc = t < 0 ? 0 : (t >= a.C ? a.C - 1 : t);
+  ce = mx + logf(se) - ld1(lb + (size_t)tc * a.HW);
+  pt = expf(-ce);
+  if (pc)
+    for (int c = 0; c < cmax && c < a.C; ++c) pc[c] = expf(ld1(lb + (size_t)c * a.HW) - mx) / se;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dice_fwd_kernel(DiceArgs a, float* part) {
+  __shared__ float r[4][256];
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (i < a.N * a.HW) {
+    float p1, tf, ce, pt;
+    dice_pixel<T>(a, i, p1, tf, ce, pt, nullptr, 0);
+    v[0] = p1 * tf;
+    v[1] = p1;
+    v[2] = tf;
+    v[3] = a.focal ? a.alpha * powf(1.f - pt, a.gamma) * ce : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k][threadIdx.x] += r[k][threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) part[4 * blockIdx.x + threadIdx.x] = r[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void dice_finalize_kernel(const float* part, int P, double* out) {
+  __shared__ double r[4][256];
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int p = threadIdx.x; p < P; p += 256)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] += part[4 * p + k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k][threadIdx.x] = s[k];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k][threadIdx.x] += r[k][threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) out[threadIdx.x] = r[threadIdx.x][0];
+}
+
+// stats: (I, P, T, focal sum) from dice_fwd; grad = wd * dDice + wf * dFocal, scaled by gout
+template <typename T>
+__global__ __launch_bounds__(256) void dice_bwd_kernel(DiceArgs a, const double* stats,
+                                                       const float* gout, float smooth, float wd,
+                                                       float wf, void* dlogits) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.N * a.HW) return;
+  const long long n = i / a.HW, p = i - n * a.HW;
+  float p1, tf, ce, pt;
+  dice_pixel<T>(a, i, p1, tf, ce, pt, nullptr, 0);
+  const double I = stats[0], den = stats[1] + stats[2] + (double)smooth;
+  // d(1 - dice)/dp1 = -(2 t den - (2 I + s)) / den^2
+  const float gd = (float)(-(2.0 * tf * den - (2.0 * I + smooth)) / (den * den)) * wd * gout[0];
+  float gf = 0.f;
+  if (a.focal) {
+    const float om = 1.f - pt;
+    const float dfdce = a.alpha * (powf(om, a.gamma) + ce * a.gamma * powf(om, a.gamma - 1.f) * pt);
+    gf = dfdce * wf * gout[0] / (float)(a.N * a.HW);
+  }
+  const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
+  T* db = (T*)dlogits + (size_t)n * a.C * a.HW + p;
+  if (a.C == 1) {
+    st1(db, gd * p1 * (1.f - p1));
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
+  float se = 0.f;
+  for (int c = 0; c < a.C; ++c) se += expf(ld1(lb + (size_t)c * a.HW) - mx);
+  const long long t = a.target[i];
+  for (int c = 0; c < a.C; ++c) {
+    const float pcv = expf(ld1(lb + (size_t)c * a.HW) - mx) / se;
+    const float dice_c = gd * p1 * ((c == 1 ? 1.f : 0.f) - pcv);
+    const float focal_c = gf * (pcv - (c == t ? 1.f : 0.f));
+    st1(db + (size_t)c * a.HW, dice_c + focal_c);
+  }
+}
+
+int dice_loss_fwd(const void* logits, int dtype, const long long* target, int N, int C, long long HW,
+                  float alpha, float gamma, int focal, float* part, double* stats, hipStream_t st) {
+  if (C < 1 || (focal && C < 2)) {
+    set_error("dice_loss: C=%d (focal term needs C > 1)", C);
+    return E_INVALID;
+  }
+  DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};
+  const int P = ce_parts(N, HW);
+  if (dtype == DT_F32) dice_fwd_kernel<float><<<P, 256, 0, st>>>(a, part);
+  else dice_fwd_kernel<bf16><<<P, 256, 0, st>>>(a, part);
+  if (int rc = check_launch("dice_fwd")) return rc;
+  dice_finalize_kernel<<<1, 256, 0, st>>>(part, P, stats);
+  return check_launch("dice_finalize");
+}
+
+int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N, int C, long long HW,
+                  float alpha, float gamma, int focal, const double* stats, const float* gout,
+                  float smooth, float wd, float wf, void* dlogits, hipStream_t st) {
+  DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};
+  const int P = ce_parts(N, HW);
+  if (dtype == DT_F32) dice_bwd_kernel<float><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
+  else dice_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
+  return check_launch("dice_bwd");
+}
+
 // ---- dropout on an NHWC activation, mask indexed in NCHW order (matches the oracle) ----------
 
 // thread = one 16-B channel vector of one pixel; 32-bit index math (pixels * C/V < 2^31)

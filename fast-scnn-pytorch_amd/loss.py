@@ -196,3 +196,92 @@ class MixSoftmaxCrossEntropyOHEMLoss(SoftmaxCrossEntropyOHEMLoss):
             for p in preds[1:]:
                 loss = loss + self.aux_weight * super().forward(p, target)
         return loss
+
+
+# ---- Dice / Focal + Dice (utils/loss.py:12-100; train.py:183-188) ----------------------------
+class _DiceFocalFn(torch.autograd.Function):
+    """dice_weight * (1 - dice) + focal_weight * mean(focal) of one prediction (one kernel for the
+    per-pixel terms, fixed-order fp64 sums)."""
+
+    @staticmethod
+    def forward(ctx, pred, target, smooth, dice_weight, focal_weight, alpha, gamma):
+        if not pred.is_cuda:
+            raise RuntimeError("Dice loss needs ROCm device tensors")
+        if pred.dim() != 4:
+            raise RuntimeError("Dice loss: expected logits [N, C, H, W]")
+        pred = pred.contiguous()
+        target = target.to(device=pred.device, dtype=torch.int64).contiguous()
+        N, C, H, W = pred.shape
+        if target.numel() != N * H * W:
+            raise RuntimeError("Dice loss: target %s does not match %s"
+                               % (tuple(target.shape), tuple(pred.shape)))
+        focal = 1 if focal_weight != 0.0 else 0
+        parts = int(_lib.load().fscnn_ce_parts(N, H * W))
+        part = torch.empty(parts * 4, dtype=torch.float32, device=pred.device)
+        stats = torch.empty(4, dtype=torch.float64, device=pred.device)
+        _lib.call("fscnn_dice_fwd", _lib.ptr(pred), _lib.dtype_code(pred.dtype), _lib.ptr(target),
+                  N, C, H * W, ctypes.c_float(alpha), ctypes.c_float(gamma), focal, _lib.ptr(part),
+                  _lib.ptr(stats), _lib.stream_ptr(pred.device))
+        dice = (2.0 * stats[0] + smooth) / (stats[1] + stats[2] + smooth)
+        loss = dice_weight * (1.0 - dice) + focal_weight * stats[3] / float(N * H * W)
+        ctx.save_for_backward(pred, target, stats)
+        ctx.args = (float(smooth), float(dice_weight), float(focal_weight), float(alpha),
+                    float(gamma), focal)
+        return loss.to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, grad):
+        pred, target, stats = ctx.saved_tensors
+        smooth, dw, fw, alpha, gamma, focal = ctx.args
+        N, C, H, W = pred.shape
+        g = grad.to(torch.float32).reshape(1).contiguous()
+        dpred = torch.empty_like(pred)
+        _lib.call("fscnn_dice_bwd", _lib.ptr(pred), _lib.dtype_code(pred.dtype), _lib.ptr(target),
+                  N, C, H * W, ctypes.c_float(alpha), ctypes.c_float(gamma), focal,
+                  _lib.ptr(stats), _lib.ptr(g), ctypes.c_float(smooth), ctypes.c_float(dw),
+                  ctypes.c_float(fw), _lib.ptr(dpred), _lib.stream_ptr(pred.device))
+        return dpred, None, None, None, None, None, None
+
+
+class DiceLoss(nn.Module):
+    """utils/loss.py:12-39 on the HIP path."""
+
+    def __init__(self, smooth=1e-6, **kwargs):
+        super().__init__()
+        self.smooth = smooth
+
+    def forward(self, pred, target):
+        return _DiceFocalFn.apply(pred, target, self.smooth, 1.0, 0.0, 0.5, 2.0)
+
+
+class MixDiceLoss(nn.Module):
+    """utils/loss.py:42-68 on the HIP path."""
+
+    def __init__(self, aux=True, aux_weight=0.4, smooth=1e-6, **kwargs):
+        super().__init__()
+        self.aux = aux
+        self.aux_weight = aux_weight
+        self.dice_loss = DiceLoss(smooth=smooth)
+
+    def forward(self, preds, target):
+        if isinstance(preds, tuple):
+            loss = self.dice_loss(preds[0], target)
+            if self.aux and len(preds) > 1:
+                loss = loss + self.aux_weight * self.dice_loss(preds[1], target)
+            return loss
+        return self.dice_loss(preds, target)
+
+
+class FocalDiceLoss(nn.Module):
+    """utils/loss.py:71-100 on the HIP path (multi-class logits, C > 1)."""
+
+    def __init__(self, alpha=0.5, gamma=2.0, dice_weight=0.5, smooth=1e-6, **kwargs):
+        super().__init__()
+        self.alpha = alpha
+        self.gamma = gamma
+        self.dice_weight = dice_weight
+        self.smooth = smooth
+
+    def forward(self, pred, target):
+        return _DiceFocalFn.apply(pred, target, self.smooth, self.dice_weight,
+                                  1.0 - self.dice_weight, self.alpha, self.gamma)

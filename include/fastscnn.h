@@ -123,6 +123,20 @@ int fscnn_ce_weighted_bwd(const void* logits, int dtype, const long long* target
                           const float* prob, float thr, const float* grad_out, const float* out2,
                           void* dlogits, void* stream);
 
+/* Dice / Focal+Dice criteria (utils/loss.py:12-100; train.py:183-188, binary lane segmentation):
+ * fscnn_dice_fwd writes stats[4] (device fp64) = (sum p1*t, sum p1, sum t, sum focal_i) with
+ *   p1 = softmax(logits)[:, 1] (C > 1) or sigmoid (C == 1), t = float(target), focal_i =
+ *   alpha (1 - pt)^gamma ce_i (only when focal != 0; C > 1); part: ce_parts(N, HW) * 4 floats.
+ * fscnn_dice_bwd: d/dlogits of dice_weight * (1 - dice) + focal_weight * mean(focal), scaled by
+ *   *grad_out (device). */
+int fscnn_dice_fwd(const void* logits, int dtype, const long long* target, int N, int C,
+                   long long HW, float alpha, float gamma, int focal, float* part, double* stats,
+                   void* stream);
+int fscnn_dice_bwd(const void* logits, int dtype, const long long* target, int N, int C,
+                   long long HW, float alpha, float gamma, int focal, const double* stats,
+                   const float* grad_out, float smooth, float dice_weight, float focal_weight,
+                   void* dlogits, void* stream);
+
 /* GPU input path.
  * fscnn_normalize_u8: transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107,
  *   eval.py:22-25, demo.py:37-40) of N uint8 HWC RGB images into the NCHW network input

@@ -254,6 +254,24 @@ def ohem_cross_entropy(predict, target, ignore_label=-1, thresh=0.7, min_kept=25
     return F.cross_entropy(predict, t, weight=weight, ignore_index=ignore_label)
 
 
+def dice_loss(pred, target, smooth=1e-6):
+    """DiceLoss (utils/loss.py:12-39): 1 - (2 sum(p t) + s) / (sum p + sum t + s) with p the
+    softmax probability of class 1 (C > 1) or sigmoid(logit) (C == 1)."""
+    p = F.softmax(pred, dim=1)[:, 1] if pred.size(1) > 1 else torch.sigmoid(pred.squeeze(1))
+    p = p.contiguous().view(-1)
+    t = target.contiguous().view(-1).to(p.dtype)
+    inter = (p * t).sum()
+    return 1 - (2. * inter + smooth) / (p.sum() + t.sum() + smooth)
+
+
+def focal_dice_loss(pred, target, alpha=0.5, gamma=2.0, dice_weight=0.5, smooth=1e-6):
+    """FocalDiceLoss (utils/loss.py:71-100), multi-class logits."""
+    ce = F.cross_entropy(pred, target, reduction="none")
+    pt = torch.exp(-ce)
+    focal = (alpha * (1 - pt) ** gamma * ce).mean()
+    return (1 - dice_weight) * focal + dice_weight * dice_loss(pred, target, smooth)
+
+
 def to_tensor_normalize(img_hwc_u8, mean, std):
     """transforms.ToTensor() + transforms.Normalize(mean, std) (train.py:104-107): uint8 HWC ->
     fp32 CHW, torchvision's operation order (float().div(255), sub_(mean), div_(std))."""

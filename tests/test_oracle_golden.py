@@ -117,3 +117,24 @@ def test_oracle_ohem_matches_reference(case):
     if case == "kth":  # the k-th smallest threshold branch is what this case exercises
         _, thr = ref.ohem_target(x, t, -1, 0.7, int(g[case + ".min_kept"]))
         assert thr > 0.7
+
+
+@pytest.mark.parametrize("case", ["dice_c2", "dice_c1", "focal_c2", "focal_c4", "mix_aux"])
+def test_oracle_dice_matches_reference(case):
+    """oracle Dice / Focal+Dice against the reference criteria run on CPU
+    (tools/gen_dice_golden.py)."""
+    g = load_golden("dice")
+    x = torch.from_numpy(g[case + ".logits"]).requires_grad_(True)
+    t = torch.from_numpy(g[case + ".target"])
+    if case.startswith("dice"):
+        loss = ref.dice_loss(x, t)
+    elif case == "focal_c2":
+        loss = ref.focal_dice_loss(x, t)
+    elif case == "focal_c4":
+        loss = ref.focal_dice_loss(x, t, alpha=0.25, gamma=1.5)
+    else:
+        x2 = torch.from_numpy(g[case + ".logits2"]).requires_grad_(True)
+        loss = ref.dice_loss(x, t) + 0.4 * ref.dice_loss(x2, t)
+    loss.backward()
+    assert abs(loss.item() - float(g[case + ".loss"])) <= 1e-6
+    np.testing.assert_allclose(x.grad.numpy(), g[case + ".grad"], rtol=0, atol=1e-8)
