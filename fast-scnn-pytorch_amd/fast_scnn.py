@@ -540,5 +540,14 @@ def get_fast_scnn(dataset="citys", pretrained=False, root="./weights", map_cpu=F
     if pretrained:
         path = os.path.join(root, "fast_scnn_%s.pth" % acronyms[dataset])
         sd = torch.load(path, map_location="cpu" if map_cpu else None, weights_only=True)
-        model.load_state_dict(sd)
+        model.load_state_dict(strip_module_prefix(sd))
     return model
+
+
+def strip_module_prefix(state_dict):
+    """Checkpoints saved from the DataParallel / DistributedFastSCNN wrapper (train.py:449 saves
+    ``model.state_dict()`` with a ``module.`` prefix) load into a bare FastSCNN (SURVEY §8(f) row
+    4); other keys are left as they are."""
+    if all(k.startswith("module.") for k in state_dict):
+        return type(state_dict)((k[len("module."):], v) for k, v in state_dict.items())
+    return state_dict

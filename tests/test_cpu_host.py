@@ -108,3 +108,18 @@ def test_module_tree_and_arena_on_cpu():
     with pytest.raises(TypeError):
         get_fast_scnn("tusimple", num_classes=2)  # reference behaviour (duplicate argument)
     assert FastSCNN(2).classifier.conv[1].out_channels == 2
+
+
+def test_pretrained_checkpoint_with_module_prefix(tmp_path):
+    """train.py:449 saves the DataParallel-wrapped state_dict ('module.' keys); get_fast_scnn
+    (pretrained=True) loads it into the bare model."""
+    from models.fast_scnn import get_fast_scnn
+    src = get_fast_scnn("tusimple")
+    with torch.no_grad():
+        for p in src.parameters():
+            p.add_(0.5)
+    sd = {"module." + k: v for k, v in src.state_dict().items()}
+    torch.save(sd, str(tmp_path / "fast_scnn_tusimple.pth"))
+    m = get_fast_scnn("tusimple", pretrained=True, root=str(tmp_path), map_cpu=True)
+    for (k, a), (_, b) in zip(m.state_dict().items(), src.state_dict().items()):
+        assert torch.equal(a, b), k
