@@ -41,6 +41,16 @@ struct DwArgs {
   // lazily applied BN+ReLU of x (train: x is the producer's raw conv output z) or null
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
+  // fused BatchNorm-backward partial sums of the OUTPUT when it is the dy of a BN (dgrad):
+  // per workgroup record [2][C]: sum gv, sum gv*(z-mean)*invstd with gv = output (as stored) masked
+  // by the ReLU of that BN (mode 2: fmaf(z, bscale, bshift) > 0; mode 0: no ReLU)
+  float* bpart = nullptr;
+  const void* bz = nullptr;
+  const float* bmean = nullptr;
+  const float* binvstd = nullptr;
+  const float* bscale = nullptr;
+  const float* bshift = nullptr;
+  int bmode = 0;
 };
 
 struct DwBwdArgs {
@@ -52,6 +62,16 @@ struct DwBwdArgs {
   float* slab;      // [parts][9][C] (wgrad)
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
   const float* x_shift = nullptr;
+  // fused BatchNorm-backward partial sums of the OUTPUT when it is the dy of a BN (dgrad):
+  // per workgroup record [2][C]: sum gv, sum gv*(z-mean)*invstd with gv = output (as stored) masked
+  // by the ReLU of that BN (mode 2: fmaf(z, bscale, bshift) > 0; mode 0: no ReLU)
+  float* bpart = nullptr;
+  const void* bz = nullptr;
+  const float* bmean = nullptr;
+  const float* binvstd = nullptr;
+  const float* bscale = nullptr;
+  const float* bshift = nullptr;
+  int bmode = 0;
 };
 
 struct GemmArgs {
@@ -267,6 +287,7 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
+int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride);  // records of bpart
 int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
 int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st);
