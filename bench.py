@@ -30,14 +30,17 @@ sys.path.insert(0, ROOT)
 METRIC = "images/sec fwd+bwd @1024x2048 bs=8 per GPU; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0
 MFMA_PEAK_TFS = {"bf16": 2500.0, "fp32": 157.3}
+# launch-profiler kinds (csrc/common.hpp ProfKind); each launcher accounts the algorithmic bytes /
+# flops of SURVEY.md §8(d) for its launch shape (csrc/*.hip ProfScope), DESIGN.md §3
 PROF_KINDS = {1: "conv0_fwd", 2: "dw_fwd", 3: "dw_dgrad", 4: "dw_wgrad", 5: "gemm_nt",
-              6: "gemm_tn", 9: "upsample", 11: "ce_head",
-              12: "conv0_wgrad"}
+              6: "gemm_tn", 7: "bn_apply", 8: "bn_bwd_apply", 9: "upsample", 11: "ce_head",
+              12: "conv0_wgrad", 13: "bn_bwd_reduce", 14: "bn_finalize"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); default: WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8)
@@ -50,8 +53,50 @@ def parse():
     ap.add_argument("--no-forward", action="store_true")
     ap.add_argument("--unfused-loss", action="store_true",
                     help="materialise full-res logits and run the separate CE kernels")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: this process's CPU share)")
+    ap.add_argument("--no-cfg5", action="store_true")
     return ap.parse_args()
+
+
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run as a CHILD process, before this process touches the GPU, and exit
+    with its status (train.py:170-171's DataParallel over N devices becomes N processes)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_share():
+    """Threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS when set."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def prof(lib, kind, fn, max_launches):
@@ -67,16 +112,43 @@ def prof(lib, kind, fn, max_launches):
 
 
 def cpu_baseline(args):
-    """Oracle restatement (port) of one train step on a bounded sample, timed on host cores."""
+    """Oracle restatement (port) timed on this host's cores on bounded samples: one train step
+    (the metric's unit), the cfg2 forward (8 x 3 x 1024 x 2048, eval) beside forward_fp32, and the
+    cfg1 forward (1 x 3 x 768 x 768, the demo.py path)."""
     import numpy as np
     import torch
     from fast_scnn_pytorch_amd import arch, portable_init
     from oracle import fast_scnn_ref as ref  # checker / CPU baseline only
-    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    threads = args.cpu_threads or cpu_share()
     torch.set_num_threads(threads)
-    nb = 2
     sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
           arch.portable_state_dict(args.classes, seed=0).items()}
+
+    def timed(fn, reps, budget):
+        fn()
+        times = []
+        t_end = time.perf_counter() + budget
+        while len(times) < reps and (not times or time.perf_counter() < t_end):
+            t0 = time.perf_counter()
+            fn()
+            times.append(time.perf_counter() - t0)
+        return sorted(times)[len(times) // 2], len(times)
+
+    out = {}
+    with torch.no_grad():
+        x8 = torch.from_numpy(portable_init.input_tensor(1, (8, 3, args.height, args.width)))
+        med, n = timed(lambda: ref.forward(sd, x8, args.classes), 3, 12.0)
+        out["forward_cfg2"] = {"value": round(8 / med, 3), "unit": "images/s",
+                               "ms_per_batch": round(1e3 * med, 1),
+                               "sample": "eval fp32 8x3x%dx%d, median of %d after 1 warm-up"
+                                         % (args.height, args.width, n)}
+        del x8
+        x1 = torch.from_numpy(portable_init.input_tensor(1, (1, 3, 768, 768)))
+        med, n = timed(lambda: ref.forward(sd, x1, args.classes), 10, 5.0)
+        out["forward_cfg1"] = {"value": round(1 / med, 3), "unit": "images/s",
+                               "ms_per_image": round(1e3 * med, 2),
+                               "sample": "eval fp32 1x3x768x768 (demo.py path), median of %d" % n}
+    nb = 2
     for k, v in sd.items():
         if v.is_floating_point() and "running" not in k:
             v.requires_grad_(True)
@@ -90,22 +162,24 @@ def cpu_baseline(args):
         outs, _, _ = ref.forward(sd, x, args.classes, training=True, dropout_seed=5)
         ref.cross_entropy(outs[0], t).backward()
 
-    step()
-    times = []
-    t_end = time.perf_counter() + 25.0
-    while len(times) < 3 and (not times or time.perf_counter() < t_end):
-        t0 = time.perf_counter()
-        step()
-        times.append(time.perf_counter() - t0)
-    med = sorted(times)[len(times) // 2]
-    return {"value": round(nb / med, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": "oracle/fast_scnn_ref.py train step (fwd+CE+bwd, fp32) on %d x 3 x %d x %d, "
-                      "median of %d after 1 warm-up, torch CPU %d threads"
-                      % (nb, args.height, args.width, len(times), threads)}
+    med, n = timed(step, 3, 25.0)
+    res = {"value": round(nb / med, 4), "unit": "images/s", "cores": threads, "kind": "port",
+           "sample": "oracle/fast_scnn_ref.py train step (fwd+CE+bwd, fp32) on %d x 3 x %d x %d, "
+                     "median of %d after 1 warm-up, torch CPU %d threads"
+                     % (nb, args.height, args.width, n, threads),
+           "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+           "torch": torch.__version__}
+    res.update(out)
+    return res
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, env_world))
     import torch
     import torch.distributed as dist
     import _fscnn_boot
@@ -196,10 +270,13 @@ def main():
     _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
                                   ctypes.byref(f)), "fscnn_prof_end")
     last_loss = float(loss.item())
+    per_rank_ms = [round(1e3 * elapsed / args.steps, 3)]
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        allt = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(allt, tt)
+        per_rank_ms = [round(1e3 * float(v.item()) / args.steps, 3) for v in allt]
+        elapsed = max(float(v.item()) for v in allt)
 
     value = world * B * args.steps / elapsed
     avg_ms = ms.value / max(1, n.value)
@@ -236,31 +313,60 @@ def main():
                    "per_gpu_batch": B, "resolution": [H, W], "parallelism": "dp%d" % world},
         "roofline": roof,
         "loss": {"after_warmup": round(first_loss, 5), "final": round(last_loss, 5)},
+        "per_rank_ms_per_step": per_rank_ms,
+        "comm": {"backend": dist.get_backend() if world > 1 else None,
+                 "world_size": dist.get_world_size() if world > 1 else 1,
+                 "buckets": 4 if world > 1 else 0},
     }
     if census:
         result["kernel_ms_per_step_census"] = census
 
-    # forward-only fp32 inference (cfg2): north-star forward target (rank 0, N=1 only)
+    # forward-only inference (rank 0, N=1 only): cfg2 fp32 (north-star forward target), cfg1
+    # (demo.py: 1 x 3 x 768 x 768, latency) and cfg5 (TuSimple 32 x 3 x 480 x 640, C=2)
     if rank == 0 and world == 1 and not args.no_forward:
         model.eval()
         x32 = x.float()
+
+        def fwd_rate(m, xin, nrep):
+            with torch.no_grad():
+                for _ in range(3):
+                    m(xin)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(nrep):
+                    m(xin)
+                torch.cuda.synchronize()
+            return (time.perf_counter() - t1) / nrep
+
+        fe = fwd_rate(model, x32, max(5, args.steps // 2))
         with torch.no_grad():
-            for _ in range(3):
-                model(x32)
-            torch.cuda.synchronize()
-            nrep = max(5, args.steps // 2)
-            t1 = time.perf_counter()
-            for _ in range(nrep):
-                model(x32)
-            torch.cuda.synchronize()
-            fe = time.perf_counter() - t1
             fms, fn, fb, ff = prof(lib, 2, lambda: model(x32), 256)
         dw_gbs = fb / max(fn, 1) / (fms / max(fn, 1) * 1e-3) / 1e9 if fms > 0 else 0
-        result["forward_fp32"] = {"value": round(B * nrep / fe, 2), "unit": "images/s",
-                                  "ms_per_batch": round(1e3 * fe / nrep, 3),
+        result["forward_fp32"] = {"value": round(B / fe, 2), "unit": "images/s",
+                                  "ms_per_batch": round(1e3 * fe, 3),
                                   "config": "cfg2 eval fp32 %dx3x%dx%d" % (B, H, W),
                                   "dw_fwd_GBps": round(dw_gbs, 1),
                                   "dw_fwd_hbm_frac": round(dw_gbs / HBM_PEAK_GBS, 4)}
+        x1 = torch.from_numpy(portable_init.input_tensor(1, (1, 3, 768, 768))).to(dev)
+        f1 = fwd_rate(model, x1, 20)
+        result["forward_cfg1"] = {"value": round(1 / f1, 2), "unit": "images/s",
+                                  "ms_per_image": round(1e3 * f1, 3),
+                                  "config": "cfg1 eval fp32 1x3x768x768 (demo.py path)"}
+        del x1
+        if not args.no_cfg5:
+            m5 = FastSCNN(2)
+            m5.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                                arch.portable_state_dict(2, seed=0).items()})
+            m5 = m5.to(dev).eval()
+            x5 = torch.from_numpy(portable_init.input_tensor(1, (32, 3, 480, 640))).to(dev)
+            dt5 = getattr(m5, "CFG5_DTYPE", torch.float32)
+            x5 = x5.to(dt5)
+            f5 = fwd_rate(m5, x5, 10)
+            result["forward_cfg5"] = {"value": round(32 / f5, 2), "unit": "images/s",
+                                      "ms_per_batch": round(1e3 * f5, 3),
+                                      "dtype": str(dt5).replace("torch.", ""),
+                                      "config": "cfg5 eval 32x3x480x640, 2 classes"}
+            del m5, x5
         model.train()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -42,10 +42,11 @@ SIGNATURES = {
     "fscnn_ohem_prob": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_float, c_vp, c_vp,
                                 c_vp]),
     "fscnn_kth_smallest": (c_int, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp]),
+    "fscnn_ohem_threshold": (c_int, [c_vp, c_ll, c_vp, c_ll, c_float, c_vp, c_vp, c_vp]),
     "fscnn_ce_weighted_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
-                                      c_float, c_vp, c_vp, c_vp]),
+                                      c_vp, c_vp, c_vp, c_vp]),
     "fscnn_ce_weighted_bwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
-                                      c_float, c_vp, c_vp, c_vp, c_vp]),
+                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
     "fscnn_dice_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_float, c_float, c_int,
                                c_vp, c_vp, c_vp]),
     "fscnn_dice_bwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_float, c_float, c_int,

@@ -187,6 +187,7 @@ int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
     set_error("bn_finalize: P=%d C=%d", a.P, a.C);
     return E_INVALID;
   }
+  ProfScope ps(PK_BN_FIN, st, 12.0 * a.P * a.C, 0.0);
   int Q = a.P;
   if (a.P > BN_Q) {
     Q = BN_Q;
@@ -237,6 +238,10 @@ int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st) {
   int V = dtype == DT_F32 ? 4 : 8;
   if (a.C % V) { set_error("bn_apply: C=%d not a multiple of %d", a.C, V); return E_INVALID; }
   long long total = a.M * (a.C / V);
+  ProfScope ps(PK_BN_APPLY, st,
+               (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C *
+                   (2 + (a.z2 ? 1 : 0) + (a.res ? 1 : 0)),
+               0.0);
   unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) bn_apply_kernel<float><<<grid, 256, 0, st>>>(a);
   else bn_apply_kernel<bf16><<<grid, 256, 0, st>>>(a);
@@ -344,6 +349,8 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
   bn_bwd_shape(a.C, V, bx, by);
   int rpb;
   int P = bn_bwd_parts(a.M, a.C, dtype, &rpb);
+  ProfScope ps(PK_BN_BWD_RED, st, (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * (a.mask ? 3 : 2),
+               0.0);
   BnBwdArgs b = a;
   b.rows_per_block = rpb;
   dim3 grid(cdiv(a.C / V, bx), P), block(bx, by);
@@ -451,6 +458,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_fin_kernel(float* part, int P
 
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
                     float* coef, hipStream_t st, unsigned* counters) {
+  ProfScope ps(PK_BN_FIN, st, 8.0 * P * C, 0.0);
   int Q = P;
   if (P > BN_Q) {
     Q = BN_Q;
@@ -514,6 +522,9 @@ int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
   int V = dtype == DT_F32 ? 4 : 8;
   long long total = a.M * (a.C / V);
   unsigned grid = (unsigned)((total + 255) / 256);
+  ProfScope ps(PK_BN_BWD, st,
+               (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * (2 + (a.coef || a.relu_z ? 1 : 0) + (a.mask ? 1 : 0)),
+               0.0);
   if (dtype == DT_F32) bn_bwd_apply_launch<float>(a, grid, st);
   else bn_bwd_apply_launch<bf16>(a, grid, st);
   return check_launch("bn_bwd_apply");

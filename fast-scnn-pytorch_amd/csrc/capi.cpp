@@ -100,7 +100,8 @@ extern "C" int fscnn_prof_end(double* total_ms, long long* launches, double* byt
 extern "C" const char* fscnn_prof_kind_name(int kind) {
   static const char* names[PK_COUNT] = {"none", "conv0_fwd", "dw_fwd", "dw_dgrad", "dw_wgrad",
                                         "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
-                                        "upsample_bwd", "cross_entropy", "conv0_wgrad"};
+                                        "upsample_bwd", "cross_entropy", "conv0_wgrad",
+                                        "bn_bwd_reduce", "bn_finalize"};
   return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
 }
 
@@ -337,9 +338,23 @@ int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* 
   return kth_smallest(values, n, k, hist, out, S(stream));
 }
 
+int fscnn_ohem_threshold(const float* prob, long long n, const unsigned long long* counts,
+                         long long min_kept, float thresh, unsigned* work, float* thr, void* stream) {
+  if (!prob || !counts || !work || !thr) {
+    set_error("fscnn_ohem_threshold: null argument");
+    return E_INVALID;
+  }
+  return ohem_threshold_dev(prob, n, counts, min_kept, thresh, work, thr, S(stream));
+}
+
 int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
                           long long HW, long long ignore_index, const float* weight,
-                          const float* prob, float thr, float* part, float* out2, void* stream) {
+                          const float* prob, const float* thr, float* part, float* out2,
+                          void* stream) {
+  if (prob && !thr) {
+    set_error("fscnn_ce_weighted_fwd: prob without thr");
+    return E_INVALID;
+  }
   CeArgs a{};
   a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target;
   a.ignore_index = ignore_index; a.part = part; a.weight = weight; a.prob = prob; a.thr = thr;
@@ -348,8 +363,12 @@ int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target
 
 int fscnn_ce_weighted_bwd(const void* logits, int dtype, const long long* target, int N, int C,
                           long long HW, long long ignore_index, const float* weight,
-                          const float* prob, float thr, const float* grad_out, const float* out2,
-                          void* dlogits, void* stream) {
+                          const float* prob, const float* thr, const float* grad_out,
+                          const float* out2, void* dlogits, void* stream) {
+  if (prob && !thr) {
+    set_error("fscnn_ce_weighted_bwd: prob without thr");
+    return E_INVALID;
+  }
   CeArgs a{};
   a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target;
   a.ignore_index = ignore_index; a.dlogits = dlogits; a.weight = weight; a.prob = prob; a.thr = thr;

@@ -197,7 +197,8 @@ enum Status : int { OK = 0, E_INVALID = -1, E_UNSUPPORTED = -2, E_HIP = -3 };
 // ---- in-library launch profiler (bench.py roofline: HIP events on the launch stream) ---------
 enum ProfKind : int {
   PK_NONE = 0, PK_CONV0_FWD, PK_DW_FWD, PK_DW_DGRAD, PK_DW_WGRAD, PK_GEMM_NT, PK_GEMM_TN,
-  PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_CONV0_WGRAD, PK_COUNT
+  PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_CONV0_WGRAD, PK_BN_BWD_RED, PK_BN_FIN,
+  PK_COUNT
 };
 extern int g_prof_kind;  // kind being recorded (PK_NONE = off)
 void prof_start(hipStream_t st);

@@ -211,57 +211,6 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
       }
     }
   }
-  if constexpr (FLIP) {
-    if (a.bpart != nullptr) {
-      // ---- fused BN-backward partials of dx (see DwArgs::bpart) -----------------------------
-      float s1[4], s2[4], bmu[4], bis[4], bsc[4], bsh[4];
-      const bool m2 = a.bmode == 2;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s1[j] = s2[j] = 0.f;
-        bmu[j] = a.bmean[c0 + j];
-        bis[j] = a.binvstd[c0 + j];
-        bsc[j] = m2 ? a.bscale[c0 + j] : 0.f;
-        bsh[j] = m2 ? a.bshift[c0 + j] : 1.f;
-      }
-#pragma unroll
-      for (int r = 0; r < G::HS; ++r) {
-        if (r >= nrow) continue;
-        const T* zb = (const T*)a.bz + (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0) * a.C + c0;
-#pragma unroll
-        for (int p = 0; p < G::WS; ++p) {
-          if (p >= ncol) continue;
-          float z[4];
-          quad_ld(zb + (size_t)p * a.C, z);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float gv = acc[r][p][j];
-            if constexpr (sizeof(T) == 2) gv = bf2f(f2bf(gv));  // the value as stored
-            gv = fmaf(z[j], bsc[j], bsh[j]) > 0.f ? gv : 0.f;
-            s1[j] += gv;
-            s2[j] += gv * (z[j] - bmu[j]) * bis[j];
-          }
-        }
-      }
-      float* rec = a.bpart + ((size_t)bz * gridDim.y + by) * 2 * a.C;
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s_red[(grp * QB + q) * 4 + j] = pass ? s2[j] : s1[j];
-        __syncthreads();
-        if (grp == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float t = 0.f;
-            for (int g2 = 0; g2 < G::G; ++g2) t += s_red[(g2 * QB + q) * 4 + j];
-            rec[pass * a.C + c0 + j] = t;
-          }
-        }
-        __syncthreads();
-      }
-      return;
-    }
-  }
   if (a.part == nullptr) return;
   // ---- per-channel (mean, M2, count) over the tile (train-mode BN statistics) ---------------
   const int trows = min(G::TH, a.Ho - th0), tcols = min(G::TW, a.Wo - tw0);
@@ -391,7 +340,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   const int h0 = (bz - n * nb) * 2;
   const int w0 = (by * BY + ty) * 4;
   const bool active = cv < CV && w0 < a.W;
-  if (!active && a.bpart == nullptr) return;  // (the partials below need every thread)
+  if (!active) return;
   const int cvc = active ? cv : 0;
   float wt[9][V];
   const float* wp = a.w + (size_t)cvc * V * 9;
@@ -434,87 +383,17 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
       }
     }
   }
-  if (active) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      if (h0 + r >= a.H) continue;
-      T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + (size_t)cv * V;
+  for (int r = 0; r < 2; ++r) {
+    if (h0 + r >= a.H) continue;
+    T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + (size_t)cv * V;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (w0 + q < a.W) stv(db + (size_t)q * a.C, acc[r][q]);
-    }
+    for (int q = 0; q < 4; ++q)
+      if (w0 + q < a.W) stv(db + (size_t)q * a.C, acc[r][q]);
   }
-  if (a.bpart == nullptr) return;
-  // ---- fused BN-backward partials of dx (see DwBwdArgs::bpart): fixed-order column reduction
-  // over the BY pixel groups of the workgroup -> one [2][C] record per (column tile, row pair)
-  __shared__ float s_bred[256 * 8];
-  float s1[V], s2[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
-  if (active) {
-    const bool m2 = a.bmode == 2;
-    float bmu[V], bis[V], bsc[V], bsh[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const int c = cv * V + j;
-      bmu[j] = a.bmean[c];
-      bis[j] = a.binvstd[c];
-      bsc[j] = m2 ? a.bscale[c] : 0.f;
-      bsh[j] = m2 ? a.bshift[c] : 1.f;
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      if (h0 + r >= a.H) continue;
-      const T* zb = (const T*)a.bz + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + (size_t)cv * V;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (w0 + q >= a.W) continue;
-        float z[V];
-        ldv(zb + (size_t)q * a.C, z);
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-          float gv = acc[r][q][j];
-          if constexpr (V == 8) gv = bf2f(f2bf(gv));  // the value as stored
-          gv = fmaf(z[j], bsc[j], bsh[j]) > 0.f ? gv : 0.f;
-          s1[j] += gv;
-          s2[j] += gv * (z[j] - bmu[j]) * bis[j];
-        }
-      }
-    }
-  }
-  float* rec = a.bpart + ((size_t)bz * gridDim.y + by) * 2 * a.C;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < V; ++j) s_bred[(ty * BX + tx) * V + j] = pass ? s2[j] : s1[j];
-    __syncthreads();
-    if (ty == 0 && cv < CV) {
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float t = 0.f;
-        for (int y = 0; y < BY; ++y) t += s_bred[(y * BX + tx) * V + j];
-        rec[pass * a.C + cv * V + j] = t;
-      }
-    }
-  }
-}
-
-// records of the fused BN-backward partials written by dw_dgrad (dx is [N][H][W][C])
-int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
-  const int V = dtype == DT_F32 ? 4 : 8;
-  if (stride == 1) return dw_parts(N, H, W, C, dtype, 1);
-  int bx, by;
-  dw_block_shape(C, V, bx, by);
-  return cdiv(W, by * 4) * N * ((H + 1) / 2);
 }
 
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
-  if (a.bpart && (!a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
-                  (a.bmode != 0 && a.bmode != 2))) {
-    set_error("dw_dgrad: inconsistent fused BN-backward arguments");
-    return E_INVALID;
-  }
   const int V = dtype == DT_F32 ? 4 : 8;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
@@ -524,8 +403,6 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     DwArgs f{};
     f.N = a.N; f.H = a.Ho; f.W = a.Wo; f.C = a.C; f.Ho = a.H; f.Wo = a.W; f.stride = 1;
     f.x = a.dy; f.w = a.w; f.y = a.dx;
-    f.bpart = a.bpart; f.bz = a.bz; f.bmean = a.bmean; f.binvstd = a.binvstd;
-    f.bscale = a.bscale; f.bshift = a.bshift; f.bmode = a.bmode;
     return dw_launch_fwd<true, false>(f, dtype, st);
   }
   int bx, by;

@@ -41,16 +41,6 @@ struct DwArgs {
   // lazily applied BN+ReLU of x (train: x is the producer's raw conv output z) or null
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
-  // fused BatchNorm-backward partial sums of the OUTPUT when it is the dy of a BN (dgrad):
-  // per workgroup record [2][C]: sum gv, sum gv*(z-mean)*invstd with gv = output (as stored) masked
-  // by the ReLU of that BN (mode 2: fmaf(z, bscale, bshift) > 0; mode 0: no ReLU)
-  float* bpart = nullptr;
-  const void* bz = nullptr;
-  const float* bmean = nullptr;
-  const float* binvstd = nullptr;
-  const float* bscale = nullptr;
-  const float* bshift = nullptr;
-  int bmode = 0;
 };
 
 struct DwBwdArgs {
@@ -62,16 +52,6 @@ struct DwBwdArgs {
   float* slab;      // [parts][9][C] (wgrad)
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
   const float* x_shift = nullptr;
-  // fused BatchNorm-backward partial sums of the OUTPUT when it is the dy of a BN (dgrad):
-  // per workgroup record [2][C]: sum gv, sum gv*(z-mean)*invstd with gv = output (as stored) masked
-  // by the ReLU of that BN (mode 2: fmaf(z, bscale, bshift) > 0; mode 0: no ReLU)
-  float* bpart = nullptr;
-  const void* bz = nullptr;
-  const float* bmean = nullptr;
-  const float* binvstd = nullptr;
-  const float* bscale = nullptr;
-  const float* bshift = nullptr;
-  int bmode = 0;
 };
 
 struct GemmArgs {
@@ -225,10 +205,10 @@ struct CeArgs {
   const float* scale;     // device scalar: grad_out / count (computed by ce_finalize)
   void* dlogits;          // [N][C][HW] or null
   // OHEM (utils/loss.py:127-176): class weights [C] (weighted mean: sum w*nll / sum w) and the
-  // kept mask prob[i] <= thr (prob from ohem_prob); null = plain CE
+  // kept mask prob[i] <= *thr (prob from ohem_prob, thr a device scalar); null = plain CE
   const float* weight = nullptr;
   const float* prob = nullptr;
-  float thr = 0.f;
+  const float* thr = nullptr;
 };
 
 // Fused training head: bilinear(align_corners) upsample of the low-res logits to the input
@@ -287,7 +267,6 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
-int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride);  // records of bpart
 int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
 int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st);
@@ -353,6 +332,11 @@ int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* co
               hipStream_t st);
 int kth_smallest(const float* key, long long n, long long k, unsigned* hist, float* out,
                  hipStream_t st);
+// the whole OHEM threshold on the device from ohem_prob's counters (no host synchronisation):
+// *thr = inf (keep all labelled) / thresh / the k-th smallest label probability; work: 2056 uint32
+int ohem_threshold_dev(const float* key, long long n, const unsigned long long* counts,
+                       long long min_kept, float thresh, unsigned* work, float* thr,
+                       hipStream_t st);
 // Dice / Focal+Dice criteria (misc.hip): stats = (sum p1 t, sum p1, sum t, sum focal) in fp64
 int dice_loss_fwd(const void* logits, int dtype, const long long* target, int N, int C, long long HW,
                   float alpha, float gamma, int focal, float* part, double* stats, hipStream_t st);

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeArgs a) {
   if (i < total) {
     long long n = i / a.HW, p = i - n * a.HW;
     long long t = a.target[i];
-    if (t != a.ignore_index && t >= 0 && t < a.C && (!a.prob || a.prob[i] <= a.thr)) {
+    if (t != a.ignore_index && t >= 0 && t < a.C && (!a.prob || a.prob[i] <= *a.thr)) {
       const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
       float mx = -INFINITY;
       for (int c = 0; c < a.C; ++c) mx = fmaxf(mx, ld1(lb + (size_t)c * a.HW));
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(CeArgs a, const float* gout
   long long t = a.target[i];
   const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
   T* db = (T*)a.dlogits + (size_t)n * a.C * a.HW + p;
-  if (t == a.ignore_index || t < 0 || t >= a.C || (a.prob && !(a.prob[i] <= a.thr))) {
+  if (t == a.ignore_index || t < 0 || t >= a.C || (a.prob && !(a.prob[i] <= *a.thr))) {
     for (int c = 0; c < a.C; ++c) st1(db + (size_t)c * a.HW, 0.f);
     return;
   }
@@ -216,6 +216,122 @@ int kth_smallest(const float* key, long long n, long long k, unsigned* hist, flo
   uint32_t bits = prefix;
   memcpy(out, &bits, 4);
   return OK;
+}
+
+// Device-resident form of the same selection (no host round trip, so a train step with the OHEM
+// criterion never synchronises): state = {active, k, prefix, pshift}, hist 2048 bins, thr_out.
+//   init  : thr = inf if min_kept >= #labelled (reference: keep every labelled pixel), else
+//           thresh; the radix select runs only when #(prob <= thresh) < k = min(#labelled, min_kept)
+//   3 x (hist over the keys matching the prefix, pick: one workgroup scans the bins, extends the
+//        prefix and re-zeroes the bins for the next digit)
+//   final : thr = the selected bit pattern when the select ran.
+struct OhemSel {
+  unsigned active, prefix;
+  int pshift;
+  unsigned pad;
+  unsigned long long k;
+};
+
+__global__ void ohem_sel_init_kernel(const unsigned long long* counts, long long min_kept,
+                                     float thresh, OhemSel* s, unsigned* hist, float* thr) {
+  for (int j = threadIdx.x; j < 2048; j += blockDim.x) hist[j] = 0u;
+  if (threadIdx.x != 0) return;
+  const unsigned long long num_valid = counts[0], n_le = counts[1];
+  s->active = 0u; s->prefix = 0u; s->pshift = 32; s->k = 0ull;
+  if ((unsigned long long)min_kept >= num_valid) {  // (min_kept >= 0)
+    *thr = INFINITY;
+    return;
+  }
+  *thr = thresh;
+  if (min_kept > 0) {
+    const unsigned long long k = (unsigned long long)min_kept < num_valid ? (unsigned long long)min_kept
+                                                                          : num_valid;
+    if (n_le < k) { s->active = 1u; s->k = k; }
+  }
+}
+
+__global__ __launch_bounds__(256) void ohem_sel_hist_kernel(const float* key, long long n, int shift,
+                                                            unsigned bins, const OhemSel* s,
+                                                            unsigned* hist) {
+  if (!s->active) return;
+  const int pshift = s->pshift;
+  const unsigned prefix = s->prefix;
+  __shared__ unsigned s_h[2048];
+  for (unsigned j = threadIdx.x; j < bins; j += blockDim.x) s_h[j] = 0u;
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const unsigned u = __float_as_uint(key[i]);
+    const bool in = pshift >= 32 || (u >> pshift) == prefix;
+    if (in) atomicAdd(&s_h[(u >> shift) & (bins - 1)], 1u);
+  }
+  __syncthreads();
+  for (unsigned j = threadIdx.x; j < bins; j += blockDim.x)
+    if (s_h[j]) atomicAdd(&hist[j], s_h[j]);
+}
+
+// one workgroup: exclusive scan of the bins in 256 chunks, the chunk holding the k-th key picks
+__global__ __launch_bounds__(256) void ohem_sel_pick_kernel(OhemSel* s, unsigned* hist, unsigned bins,
+                                                            int width, int shift) {
+  if (!s->active) return;
+  __shared__ unsigned long long s_sum[256];
+  const unsigned per = (bins + 255) / 256;
+  const unsigned b0 = threadIdx.x * per;
+  unsigned long long own = 0;
+  for (unsigned j = 0; j < per; ++j)
+    if (b0 + j < bins) own += hist[b0 + j];
+  s_sum[threadIdx.x] = own;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 256 serial adds: tiny
+    unsigned long long run = 0;
+    for (int t = 0; t < 256; ++t) {
+      const unsigned long long v = s_sum[t];
+      s_sum[t] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  const unsigned long long k = s->k;
+  unsigned long long before = s_sum[threadIdx.x];
+  __syncthreads();
+  if (before < k && before + own >= k) {  // exactly one thread
+    unsigned long long kk = k - before;
+    unsigned b = b0;
+    for (;; ++b) {
+      const unsigned long long h = hist[b];
+      if (h >= kk) break;
+      kk -= h;
+    }
+    s->prefix = (s->prefix << width) | b;
+    s->pshift = shift;
+    s->k = kk;
+  }
+  __syncthreads();
+  for (unsigned j = threadIdx.x; j < bins; j += blockDim.x) hist[j] = 0u;
+}
+
+__global__ void ohem_sel_final_kernel(const OhemSel* s, float* thr) {
+  if (threadIdx.x == 0 && s->active) *thr = __uint_as_float(s->prefix);
+}
+
+int ohem_threshold_dev(const float* key, long long n, const unsigned long long* counts,
+                       long long min_kept, float thresh, unsigned* work, float* thr,
+                       hipStream_t st) {
+  if (n <= 0 || min_kept < 0) {
+    set_error("ohem_threshold: n=%lld min_kept=%lld", n, min_kept);
+    return E_INVALID;
+  }
+  OhemSel* s = reinterpret_cast<OhemSel*>(work + 2048);
+  ohem_sel_init_kernel<<<1, 256, 0, st>>>(counts, min_kept, thresh, s, work, thr);
+  static const int shifts[3] = {21, 10, 0}, widths[3] = {11, 11, 10};
+  const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 2048);
+  for (int d = 0; d < 3; ++d) {
+    const unsigned bins = 1u << widths[d];
+    ohem_sel_hist_kernel<<<grid, 256, 0, st>>>(key, n, shifts[d], bins, s, work);
+    ohem_sel_pick_kernel<<<1, 256, 0, st>>>(s, work, bins, widths[d], shifts[d]);
+  }
+  ohem_sel_final_kernel<<<1, 64, 0, st>>>(s, thr);
+  return check_launch("ohem_threshold");
 }
 
 // ---- Dice / Focal+Dice (utils/loss.py:12-100; train.py:183-188 for binary lane segmentation) ----

@@ -153,17 +153,6 @@ struct Alloc {
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
 
-// FSCNN_DW_BNFUSE=1: depthwise dgrads emit the BN-backward partial sums of their output (skips
-// bn_bwd_reduce).  Off by default: measured +0.06 ms/step on cfg3 (the stride-2 dgrad gets 3x
-// slower with the z re-read and block reduction than the reduce pass it replaces).
-bool dw_bnfuse_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_DW_BNFUSE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 bool lazy_bn_enabled() {  // FSCNN_LAZY_BN=0 materialises every BN output (A/B measurements)
   static const bool on = [] {
     const char* e = getenv("FSCNN_LAZY_BN");
@@ -388,17 +377,6 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
       s = (size_t)gemm_parts((int)u.M) * 2 * u.C;  // fused dgrad-epilogue records
       if (s > bnp) bnp = s;
     };
-    // records written by depthwise dgrads with fused BN-backward partials
-    auto dw_upd = [&](int Hh, int Ww, int Cc, int s) {
-      const size_t r = (size_t)dw_dgrad_parts(N, Hh, Ww, Cc, dtype, s) * 2 * Cc;
-      if (r > bnp) bnp = r;
-    };
-    dw_upd(pl.H1, pl.W1, 32, 2); dw_upd(pl.H2, pl.W2, 48, 2); dw_upd(pl.H3, pl.W3, 128, 1);
-    for (int i = 0; i < 9; ++i) {
-      const int Hin = i == 0 ? pl.H3 : (i <= 3 ? pl.H4 : pl.H5);
-      const int Win = i == 0 ? pl.W3 : (i <= 3 ? pl.W4 : pl.W5);
-      dw_upd(Hin, Win, net.lb[i].cin * 6, net.lb[i].stride);
-    }
     bn_upd(pl.c0); bn_upd(pl.l1dw); bn_upd(pl.l1pw); bn_upd(pl.l2dw); bn_upd(pl.l2pw);
     for (int i = 0; i < 9; ++i) { bn_upd(pl.lbe[i]); bn_upd(pl.lbd[i]); bn_upd(pl.lbp[i]); }
     for (int i = 0; i < 4; ++i) bn_upd(pl.ppk[i]);
@@ -878,20 +856,10 @@ struct Exec {
   BTarget relu_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 2; return t; }
   BTarget plain_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 0; return t; }
   static int pre(const Unit& u) { return gemm_parts((int)u.M); }
-  // records already written by a depthwise dgrad with fused partials (0: run the reduce)
-  int dw_pre(int H, int Wd, int C, int stride) const {
-    return dw_bnfuse_enabled() ? dw_dgrad_parts(pl.N, H, Wd, C, dt, stride) : 0;
-  }
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
   int dw_bwd(const ConvL& c, int C, const void* dz, In X, int H, int Wd, int Ho, int Wo,
-             int stride, void* dX, BTarget bt = BTarget()) {
+             int stride, void* dX) {
     DwBwdArgs d{};
-    if (bt.u && train && dw_bnfuse_enabled()) {  // dX is the dy of bt.u's BN: fused partials
-      const Unit& u = *bt.u;
-      d.bpart = (float*)Bw(pl.bnpart);
-      d.bz = W(u.z); d.bmean = Wf(u.mean); d.binvstd = Wf(u.invstd);
-      d.bscale = Wf(u.scale); d.bshift = Wf(u.shift); d.bmode = bt.mode;
-    }
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
     d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz; d.w = P(c.w); d.dx = dX;
     const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
@@ -941,10 +909,8 @@ struct Exec {
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw)));
     TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz, pre(pl.c2dw)));
-    TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
-               relu_target(pl.c1pw)));
-    TRY(bn_bwd_relu(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, dz,
-                    dw_pre(pl.H3, pl.W3, 128, 1)));
+    TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
+    TRY(bn_bwd_relu(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, dz));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw)));
     TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz, pre(pl.c1dw)));
@@ -1019,8 +985,8 @@ struct Exec {
     TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz, false, i < 8 ? pre(up) : 0));
     TRY(pw_bwd(l.p, up.M, dz, l.cout, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
     TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz, pre(ud)));
-    TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue)));
-    TRY(bn_bwd_relu(ue, l.be, Bw(ue.ga), e, dz, dw_pre(Hin, Win, e, l.stride)));
+    TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
+    TRY(bn_bwd_relu(ue, l.be, Bw(ue.ga), e, dz));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
@@ -1035,17 +1001,13 @@ struct Exec {
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw)));
     TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz, pre(pl.l2dw)));
-    TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
-               relu_target(pl.l1pw)));
-    TRY(bn_bwd_relu(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, dz,
-                    dw_pre(pl.H2, pl.W2, 48, 2)));
+    TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
+    TRY(bn_bwd_relu(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, dz));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw)));
     TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz, pre(pl.l1dw)));
-    TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
-               relu_target(pl.c0)));
-    TRY(bn_bwd_relu(pl.c0, net.b0, Bw(pl.c0.ga), 32, dz,
-                    dw_pre(pl.H1, pl.W1, 32, 2)));
+    TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
+    TRY(bn_bwd_relu(pl.c0, net.b0, Bw(pl.c0.ga), 32, dz));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;

@@ -44,17 +44,26 @@ def normalize_images(images, mean=IMAGENET_MEAN, std=IMAGENET_STD, dtype=torch.f
 
 
 class CityscapesLabelMap:
-    """``CitySegmentation._class_to_index`` on the device (label ids outside the table -> -1;
-    the reference asserts on them)."""
+    """``CitySegmentation._class_to_index`` on the device.
 
-    def __init__(self, key=CITYSCAPES_KEY, offset=1, device="cuda"):
+    Like the reference (data_loader/cityscapes.py:66-68 ``assert value in self._mapping``), a
+    label id outside the table raises ``AssertionError`` (one device reduction + host read per
+    call: this is the data-loading path, where the reference inspects every mask on the CPU).
+    ``strict=False`` maps such ids to -1 (ignored) without the check."""
+
+    def __init__(self, key=CITYSCAPES_KEY, offset=1, device="cuda", strict=True):
         self.lut = torch.tensor(key, dtype=torch.int64, device=device)
         self.offset = int(offset)
+        self.strict = bool(strict)
 
     def __call__(self, mask):
         if mask.dtype != torch.uint8 or not mask.is_cuda:
             raise RuntimeError("CityscapesLabelMap: expected a uint8 ROCm device tensor")
         mask = mask.contiguous()
+        if self.strict and mask.numel():
+            hi = int(mask.max())  # uint8 ids are >= 0 > -offset; valid ids are < len - offset
+            assert hi < self.lut.numel() - self.offset, \
+                "label id %d is not in the Cityscapes mapping" % hi
         out = torch.empty(mask.shape, dtype=torch.int64, device=mask.device)
         _lib.call("fscnn_remap_labels", _lib.ptr(mask), mask.numel(), _lib.ptr(self.lut),
                   self.lut.numel(), self.offset, -1, _lib.ptr(out), _lib.stream_ptr(mask.device))

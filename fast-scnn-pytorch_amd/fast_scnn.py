@@ -204,10 +204,12 @@ class _FastSCNNFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, model, *params):
-        outs, ws, seed, dt = model._run_forward(x, train=True)
+        outs, ws, seed, dt, xc = model._run_forward(x, train=True)
         ctx.model = model
         ctx.ws, ctx.seed, ctx.dt = ws, seed, dt
-        ctx.save_for_backward(x)
+        # the converted dense NCHW fp32/bf16 copy the forward read, not the caller's tensor: the
+        # conv0 weight gradient re-reads it as dense NCHW (channels_last / fp16 / expanded inputs)
+        ctx.save_for_backward(xc)
         return outs if len(outs) > 1 else outs[0]
 
     @staticmethod
@@ -224,10 +226,10 @@ class _FastSCNNLossFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, target, ignore_index, model, *params):
-        loss2, ws, seed, dt = model._run_forward_loss(x, target, ignore_index)
+        loss2, ws, seed, dt, xc = model._run_forward_loss(x, target, ignore_index)
         ctx.model = model
         ctx.ws, ctx.seed, ctx.dt, ctx.loss2 = ws, seed, dt, loss2
-        ctx.save_for_backward(x)
+        ctx.save_for_backward(xc)
         return loss2[0].clone()
 
     @staticmethod
@@ -385,7 +387,7 @@ class FastSCNN(nn.Module):
                       *rest)
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
-        return ((out, aux_out) if self.aux else (out,)), ws, seed, dt
+        return ((out, aux_out) if self.aux else (out,)), ws, seed, dt, x
 
     def predict(self, x, dtype=torch.int64):
         """``torch.argmax(self(x)[0], 1)`` of an eval-mode model (eval.py:43-45, demo.py:43-48)
@@ -455,6 +457,9 @@ class FastSCNN(nn.Module):
             x = x.float()
         x = x.contiguous()
         target = target.to(torch.int64).contiguous()
+        from . import loss as _loss
+        if _loss.CHECK_TARGETS:
+            _loss.check_targets(target, self.num_classes, ignore_index)
         plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), True)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         loss2 = torch.empty(2, dtype=torch.float32, device=x.device)
@@ -469,7 +474,7 @@ class FastSCNN(nn.Module):
                   _lib.c_float(self._momentum()), _lib.stream_ptr(x.device))
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
-        return loss2, ws, seed, dt
+        return loss2, ws, seed, dt, x
 
     def forward_loss(self, x, target, ignore_index=-1):
         """Fused train-step head: ``criterion(self(x)[0], target)`` of train.py:270-271 for

@@ -1,11 +1,10 @@
 """Cross-entropy criterion on the HIP path (the consumer of the logits in train.py:270-271).
 
 ``SoftmaxCrossEntropyOHEMLoss`` / ``MixSoftmaxCrossEntropyOHEMLoss`` mirror utils/loss.py:127-206
-(the default criterion of train.py:190-191): the label probabilities, the OHEM threshold (k-th
-smallest label probability by a radix select when fewer than ``min_kept`` pixels fall under
-``thresh``) and the class-weighted CE over the kept pixels all run on the device; only the two
-selection counters (and, rarely, the radix digits) come back to the host, where the reference
-copies the whole logits tensor.
+(train.py's ``--loss-type ce`` criterion, train.py:190-191): the label probabilities, the OHEM
+threshold (k-th smallest label probability by a radix select when fewer than ``min_kept`` pixels
+fall under ``thresh``) and the class-weighted CE over the kept pixels all run on the device with
+no host synchronisation, where the reference copies the whole logits tensor to numpy.
 
 ``MixSoftmaxCrossEntropyLoss`` mirrors utils/loss.py:103-124 (``nn.CrossEntropyLoss`` with
 ``ignore_index=-1`` over a tuple of predictions, aux terms weighted by ``aux_weight``).  One
@@ -13,12 +12,29 @@ fused kernel computes log-softmax + NLL per pixel with fixed-order partial sums;
 recomputes the softmax and writes ``(softmax - onehot) * grad / count`` in one pass.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
 import torch.nn as nn
 
 from . import _lib
+
+
+# Targets outside [0, C) other than ignore_index: nn.CrossEntropyLoss raises (IndexError on the
+# CPU, a device assert on CUDA).  The kernels here treat them as ignored, which keeps the step free
+# of host synchronisation; FSCNN_CHECK_TARGETS=1 (or CHECK_TARGETS = True) adds the reference's
+# failure as one device reduction + host read per loss call (a debugging aid: it syncs).
+CHECK_TARGETS = os.environ.get("FSCNN_CHECK_TARGETS", "0") == "1"
+
+
+def check_targets(target, num_classes, ignore_index):
+    """Raise IndexError like aten's nll_loss if a target is neither ignore_index nor in
+    [0, num_classes)."""
+    bad = (target != ignore_index) & ((target < 0) | (target >= num_classes))
+    if bool(bad.any()):
+        v = int(target[bad].flatten()[0])
+        raise IndexError("Target %d is out of bounds." % v)
 
 
 class _CrossEntropyFn(torch.autograd.Function):
@@ -31,6 +47,8 @@ class _CrossEntropyFn(torch.autograd.Function):
         logits = logits.contiguous()
         target = target.to(torch.int64).contiguous()
         N, C, H, W = logits.shape
+        if CHECK_TARGETS:
+            check_targets(target, C, ignore_index)
         HW = H * W
         parts = int(_lib.load().fscnn_ce_parts(N, HW))
         part = torch.empty(parts * 2, dtype=torch.float32, device=logits.device)
@@ -85,33 +103,25 @@ OHEM_CLASS_WEIGHT = (0.8373, 0.918, 0.866, 1.0345, 1.0166, 0.9969, 0.9754, 1.048
 
 def ohem_threshold(logits, target, ignore_index, thresh, min_kept):
     """(prob, threshold) of SoftmaxCrossEntropyOHEMLoss.forward (utils/loss.py:151-170): prob of
-    the label per pixel (device) and the float32 threshold a pixel's prob must not exceed to be
-    kept (inf: every labelled pixel)."""
+    the label per pixel and the float32 threshold a pixel's prob must not exceed to be kept (inf:
+    every labelled pixel), both on the device.  The counters and the k-th-smallest radix select
+    never leave the device, so the step has no host synchronisation (the reference's
+    ``print('Labels: ...')`` on the keep-all branch, which would need one, is not reproduced)."""
     N, C, H, W = logits.shape
     HW = H * W
     dev = logits.device
     st = _lib.stream_ptr(dev)
     prob = torch.empty(N * HW, dtype=torch.float32, device=dev)
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    work = torch.empty(2056, dtype=torch.int32, device=dev)
+    thr = torch.empty(1, dtype=torch.float32, device=dev)
     thr32 = float(np.float32(thresh))
     _lib.call("fscnn_ohem_prob", _lib.ptr(logits), _lib.dtype_code(logits.dtype), _lib.ptr(target),
               N, C, HW, int(ignore_index), ctypes.c_float(thr32), _lib.ptr(prob), _lib.ptr(counts),
               st)
-    num_valid, n_le = (int(v) for v in counts.tolist())
-    threshold = float("inf")
-    if min_kept >= num_valid:
-        print('Labels: {}'.format(num_valid))
-    elif num_valid > 0:
-        threshold = thr32
-        if min_kept > 0:
-            k = min(num_valid, min_kept)
-            if n_le < k:  # the k-th smallest label probability exceeds thresh
-                hist = torch.empty(2048, dtype=torch.int32, device=dev)
-                out = ctypes.c_float()
-                _lib.call("fscnn_kth_smallest", _lib.ptr(prob), prob.numel(), k, _lib.ptr(hist),
-                          ctypes.cast(ctypes.pointer(out), ctypes.c_void_p), st)
-                threshold = out.value
-    return prob, threshold
+    _lib.call("fscnn_ohem_threshold", _lib.ptr(prob), prob.numel(), _lib.ptr(counts),
+              int(min_kept), ctypes.c_float(thr32), _lib.ptr(work), _lib.ptr(thr), st)
+    return prob, thr
 
 
 class _OhemCrossEntropyFn(torch.autograd.Function):
@@ -125,6 +135,8 @@ class _OhemCrossEntropyFn(torch.autograd.Function):
         if weight is not None and weight.numel() != C:
             raise RuntimeError("weight tensor should be defined either for all %d classes or no "
                                "classes but got weight tensor of shape: [%d]" % (C, weight.numel()))
+        if CHECK_TARGETS:
+            check_targets(target, C, ignore_index)
         prob, thr = ohem_threshold(logits, target, ignore_index, thresh, min_kept)
         parts = int(_lib.load().fscnn_ce_parts(N, H * W))
         part = torch.empty(parts * 2, dtype=torch.float32, device=logits.device)
@@ -132,22 +144,22 @@ class _OhemCrossEntropyFn(torch.autograd.Function):
         wp = _lib.ptr(weight) if weight is not None else None
         _lib.call("fscnn_ce_weighted_fwd", _lib.ptr(logits), _lib.dtype_code(logits.dtype),
                   _lib.ptr(target), N, C, H * W, int(ignore_index), wp, _lib.ptr(prob),
-                  ctypes.c_float(thr), _lib.ptr(part), _lib.ptr(out2),
+                  _lib.ptr(thr), _lib.ptr(part), _lib.ptr(out2),
                   _lib.stream_ptr(logits.device))
-        ctx.save_for_backward(logits, target, prob, out2)
-        ctx.weight, ctx.thr, ctx.ignore_index = weight, thr, int(ignore_index)
+        ctx.save_for_backward(logits, target, prob, out2, thr)
+        ctx.weight, ctx.ignore_index = weight, int(ignore_index)
         return out2[0].clone()
 
     @staticmethod
     def backward(ctx, grad):
-        logits, target, prob, out2 = ctx.saved_tensors
+        logits, target, prob, out2, thr = ctx.saved_tensors
         N, C, H, W = logits.shape
         g = grad.to(torch.float32).reshape(1).contiguous()
         dlogits = torch.empty_like(logits)
         wp = _lib.ptr(ctx.weight) if ctx.weight is not None else None
         _lib.call("fscnn_ce_weighted_bwd", _lib.ptr(logits), _lib.dtype_code(logits.dtype),
                   _lib.ptr(target), N, C, H * W, ctx.ignore_index, wp, _lib.ptr(prob),
-                  ctypes.c_float(ctx.thr), _lib.ptr(g), _lib.ptr(out2), _lib.ptr(dlogits),
+                  _lib.ptr(thr), _lib.ptr(g), _lib.ptr(out2), _lib.ptr(dlogits),
                   _lib.stream_ptr(logits.device))
         return dlogits, None, None, None, None, None
 
@@ -174,7 +186,11 @@ class SoftmaxCrossEntropyOHEMLoss(nn.Module):
         assert predict.size(0) == target.size(0)
         assert predict.size(2) == target.size(1)
         assert predict.size(3) == target.size(2)
-        w = self.weight.to(predict.device) if self.weight is not None else None
+        w = None
+        if self.weight is not None:
+            if self.weight.device != predict.device:  # once: later steps do no H2D copy
+                self.weight = self.weight.to(predict.device)
+            w = self.weight
         return _OhemCrossEntropyFn.apply(predict, target, self.ignore_label, self.thresh,
                                          self.min_kept, w)
 

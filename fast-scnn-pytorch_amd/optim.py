@@ -2,7 +2,9 @@
 
 When every parameter of a group is a view of one flat arena and every ``.grad`` a view of one
 flat gradient buffer at the same offsets (what ``FastSCNN`` produces), the whole step is ONE
-kernel over the arena.  Otherwise it falls back to one launch per tensor (still the HIP kernel).
+kernel over the arena (one per contiguous run when frozen parameters or another group's tensors
+sit inside the group's span: those are never touched).  Otherwise it falls back to one launch
+per tensor (still the HIP kernel).
 State keeps torch's ``momentum_buffer`` key so ``state_dict()`` interoperates.
 """
 import torch
@@ -20,6 +22,27 @@ def _flat_base(tensors):
             return None
         offs.append(t.storage_offset())
     return st, offs
+
+
+def _runs(offs, numels, align=16):
+    """Split tensors (sorted by offset) into maximal runs that tile a flat span with nothing but
+    alignment padding between neighbours: [(lo, hi)] in elements.  A parameter of another group,
+    or one without a gradient (frozen), that lies between two tensors breaks the run, so the
+    fused launch never touches it (torch.optim.SGD skips grad-None parameters)."""
+    order = sorted(range(len(offs)), key=lambda i: offs[i])
+    runs = []
+    lo = hi = None
+    for i in order:
+        o, n = offs[i], numels[i]
+        if lo is not None and o == (hi + align - 1) // align * align:
+            hi = o + n
+            continue
+        if lo is not None:
+            runs.append((lo, hi))
+        lo, hi = o, o + n
+    if lo is not None:
+        runs.append((lo, hi))
+    return runs
 
 
 class FusedSGD(torch.optim.Optimizer):
@@ -45,10 +68,15 @@ class FusedSGD(torch.optim.Optimizer):
                   int(group["nesterov"]), int(first), _lib.c_float(group["grad_scale"]),
                   _lib.stream_ptr())
 
+    def _launch_runs(self, pbase, gbase, flat, lo, runs, group, first):
+        for a, b in runs:
+            self._launch(pbase + a * 4, gbase + a * 4, flat.data_ptr() + (a - lo) * 4, b - a,
+                         group, first)
+
     def _fast_step(self, gi, group):
         """Steady-state path: same parameter views as the cached fused plan and every grad a
         view of one base at the parameters' offsets (what FastSCNN's backward returns) -> one
-        launch without re-deriving the plan.  Returns False when the plan does not apply."""
+        launch per contiguous run without re-deriving the plan.  False when it does not apply."""
         aux = self._aux.get(gi)
         plan = aux.get("plan") if aux else None
         params = group["params"]
@@ -68,8 +96,8 @@ class FusedSGD(torch.optim.Optimizer):
             if g is None or g._base is not base or g.storage_offset() != o:
                 return False
         gptr = base.untyped_storage().data_ptr()
-        self._launch(plan["pbase"], gptr + plan["lo"] * 4, aux["flat"].data_ptr(),
-                     plan["len"], group, False)
+        self._launch_runs(plan["pbase"], gptr, aux["flat"], plan["lo"], plan["runs"], group,
+                          False)
         return True
 
     @torch.no_grad()
@@ -95,8 +123,8 @@ class FusedSGD(torch.optim.Optimizer):
                      all(p.grad.dtype == torch.float32 for p in params) and
                      not any(("momentum_buffer" in self.state[p]) != (not first) for p in params))
             if fused:
-                lo = min(pb[1])
-                hi = max(o + p.numel() for o, p in zip(pb[1], params))
+                runs = _runs(pb[1], [p.numel() for p in params])
+                lo, hi = runs[0][0], runs[-1][1]
                 flat = aux.get("flat")
                 if flat is None or flat.numel() != hi - lo or first:
                     flat = torch.zeros(hi - lo, dtype=torch.float32, device=params[0].device)
@@ -107,12 +135,14 @@ class FusedSGD(torch.optim.Optimizer):
                         if old is not None and not first:  # e.g. after load_state_dict
                             view.copy_(old)
                         self.state[p]["momentum_buffer"] = view
-                self._launch(pb[0] + lo * 4, gb[0] + lo * 4, flat.data_ptr(), hi - lo, group,
-                             first)
-                if len(params) == len(group["params"]) and pb[1] == gb[1]:
+                # pointer base of element 0 of the storage: offsets are in elements
+                self._launch_runs(pb[0], gb[0], flat, lo, runs, group, first)
+                if len(params) == len(group["params"]):
                     aux["plan"] = {"n": len(params), "p0": params[0].data_ptr(),
-                                            "p1": params[-1].data_ptr(), "offs": list(gb[1]),
-                                            "pbase": pb[0] + lo * 4, "lo": lo, "len": hi - lo}
+                                   "p1": params[-1].data_ptr(), "offs": list(gb[1]),
+                                   "pbase": pb[0], "lo": lo, "runs": runs}
+                else:
+                    aux.pop("plan", None)
             else:
                 for p in params:
                     st = self.state[p]

@@ -107,21 +107,29 @@ int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, 
  *   pixels); counts[0] += #labelled, counts[1] += #(prob <= thresh)  (device uint64 x 2).
  * fscnn_kth_smallest: k-th smallest of n non-negative floats (the OHEM threshold); writes the
  *   HOST float *out; hist is device scratch of 2048 uint32; synchronises the stream.
+ * fscnn_ohem_threshold: the whole threshold rule of utils/loss.py:159-170 on the device, from
+ *   fscnn_ohem_prob's counters: *thr (device float) = inf when min_kept >= #labelled, else thresh,
+ *   raised to the k-th smallest label probability (k = min(#labelled, min_kept)) when fewer than
+ *   k labelled pixels have prob <= thresh.  work: 2056 uint32 device scratch.  No host sync
+ *   (the reference's print of the label count on the first branch is not reproduced).
  * fscnn_ce_weighted_fwd / _bwd: nn.CrossEntropyLoss(weight, ignore_index) over the pixels with
- *   prob <= thr (prob null: all labelled pixels; weight null: unweighted); out2 = (weighted mean
- *   loss, sum of weights); part as for fscnn_ce_fwd. */
+ *   prob <= *thr (thr a device float; prob null: all labelled pixels; weight null: unweighted);
+ *   out2 = (weighted mean loss, sum of weights); part as for fscnn_ce_fwd. */
 int fscnn_ohem_prob(const void* logits, int dtype, const long long* target, int N, int C,
                     long long HW, long long ignore_index, float thresh, float* prob,
                     unsigned long long* counts, void* stream);
 int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* hist, float* out,
                        void* stream);
+int fscnn_ohem_threshold(const float* prob, long long n, const unsigned long long* counts,
+                         long long min_kept, float thresh, unsigned* work, float* thr, void* stream);
 int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
                           long long HW, long long ignore_index, const float* weight,
-                          const float* prob, float thr, float* part, float* out2, void* stream);
+                          const float* prob, const float* thr, float* part, float* out2,
+                          void* stream);
 int fscnn_ce_weighted_bwd(const void* logits, int dtype, const long long* target, int N, int C,
                           long long HW, long long ignore_index, const float* weight,
-                          const float* prob, float thr, const float* grad_out, const float* out2,
-                          void* dlogits, void* stream);
+                          const float* prob, const float* thr, const float* grad_out,
+                          const float* out2, void* dlogits, void* stream);
 
 /* Dice / Focal+Dice criteria (utils/loss.py:12-100; train.py:183-188, binary lane segmentation):
  * fscnn_dice_fwd writes stats[4] (device fp64) = (sum p1*t, sum p1, sum t, sum focal_i) with

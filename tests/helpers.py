@@ -61,6 +61,30 @@ def oracle_bf16_emulated(sd, x, nc):
         F.conv2d = oc
 
 
+def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True):
+    """One train step (forward, CE(ignore -1), backward) of the oracle: fp64 when ``emulate`` is
+    False, else fp32 with every conv input / weight / output rounded to bf16 — and, because
+    autograd casts gradients back through those roundings, every conv input / output gradient
+    rounded to bf16 as well (cfg3's storage precision).  Returns (loss, {name: fp64 grad})."""
+    import torch.nn.functional as F
+    from oracle import fast_scnn_ref as ref
+    dt = torch.float32 if emulate else torch.float64
+    s = {k: (v.detach().clone().to(dt).requires_grad_(True)
+             if v.is_floating_point() and "running" not in k else
+             (v.to(dt) if v.is_floating_point() else v)) for k, v in sd.items()}
+    oc = F.conv2d
+    if emulate:
+        q = lambda v: v.to(torch.bfloat16).float()  # noqa: E731
+        F.conv2d = lambda a, w, b=None, *r, **k: q(oc(q(a), q(w), b, *r, **k))
+    try:
+        outs, _, _ = ref.forward(s, x.to(dt), nc, training=True, dropout_seed=drop_seed)
+        loss = ref.cross_entropy(outs[0], t)
+        loss.backward()
+    finally:
+        F.conv2d = oc
+    return loss.item(), {k: v.grad.double() for k, v in s.items() if v.grad is not None}
+
+
 def argmax_agreement(logits, ref_argmax, ref_logits=None, margin_tol=1e-4):
     """Fraction of equal argmax pixels, and count of disagreements at margin > margin_tol.
 

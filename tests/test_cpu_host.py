@@ -123,3 +123,15 @@ def test_pretrained_checkpoint_with_module_prefix(tmp_path):
     m = get_fast_scnn("tusimple", pretrained=True, root=str(tmp_path), map_cpu=True)
     for (k, a), (_, b) in zip(m.state_dict().items(), src.state_dict().items()):
         assert torch.equal(a, b), k
+
+
+def test_fused_sgd_runs_split_at_foreign_tensors():
+    """FusedSGD launches one fused kernel per run of tensors that tile a span with nothing but
+    64-B alignment padding between them; a frozen / other-group tensor in between splits it."""
+    from fast_scnn_pytorch_amd.optim import _runs
+    # contiguous 16-float aligned tensors: [0,10) [16,40) [48,48+16)
+    assert _runs([0, 16, 48], [10, 24, 16]) == [(0, 64)]
+    # a foreign tensor occupies [16, 40): runs split around it
+    assert _runs([0, 48], [10, 16]) == [(0, 10), (48, 64)]
+    # order-independent
+    assert _runs([48, 0, 16], [16, 10, 24]) == [(0, 64)]

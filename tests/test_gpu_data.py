@@ -41,6 +41,10 @@ def test_cityscapes_label_map():
     mask = rng.integers(0, 34, (2, 77, 130)).astype(np.uint8)
     got = CityscapesLabelMap()(torch.from_numpy(mask).to(DEV)).cpu().numpy()
     np.testing.assert_array_equal(got, ref.cityscapes_class_to_index(mask))
-    # ids beyond the table (e.g. 255) map to -1 instead of the reference's assert
-    out = CityscapesLabelMap()(torch.tensor([255, 7, 33], dtype=torch.uint8, device=DEV)).cpu()
+    # ids beyond the table (e.g. 255) fail like the reference's assert (cityscapes.py:66-68) ...
+    bad = torch.tensor([255, 7, 33], dtype=torch.uint8, device=DEV)
+    with pytest.raises(AssertionError):
+        CityscapesLabelMap()(bad)
+    # ... or, with strict=False, are mapped to the ignore label
+    out = CityscapesLabelMap(strict=False)(bad).cpu()
     assert out.tolist() == [-1, 0, 18]
