@@ -6,7 +6,8 @@
 // want: lane l holds A[row l&15][8 consecutive k] (bf16 16x16x32) or A[row l&15][k] (fp32
 // 16x16x4), so every fragment is one ds_read_b128 from a [row][k] LDS image.
 //
-// gemm_nt   forward and dgrad (dgrad reads W^T through the "b_trans" staging path).  Tile
+// gemm_nt   forward and dgrad (the executor's dgrads read a per-step transposed weight copy;
+//           the "b_trans" staging path remains for the C ABI).  Tile
 //           128 rows x 16*NT cols, 4 waves of 32 rows, K staged in 128-B chunks (32 fp32 /
 //           64 bf16), register-staged double-buffered LDS.  Epilogue fuses conv bias, BN
 //           (scale/shift), residual add, ReLU and, in train mode, the per-channel BN statistics
@@ -504,16 +505,24 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   if (stream_on && !at && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
   const bool bs = a.bpart != nullptr;
   if (bs && (a.part || !a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
-             (a.bmode != 0 && a.bmode != 2) || a.ldbz % V || !a.b_trans)) {
+             (a.bmode != 0 && a.bmode != 2) || a.ldbz % V)) {
     set_error("gemm_nt: inconsistent fused BN-backward arguments");
     return E_INVALID;
   }
+  // b_trans (B read as [K][N]) stays for the C ABI's fscnn_pw_gemm; the executor's dgrads read
+  // the per-step transposed weights (non-transposed B)
+  if (bs && a.b_trans) {
+    set_error("gemm_nt: fused BN-backward partials need a non-transposed B");
+    return E_UNSUPPORTED;
+  }
   if (dtype == DT_F32) {
-    if (a.b_trans) { if (bs) launch_nt<float, true, true>(a, nt, st); else launch_nt<float, true, false>(a, nt, st); }
+    if (a.b_trans) launch_nt<float, true, false>(a, nt, st);
+    else if (bs) launch_nt<float, false, true>(a, nt, st);
     else if (at) launch_nt<float, false, false, true>(a, nt, st);
     else launch_nt<float, false, false>(a, nt, st);
   } else {
-    if (a.b_trans) { if (bs) launch_nt<bf16, true, true>(a, nt, st); else launch_nt<bf16, true, false>(a, nt, st); }
+    if (a.b_trans) launch_nt<bf16, true, false>(a, nt, st);
+    else if (bs) launch_nt<bf16, false, true>(a, nt, st);
     else if (at) launch_nt<bf16, false, false, true>(a, nt, st);
     else launch_nt<bf16, false, false>(a, nt, st);
   }

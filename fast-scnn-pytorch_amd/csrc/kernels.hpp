@@ -361,6 +361,22 @@ int col2im3(const Col2ImArgs& a, int dtype, hipStream_t st);
 int set_u64(uint64_t* p, uint64_t v, hipStream_t st);
 int sgd(const SgdArgs& a, hipStream_t st);
 int cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st);
+// per-step weight operands from the fp32 arena: plain casts and zero-padded transposes (misc.hip)
+constexpr int PREP_MAXJOBS = 48;
+struct PrepJob {
+  long long src;   // P offset (floats)
+  long long dst;   // element offset in the destination
+  int R, Cc;       // source [R][Cc] (row-major)
+  int ld;          // trans: destination [Cc][ld] with ld >= R (columns >= R zero)
+  int trans;
+};
+struct PrepTable {
+  int n = 0;
+  long long total = 0;
+  long long start[PREP_MAXJOBS + 1] = {};
+  PrepJob j[PREP_MAXJOBS];
+};
+int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t st);
 int fill_f32(float* x, long long n, float v, hipStream_t st);
 
 }  // namespace fscnn

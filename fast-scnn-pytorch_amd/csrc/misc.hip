@@ -687,6 +687,52 @@ int sgd(const SgdArgs& a, hipStream_t st) {
   return check_launch("sgd");
 }
 
+// ---- per-step weight preparation ---------------------------------------------------------------
+// One launch builds the compute-dtype weight operands of a training step from the fp32 master
+// arena P: the plain cast of the whole arena (bf16 steps) and, for every dense conv, W^T
+// [cin*k*k][ld] zero-padded past cout (the dgrad's non-transposed B operand).  Element i of the
+// flattened job table belongs to the job whose [start, start') range holds it.
+template <typename T>
+__global__ __launch_bounds__(256) void weights_prep_kernel(PrepTable t, const float* P, T* dst) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < t.total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = t.n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (t.start[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const PrepJob& J = t.j[lo];
+    const long long idx = i - t.start[lo];
+    float v;
+    if (J.trans) {
+      const long long n = idx / J.ld;
+      const int k = (int)(idx - n * J.ld);
+      v = k < J.R ? P[J.src + (long long)k * J.Cc + n] : 0.f;
+    } else {
+      v = P[J.src + idx];
+    }
+    st1(dst + J.dst + idx, v);
+  }
+}
+
+int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t st) {
+  if (t.n <= 0 || t.n > PREP_MAXJOBS) {
+    set_error("weights_prep: %d jobs", t.n);
+    return E_INVALID;
+  }
+  t.total = 0;
+  for (int k = 0; k < t.n; ++k) {
+    t.start[k] = t.total;
+    t.total += t.j[k].trans ? (long long)t.j[k].Cc * t.j[k].ld : t.j[k].R * (long long)t.j[k].Cc;
+  }
+  t.start[t.n] = t.total;
+  const unsigned grid = (unsigned)std::min<long long>((t.total + 255) / 256, 4096);
+  if (dtype == DT_F32) weights_prep_kernel<float><<<grid, 256, 0, st>>>(t, P, (float*)dst);
+  else weights_prep_kernel<bf16><<<grid, 256, 0, st>>>(t, P, (bf16*)dst);
+  return check_launch("weights_prep");
+}
+
 // ---- casts ------------------------------------------------------------------------------------
 __global__ void cast_f32_bf16_kernel(const float* x, uint16_t* y, long long n) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;

@@ -46,6 +46,11 @@ struct Builder {
     c.cin = cin; c.cout = cout; c.k = k; c.groups = groups;
     c.w = palloc(key + ".weight", {cout, cin / groups, k, k});
     if (bias) c.b = palloc(key + ".bias", {cout});
+    if (groups == 1 && !(k == 3 && cin == 3)) {  // dense convs with a dgrad (not conv0)
+      c.ldt = (cout + 7) / 8 * 8;
+      c.wt = n.wt_total;
+      n.wt_total += (long long)cin * k * k * c.ldt;
+    }
     return c;
   }
   BnL bn(const std::string& key, int C) {
@@ -205,6 +210,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     return E_INVALID;
   }
   if (dtype == DT_BF16) pl.pbf = A.get((size_t)net.p_total * 2);
+  if (train) pl.wt = A.get((size_t)net.wt_total * E);
   unit(pl.c0, M0, 32, conv0_parts(N, pl.H1, pl.W1));
   unit(pl.l1dw, M1, 32, dw_parts(N, pl.H2, pl.W2, 32, dtype, 2));
   unit(pl.l1pw, M1, 48, gemm_parts((int)M1));
@@ -446,6 +452,33 @@ struct Exec {
     if (dt == DT_F32) return r.P + c.w;
     return ws + pl.pbf + (size_t)c.w * 2;
   }
+  // W^T [cin*k*k][ldt] in the storage dtype (train plans): the dgrad's B operand
+  const void* WT(const ConvL& c) const { return ws + pl.wt + (size_t)c.wt * E; }
+
+  // bf16 cast of the arena and the transposed dgrad weights, one launch per step
+  int prep_weights() {
+    PrepTable t;
+    if (dt == DT_BF16) {
+      PrepJob& j = t.j[t.n++];
+      j.src = 0; j.dst = (long long)(pl.pbf / 2); j.R = 1; j.Cc = (int)net.p_total; j.ld = 0;
+      j.trans = 0;
+    }
+    if (train) {
+      auto add = [&](const ConvL& c) {
+        PrepJob& j = t.j[t.n++];
+        j.src = c.w; j.dst = (long long)(pl.wt / E) + c.wt; j.R = c.cout;
+        j.Cc = c.cin * c.k * c.k; j.ld = c.ldt; j.trans = 1;
+      };
+      add(net.ltd1.pw); add(net.ltd2.pw);
+      for (int i = 0; i < 9; ++i) { add(net.lb[i].e); add(net.lb[i].p); }
+      for (int i = 0; i < 4; ++i) add(net.ppm_c[i]);
+      add(net.ppm_o); add(net.ffm_low); add(net.ffm_high);
+      add(net.cls1.pw); add(net.cls2.pw); add(net.cls_out);
+      if (net.aux) { add(net.aux0); add(net.aux4); }
+    }
+    if (!t.n) return OK;
+    return weights_prep(t, r.P, ws, dt, r.st);
+  }
 
   // ---- deferred weight-gradient reductions ----------------------------------------------
   RedTable red;
@@ -594,7 +627,7 @@ struct Exec {
   // ================================ forward ================================================
   int forward() {
     const int N = pl.N;
-    if (dt == DT_BF16) TRY(cast_f32_bf16(r.P, W(pl.pbf), net.p_total, r.st));
+    TRY(prep_weights());
     if (!train) TRY(fold_all());
     // ---- LearningToDownsample ----
     {
@@ -847,7 +880,7 @@ struct Exec {
     if (!dX) return OK;
     GemmArgs g{};
     g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz; g.lda = lddz;
-    g.B = Wg(c); g.ldb = K; g.b_trans = 1;
+    g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
     if (bt.u && train) set_btarget(g, bt);

@@ -21,6 +21,10 @@ struct TSpec {
 struct ConvL {
   long long w = -1, b = -1;  // offsets into P (floats), -1 = none
   int cin = 0, cout = 0, k = 1, groups = 1;
+  // dense convs: W^T [cin*k*k][ldt] (zero-padded to ldt = cout rounded up to 8) in the compute
+  // dtype at element offset wt of the plan's transposed-weight arena (the dgrad's B operand)
+  long long wt = -1;
+  int ldt = 0;
 };
 struct BnL {
   long long g = -1, b = -1;   // P offsets
@@ -49,6 +53,7 @@ struct Net {
   ConvL cls_out;
   ConvL aux0; BnL aux1; ConvL aux4;
   long long stage_p_begin[4];  // P offset where each backward stage's parameters start
+  long long wt_total = 0;      // elements of the transposed-weight arena
 };
 
 int net_build(int num_classes, int aux, Net& net);
@@ -86,6 +91,7 @@ struct Plan {
   Unit aux0;
   size_t concat = 0, pooled = 0, feats_a = 0, feats_z = 0, up_low = 0, f = 0, drop = 0,
          logits = 0, aux_drop = 0, aux_logits = 0, aux_col = 0, pbf = 0, fold_tmp = 0;
+  size_t wt = 0;                    // transposed weights (train plans), net.wt_total elements
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   size_t fcnt = 0, bcnt = 0;        // BN fold+finalize arrival counters (ws / bws), 64 each
