@@ -97,9 +97,9 @@ __device__ __forceinline__ void bn_stats_fold_body(float* part, int P, int C, in
     s2 = (sh[2][0][cx] + sh[2][1][cx]) + (sh[2][2][cx] + sh[2][3][cx]);
     float* rec = part + (size_t)q * 3 * C;
     const double mean = n > 0.0 ? s1 / n : 0.0;
-    rec[c] = (float)mean;
-    rec[C + c] = n > 0.0 ? (float)fmax(s2 - n * mean * mean, 0.0) : 0.f;
-    rec[2 * C + c] = (float)n;
+    st_wt(rec + c, (float)mean);
+    st_wt(rec + C + c, n > 0.0 ? (float)fmax(s2 - n * mean * mean, 0.0) : 0.f);
+    st_wt(rec + 2 * C + c, (float)n);
   }
 }
 
@@ -120,7 +120,7 @@ __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q
     for (int u = 0; u < BN_Q / 4; ++u) {
       const int q = ty + 4 * u;
       const float* rec = a.part + (size_t)(q < Q ? q : 0) * 3 * a.C;  // clamped + select
-      const float t0 = rec[2 * a.C + c], t1 = rec[c], t2 = rec[a.C + c];
+      const float t0 = ld_wt(rec + 2 * a.C + c), t1 = ld_wt(rec + c), t2 = ld_wt(rec + a.C + c);
       rn[u] = q < Q ? t0 : 0.f;
       rm[u] = q < Q ? t1 : 0.f;
       r2[u] = q < Q ? t2 : 0.f;
@@ -156,30 +156,16 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int 
   bn_finalize_chunk(a, Q, blockIdx.x);
 }
 
-// Fold + finalize in ONE launch: every (chunk, q) workgroup folds its residue class into slot q,
-// publishes it (agent-scope release, then a per-chunk arrival counter); the last workgroup of a
-// chunk to arrive acquires and finishes that chunk, then re-arms the counter for the next BN.
-// (Placement-independent release/acquire protocol; counters zeroed once per executor call.)
-__device__ __forceinline__ bool bn_last_arrival(unsigned* ctr) {
-  __shared__ int s_last;
-  __threadfence();  // release: this thread's slot writes are visible device-wide
-  __syncthreads();
-  if (threadIdx.x == 0 && threadIdx.y == 0) {
-    const unsigned prev = atomicAdd(&ctr[blockIdx.x], 1u);
-    s_last = prev == gridDim.y - 1;
-  }
-  __syncthreads();
-  if (!s_last) return false;
-  __threadfence();  // acquire: other workgroups' slots
-  return true;
-}
-
+// Fold + finalize in ONE launch: every (chunk, q) workgroup folds its residue class into slot q
+// (write-through stores), then arrives on the chunk's counter (common.hpp arrive_last); the last
+// workgroup of a chunk reads the slots back with sc1 loads and finishes the chunk.  Counters are
+// zero on entry (zeroed by the step's weights_prep launch) and reset by the last arriver.
 __global__ __launch_bounds__(256) void bn_stats_fold_fin_kernel(BnFinalizeArgs a, int Q,
                                                                 unsigned* ctr) {
   bn_stats_fold_body(a.part, a.P, a.C, Q);
-  if (!bn_last_arrival(ctr)) return;
+  if (!arrive_last(ctr + blockIdx.x, gridDim.y)) return;
   bn_finalize_chunk(a, Q, blockIdx.x);
-  if (threadIdx.x == 0 && threadIdx.y == 0) ctr[blockIdx.x] = 0;
+  reset_counter(ctr + blockIdx.x);
 }
 
 int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
@@ -394,9 +380,10 @@ __device__ __forceinline__ void bn_bwd_fold_body(float* part, int P, int C, int 
   sh[1][ty][cx] = s2;
   __syncthreads();
   if (ty == 0 && c < C) {
-    part[(size_t)q * 2 * C + c] = (float)((sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx]));
-    part[(size_t)q * 2 * C + C + c] =
-        (float)((sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx]));
+    st_wt(part + (size_t)q * 2 * C + c,
+          (float)((sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx])));
+    st_wt(part + (size_t)q * 2 * C + C + c,
+          (float)((sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx])));
   }
 }
 
@@ -418,7 +405,7 @@ __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, 
     for (int u = 0; u < BN_Q / 4; ++u) {
       const int q = ty + 4 * u;
       const size_t qc = (size_t)(q < Q ? q : 0) * 2 * C;  // clamped + select
-      const float t1 = part[qc + c], t2 = part[qc + C + c];
+      const float t1 = ld_wt(part + qc + c), t2 = ld_wt(part + qc + C + c);
       a1[u] = q < Q ? t1 : 0.f;
       a2[u] = q < Q ? t2 : 0.f;
     }
@@ -451,9 +438,9 @@ __global__ __launch_bounds__(256) void bn_bwd_fold_fin_kernel(float* part, int P
                                                               float* dbeta, float* coef,
                                                               unsigned* ctr) {
   bn_bwd_fold_body(part, P, C, Q);
-  if (!bn_last_arrival(ctr)) return;
+  if (!arrive_last(ctr + blockIdx.x, gridDim.y)) return;
   bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
-  if (threadIdx.x == 0 && threadIdx.y == 0) ctr[blockIdx.x] = 0;
+  reset_counter(ctr + blockIdx.x);
 }
 
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,

@@ -98,6 +98,38 @@ __device__ __forceinline__ Welford wf_merge(Welford a, Welford b) {
   return r;
 }
 
+// ---- in-launch hand-off between workgroups (MI355X_MICROARCH.md, inter-workgroup visibility) ----
+// Per-XCD L2s are not coherent, and an agent-scope release fence writes back the XCD's whole L2
+// (microseconds).  Small hand-offs therefore go write-through instead: every byte a workgroup
+// publishes is stored with an `sc1` store (st_wt), each storing wave drains its stores
+// (s_waitcnt vmcnt(0)), the workgroup barriers, and ONE lane adds to an agent-scope counter; the
+// workgroup whose add returns expected-1 is the last arriver and reads the published bytes with
+// `sc1` loads (ld_wt), which bypass its L1.  No workgroup ever waits for another (no spin), and
+// the last arriver resets the counter for the next launch.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every thread of the workgroup calls this after its st_wt stores; true in the last arriver
+__device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned expected) {
+  __shared__ unsigned s_old;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0 && threadIdx.z == 0)
+    s_old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool last = s_old == expected - 1;
+  // no instruction: keeps the compiler from hoisting the last arriver's sc1 loads above the add
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return last;
+}
+__device__ __forceinline__ void reset_counter(unsigned* ctr) {
+  if (threadIdx.x == 0 && threadIdx.y == 0 && threadIdx.z == 0)
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- 4-element vectors (16 B fp32 / 8 B bf16) ------------------------------------------------
 __device__ __forceinline__ void st4v(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);

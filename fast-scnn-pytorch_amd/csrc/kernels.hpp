@@ -368,7 +368,7 @@ struct PrepJob {
   long long dst;   // element offset in the destination
   int R, Cc;       // source [R][Cc] (row-major)
   int ld;          // trans: destination [Cc][ld] with ld >= R (columns >= R zero)
-  int trans;
+  int trans;       // 0 cast, 1 transpose, 2 zero fill of R*Cc elements
 };
 struct PrepTable {
   int n = 0;

@@ -705,7 +705,9 @@ __global__ __launch_bounds__(256) void weights_prep_kernel(PrepTable t, const fl
     const PrepJob& J = t.j[lo];
     const long long idx = i - t.start[lo];
     float v;
-    if (J.trans) {
+    if (J.trans == 2) {
+      v = 0.f;  // zero fill (counters)
+    } else if (J.trans) {
       const long long n = idx / J.ld;
       const int k = (int)(idx - n * J.ld);
       v = k < J.R ? P[J.src + (long long)k * J.Cc + n] : 0.f;
@@ -724,7 +726,8 @@ int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t
   t.total = 0;
   for (int k = 0; k < t.n; ++k) {
     t.start[k] = t.total;
-    t.total += t.j[k].trans ? (long long)t.j[k].Cc * t.j[k].ld : t.j[k].R * (long long)t.j[k].Cc;
+    t.total += t.j[k].trans == 1 ? (long long)t.j[k].Cc * t.j[k].ld
+                                 : t.j[k].R * (long long)t.j[k].Cc;
   }
   t.start[t.n] = t.total;
   const unsigned grid = (unsigned)std::min<long long>((t.total + 255) / 256, 4096);

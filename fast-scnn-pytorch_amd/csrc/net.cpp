@@ -260,7 +260,10 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   }
   if (train) {
     pl.seed_slot = A.get(64);
-    pl.fcnt = A.get(64 * 4);
+    // arrival counters of the one-launch BN fold+finalize (forward and backward), zeroed by the
+    // step's weights_prep launch and left zero by every launch that uses them
+    pl.fcnt = A.get(2 * 64 * 4);
+    pl.bcnt = pl.fcnt + 64 * 4;
   }
   if (train && lazy_bn_enabled()) {
     // BN+ReLU outputs whose only consumers are GEMM / depthwise operands (and the wgrads reading
@@ -373,7 +376,6 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     add_slab((size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864);
     pl.slab_floats = slab;
     pl.slab = B.get(slab * 4);
-    pl.bcnt = B.get(64 * 4);
     // BN backward partials: max P*2*C
     size_t bnp = 0;
     auto bn_upd = [&](const Unit& u) {
@@ -475,6 +477,9 @@ struct Exec {
       add(net.ppm_o); add(net.ffm_low); add(net.ffm_high);
       add(net.cls1.pw); add(net.cls2.pw); add(net.cls_out);
       if (net.aux) { add(net.aux0); add(net.aux4); }
+      PrepJob& z = t.j[t.n++];  // BN arrival counters (fcnt, bcnt: 2 x 64 uint32)
+      z.src = 0; z.dst = (long long)(pl.fcnt / E); z.R = 1; z.Cc = (int)(2 * 64 * 4 / E); z.ld = 0;
+      z.trans = 2;
     }
     if (!t.n) return OK;
     return weights_prep(t, r.P, ws, dt, r.st);
@@ -540,8 +545,8 @@ struct Exec {
     f.momentum = r.momentum;
     f.bias = nullptr;
     f.mean = Wf(u.mean); f.invstd = Wf(u.invstd); f.scale = Wf(u.scale); f.shift = Wf(u.shift);
-    return bn_finalize(f, r.st);  // two launches: the single-launch arrival-counter variant
-                                  // (f.counters) measured slower (agent-scope release per block)
+    f.counters = (unsigned*)W(pl.fcnt);  // one launch (fold + last-arriver finalize)
+    return bn_finalize(f, r.st);
   }
   int apply(const Unit& u, bool relu, const void* res = nullptr, int ldres = 0) {
     BnApplyArgs a{};
@@ -843,7 +848,8 @@ struct Exec {
       P = bn_bwd_parts(u.M, u.C, dt, &rpb);
     }
     float* coef = (float*)Bw(pl.coef);
-    TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b), coef, r.st));
+    TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b), coef, r.st,
+                        (unsigned*)W(pl.bcnt)));
     b.coef = coef;
     b.dz = dz; b.lddz = u.C;
     return bn_bwd_apply(b, dt, r.st);
