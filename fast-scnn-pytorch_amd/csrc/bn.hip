@@ -37,38 +37,29 @@ int bn_fold(const FoldTable& t, hipStream_t st) {
 }
 
 // ---- train: merge partial records ------------------------------------------------------------
-// Two coalesced levels, in place (the records are consumed):
-//   fold : workgroup (64-channel chunk, q) — thread (c, ty) merges records p = q + Q*(ty + 4k),
-//          i.e. every record of residue class q mod Q, which no other thread touches; the 4 ty
-//          partials are merged in fixed order and the result overwrites record slot q.
+// Two coalesced levels, in place (the records are consumed), workgroups of 64 channels x BN_TY:
+//   fold : workgroup (64-channel chunk, q) — thread (c, ty) merges records p = q + Q*(ty + TY*k),
+//          i.e. every record of residue class q mod Q, which no other thread touches; the TY
+//          partials are summed in fixed order and the result overwrites record slot q.
 //   final: workgroup per 64-channel chunk merges slots 0..Q-1 (fixed order) and finishes.
-// Merges run in fp64 on (n, n*mean, M2 + n*mean^2) sums; lanes walk channels, so every record
-// row is read as contiguous 256-B segments.
+// Merges run in fp64 on (n, n*mean, M2 + n*mean^2) sums (no division until the end: an fp64
+// divide is a ~40-instruction sequence, and a chain of them dominated the finalize); lanes walk
+// channels, so every record row is read as contiguous 256-B segments.
 constexpr int BN_Q = 64;
-
-__device__ __forceinline__ void bn_sum3(double& n, double& s1, double& s2, const float* rec, int C,
-                                        int c) {
-  const double cn = rec[2 * C + c];
-  if (cn > 0.0) {
-    const double m = rec[c];
-    n += cn;
-    s1 += cn * m;
-    s2 += (double)rec[C + c] + cn * m * m;
-  }
-}
+constexpr int BN_TY = 16;
 
 __device__ __forceinline__ void bn_stats_fold_body(float* part, int P, int C, int Q) {
-  __shared__ double sh[3][4][64];
+  __shared__ double sh[3][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = blockIdx.x * 64 + cx, q = blockIdx.y;
   double n = 0.0, s1 = 0.0, s2 = 0.0;
   if (c < C) {
     // batches of 8 records: all loads issued before the fp64 accumulation (no serialized trips)
-    for (int p0 = q + Q * ty; p0 < P; p0 += 32 * Q) {
+    for (int p0 = q + Q * ty; p0 < P; p0 += 8 * BN_TY * Q) {
       float rm[8], r2[8], rn[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int p = p0 + 4 * Q * u;
+        const int p = p0 + BN_TY * Q * u;
         const float* rec = part + (size_t)(p < P ? p : p0) * 3 * C;  // clamped + select
         const float t0 = rec[c], t1 = rec[C + c], t2 = rec[2 * C + c];
         rm[u] = p < P ? t0 : 0.f;
@@ -77,13 +68,10 @@ __device__ __forceinline__ void bn_stats_fold_body(float* part, int P, int C, in
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const double cn = rn[u];
-        if (cn > 0.0) {
-          const double m = rm[u];
-          n += cn;
-          s1 += cn * m;
-          s2 += (double)r2[u] + cn * m * m;
-        }
+        const double cn = rn[u], m = rm[u];
+        n += cn;
+        s1 += cn * m;
+        s2 += (double)r2[u] + cn * m * m;
       }
     }
   }
@@ -92,9 +80,13 @@ __device__ __forceinline__ void bn_stats_fold_body(float* part, int P, int C, in
   sh[2][ty][cx] = s2;
   __syncthreads();
   if (ty == 0 && c < C) {
-    n = (sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx]);
-    s1 = (sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx]);
-    s2 = (sh[2][0][cx] + sh[2][1][cx]) + (sh[2][2][cx] + sh[2][3][cx]);
+    n = s1 = s2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < BN_TY; ++t) {
+      n += sh[0][t][cx];
+      s1 += sh[1][t][cx];
+      s2 += sh[2][t][cx];
+    }
     float* rec = part + (size_t)q * 3 * C;
     const double mean = n > 0.0 ? s1 / n : 0.0;
     st_wt(rec + c, (float)mean);
@@ -103,22 +95,22 @@ __device__ __forceinline__ void bn_stats_fold_body(float* part, int P, int C, in
   }
 }
 
-__global__ __launch_bounds__(256) void bn_stats_fold_kernel(float* part, int P, int C, int Q) {
+__global__ __launch_bounds__(1024) void bn_stats_fold_kernel(float* part, int P, int C, int Q) {
   bn_stats_fold_body(part, P, C, Q);
 }
 
-// merge the Q folded records of channels [64*chunk, 64*chunk + 64) and finish (block 64 x 4)
+// merge the Q <= BN_Q folded records of channels [64*chunk, 64*chunk + 64) and finish
 __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q, int chunk) {
-  __shared__ Welford sh[4][64];
+  __shared__ double sh[3][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = chunk * 64 + cx;
-  Welford w = {0.0, 0.0, 0.0};
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
   if (c < a.C) {
-    // Q <= BN_Q = 64: the thread's <= 16 records are loaded at once, then merged in order
-    float rm[BN_Q / 4], r2[BN_Q / 4], rn[BN_Q / 4];
+    constexpr int U = BN_Q / BN_TY;
+    float rm[U], r2[U], rn[U];
 #pragma unroll
-    for (int u = 0; u < BN_Q / 4; ++u) {
-      const int q = ty + 4 * u;
+    for (int u = 0; u < U; ++u) {
+      const int q = ty + BN_TY * u;
       const float* rec = a.part + (size_t)(q < Q ? q : 0) * 3 * a.C;  // clamped + select
       const float t0 = ld_wt(rec + 2 * a.C + c), t1 = ld_wt(rec + c), t2 = ld_wt(rec + a.C + c);
       rn[u] = q < Q ? t0 : 0.f;
@@ -126,17 +118,29 @@ __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q
       r2[u] = q < Q ? t2 : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < BN_Q / 4; ++u) {
-      Welford b = {(double)rn[u], (double)rm[u], (double)r2[u]};
-      if (b.n > 0) w = wf_merge(w, b);
+    for (int u = 0; u < U; ++u) {
+      const double cn = rn[u], m = rm[u];
+      n += cn;
+      s1 += cn * m;
+      s2 += (double)r2[u] + cn * m * m;
     }
   }
-  sh[ty][cx] = w;
+  sh[0][ty][cx] = n;
+  sh[1][ty][cx] = s1;
+  sh[2][ty][cx] = s2;
   __syncthreads();
   if (ty != 0 || c >= a.C) return;
-  w = wf_merge(wf_merge(sh[0][cx], sh[1][cx]), wf_merge(sh[2][cx], sh[3][cx]));
-  const double n = w.n, mean = w.mean + (a.bias ? (double)a.bias[c] : 0.0);
-  const double var = n > 0 ? w.m2 / n : 0.0;
+  n = s1 = s2 = 0.0;
+#pragma unroll
+  for (int t = 0; t < BN_TY; ++t) {
+    n += sh[0][t][cx];
+    s1 += sh[1][t][cx];
+    s2 += sh[2][t][cx];
+  }
+  const double mu = n > 0.0 ? s1 / n : 0.0;
+  const double m2 = n > 0.0 ? fmax(s2 - n * mu * mu, 0.0) : 0.0;
+  const double mean = mu + (a.bias ? (double)a.bias[c] : 0.0);
+  const double var = n > 0 ? m2 / n : 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)BN_EPS));
   const float scale = a.gamma[c] * invstd;
   a.mean[c] = (float)mean;
@@ -146,13 +150,13 @@ __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q
   if (a.rmean) {
     const float m = a.momentum;
     a.rmean[c] = (1.f - m) * a.rmean[c] + m * (float)mean;
-    const float unb = n > 1 ? (float)(w.m2 / (n - 1.0)) : (float)var;
+    const float unb = n > 1 ? (float)(m2 / (n - 1.0)) : (float)var;
     a.rvar[c] = (1.f - m) * a.rvar[c] + m * unb;
   }
   if (a.nbt && c == 0) a.nbt[0] += 1;
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
   bn_finalize_chunk(a, Q, blockIdx.x);
 }
 
@@ -160,8 +164,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BnFinalizeArgs a, int 
 // (write-through stores), then arrives on the chunk's counter (common.hpp arrive_last); the last
 // workgroup of a chunk reads the slots back with sc1 loads and finishes the chunk.  Counters are
 // zero on entry (zeroed by the step's weights_prep launch) and reset by the last arriver.
-__global__ __launch_bounds__(256) void bn_stats_fold_fin_kernel(BnFinalizeArgs a, int Q,
-                                                                unsigned* ctr) {
+__global__ __launch_bounds__(1024) void bn_stats_fold_fin_kernel(BnFinalizeArgs a, int Q,
+                                                                 unsigned* ctr) {
   bn_stats_fold_body(a.part, a.P, a.C, Q);
   if (!arrive_last(ctr + blockIdx.x, gridDim.y)) return;
   bn_finalize_chunk(a, Q, blockIdx.x);
@@ -175,15 +179,16 @@ int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
   }
   ProfScope ps(PK_BN_FIN, st, 12.0 * a.P * a.C, 0.0);
   int Q = a.P;
+  const dim3 blk(64, BN_TY);
   if (a.P > BN_Q) {
     Q = BN_Q;
     if (a.counters) {
-      bn_stats_fold_fin_kernel<<<dim3(cdiv(a.C, 64), Q), dim3(64, 4), 0, st>>>(a, Q, a.counters);
+      bn_stats_fold_fin_kernel<<<dim3(cdiv(a.C, 64), Q), blk, 0, st>>>(a, Q, a.counters);
       return check_launch("bn_finalize");
     }
-    bn_stats_fold_kernel<<<dim3(cdiv(a.C, 64), Q), dim3(64, 4), 0, st>>>(a.part, a.P, a.C, Q);
+    bn_stats_fold_kernel<<<dim3(cdiv(a.C, 64), Q), blk, 0, st>>>(a.part, a.P, a.C, Q);
   }
-  bn_finalize_kernel<<<cdiv(a.C, 64), dim3(64, 4), 0, st>>>(a, Q);
+  bn_finalize_kernel<<<cdiv(a.C, 64), blk, 0, st>>>(a, Q);
   return check_launch("bn_finalize");
 }
 
@@ -355,16 +360,16 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
 // merge [P][2][C] -> dgamma, dbeta (written to the gradient arena) and coef [2][C]; same
 // two-level in-place scheme as bn_finalize (fold residue classes mod Q, then fixed-order merge)
 __device__ __forceinline__ void bn_bwd_fold_body(float* part, int P, int C, int Q) {
-  __shared__ double sh[2][4][64];
+  __shared__ double sh[2][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = blockIdx.x * 64 + cx, q = blockIdx.y;
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
-    for (int p0 = q + Q * ty; p0 < P; p0 += 32 * Q) {
+    for (int p0 = q + Q * ty; p0 < P; p0 += 8 * BN_TY * Q) {
       float a1[8], a2[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int p = p0 + 4 * Q * u;
+        const int p = p0 + BN_TY * Q * u;
         const size_t pc = (size_t)(p < P ? p : p0) * 2 * C;  // clamped + select
         const float t1 = part[pc + c], t2 = part[pc + C + c];
         a1[u] = p < P ? t1 : 0.f;
@@ -380,37 +385,41 @@ __device__ __forceinline__ void bn_bwd_fold_body(float* part, int P, int C, int 
   sh[1][ty][cx] = s2;
   __syncthreads();
   if (ty == 0 && c < C) {
-    st_wt(part + (size_t)q * 2 * C + c,
-          (float)((sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx])));
-    st_wt(part + (size_t)q * 2 * C + C + c,
-          (float)((sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx])));
+    s1 = s2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < BN_TY; ++t) {
+      s1 += sh[0][t][cx];
+      s2 += sh[1][t][cx];
+    }
+    st_wt(part + (size_t)q * 2 * C + c, (float)s1);
+    st_wt(part + (size_t)q * 2 * C + C + c, (float)s2);
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_fold_kernel(float* part, int P, int C, int Q) {
+__global__ __launch_bounds__(1024) void bn_bwd_fold_kernel(float* part, int P, int C, int Q) {
   bn_bwd_fold_body(part, P, C, Q);
 }
 
 __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, int C, double count,
                                                       float* dgamma, float* dbeta, float* coef,
                                                       int chunk) {
-  __shared__ double shf[2][4][64];
-  double (*sh)[4][64] = shf;
+  __shared__ double sh[2][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = chunk * 64 + cx;
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
-    float a1[BN_Q / 4], a2[BN_Q / 4];
+    constexpr int U = BN_Q / BN_TY;
+    float a1[U], a2[U];
 #pragma unroll
-    for (int u = 0; u < BN_Q / 4; ++u) {
-      const int q = ty + 4 * u;
+    for (int u = 0; u < U; ++u) {
+      const int q = ty + BN_TY * u;
       const size_t qc = (size_t)(q < Q ? q : 0) * 2 * C;  // clamped + select
       const float t1 = ld_wt(part + qc + c), t2 = ld_wt(part + qc + C + c);
       a1[u] = q < Q ? t1 : 0.f;
       a2[u] = q < Q ? t2 : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < BN_Q / 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       s1 += a1[u];
       s2 += a2[u];
     }
@@ -419,24 +428,28 @@ __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, 
   sh[1][ty][cx] = s2;
   __syncthreads();
   if (ty != 0 || c >= C) return;
-  s1 = (sh[0][0][cx] + sh[0][1][cx]) + (sh[0][2][cx] + sh[0][3][cx]);
-  s2 = (sh[1][0][cx] + sh[1][1][cx]) + (sh[1][2][cx] + sh[1][3][cx]);
+  s1 = s2 = 0.0;
+#pragma unroll
+  for (int t = 0; t < BN_TY; ++t) {
+    s1 += sh[0][t][cx];
+    s2 += sh[1][t][cx];
+  }
   if (dbeta) dbeta[c] = (float)s1;
   if (dgamma) dgamma[c] = (float)s2;
   coef[c] = (float)(s1 / count);
   coef[C + c] = (float)(s2 / count);
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* part, int Q, int C,
-                                                              double count, float* dgamma,
-                                                              float* dbeta, float* coef) {
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* part, int Q, int C,
+                                                               double count, float* dgamma,
+                                                               float* dbeta, float* coef) {
   bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_fold_fin_kernel(float* part, int P, int C, int Q,
-                                                              double count, float* dgamma,
-                                                              float* dbeta, float* coef,
-                                                              unsigned* ctr) {
+__global__ __launch_bounds__(1024) void bn_bwd_fold_fin_kernel(float* part, int P, int C, int Q,
+                                                               double count, float* dgamma,
+                                                               float* dbeta, float* coef,
+                                                               unsigned* ctr) {
   bn_bwd_fold_body(part, P, C, Q);
   if (!arrive_last(ctr + blockIdx.x, gridDim.y)) return;
   bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
@@ -447,17 +460,17 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
                     float* coef, hipStream_t st, unsigned* counters) {
   ProfScope ps(PK_BN_FIN, st, 8.0 * P * C, 0.0);
   int Q = P;
+  const dim3 blk(64, BN_TY);
   if (P > BN_Q) {
     Q = BN_Q;
     if (counters) {
-      bn_bwd_fold_fin_kernel<<<dim3(cdiv(C, 64), Q), dim3(64, 4), 0, st>>>(part, P, C, Q, count,
-                                                                            dgamma, dbeta, coef,
-                                                                            counters);
+      bn_bwd_fold_fin_kernel<<<dim3(cdiv(C, 64), Q), blk, 0, st>>>(part, P, C, Q, count, dgamma,
+                                                                  dbeta, coef, counters);
       return check_launch("bn_bwd_finalize");
     }
-    bn_bwd_fold_kernel<<<dim3(cdiv(C, 64), Q), dim3(64, 4), 0, st>>>(part, P, C, Q);
+    bn_bwd_fold_kernel<<<dim3(cdiv(C, 64), Q), blk, 0, st>>>(part, P, C, Q);
   }
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), dim3(64, 4), 0, st>>>(part, Q, C, count, dgamma, dbeta, coef);
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), blk, 0, st>>>(part, Q, C, count, dgamma, dbeta, coef);
   return check_launch("bn_bwd_finalize");
 }
 
