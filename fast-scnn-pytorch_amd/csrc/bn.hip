@@ -402,7 +402,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_fold_kernel(float* part, int P, i
 
 __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, int C, double count,
                                                       float* dgamma, float* dbeta, float* coef,
-                                                      int chunk) {
+                                                      int chunk, const BnBwdTab& t) {
   __shared__ double sh[2][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = chunk * 64 + cx;
@@ -436,28 +436,42 @@ __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, 
   }
   if (dbeta) dbeta[c] = (float)s1;
   if (dgamma) dgamma[c] = (float)s2;
-  coef[c] = (float)(s1 / count);
-  coef[C + c] = (float)(s2 / count);
+  const float c0 = (float)(s1 / count), c1 = (float)(s2 / count);
+  coef[c] = c0;
+  coef[C + c] = c1;
+  if (t.tab) {  // dz = scale*(dy_r - c0 - (z - mean)*invstd*c1) = al*dy_r + gz*z + be
+    const float sc = t.scale[c];
+    const float gz = -sc * c1 * t.invstd[c];
+    float4 v;
+    v.x = sc;
+    v.y = -sc * c0 - gz * t.mean[c];
+    v.z = gz;
+    v.w = t.relu ? sc : 0.f;
+    float* e = t.tab + (size_t)c * BWDX_STRIDE;
+    *reinterpret_cast<float4*>(e) = v;
+    e[4] = t.relu ? t.shift[c] : 1.f;
+  }
 }
 
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* part, int Q, int C,
                                                                double count, float* dgamma,
-                                                               float* dbeta, float* coef) {
-  bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
+                                                               float* dbeta, float* coef,
+                                                               BnBwdTab t) {
+  bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x, t);
 }
 
 __global__ __launch_bounds__(1024) void bn_bwd_fold_fin_kernel(float* part, int P, int C, int Q,
                                                                double count, float* dgamma,
                                                                float* dbeta, float* coef,
-                                                               unsigned* ctr) {
+                                                               unsigned* ctr, BnBwdTab t) {
   bn_bwd_fold_body(part, P, C, Q);
   if (!arrive_last(ctr + blockIdx.x, gridDim.y)) return;
-  bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x);
+  bn_bwd_finalize_chunk(part, Q, C, count, dgamma, dbeta, coef, blockIdx.x, t);
   reset_counter(ctr + blockIdx.x);
 }
 
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
-                    float* coef, hipStream_t st, unsigned* counters) {
+                    float* coef, hipStream_t st, unsigned* counters, const BnBwdTab& tab) {
   ProfScope ps(PK_BN_FIN, st, 8.0 * P * C, 0.0);
   int Q = P;
   const dim3 blk(64, BN_TY);
@@ -465,12 +479,12 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
     Q = BN_Q;
     if (counters) {
       bn_bwd_fold_fin_kernel<<<dim3(cdiv(C, 64), Q), blk, 0, st>>>(part, P, C, Q, count, dgamma,
-                                                                  dbeta, coef, counters);
+                                                                  dbeta, coef, counters, tab);
       return check_launch("bn_bwd_finalize");
     }
     bn_bwd_fold_kernel<<<dim3(cdiv(C, 64), Q), blk, 0, st>>>(part, P, C, Q);
   }
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), blk, 0, st>>>(part, Q, C, count, dgamma, dbeta, coef);
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), blk, 0, st>>>(part, Q, C, count, dgamma, dbeta, coef, tab);
   return check_launch("bn_bwd_finalize");
 }
 

@@ -177,6 +177,55 @@ __device__ __forceinline__ uint4 bnrelu_vec(const uint4& t, const float* sc, con
   }
 }
 
+// ---- BatchNorm backward applied while a consumer stages its operand -------------------------
+// The dz of a train-mode BatchNorm(+ReLU) is never stored: its consumers (the conv's wgrad and
+// dgrad) read dy and the saved pre-BN tensor z and form, per element,
+//     dz = alpha * [fmaf(z, sc, sh) > 0] * dy + (gz * z + beta)       (rounded to the storage type)
+// i.e. scale * (dy_r - mean(dy_r) - xhat * mean(dy_r * xhat)) with the BN-backward sums folded into
+// per-channel (alpha, beta, gz) by bn_bwd_finalize; (sc, sh) is the forward BN affine that
+// recomputes the ReLU mask (no ReLU: sc = 0, sh = 1).  Table: tab[c * 8 + {0..4}].
+constexpr int BWDX_STRIDE = 8;
+template <typename T>
+__device__ __forceinline__ uint4 packv(const float (&o)[VecW<T>::V]) {
+  if constexpr (sizeof(T) == 4) {
+    return make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
+                      __float_as_uint(o[3]));
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(o[2 * i]) | ((uint32_t)f2bf(o[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+// per-lane coefficients of V consecutive channels c..c+V-1 (registers)
+template <typename T>
+struct BwdXCoef {
+  float al[VecW<T>::V], be[VecW<T>::V], gz[VecW<T>::V], sc[VecW<T>::V], sh[VecW<T>::V];
+  __device__ __forceinline__ void load(const float* tab, int c) {
+#pragma unroll
+    for (int j = 0; j < VecW<T>::V; ++j) {
+      const float4 t = *reinterpret_cast<const float4*>(tab + (size_t)(c + j) * BWDX_STRIDE);
+      al[j] = t.x; be[j] = t.y; gz[j] = t.z; sc[j] = t.w;
+      sh[j] = tab[(size_t)(c + j) * BWDX_STRIDE + 4];
+    }
+  }
+};
+template <typename T>
+__device__ __forceinline__ uint4 bwdx_apply(const uint4& dy, const uint4& z, const float* al,
+                                            const float* be, const float* gz, const float* sc,
+                                            const float* sh) {
+  constexpr int V = VecW<T>::V;
+  float g[V], zz[V], o[V];
+  unpackv(dy, g);
+  unpackv(z, zz);
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const float gv = fmaf(zz[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+    o[j] = fmaf(al[j], gv, fmaf(gz[j], zz[j], be[j]));
+  }
+  return packv<T>(o);
+}
+
 // ---- dropout keep-mask: a pure function of (seed, NCHW linear index) -------------------------
 // Must match oracle/fast_scnn_ref.py:dropout_mask bit for bit.
 // keep iff (hash >> 40) >= thr, thr = ceil(p * 2^24)  (<=> 24-bit uniform u >= p)

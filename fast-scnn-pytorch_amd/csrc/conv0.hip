@@ -458,7 +458,7 @@ __device__ __forceinline__ bf16 cw_cvt<bf16>(float v) {
   return r;
 }
 
-template <typename T, bool XB>
+template <typename T, bool XB, bool DX = false>
 __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
   constexpr int LD = CwOps<T>::LD;
   constexpr int V = VecW<T>::V;
@@ -475,6 +475,9 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
 
   // taps 27..31 of X^T stay zero
   for (int i = tid; i < 5 * LD; i += 256) sX[27 * LD + i] = cw_cvt<T>(0.f);
+  // DX: a thread's dZ vectors all cover channels (tid * V) & 31 .. +V
+  BwdXCoef<T> dxc;
+  if constexpr (DX) dxc.load(a.tab, (tid * V) & 31);
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -507,13 +510,24 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
     }
     // dZ tile: npx*32 contiguous elements as 16-B vectors (V elements), transposed into sD
     constexpr int NV = CW_TP * 32 / V / 256;  // vectors per thread (4 bf16 / 8 f32)
-    uint4 dv[NV];
+    uint4 dv[NV], zv[DX ? NV : 1];
     const T* dz = (const T*)a.dz + ((size_t)row * a.Wo + wo0) * 32;
+    const T* zb = (const T*)a.zz + ((size_t)row * a.Wo + wo0) * 32;
 #pragma unroll
     for (int q = 0; q < NV; ++q) {
       const int i = tid + 256 * q;
       const int p = (i * V) >> 5;
-      dv[q] = sel4(p < npx, *reinterpret_cast<const uint4*>(dz + (size_t)(p < npx ? i : 0) * V));
+      const size_t o = (size_t)(p < npx ? i : 0) * V;
+      dv[q] = *reinterpret_cast<const uint4*>(dz + o);
+      if constexpr (DX) zv[q] = *reinterpret_cast<const uint4*>(zb + o);
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int i = tid + 256 * q;
+      const int p = (i * V) >> 5;
+      uint4 v = dv[q];
+      if constexpr (DX) v = bwdx_apply<T>(v, zv[q], dxc.al, dxc.be, dxc.gz, dxc.sc, dxc.sh);
+      dv[q] = sel4(p < npx, v);
     }
     __syncthreads();  // previous tile's MFMA reads are done
 #pragma unroll
@@ -572,13 +586,24 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
   ProfScope ps(PK_CONV0_WGRAD, st,
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (dz_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
                2.0 * 27 * 32 * px);
-  if (dz_dtype == DT_F32) {
-    if (a.x_bf16) conv0_wgrad_kernel<float, true><<<P, 256, 0, st>>>(a);
-    else conv0_wgrad_kernel<float, false><<<P, 256, 0, st>>>(a);
-  } else {
-    if (a.x_bf16) conv0_wgrad_kernel<bf16, true><<<P, 256, 0, st>>>(a);
-    else conv0_wgrad_kernel<bf16, false><<<P, 256, 0, st>>>(a);
+  const bool dx = a.tab != nullptr;
+  if (dx && (!a.zz || (uintptr_t)a.zz % 16)) {
+    set_error("conv0_wgrad: BN-backward transform needs a 16-B aligned z");
+    return E_INVALID;
   }
+#define CW_LAUNCH(T)                                                                  \
+  do {                                                                                \
+    if (dx) {                                                                         \
+      if (a.x_bf16) conv0_wgrad_kernel<T, true, true><<<P, 256, 0, st>>>(a);          \
+      else conv0_wgrad_kernel<T, false, true><<<P, 256, 0, st>>>(a);                  \
+    } else {                                                                          \
+      if (a.x_bf16) conv0_wgrad_kernel<T, true><<<P, 256, 0, st>>>(a);                \
+      else conv0_wgrad_kernel<T, false><<<P, 256, 0, st>>>(a);                        \
+    }                                                                                 \
+  } while (0)
+  if (dz_dtype == DT_F32) CW_LAUNCH(float);
+  else CW_LAUNCH(bf16);
+#undef CW_LAUNCH
   return check_launch("conv0_wgrad");
 }
 

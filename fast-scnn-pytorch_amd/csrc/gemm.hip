@@ -87,7 +87,7 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
   }
 }
 
-template <typename T, int NT, bool BT, bool BS, bool AT>
+template <typename T, int NT, bool BT, bool BS, bool AT, bool AX = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int A_PER = G_BM * G_VROW / 256;            // 4
   constexpr int B_PER = (BN * G_VROW + 255) / 256;      // vectors per thread (non-trans)
   uint4 ra[A_PER];
+  uint4 raz[AX ? A_PER : 1];  // AX: the pre-BN z beside dy (A = bwdx_apply(dy, z))
   uint4 rb[BT ? 1 : B_PER];
   // transposed-B staging: KC rows (k) x BN cols (n) of scalars, held as raw 16-B vectors along n
   constexpr int BT_VEC = KC * BN / V;                   // vectors per chunk
@@ -142,6 +143,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       const bool ok = m < a.M && k < a.K;
       const size_t off = ok ? (size_t)m * a.lda + k : 0;
       ra[i] = *reinterpret_cast<const uint4*>(A + off);
+      if constexpr (AX)
+        raz[i] = *reinterpret_cast<const uint4*>((const T*)a.az + (ok ? (size_t)m * a.K + k : 0));
     }
     if (!BT) {
 #pragma unroll
@@ -168,8 +171,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // Tail masks (and the lazy BN+ReLU of A) are applied when a chunk is written to LDS, i.e. after
   // the current chunk's MFMAs: applying them right after issuing the loads made every wave wait
   // for the next chunk's loads before computing (no fetch/compute overlap).
+  // AX: a thread's A vectors all cover k = k0 + (tid & 7) * V, so one coefficient set per chunk
+  BwdXCoef<T> axc;
   auto store_chunk = [&](int buf, int c) {
     const int k0 = c * KC;
+    if constexpr (AX) {
+      const int kk = k0 + (tid & 7) * V;
+      axc.load(a.atab, kk < a.K ? kk : 0);
+    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int id = tid + 256 * i;
@@ -180,6 +189,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         const int kc = k < a.K ? k : 0;
         v = bnrelu_vec<T>(v, s_at + kc, s_at + G_ATMAX + kc);
       }
+      if constexpr (AX) v = bwdx_apply<T>(v, raz[i], axc.al, axc.be, axc.gz, axc.sc, axc.sh);
       sA(buf)[row * G_VPAD + vv] = zero_tail<T>(v, m < a.M ? a.K - k : 0);
     }
     if (!BT) {
@@ -450,7 +460,7 @@ static int pick_nt(int N) {
 
 int gemm_parts(int M) { return cdiv(M, G_BM); }
 
-template <typename T, bool BT, bool BS, bool AT = false>
+template <typename T, bool BT, bool BS, bool AT = false, bool AX = false>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   constexpr int V = VecW<T>::V;
@@ -462,11 +472,11 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS, AT><<<grid, 256, shm, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
   }
 }
 
@@ -492,7 +502,14 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     nt /= 2;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
-  ProfScope ps(PK_GEMM_NT, st, E * (M * K + M * N * (a.R ? 2 : 1) + N * K), 2.0 * M * N * K);
+  const bool ax = a.atab != nullptr;
+  ProfScope ps(PK_GEMM_NT, st,
+               E * (M * K * (ax ? 2 : 1) + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
+               2.0 * M * N * K);
+  if (ax && (!a.az || a.a_scale || a.b_trans || a.K % V)) {
+    set_error("gemm_nt: BN-backward A transform needs z, a plain B and K %% %d == 0", V);
+    return E_UNSUPPORTED;
+  }
   static const bool stream_on = [] {
     const char* e = getenv("FSCNN_GEMM_STREAM");
     return !(e && e[0] == '0');
@@ -502,7 +519,7 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     set_error("gemm_nt: lazy BN on A needs a plain GEMM with K <= %d, K %% %d == 0", G_ATMAX, V);
     return E_UNSUPPORTED;
   }
-  if (stream_on && !at && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
+  if (stream_on && !at && !ax && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
   const bool bs = a.bpart != nullptr;
   if (bs && (a.part || !a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
              (a.bmode != 0 && a.bmode != 2) || a.ldbz % V)) {
@@ -517,11 +534,15 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   }
   if (dtype == DT_F32) {
     if (a.b_trans) launch_nt<float, true, false>(a, nt, st);
+    else if (ax) { if (bs) launch_nt<float, false, true, false, true>(a, nt, st);
+                   else launch_nt<float, false, false, false, true>(a, nt, st); }
     else if (bs) launch_nt<float, false, true>(a, nt, st);
     else if (at) launch_nt<float, false, false, true>(a, nt, st);
     else launch_nt<float, false, false>(a, nt, st);
   } else {
     if (a.b_trans) launch_nt<bf16, true, false>(a, nt, st);
+    else if (ax) { if (bs) launch_nt<bf16, false, true, false, true>(a, nt, st);
+                   else launch_nt<bf16, false, false, false, true>(a, nt, st); }
     else if (bs) launch_nt<bf16, false, true>(a, nt, st);
     else if (at) launch_nt<bf16, false, false, true>(a, nt, st);
     else launch_nt<bf16, false, false>(a, nt, st);
@@ -570,7 +591,7 @@ struct TnOps<bf16> {
 // 16-B vectors along n / k (coalesced), written TRANSPOSED into LDS (sDt[n][m], sXt[k][m]) so each
 // MFMA operand is one or two 16-B ds_reads; the next chunk's global loads are issued before the
 // current chunk's MFMAs.
-template <typename T, bool XT>
+template <typename T, bool XT, bool DX = false>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int LD = TnOps<T>::LD;
@@ -601,6 +622,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int VPR = TN_T / V;                 // vectors per staged row
   constexpr int PAIRS = TN_MC / 2 * VPR / 256;  // row pairs per thread (1 bf16 / 2 f32)
   uint4 rd[PAIRS][2], rx[PAIRS][2];
+  uint4 rdz[DX ? PAIRS : 1][2];  // DX: the pre-BN z beside dy (D = bwdx_apply(dy, z))
   auto load = [&](int mc) {
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
@@ -612,6 +634,8 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
         const int m = mc + 2 * rp + h;
         const bool okd = m < me && n < a.N, okx = m < me && k < a.K;
         rd[i][h] = *reinterpret_cast<const uint4*>(D + (okd ? (size_t)m * a.ldd + n : 0));
+        if constexpr (DX)
+          rdz[i][h] = *reinterpret_cast<const uint4*>((const T*)a.dzz + (okd ? (size_t)m * a.N + n : 0));
         rx[i][h] = *reinterpret_cast<const uint4*>(X + (okx ? (size_t)m * a.ldx + k : 0));
       }
     }
@@ -629,6 +653,12 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
       xsh[j] = a.x_shift[k];
     }
   }
+  // DX: likewise a thread's D vectors all cover n = n0 + (tid % VPR) * V
+  BwdXCoef<T> dxc;
+  if constexpr (DX) {
+    const int nb = n0 + (tid % VPR) * V;
+    dxc.load(a.dtab, nb < a.N ? nb : 0);
+  }
   // tail masks (and XT) right before the LDS stores, not right after issuing the loads (which
   // would make the wave wait for them before the current chunk's MFMAs)
   auto mask = [&](int mc) {
@@ -640,7 +670,9 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const bool okm = mc + 2 * rp + h < me;
-        rd[i][h] = zero_tail<T>(rd[i][h], okm ? a.N - n : 0);
+        uint4 dv = rd[i][h];
+        if constexpr (DX) dv = bwdx_apply<T>(dv, rdz[i][h], dxc.al, dxc.be, dxc.gz, dxc.sc, dxc.sh);
+        rd[i][h] = zero_tail<T>(dv, okm ? a.N - n : 0);
         uint4 xv = rx[i][h];
         if constexpr (XT) xv = bnrelu_vec<T>(xv, xsc, xsh);
         rx[i][h] = zero_tail<T>(xv, okm ? a.K - k : 0);
@@ -722,19 +754,30 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
   dim3 grid(cdiv(a.N, TN_T) * cdiv(a.K, TN_T) * splits);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
-  ProfScope ps(PK_GEMM_TN, st, E * (M * N + M * K) + 4.0 * N * K, 2.0 * M * N * K);
+  const bool dx = a.dtab != nullptr;
+  ProfScope ps(PK_GEMM_TN, st, E * (M * N * (dx ? 2 : 1) + M * K) + 4.0 * N * K, 2.0 * M * N * K);
   const bool xt = a.x_scale != nullptr;
   if (xt && (!a.x_shift || a.K % V)) {
     set_error("gemm_tn: lazy BN on X needs x_shift and K %% %d == 0", V);
     return E_UNSUPPORTED;
   }
-  if (dtype == DT_F32) {
-    if (xt) gemm_tn_kernel<float, true><<<grid, 256, 0, st>>>(a);
-    else gemm_tn_kernel<float, false><<<grid, 256, 0, st>>>(a);
-  } else {
-    if (xt) gemm_tn_kernel<bf16, true><<<grid, 256, 0, st>>>(a);
-    else gemm_tn_kernel<bf16, false><<<grid, 256, 0, st>>>(a);
+  if (dx && (!a.dzz || a.N % V)) {
+    set_error("gemm_tn: BN-backward D transform needs z and N %% %d == 0", V);
+    return E_UNSUPPORTED;
   }
+#define TN_LAUNCH(T)                                                                  \
+  do {                                                                                \
+    if (dx) {                                                                         \
+      if (xt) gemm_tn_kernel<T, true, true><<<grid, 256, 0, st>>>(a);                 \
+      else gemm_tn_kernel<T, false, true><<<grid, 256, 0, st>>>(a);                   \
+    } else {                                                                          \
+      if (xt) gemm_tn_kernel<T, true><<<grid, 256, 0, st>>>(a);                       \
+      else gemm_tn_kernel<T, false><<<grid, 256, 0, st>>>(a);                         \
+    }                                                                                 \
+  } while (0)
+  if (dtype == DT_F32) TN_LAUNCH(float);
+  else TN_LAUNCH(bf16);
+#undef TN_LAUNCH
   return check_launch("gemm_tn");
 }
 

@@ -24,9 +24,11 @@ struct Conv0WgradArgs {
   const void* x;
   int x_bf16;
   int N, H, W, Ho, Wo;
-  const void* dz;  // NHWC [N,Ho,Wo,32]
+  const void* dz;  // NHWC [N,Ho,Wo,32] (dy when zz is set)
   float* slab;     // [parts][864]
   int rows_per_block;
+  const void* zz = nullptr;   // BN backward applied on load: z [N,Ho,Wo,32], tab [32][8]
+  const float* tab = nullptr;
 };
 
 struct DwArgs {
@@ -81,6 +83,10 @@ struct GemmArgs {
   // z, the GEMM consumes relu(fmaf(z, a_scale[k], a_shift[k]))) or null
   const float* a_scale = nullptr;
   const float* a_shift = nullptr;
+  // BN backward applied to the A operand (dgrad of a conv whose output BN's dz is never
+  // stored): A is dy, az the saved pre-BN tensor [M][K] (ld K), atab [K][BWDX_STRIDE]
+  const void* az = nullptr;
+  const float* atab = nullptr;
 };
 
 struct GemmTnArgs {
@@ -94,6 +100,8 @@ struct GemmTnArgs {
   int splits;
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of X (see GemmArgs::a_scale) or null
   const float* x_shift = nullptr;
+  const void* dzz = nullptr;       // BN backward applied to D (see GemmArgs::az): z [M][N], or null
+  const float* dtab = nullptr;
 };
 
 struct FoldEntry {
@@ -306,8 +314,19 @@ int bn_finalize(const BnFinalizeArgs& a, hipStream_t st);
 int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st);
 int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
 int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);
+// tab (optional): the per-channel operand-transform table of common.hpp bwdx_apply, built from
+// the forward BN (scale, shift, mean, invstd; relu: the ReLU mask is recomputed from z)
+struct BnBwdTab {
+  float* tab = nullptr;
+  const float* scale = nullptr;
+  const float* shift = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  int relu = 0;
+};
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
-                    float* coef, hipStream_t st, unsigned* counters = nullptr);
+                    float* coef, hipStream_t st, unsigned* counters = nullptr,
+                    const BnBwdTab& tab = BnBwdTab());
 int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st);
 
 int up_nhwc(const UpArgs& a, int dtype, hipStream_t st);

@@ -158,6 +158,17 @@ struct Alloc {
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
 
+// FSCNN_FUSE_BNBWD=0 materialises every BN-backward dz (bn_bwd_apply) for A/B measurements;
+// by default the dz of a BN whose consumers are pointwise GEMMs / conv0 is formed by those
+// consumers while they stage their operand (common.hpp bwdx_apply)
+bool fuse_bnbwd_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_FUSE_BNBWD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool lazy_bn_enabled() {  // FSCNN_LAZY_BN=0 materialises every BN output (A/B measurements)
   static const bool on = [] {
     const char* e = getenv("FSCNN_LAZY_BN");
@@ -392,6 +403,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     if (net.aux) bn_upd(pl.aux0);
     pl.bnpart = B.get(bnp * 4);
     pl.coef = B.get(2 * 1024 * 4);
+    pl.xtab = B.get((size_t)1024 * BWDX_STRIDE * 4);
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
     pl.bws_bytes = B.top;
     auto gu = [&](const std::string& n, const Unit& u) {
@@ -811,7 +823,7 @@ struct Exec {
     b.d_idx = (long long)pl.W3 * pl.Cp; b.d_in = pl.Cp;
     TRY(axis_bwd(b, DT_F32, dt, r.st));
     const bool drop = r.dropout_p > 0.f;
-    TRY(pw_bwd(net.aux4, u.M, Bw(pl.g_auxlog), pl.Cp, raw(drop ? W(pl.aux_drop) : W(u.a), 32),
+    TRY(pw_bwd(net.aux4, u.M, plain(Bw(pl.g_auxlog), pl.Cp), raw(drop ? W(pl.aux_drop) : W(u.a), 32),
                drop ? Bw(pl.g_aux) : Bw(u.ga), 32));
     if (drop) {
       DropArgs d{};
@@ -820,8 +832,9 @@ struct Exec {
       d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
       TRY(dropout(d, dt, r.st));
     }
-    TRY(bn_bwd_relu(u, net.aux1, Bw(u.ga), 32, dz));
-    TRY(pw_bwd(net.aux0, u.M, dz, 32, raw(W(pl.aux_col), 576), Bw(pl.aux_dcol), 576));
+    Dz d;
+    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, 0, dz, d));
+    TRY(pw_bwd(net.aux0, u.M, d, raw(W(pl.aux_col), 576), Bw(pl.aux_dcol), 576));
     Col2ImArgs cc{};
     cc.N = N; cc.H = pl.H3; cc.W = pl.W3; cc.C = 64; cc.dcol = Bw(pl.aux_dcol); cc.ldcol = 576;
     cc.dx = Bw(pl.l2pw.ga); cc.lddx = 64; cc.accumulate = 1;
@@ -832,6 +845,44 @@ struct Exec {
   // BN backward of unit u: dy = u.ga (ld u.ga_ld), mask = relu output (or null) → dz scratch
   // P_pre > 0: the producer of dy (a dgrad GEMM with bpart set) already wrote P_pre partial
   // records into bnpart, so the reduce pass is skipped.
+  // dz operand of a conv backward: a materialised tensor, or dy + z + transform table
+  struct Dz {
+    const void* p;
+    int ld;
+    const void* z;
+    const float* tab;
+  };
+  static Dz plain(const void* p, int ld) { return {p, ld, nullptr, nullptr}; }
+  // fused form (fuse_bnbwd_enabled): reduce + finalize only; the consumers apply it on load
+  int bn_bwd_x(const Unit& u, const BnL& bn, const void* dy, int lddy, bool relu_z, int P_pre,
+               void* dz, Dz& out) {
+    if (!fuse_bnbwd_enabled() || !train) {
+      TRY(bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, relu_z, P_pre));
+      out = plain(dz, u.C);
+      return OK;
+    }
+    BnBwdArgs b{};
+    b.M = u.M; b.C = u.C;
+    b.dy = dy; b.lddy = lddy; b.mask = nullptr; b.ldmask = 0;
+    b.z = W(u.z); b.ldz = u.C;
+    b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
+    b.shift = Wf(u.shift); b.relu_z = relu_z;
+    b.part = (float*)Bw(pl.bnpart);
+    int P = P_pre;
+    if (!P) {
+      TRY(bn_bwd_reduce(b, dt, r.st));
+      int rpb;
+      P = bn_bwd_parts(u.M, u.C, dt, &rpb);
+    }
+    BnBwdTab tb;
+    tb.tab = (float*)Bw(pl.xtab);
+    tb.scale = Wf(u.scale); tb.shift = Wf(u.shift); tb.mean = Wf(u.mean); tb.invstd = Wf(u.invstd);
+    tb.relu = relu_z;
+    TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b),
+                        (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb));
+    out = {dy, lddy, W(u.z), tb.tab};
+    return OK;
+  }
   int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
              int ldmask, void* dz, bool relu_z = false, int P_pre = 0) {
     BnBwdArgs b{};
@@ -866,12 +917,13 @@ struct Exec {
     g.bmode = t.mode;
   }
   // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
-  int pw_bwd(const ConvL& c, long long M, const void* dz, int lddz, In X, void* dX, int lddx,
+  int pw_bwd(const ConvL& c, long long M, Dz dz, In X, void* dX, int lddx,
              const void* R = nullptr, int ldr = 0, BTarget bt = BTarget()) {
     const int K = c.cin * c.k * c.k;
     GemmTnArgs t{};
-    t.M = (int)M; t.N = c.cout; t.K = K; t.D = dz; t.ldd = lddz; t.X = X.p; t.ldx = X.ld;
+    t.M = (int)M; t.N = c.cout; t.K = K; t.D = dz.p; t.ldd = dz.ld; t.X = X.p; t.ldx = X.ld;
     t.x_scale = X.sc; t.x_shift = X.sh;
+    t.dzz = dz.z; t.dtab = dz.tab;
     int S = gemm_tn_splits((int)M, c.cout, K);
     t.slab = slab_alloc((size_t)S * c.cout * K);
     if (!t.slab) return slab_oom();
@@ -880,12 +932,17 @@ struct Exec {
     if (c.b >= 0) {
       float* part = slab_alloc((size_t)colsum_parts((int)M) * c.cout);
       if (!part) return slab_oom();
-      TRY(colsum(dz, (int)M, c.cout, lddz, part, dt, r.st));
+      if (dz.tab) {
+        set_error("pw_bwd: bias gradient of a fused BN-backward operand");
+        return E_UNSUPPORTED;
+      }
+      TRY(colsum(dz.p, (int)M, c.cout, dz.ld, part, dt, r.st));
       TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
     if (!dX) return OK;
     GemmArgs g{};
-    g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz; g.lda = lddz;
+    g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
+    g.az = dz.z; g.atab = dz.tab;
     g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
@@ -933,7 +990,7 @@ struct Exec {
     }
     // classifier 1x1 (+bias), dropout
     const bool drop = r.dropout_p > 0.f;
-    TRY(pw_bwd(net.cls_out, pl.c2pw.M, Bw(pl.g_logits), pl.Cp,
+    TRY(pw_bwd(net.cls_out, pl.c2pw.M, plain(Bw(pl.g_logits), pl.Cp),
                raw(drop ? W(pl.drop) : W(pl.c2pw.a), 128), drop ? Bw(pl.g_drop) : Bw(pl.c2pw.ga),
                128));
     if (drop) {
@@ -944,13 +1001,14 @@ struct Exec {
       TRY(dropout(d, dt, r.st));
     }
     // classifier dsconv2, dsconv1
-    TRY(bn_bwd_relu(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, dz));
-    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, dz, 128, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
+    Dz d;
+    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, 0, dz, d));
+    TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw)));
     TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz, pre(pl.c2dw)));
     TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
-    TRY(bn_bwd_relu(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, dz));
-    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, dz, 128, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
+    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, 0, dz, d));
+    TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw)));
     TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz, pre(pl.c1dw)));
     TRY(dw_bwd(net.cls1.dw, 128, dz, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
@@ -958,13 +1016,13 @@ struct Exec {
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_low, pl.flow.M, dz, 128, act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
+    TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(dz, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw)));
     TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz, pre(pl.fdw)));
     TRY(dw_bwd(net.ffm_dw, 128, dz, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, dz, 128, raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
+    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(dz, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
     if (net.aux) TRY(backward_aux());
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     {
@@ -982,8 +1040,8 @@ struct Exec {
       TRY(axis_bwd(b, DT_F32, dt, r.st));
     }
     // PPM out 1x1 (256→128) over the concat buffer
-    TRY(bn_bwd_relu(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, dz));
-    TRY(pw_bwd(net.ppm_o, pl.po.M, dz, 128, raw(W(pl.concat), 256), Bw(pl.g_concat), 256));
+    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, 0, dz, d));
+    TRY(pw_bwd(net.ppm_o, pl.po.M, d, raw(W(pl.concat), 256), Bw(pl.g_concat), 256));
     {
       PpmUpArgs u{};
       u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = nullptr;
@@ -995,7 +1053,7 @@ struct Exec {
         size_t off = (size_t)base[i] * N;
         TRY(bn_bwd(u4, net.ppm_b[i], (char*)Bw(pl.g_feats) + off * 32 * E, 32,
                    (char*)W(pl.feats_a) + off * 32 * E, 32, dz));
-        TRY(pw_bwd(net.ppm_c[i], u4.M, dz, 32, raw((char*)W(pl.pooled) + off * 128 * E, 128),
+        TRY(pw_bwd(net.ppm_c[i], u4.M, plain(dz, 32), raw((char*)W(pl.pooled) + off * 128 * E, 128),
                    (char*)Bw(pl.g_pooled) + off * 128 * E, 128));
       }
       PoolBwdArgs p{};
@@ -1021,37 +1079,40 @@ struct Exec {
     const int e = l.cin * 6;
     // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
     // block: its dy is the PPM concat gradient)
-    TRY(bn_bwd(up, l.bp, Bw(up.ga), up.ga_ld, nullptr, 0, dz, false, i < 8 ? pre(up) : 0));
-    TRY(pw_bwd(l.p, up.M, dz, l.cout, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
+    Dz d;
+    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, i < 8 ? pre(up) : 0, dz, d));
+    TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
     TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz, pre(ud)));
     TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
-    TRY(bn_bwd_relu(ue, l.be, Bw(ue.ga), e, dz));
+    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, 0, dz, d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
     // the dgrad is the dy of the previous block's project BN (or of LTD.dsconv2's pw BN)
     const BTarget bt = i == 0 ? relu_target(pl.l2pw) : plain_target(pl.lbp[i - 1]);
-    return pw_bwd(l.e, ue.M, dz, e, raw(x, xld), gx, gxld, R, ldr, bt);
+    return pw_bwd(l.e, ue.M, d, raw(x, xld), gx, gxld, R, ldr, bt);
   }
 
   int backward_ltd() {
     void* dz = Bw(pl.dz);
-    TRY(bn_bwd_relu(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, dz, pre(pl.l2pw)));
-    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, dz, 64, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
+    Dz d;
+    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, pre(pl.l2pw), dz, d));
+    TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw)));
     TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz, pre(pl.l2dw)));
     TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
-    TRY(bn_bwd_relu(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, dz));
-    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, dz, 48, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
+    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, 0, dz, d));
+    TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw)));
     TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz, pre(pl.l1dw)));
     TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
-    TRY(bn_bwd_relu(pl.c0, net.b0, Bw(pl.c0.ga), 32, dz));
+    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, 0, dz, d));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
     const int S = conv0_wgrad_parts(pl.N, pl.H1, pl.W1, 8);
-    c.dz = dz; c.slab = slab_alloc((size_t)S * 864); c.rows_per_block = 8;
+    c.dz = d.p; c.zz = d.z; c.tab = d.tab; c.slab = slab_alloc((size_t)S * 864);
+    c.rows_per_block = 8;
     if (!c.slab) return slab_oom();
     TRY(conv0_wgrad(c, dt, r.st));
     return defer_reduce(c.slab, S, 864, G(net.c0.w), 0);
