@@ -584,7 +584,8 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
   }
   const double px = (double)a.N * a.Ho * a.Wo;
   ProfScope ps(PK_CONV0_WGRAD, st,
-               (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (dz_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
+               (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W +
+                   (dz_dtype == DT_F32 ? 4.0 : 2.0) * px * 32 * (a.tab ? 2 : 1),
                2.0 * 27 * 32 * px);
   const bool dx = a.tab != nullptr;
   if (dx && (!a.zz || (uintptr_t)a.zz % 16)) {

@@ -97,7 +97,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // run 4-5 workgroups per CU instead of 2.
   constexpr int CLD = BN + 4;                       // epilogue tile row stride (floats)
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  const int nbuf = (a.K + KC - 1) / KC > 1 ? 2 : 1;
+  // AT kernels keep one LDS buffer (extra barrier per chunk) so their 6 KB scale/shift table
+  // still leaves room for 3 workgroups per CU (double-buffered: 82 KB, 1 per CU)
+  const int nbuf = ((a.K + KC - 1) / KC > 1 && !AT) ? 2 : 1;
   uint4* sAbase = reinterpret_cast<uint4*>(s_dyn);
   uint4* sBbase = sAbase + nbuf * G_BM * G_VPAD;
   auto sA = [&](int b) { return sAbase + b * G_BM * G_VPAD; };
@@ -250,7 +252,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
     }
-    if (c + 1 < nchunks) store_chunk(buf ^ 1, c + 1);
+    if (c + 1 < nchunks) {
+      if (nbuf == 1) __syncthreads();  // every wave's MFMA reads of this chunk are done
+      store_chunk(nbuf == 2 ? buf ^ 1 : 0, c + 1);
+    }
     __syncthreads();
   }
 
@@ -465,7 +470,7 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   constexpr int V = VecW<T>::V;
   const int BN = 16 * nt;
-  const int nbuf = cdiv(a.K, G_VROW * V) > 1 ? 2 : 1;
+  const int nbuf = (cdiv(a.K, G_VROW * V) > 1 && !AT) ? 2 : 1;
   const size_t tiles = (size_t)nbuf * (G_BM + BN) * G_VPAD * 16;
   size_t ctile = (size_t)(G_BM / 2) * (BN + 4) * 4;
   const size_t red = (size_t)2 * 256 * V * 4;  // bwd-BN column reduction (2 x RG x BN floats)

@@ -158,15 +158,18 @@ struct Alloc {
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
 
-// FSCNN_FUSE_BNBWD=0 materialises every BN-backward dz (bn_bwd_apply) for A/B measurements;
-// by default the dz of a BN whose consumers are pointwise GEMMs / conv0 is formed by those
-// consumers while they stage their operand (common.hpp bwdx_apply)
-bool fuse_bnbwd_enabled() {
-  static const bool on = [] {
+// Where a BN-backward dz is formed: by bn_bwd_apply (materialised), or by its consumers while
+// they stage their operand (common.hpp bwdx_apply).  Measured on MI355X (cfg3): the streaming
+// conv0 wgrad absorbs the extra z read at ~5.4 TB/s (c0's 800 MB apply, 189 us, becomes +49 us),
+// while the latency-bound pointwise wgrad / dgrad GEMMs slow down by more than the apply they
+// replace (+0.89 ms vs -0.58 ms over 15 BNs).  FSCNN_FUSE_BNBWD: 0 never, 1 (default) conv0
+// only, 2 every pointwise consumer too.
+int fuse_bnbwd_mode() {
+  static const int m = [] {
     const char* e = getenv("FSCNN_FUSE_BNBWD");
-    return !(e && e[0] == '0');
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
   }();
-  return on;
+  return m;
 }
 
 bool lazy_bn_enabled() {  // FSCNN_LAZY_BN=0 materialises every BN output (A/B measurements)
@@ -854,9 +857,11 @@ struct Exec {
   };
   static Dz plain(const void* p, int ld) { return {p, ld, nullptr, nullptr}; }
   // fused form (fuse_bnbwd_enabled): reduce + finalize only; the consumers apply it on load
+  // streaming: the consumer is a bandwidth-efficient streaming kernel (conv0's wgrad)
   int bn_bwd_x(const Unit& u, const BnL& bn, const void* dy, int lddy, bool relu_z, int P_pre,
-               void* dz, Dz& out) {
-    if (!fuse_bnbwd_enabled() || !train) {
+               void* dz, Dz& out, bool streaming = false) {
+    const int mode = fuse_bnbwd_mode();
+    if (!train || mode == 0 || (mode == 1 && !streaming)) {
       TRY(bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, relu_z, P_pre));
       out = plain(dz, u.C);
       return OK;
@@ -1106,7 +1111,7 @@ struct Exec {
                relu_target(pl.l1dw)));
     TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz, pre(pl.l1dw)));
     TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
-    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, 0, dz, d));
+    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, 0, dz, d, true));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
