@@ -10,7 +10,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FSCNN_LIB", os.path.join(_HERE, "libfastscnn_hip.so"))
 
-DT_F32, DT_BF16 = 0, 1
+DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 
 c_int, c_ll, c_float, c_vp, c_char_p = (ctypes.c_int, ctypes.c_longlong, ctypes.c_float,
                                         ctypes.c_void_p, ctypes.c_char_p)
@@ -155,4 +155,6 @@ def dtype_code(dt):
         return DT_F32
     if dt == torch.bfloat16:
         return DT_BF16
-    raise RuntimeError("fastscnn: unsupported dtype %s (fp32 / bf16)" % (dt,))
+    if dt == torch.float16:
+        return DT_F16
+    raise RuntimeError("fastscnn: unsupported dtype %s (fp32 / bf16 / fp16)" % (dt,))

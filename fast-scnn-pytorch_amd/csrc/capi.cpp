@@ -459,7 +459,7 @@ int fscnn_conv0_fwd(const void* x, int x_dtype, int N, int H, int W, const float
                     const float* scale, const float* shift, int relu, void* y, int y_dtype,
                     void* stream) {
   Conv0Args a{};
-  a.x = x; a.x_bf16 = x_dtype == DT_BF16; a.N = N; a.H = H; a.W = W;
+  a.x = x; a.x_bf16 = x_dtype; a.N = N; a.H = H; a.W = W;
   a.Ho = (H - 3) / 2 + 1; a.Wo = (W - 3) / 2 + 1; a.w = w; a.scale = scale; a.shift = shift;
   a.relu = relu; a.y = y;
   return conv0_fwd(a, y_dtype, S(stream));
@@ -471,7 +471,7 @@ long long fscnn_conv0_wgrad_slab_floats(int N, int H, int W) {
 int fscnn_conv0_wgrad(const void* x, int x_dtype, int N, int H, int W, const void* dz,
                       int dz_dtype, float* slab, float* dw, void* stream) {
   Conv0WgradArgs a{};
-  a.x = x; a.x_bf16 = x_dtype == DT_BF16; a.N = N; a.H = H; a.W = W;
+  a.x = x; a.x_bf16 = x_dtype; a.N = N; a.H = H; a.W = W;
   a.Ho = (H - 3) / 2 + 1; a.Wo = (W - 3) / 2 + 1; a.dz = dz; a.slab = slab;
   int rc = conv0_wgrad(a, dz_dtype, S(stream));
   if (rc) return rc;

@@ -8,13 +8,16 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <stdint.h>
 
 #include <string>
 
 namespace fscnn {
 
-enum DType : int { DT_F32 = 0, DT_BF16 = 1 };
+// DT_F16 is an input / output dtype (fp16 images in, fp16 logits out: the reference's fp16
+// autocast I/O); the arithmetic of such a call runs in the plan's dtype (bf16 for cfg5).
+enum DType : int { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
 
 struct bf16 {
   uint16_t x;
@@ -25,6 +28,14 @@ typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
+// a 16-bit input element of dtype code XT (1 bf16, 2 fp16) as fp32
+template <int XT>
+__device__ __forceinline__ float in16(uint16_t h) { return XT == 2 ? h2f(h) : bf2f(h); }
+struct f16 {
+  uint16_t x;
+};
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __hip_bfloat16 h = __float2bfloat16(f);  // RNE; lowers to v_cvt_pk_bf16_f32 on gfx950
   return *reinterpret_cast<uint16_t*>(&h);
@@ -40,6 +51,8 @@ __device__ __forceinline__ float ld1(const float* p) { return *p; }
 __device__ __forceinline__ float ld1(const bf16* p) { return bf2f(p->x); }
 __device__ __forceinline__ void st1(float* p, float v) { *p = v; }
 __device__ __forceinline__ void st1(bf16* p, float v) { p->x = f2bf(v); }
+__device__ __forceinline__ float ld1(const f16* p) { return h2f(p->x); }
+__device__ __forceinline__ void st1(f16* p, float v) { p->x = f2h(v); }
 
 // ---- 16-byte vector load/store (p must be 16 B aligned) --------------------------------------
 __device__ __forceinline__ void ldv(const float* p, float (&v)[4]) {

@@ -49,11 +49,11 @@ struct C0Mma<false> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
   }
 };
 
-template <typename TO, bool XB>
+template <typename TO, int XB>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   constexpr bool BF = sizeof(TO) == 2;  // bf16 output => bf16 MFMA operands (compute dtype)
   using M = C0Mma<BF>;
-  using TI = typename std::conditional<XB, uint16_t, float>::type;
+  using TI = typename std::conditional<XB != 0, uint16_t, float>::type;
   constexpr int VI = 16 / sizeof(TI);               // input elements per 16-B vector
   constexpr int NVR = (C0_IN_W + VI - 1) / VI;      // vectors per staged input row
   constexpr int LPV = (9 * NVR + 255) / 256;        // vector loads per thread
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       const int ci = cr / 3, r = cr - ci * 3;
       const bool ok = i < NIN && c < ncol;
       const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c : 0;
-      const float t = XB ? bf2f((uint16_t)xin[off]) : (float)xin[off];
+      const float t = XB ? in16<XB>((uint16_t)xin[off]) : (float)xin[off];
       v[k] = ok ? t : 0.f;
     }
 #pragma unroll
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       for (int j = 0; j < VI; ++j) {
         const int c = v * VI + j;
         float f;
-        if (XB) f = bf2f((uint16_t)e[j]);
+        if (XB) f = in16<XB>((uint16_t)e[j]);
         else f = (float)e[j];
         if (c < C0_IN_W) s_in[cr * C0_IN_W + c] = f;
       }
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
           float f = 0.f;
           if (c < ncol) {
             const size_t o = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c;
-            f = XB ? bf2f((uint16_t)xin[o]) : (float)xin[o];
+            f = XB ? in16<XB>((uint16_t)xin[o]) : (float)xin[o];
           }
           if (c < C0_IN_W) s_in[cr * C0_IN_W + c] = f;
         }
@@ -393,11 +393,13 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (y_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
                2.0 * 27 * 32 * px);
   if (y_dtype == DT_F32) {
-    if (a.x_bf16) conv0_fwd_kernel<float, true><<<grid, 256, 0, st>>>(a);
-    else conv0_fwd_kernel<float, false><<<grid, 256, 0, st>>>(a);
+    if (a.x_bf16 == 2) conv0_fwd_kernel<float, 2><<<grid, 256, 0, st>>>(a);
+    else if (a.x_bf16) conv0_fwd_kernel<float, 1><<<grid, 256, 0, st>>>(a);
+    else conv0_fwd_kernel<float, 0><<<grid, 256, 0, st>>>(a);
   } else {
-    if (a.x_bf16) conv0_fwd_kernel<bf16, true><<<grid, 256, 0, st>>>(a);
-    else conv0_fwd_kernel<bf16, false><<<grid, 256, 0, st>>>(a);
+    if (a.x_bf16 == 2) conv0_fwd_kernel<bf16, 2><<<grid, 256, 0, st>>>(a);
+    else if (a.x_bf16) conv0_fwd_kernel<bf16, 1><<<grid, 256, 0, st>>>(a);
+    else conv0_fwd_kernel<bf16, 0><<<grid, 256, 0, st>>>(a);
   }
   return check_launch("conv0_fwd");
 }
@@ -458,7 +460,7 @@ __device__ __forceinline__ bf16 cw_cvt<bf16>(float v) {
   return r;
 }
 
-template <typename T, bool XB, bool DX = false>
+template <typename T, int XB, bool DX = false>
 __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
   constexpr int LD = CwOps<T>::LD;
   constexpr int V = VecW<T>::V;
@@ -503,7 +505,7 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const size_t o = ok ? base + kw : 0;  // clamped load + select (branch-free)
-          const float v = XB ? bf2f(((const uint16_t*)a.x)[o]) : ((const float*)a.x)[o];
+          const float v = XB ? in16<XB>(((const uint16_t*)a.x)[o]) : ((const float*)a.x)[o];
           xv[cr * 3 + kw] = ok ? v : 0.f;
         }
       }
@@ -595,11 +597,13 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
 #define CW_LAUNCH(T)                                                                  \
   do {                                                                                \
     if (dx) {                                                                         \
-      if (a.x_bf16) conv0_wgrad_kernel<T, true, true><<<P, 256, 0, st>>>(a);          \
-      else conv0_wgrad_kernel<T, false, true><<<P, 256, 0, st>>>(a);                  \
+      if (a.x_bf16 == 2) conv0_wgrad_kernel<T, 2, true><<<P, 256, 0, st>>>(a);        \
+      else if (a.x_bf16) conv0_wgrad_kernel<T, 1, true><<<P, 256, 0, st>>>(a);        \
+      else conv0_wgrad_kernel<T, 0, true><<<P, 256, 0, st>>>(a);                      \
     } else {                                                                          \
-      if (a.x_bf16) conv0_wgrad_kernel<T, true><<<P, 256, 0, st>>>(a);                \
-      else conv0_wgrad_kernel<T, false><<<P, 256, 0, st>>>(a);                        \
+      if (a.x_bf16 == 2) conv0_wgrad_kernel<T, 2><<<P, 256, 0, st>>>(a);              \
+      else if (a.x_bf16) conv0_wgrad_kernel<T, 1><<<P, 256, 0, st>>>(a);              \
+      else conv0_wgrad_kernel<T, 0><<<P, 256, 0, st>>>(a);                            \
     }                                                                                 \
   } while (0)
   if (dz_dtype == DT_F32) CW_LAUNCH(float);

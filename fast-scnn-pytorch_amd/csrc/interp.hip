@@ -104,6 +104,11 @@ __device__ __forceinline__ void st4_nt(bf16* p, const float (&v)[4]) {
                (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
   __builtin_nontemporal_store(t, (upr_u2*)p);
 }
+__device__ __forceinline__ void st4_nt(f16* p, const float (&v)[4]) {
+  upr_u2 t = {(uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16),
+               (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16)};
+  __builtin_nontemporal_store(t, (upr_u2*)p);
+}
 
 template <typename TI, typename TO, bool VEC>
 __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
@@ -196,6 +201,8 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
     else up_nchw_rows_kernel<TI, TO, false><<<g, UPR_THREADS, lds, st>>>(a);            \
   } while (0)
     if (in_dtype == DT_F32 && out_dtype == DT_F32) UPR_LAUNCH(float, float);
+    else if (in_dtype == DT_BF16 && out_dtype == DT_F16) UPR_LAUNCH(bf16, f16);
+    else if (in_dtype == DT_F32 && out_dtype == DT_F16) UPR_LAUNCH(float, f16);
     else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) UPR_LAUNCH(bf16, bf16);
     else if (in_dtype == DT_BF16 && out_dtype == DT_F32) UPR_LAUNCH(bf16, float);
     else UPR_LAUNCH(float, bf16);
@@ -203,6 +210,8 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
     return check_launch("up_nchw");
   }
   if (in_dtype == DT_F32 && out_dtype == DT_F32) up_nchw_kernel<float, float, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_BF16 && out_dtype == DT_F16) up_nchw_kernel<bf16, f16, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_F32 && out_dtype == DT_F16) up_nchw_kernel<float, f16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) up_nchw_kernel<bf16, bf16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_F32) up_nchw_kernel<bf16, float, 0><<<grid, 256, 0, st>>>(a);
   else up_nchw_kernel<float, bf16, 0><<<grid, 256, 0, st>>>(a);

@@ -10,7 +10,7 @@ constexpr int MAX_FOLD = 64;
 
 struct Conv0Args {
   const void* x;       // NCHW [N,3,H,W]
-  int x_bf16;
+  int x_bf16;          // input dtype code: 0 fp32, 1 bf16, 2 fp16
   int N, H, W, Ho, Wo;
   const float* w;      // [32][3][3][3]
   const float* scale;  // [32] or null (eval BN fold)
@@ -22,7 +22,7 @@ struct Conv0Args {
 
 struct Conv0WgradArgs {
   const void* x;
-  int x_bf16;
+  int x_bf16;          // input dtype code: 0 fp32, 1 bf16, 2 fp16
   int N, H, W, Ho, Wo;
   const void* dz;  // NHWC [N,Ho,Wo,32] (dy when zz is set)
   float* slab;     // [parts][864]

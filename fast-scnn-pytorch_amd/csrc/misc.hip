@@ -76,6 +76,7 @@ int ce_parts(int N, long long HW) { return (int)(((long long)N * HW + 255) / 256
 int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st) {
   int P = ce_parts(a.N, a.HW);
   if (dtype == DT_F32) ce_fwd_kernel<float><<<P, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) ce_fwd_kernel<f16><<<P, 256, 0, st>>>(a);
   else ce_fwd_kernel<bf16><<<P, 256, 0, st>>>(a);
   int rc = check_launch("ce_fwd");
   if (rc) return rc;
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(CeArgs a, const float* gout
 int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hipStream_t st) {
   int P = ce_parts(a.N, a.HW);
   if (dtype == DT_F32) ce_bwd_kernel<float><<<P, 256, 0, st>>>(a, gout, stats);
+  else if (dtype == DT_F16) ce_bwd_kernel<f16><<<P, 256, 0, st>>>(a, gout, stats);
   else ce_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, gout, stats);
   return check_launch("ce_bwd");
 }
@@ -155,6 +157,7 @@ int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* co
               hipStream_t st) {
   const int P = ce_parts(a.N, a.HW);
   if (dtype == DT_F32) ohem_prob_kernel<float><<<P, 256, 0, st>>>(a, thresh, prob, counts);
+  else if (dtype == DT_F16) ohem_prob_kernel<f16><<<P, 256, 0, st>>>(a, thresh, prob, counts);
   else ohem_prob_kernel<bf16><<<P, 256, 0, st>>>(a, thresh, prob, counts);
   return check_launch("ohem_prob");
 }
@@ -464,6 +467,7 @@ int dice_loss_fwd(const void* logits, int dtype, const long long* target, int N,
   DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};
   const int P = ce_parts(N, HW);
   if (dtype == DT_F32) dice_fwd_kernel<float><<<P, 256, 0, st>>>(a, part);
+  else if (dtype == DT_F16) dice_fwd_kernel<f16><<<P, 256, 0, st>>>(a, part);
   else dice_fwd_kernel<bf16><<<P, 256, 0, st>>>(a, part);
   if (int rc = check_launch("dice_fwd")) return rc;
   dice_finalize_kernel<<<1, 256, 0, st>>>(part, P, stats);
@@ -476,6 +480,7 @@ int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N,
   DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};
   const int P = ce_parts(N, HW);
   if (dtype == DT_F32) dice_bwd_kernel<float><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
+  else if (dtype == DT_F16) dice_bwd_kernel<f16><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
   else dice_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
   return check_launch("dice_bwd");
 }

@@ -652,7 +652,7 @@ struct Exec {
     // ---- LearningToDownsample ----
     {
       Conv0Args c{};
-      c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
+      c.x = r.x; c.x_bf16 = r.x_dtype;
       c.N = N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
       c.w = P(net.c0.w);
       if (!train) { c.scale = Wf(pl.c0.scale); c.shift = Wf(pl.c0.shift); c.relu = 1; c.y = W(pl.c0.a); }
@@ -1113,7 +1113,7 @@ struct Exec {
     TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
     TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, 0, dz, d, true));
     Conv0WgradArgs c{};
-    c.x = r.x; c.x_bf16 = r.x_dtype == DT_BF16;
+    c.x = r.x; c.x_bf16 = r.x_dtype;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
     const int S = conv0_wgrad_parts(pl.N, pl.H1, pl.W1, 8);
     c.dz = d.p; c.zz = d.z; c.tab = d.tab; c.slab = slab_alloc((size_t)S * 864);
@@ -1251,6 +1251,10 @@ int run_graphed(const Plan& pl, std::vector<uint64_t> key, hipStream_t st, F&& b
 }  // namespace
 
 int net_forward(const Plan& pl, const RunArgs& r) {
+  if (r.x_dtype < DT_F32 || r.x_dtype > DT_F16 || r.out_dtype < DT_F32 || r.out_dtype > DT_F16) {
+    set_error("fscnn_forward: input / output dtype codes must be 0 (fp32), 1 (bf16) or 2 (fp16)");
+    return E_INVALID;
+  }
   if (pl.net->aux && r.target) {
     set_error("forward_loss: the fused loss head covers the main output only (aux net)");
     return E_UNSUPPORTED;

@@ -326,15 +326,24 @@ class FastSCNN(nn.Module):
 
     # ---- execution ----------------------------------------------------------------------------
     def _compute_dtype(self, x):
-        if x.dtype == torch.bfloat16:
+        """Arithmetic of the call: fp32 for fp32 input; bf16 (16-bit activations, fp32 master
+        weights / statistics / accumulation) for bf16 input, for fp16 input (the cfg5 TuSimple
+        fp16 inference and test_specific_images.py's half-precision path: fp16 images in, fp16
+        logits out, bf16 arithmetic in between) and under autocast (train.py:269's AMP)."""
+        if x.dtype in (torch.bfloat16, torch.float16):
             return torch.bfloat16
         if torch.is_autocast_enabled("cuda"):
-            # AMP (train.py:269 uses fp16 autocast): this path computes in bf16 with fp32 master
-            # weights and fp32 statistics
             return torch.bfloat16
-        if x.dtype in (torch.float32, torch.float16):
+        if x.dtype == torch.float32:
             return torch.float32
         raise RuntimeError("FastSCNN: unsupported input dtype %s" % (x.dtype,))
+
+    @staticmethod
+    def _input(x):
+        """Dense NCHW copy of the input in a dtype conv0 reads (fp32 / bf16 / fp16)."""
+        if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            x = x.float()
+        return x.contiguous()
 
     def _momentum(self):
         m = self.learning_to_downsample.conv.conv[1].momentum
@@ -360,16 +369,15 @@ class FastSCNN(nn.Module):
         if H < 32 or W < 32:
             raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
         dt = self._compute_dtype(x)
-        if x.dtype not in (torch.float32, torch.bfloat16):
-            x = x.float()
-        x = x.contiguous()
+        x = self._input(x)
         if train and N < 2:
             # the reference raises from the PPM 1x1 BatchNorm in train mode (SURVEY §0 trap 5)
             raise ValueError("Expected more than 1 value per channel when training, got input "
                              "size torch.Size([1, 32, 1, 1])")
         plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), train)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
-        out = torch.empty((N, self.num_classes, H, W), dtype=dt, device=x.device)
+        out_dt = torch.float16 if x.dtype == torch.float16 else dt
+        out = torch.empty((N, self.num_classes, H, W), dtype=out_dt, device=x.device)
         aux_out = torch.empty_like(out) if self.aux else None
         p = self._dropout_p() if train else 0.0
         seed = 0
@@ -381,10 +389,10 @@ class FastSCNN(nn.Module):
                 _lib.stream_ptr(x.device))
         if self.aux:  # models/fast_scnn.py:42-45
             _lib.call("fscnn_forward_aux", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
-                      _lib.ptr(out), _lib.ptr(aux_out), *rest)
+                      _lib.ptr(out), _lib.ptr(aux_out), _lib.dtype_code(out_dt), *rest[1:])
         else:
             _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(out),
-                      *rest)
+                      _lib.dtype_code(out_dt), *rest[1:])
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return ((out, aux_out) if self.aux else (out,)), ws, seed, dt, x
@@ -407,9 +415,7 @@ class FastSCNN(nn.Module):
         if H < 32 or W < 32:
             raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
         dt = self._compute_dtype(x)
-        if x.dtype not in (torch.float32, torch.bfloat16):
-            x = x.float()
-        x = x.contiguous()
+        x = self._input(x)
         plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), False)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         labels = torch.empty((N, H, W), dtype=dtype, device=x.device)
@@ -453,9 +459,7 @@ class FastSCNN(nn.Module):
             raise ValueError("Expected more than 1 value per channel when training, got input "
                              "size torch.Size([1, 32, 1, 1])")
         dt = self._compute_dtype(x)
-        if x.dtype not in (torch.float32, torch.bfloat16):
-            x = x.float()
-        x = x.contiguous()
+        x = self._input(x)
         target = target.to(torch.int64).contiguous()
         from . import loss as _loss
         if _loss.CHECK_TARGETS:

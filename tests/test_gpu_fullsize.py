@@ -199,3 +199,30 @@ def test_bf16_train_step_within_emulated_bf16_budget():
     for k in ("classifier.conv.1.weight", "classifier.conv.1.bias"):
         u, v = named[k].grad.detach().double().cpu().flatten(), g64[k].flatten()
         assert cos(u, v) > 0.99, k
+
+
+def test_cfg5_fp16_io_inference_within_fp16_contract():
+    """cfg5 (TuSimple 2-class, 480 x 640, fp16 inference; BASELINE.json configs[4]) with fp16
+    images in and fp16 logits out (bf16 arithmetic in between), against the
+    reference golden under SURVEY Appendix B's half-precision contract: |logit delta| <= 5e-3
+    (sampled golden logits and the fp32 oracle), argmax agreement >= 99.9 %; the fused
+    upsample+argmax path gives the labels of the returned fp16 logits."""
+    g = load_golden("cfg5_c2_480x640")
+    m = _model(g, 2)
+    x = golden_input(g)
+    with torch.no_grad():
+        out = m(x.to(DEV).half())[0]
+        lab = m.predict(x.to(DEV).half(), dtype=torch.uint8)
+    assert out.dtype == torch.float16
+    o = out.float().cpu()
+    idx = g["out0.sample_idx"]
+    d = np.abs(o.numpy().ravel()[idx] - g["out0.sample_val"]).max()
+    o64 = _oracle64(g, 2)
+    dmax = (o.double() - o64).abs().max().item()
+    agree = (o.argmax(1).to(torch.uint8).numpy() == g["out0.argmax"]).mean()
+    print("cfg5 fp16 I/O: max|d| sampled %.2e, full %.2e, argmax agreement %.6f" % (d, dmax, agree))
+    assert d <= 5e-3 and dmax <= 5e-3
+    assert agree >= 0.999
+    # labels from the fused kernel: argmax of the bf16 logits before the fp16 output rounding
+    la = (lab.cpu().numpy() == g["out0.argmax"]).mean()
+    assert la >= 0.999
