@@ -358,12 +358,12 @@ def main():
             m5.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
                                 arch.portable_state_dict(2, seed=0).items()})
             m5 = m5.to(dev).eval()
-            # fp16 images in, fp16 logits out, bf16 arithmetic
+            # fp16 images in, fp16 MFMA arithmetic (fp32 accumulation), fp16 logits out
             x5 = torch.from_numpy(portable_init.input_tensor(1, (32, 3, 480, 640))).to(dev).half()
             f5 = fwd_rate(m5, x5, 10)
             result["forward_cfg5"] = {"value": round(32 / f5, 2), "unit": "images/s",
                                       "ms_per_batch": round(1e3 * f5, 3),
-                                      "dtype": "fp16 I/O, bf16 arithmetic",
+                                      "dtype": "fp16",
                                       "config": "cfg5 eval 32x3x480x640, 2 classes"}
             del m5, x5
         model.train()

@@ -10,6 +10,7 @@
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include <string>
 
@@ -22,6 +23,10 @@ enum DType : int { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
 struct bf16 {
   uint16_t x;
 };
+struct f16 {  // IEEE half storage (inference plans of dtype DT_F16; fp16 I/O)
+  uint16_t x;
+};
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
@@ -33,9 +38,6 @@ __device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__flo
 // a 16-bit input element of dtype code XT (1 bf16, 2 fp16) as fp32
 template <int XT>
 __device__ __forceinline__ float in16(uint16_t h) { return XT == 2 ? h2f(h) : bf2f(h); }
-struct f16 {
-  uint16_t x;
-};
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __hip_bfloat16 h = __float2bfloat16(f);  // RNE; lowers to v_cvt_pk_bf16_f32 on gfx950
   return *reinterpret_cast<uint16_t*>(&h);
@@ -45,6 +47,21 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 template <typename T> struct VecW;
 template <> struct VecW<float> { static constexpr int V = 4; };
 template <> struct VecW<bf16> { static constexpr int V = 8; };
+template <> struct VecW<f16> { static constexpr int V = 8; };
+
+// a 16-bit storage element <-> fp32 (bf16 or fp16), and fp32 rounded the way T stores it
+template <typename T> __device__ __forceinline__ float s16_to(uint16_t h) {
+  if constexpr (std::is_same<T, f16>::value) return h2f(h);
+  else return bf2f(h);
+}
+template <typename T> __device__ __forceinline__ uint16_t s16_from(float f) {
+  if constexpr (std::is_same<T, f16>::value) return f2h(f);
+  else return f2bf(f);
+}
+template <typename T> __device__ __forceinline__ float round_as(float v) {
+  if constexpr (sizeof(T) == 4) return v;
+  else return s16_to<T>(s16_from<T>(v));
+}
 
 // ---- scalar load/store in storage type -------------------------------------------------------
 __device__ __forceinline__ float ld1(const float* p) { return *p; }
@@ -68,6 +85,21 @@ __device__ __forceinline__ void ldv(const bf16* p, float (&v)[8]) {
     v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
   }
 }
+__device__ __forceinline__ void ldv(const f16* p, float (&v)[8]) {
+  uint4 t = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = h2f((uint16_t)(w[i] & 0xFFFFu));
+    v[2 * i + 1] = h2f((uint16_t)(w[i] >> 16));
+  }
+}
+__device__ __forceinline__ void stv(f16* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2h(v[2 * i]) | ((uint32_t)f2h(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
 __device__ __forceinline__ void stv(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
@@ -89,6 +121,20 @@ __device__ __forceinline__ void unpackv(const uint4& t, float (&v)[8]) {
   for (int i = 0; i < 4; ++i) {
     v[2 * i] = __uint_as_float(w[i] << 16);
     v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+// raw 16-B vector of storage type T -> floats (bf16 / fp16 / fp32)
+template <typename T>
+__device__ __forceinline__ void unpack(const uint4& t, float (&v)[VecW<T>::V]) {
+  if constexpr (sizeof(T) == 4) {
+    unpackv(t, v);
+  } else {
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = s16_to<T>((uint16_t)(w[i] & 0xFFFFu));
+      v[2 * i + 1] = s16_to<T>((uint16_t)(w[i] >> 16));
+    }
   }
 }
 __device__ __forceinline__ uint4 sel4(bool ok, const uint4& t) {
@@ -157,6 +203,17 @@ __device__ __forceinline__ void ld4v(const float* p, float (&v)[4]) {
   const float4 t = *reinterpret_cast<const float4*>(p);
   v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
 }
+__device__ __forceinline__ void st4v(f16* p, const float (&v)[4]) {
+  uint2 t;
+  t.x = (uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16);
+  t.y = (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
+__device__ __forceinline__ void ld4v(const f16* p, float (&v)[4]) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p);
+  v[0] = h2f((uint16_t)(t.x & 0xFFFFu)); v[1] = h2f((uint16_t)(t.x >> 16));
+  v[2] = h2f((uint16_t)(t.y & 0xFFFFu)); v[3] = h2f((uint16_t)(t.y >> 16));
+}
 __device__ __forceinline__ void ld4v(const bf16* p, float (&v)[4]) {
   const uint2 t = *reinterpret_cast<const uint2*>(p);
   v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xFFFF0000u);
@@ -206,7 +263,8 @@ __device__ __forceinline__ uint4 packv(const float (&o)[VecW<T>::V]) {
   } else {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(o[2 * i]) | ((uint32_t)f2bf(o[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i)
+      w[i] = (uint32_t)s16_from<T>(o[2 * i]) | ((uint32_t)s16_from<T>(o[2 * i + 1]) << 16);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 }

@@ -19,10 +19,23 @@ constexpr int C0_OSTR = 36;              // LDS floats per staged output pixel (
 
 // MFMA helpers for the im2col GEMM out[px][co] = sum_k patch[px][k] * W[co][k], K = 27 -> 32:
 // lane (li, lq) supplies k = 8*lq .. 8*lq+7 for its row (pixel li / channel li).
-template <bool BF>
+template <int BF>
 struct C0Mma;
 template <>
-struct C0Mma<true> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x 16 co
+struct C0Mma<2> {  // fp16 operands (inference plans of dtype fp16): v_mfma_f32_16x16x32_f16
+  using Frag = h16x8;
+  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
+    Frag f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (_Float16)v[e];
+    return f;
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc, 0, 0, 0);
+  }
+};
+template <>
+struct C0Mma<1> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x 16 co
   using Frag = i16x8;
   static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
     Frag f;
@@ -35,7 +48,7 @@ struct C0Mma<true> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x
   }
 };
 template <>
-struct C0Mma<false> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
+struct C0Mma<0> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
   struct Frag { float v[8]; };
   static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
     Frag f;
@@ -51,7 +64,8 @@ struct C0Mma<false> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
 
 template <typename TO, int XB>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
-  constexpr bool BF = sizeof(TO) == 2;  // bf16 output => bf16 MFMA operands (compute dtype)
+  // 16-bit output => MFMA operands in that dtype (the plan's compute dtype)
+  constexpr int BF = sizeof(TO) == 4 ? 0 : (std::is_same<TO, f16>::value ? 2 : 1);
   using M = C0Mma<BF>;
   using TI = typename std::conditional<XB != 0, uint16_t, float>::type;
   constexpr int VI = 16 / sizeof(TI);               // input elements per 16-B vector
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         TO t;
-        if constexpr (BF) t.x = f2bf(acc[gi][jt][r]);
+        if constexpr (BF) t.x = s16_from<TO>(acc[gi][jt][r]);
         else t = acc[gi][jt][r];
         s_out[(wave * 64 + gi * 16 + 4 * lq + r) * OST + 16 * jt + li] = t;
       }
@@ -396,6 +410,14 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
     if (a.x_bf16 == 2) conv0_fwd_kernel<float, 2><<<grid, 256, 0, st>>>(a);
     else if (a.x_bf16) conv0_fwd_kernel<float, 1><<<grid, 256, 0, st>>>(a);
     else conv0_fwd_kernel<float, 0><<<grid, 256, 0, st>>>(a);
+  } else if (y_dtype == DT_F16) {  // inference plans only (no statistics)
+    if (a.part) {
+      set_error("conv0_fwd: fp16 arithmetic is inference-only");
+      return E_UNSUPPORTED;
+    }
+    if (a.x_bf16 == 2) conv0_fwd_kernel<f16, 2><<<grid, 256, 0, st>>>(a);
+    else if (a.x_bf16) conv0_fwd_kernel<f16, 1><<<grid, 256, 0, st>>>(a);
+    else conv0_fwd_kernel<f16, 0><<<grid, 256, 0, st>>>(a);
   } else {
     if (a.x_bf16 == 2) conv0_fwd_kernel<bf16, 2><<<grid, 256, 0, st>>>(a);
     else if (a.x_bf16) conv0_fwd_kernel<bf16, 1><<<grid, 256, 0, st>>>(a);

@@ -30,6 +30,7 @@ template <> struct DwCfg<float, 1> { static constexpr int HS = 2, WS = 4, GX = 8
 template <> struct DwCfg<float, 2> { static constexpr int HS = 1, WS = 2, GX = 8, GY = 4; };
 template <> struct DwCfg<bf16, 1> { static constexpr int HS = 2, WS = 4, GX = 4, GY = 4; };
 template <> struct DwCfg<bf16, 2> { static constexpr int HS = 2, WS = 2, GX = 4, GY = 4; };
+template <int S> struct DwCfg<f16, S> : DwCfg<bf16, S> {};
 template <typename T, int S> struct DwTile {
   static constexpr int HS = DwCfg<T, S>::HS, WS = DwCfg<T, S>::WS;
   static constexpr int GX = DwCfg<T, S>::GX, GY = DwCfg<T, S>::GY, G = GX * GY;
@@ -50,6 +51,8 @@ __device__ __forceinline__ void quad_ld(const bf16* p, float (&v)[4]) {
   v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xFFFF0000u);
   v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xFFFF0000u);
 }
+__device__ __forceinline__ void quad_ld(const f16* p, float (&v)[4]) { ld4v(p, v); }
+__device__ __forceinline__ void quad_st(f16* p, const float (&v)[4]) { st4v(p, v); }
 __device__ __forceinline__ void quad_st(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
@@ -288,6 +291,15 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   const int nthr = cbv * 32;  // = quads * groups for both dtypes
+  if (dtype == DT_F16) {  // inference plans only
+    if (FLIP || IT) {
+      set_error("dw: fp16 arithmetic is inference-only");
+      return E_UNSUPPORTED;
+    }
+    if (a.stride == 1) dw_fwd_kernel<f16, 1, false, false><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<f16, 2, false, false><<<grid, nthr, 0, st>>>(a, cbv);
+    return check_launch("dw_fwd");
+  }
   if (dtype == DT_F32) {
     if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
     else dw_fwd_kernel<float, 2, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);

@@ -52,6 +52,16 @@ struct MfmaOp<bf16> {
   }
 };
 
+template <>
+struct MfmaOp<f16> {  // inference plans of dtype fp16: v_mfma_f32_16x16x32_f16
+  static __device__ __forceinline__ void run(const uint4& a, const uint4& b, f32x4& acc) {
+    h16x8 av, bv;
+    __builtin_memcpy(&av, &a, 16);
+    __builtin_memcpy(&bv, &b, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+  }
+};
+
 template <typename T>
 __device__ __forceinline__ uint4 zero_tail(uint4 v, int valid) {
   // zero the elements >= valid of a 16-B vector (valid <= 0: all, valid >= V: none); selects only
@@ -336,7 +346,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       const int m = m0 + half * HROWS + row;
       if (!tact || row >= HROWS || m >= a.M) continue;
       float o[V], rv[V];
-      if (Rp) unpackv(rr[k], rv);
+      if (Rp) unpack<T>(rr[k], rv);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         float v = sC[row * CLD + vc * V + j];
@@ -347,12 +357,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         stv(Cp + (size_t)m * a.ldc + n, o);
         if constexpr (bst) {  // BN-backward partials of the value as stored (rounded to T)
           float z[V];
-          unpackv(zr[k], z);
+          unpack<T>(zr[k], z);
 #pragma unroll
           for (int j = 0; j < V; ++j) {
-            float gv;
-            if constexpr (V == 8) gv = bf2f(f2bf(o[j]));
-            else gv = o[j];
+            float gv = round_as<T>(o[j]);
             gv = fmaf(z[j], bsc[j], bsh[j]) > 0.f ? gv : 0.f;
             s1[j] += gv;
             s2[j] += gv * (z[j] - bmu[j]) * bis[j];
@@ -536,6 +544,14 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   if (bs && a.b_trans) {
     set_error("gemm_nt: fused BN-backward partials need a non-transposed B");
     return E_UNSUPPORTED;
+  }
+  if (dtype == DT_F16) {  // inference plans only: plain forward GEMMs
+    if (a.b_trans || bs || at || ax || a.part) {
+      set_error("gemm_nt: fp16 arithmetic is inference-only");
+      return E_UNSUPPORTED;
+    }
+    launch_nt<f16, false, false>(a, nt, st);
+    return check_launch("gemm_nt");
   }
   if (dtype == DT_F32) {
     if (a.b_trans) launch_nt<float, true, false>(a, nt, st);

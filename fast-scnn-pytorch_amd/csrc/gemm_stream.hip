@@ -43,6 +43,16 @@ struct GsMma<bf16> {
   }
 };
 
+template <>
+struct GsMma<f16> {
+  static __device__ __forceinline__ void run(const uint4& w, const uint4& x, f32x4& acc) {
+    h16x8 wv, xv;
+    __builtin_memcpy(&wv, &w, 16);
+    __builtin_memcpy(&xv, &x, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wv, xv, acc, 0, 0, 0);
+  }
+};
+
 // zero the elements >= valid of a 16-B vector with selects only (no dynamic register indexing)
 template <typename T>
 __device__ __forceinline__ uint4 gs_tail(uint4 v, int valid) {
@@ -283,6 +293,7 @@ static void gs_launch(const GemmArgs& a, hipStream_t st) {
 
 int gemm_stream(const GemmArgs& a, int dtype, hipStream_t st) {
   if (dtype == DT_F32) gs_launch<float>(a, st);
+  else if (dtype == DT_F16) gs_launch<f16>(a, st);
   else gs_launch<bf16>(a, st);
   return check_launch("gemm_stream");
 }

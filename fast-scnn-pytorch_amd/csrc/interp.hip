@@ -49,6 +49,7 @@ int up_nhwc(const UpArgs& a, int dtype, hipStream_t st) {
   long long total = (long long)a.N * a.Ho * a.Wo * (a.C / V);
   unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) up_nhwc_kernel<float><<<grid, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) up_nhwc_kernel<f16><<<grid, 256, 0, st>>>(a);
   else up_nhwc_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("up_nhwc");
 }
@@ -201,6 +202,9 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
     else up_nchw_rows_kernel<TI, TO, false><<<g, UPR_THREADS, lds, st>>>(a);            \
   } while (0)
     if (in_dtype == DT_F32 && out_dtype == DT_F32) UPR_LAUNCH(float, float);
+    else if (in_dtype == DT_F16 && out_dtype == DT_F16) UPR_LAUNCH(f16, f16);
+    else if (in_dtype == DT_F16 && out_dtype == DT_F32) UPR_LAUNCH(f16, float);
+    else if (in_dtype == DT_F16) UPR_LAUNCH(f16, bf16);
     else if (in_dtype == DT_BF16 && out_dtype == DT_F16) UPR_LAUNCH(bf16, f16);
     else if (in_dtype == DT_F32 && out_dtype == DT_F16) UPR_LAUNCH(float, f16);
     else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) UPR_LAUNCH(bf16, bf16);
@@ -210,6 +214,9 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
     return check_launch("up_nchw");
   }
   if (in_dtype == DT_F32 && out_dtype == DT_F32) up_nchw_kernel<float, float, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_F16 && out_dtype == DT_F16) up_nchw_kernel<f16, f16, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_F16 && out_dtype == DT_F32) up_nchw_kernel<f16, float, 0><<<grid, 256, 0, st>>>(a);
+  else if (in_dtype == DT_F16) up_nchw_kernel<f16, bf16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_F16) up_nchw_kernel<bf16, f16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_F32 && out_dtype == DT_F16) up_nchw_kernel<float, f16, 0><<<grid, 256, 0, st>>>(a);
   else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) up_nchw_kernel<bf16, bf16, 0><<<grid, 256, 0, st>>>(a);
@@ -277,7 +284,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_argmax_kernel(UpArgs a, TL* la
           x1 = d1 == r ? wr[r][j] : x1;
         }
         float o = lh.l0 * x0 + lh.l1 * x1;
-        if constexpr (sizeof(TI) == 2) o = bf2f(f2bf(o));  // the logits up_nchw would store
+        o = round_as<TI>(o);  // the logits up_nchw would store
         const bool gt = o > best[rr][j];
         best[rr][j] = gt ? o : best[rr][j];
         arg[rr][j] = gt ? c : arg[rr][j];
@@ -305,6 +312,9 @@ int up_argmax(const UpArgs& a, int in_dtype, void* labels, int label_u8, hipStre
   if (in_dtype == DT_F32) {
     if (label_u8) up_argmax_kernel<float, uint8_t><<<g, UPR_THREADS, lds, st>>>(a, (uint8_t*)labels);
     else up_argmax_kernel<float, long long><<<g, UPR_THREADS, lds, st>>>(a, (long long*)labels);
+  } else if (in_dtype == DT_F16) {
+    if (label_u8) up_argmax_kernel<f16, uint8_t><<<g, UPR_THREADS, lds, st>>>(a, (uint8_t*)labels);
+    else up_argmax_kernel<f16, long long><<<g, UPR_THREADS, lds, st>>>(a, (long long*)labels);
   } else {
     if (label_u8) up_argmax_kernel<bf16, uint8_t><<<g, UPR_THREADS, lds, st>>>(a, (uint8_t*)labels);
     else up_argmax_kernel<bf16, long long><<<g, UPR_THREADS, lds, st>>>(a, (long long*)labels);
@@ -491,6 +501,7 @@ int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
   }
   dim3 grid(50, a.N);
   if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) pyramid_pool_kernel<f16><<<grid, 256, 0, st>>>(a);
   else pyramid_pool_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("pyramid_pool");
 }
@@ -571,6 +582,7 @@ int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
   long long total = (long long)a.N * a.H * a.W * 4 * a.CF;
   unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) ppm_up_fwd_kernel<float><<<grid, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) ppm_up_fwd_kernel<f16><<<grid, 256, 0, st>>>(a);
   else ppm_up_fwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("ppm_up_fwd");
 }

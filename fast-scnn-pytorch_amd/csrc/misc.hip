@@ -737,6 +737,7 @@ int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t
   t.start[t.n] = t.total;
   const unsigned grid = (unsigned)std::min<long long>((t.total + 255) / 256, 4096);
   if (dtype == DT_F32) weights_prep_kernel<float><<<grid, 256, 0, st>>>(t, P, (float*)dst);
+  else if (dtype == DT_F16) weights_prep_kernel<f16><<<grid, 256, 0, st>>>(t, P, (f16*)dst);
   else weights_prep_kernel<bf16><<<grid, 256, 0, st>>>(t, P, (bf16*)dst);
   return check_launch("weights_prep");
 }

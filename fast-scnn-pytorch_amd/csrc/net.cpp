@@ -186,8 +186,8 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     set_error("plan_build: bad input shape N=%d H=%d W=%d", N, H, W);
     return E_INVALID;
   }
-  if (dtype != DT_F32 && dtype != DT_BF16) {
-    set_error("plan_build: unsupported dtype %d", dtype);
+  if (dtype != DT_F32 && dtype != DT_BF16 && !(dtype == DT_F16 && !train)) {
+    set_error("plan_build: unsupported dtype %d (fp16 arithmetic is inference-only)", dtype);
     return E_UNSUPPORTED;
   }
   pl = Plan();
@@ -223,7 +223,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     set_error("plan_build: batch too large for 32-bit row indexing");
     return E_INVALID;
   }
-  if (dtype == DT_BF16) pl.pbf = A.get((size_t)net.p_total * 2);
+  if (dtype != DT_F32) pl.pbf = A.get((size_t)net.p_total * 2);  // 16-bit weight copy
   if (train) pl.wt = A.get((size_t)net.wt_total * E);
   unit(pl.c0, M0, 32, conv0_parts(N, pl.H1, pl.W1));
   unit(pl.l1dw, M1, 32, dw_parts(N, pl.H2, pl.W2, 32, dtype, 2));
@@ -475,7 +475,7 @@ struct Exec {
   // bf16 cast of the arena and the transposed dgrad weights, one launch per step
   int prep_weights() {
     PrepTable t;
-    if (dt == DT_BF16) {
+    if (dt != DT_F32) {
       PrepJob& j = t.j[t.n++];
       j.src = 0; j.dst = (long long)(pl.pbf / 2); j.R = 1; j.Cc = (int)net.p_total; j.ld = 0;
       j.trans = 0;

@@ -325,11 +325,14 @@ class FastSCNN(nn.Module):
         return r
 
     # ---- execution ----------------------------------------------------------------------------
-    def _compute_dtype(self, x):
-        """Arithmetic of the call: fp32 for fp32 input; bf16 (16-bit activations, fp32 master
-        weights / statistics / accumulation) for bf16 input, for fp16 input (the cfg5 TuSimple
-        fp16 inference and test_specific_images.py's half-precision path: fp16 images in, fp16
-        logits out, bf16 arithmetic in between) and under autocast (train.py:269's AMP)."""
+    def _compute_dtype(self, x, train):
+        """Arithmetic of the call: fp32 for fp32 input; fp16 for fp16 input at inference (the
+        cfg5 TuSimple fp16 inference: fp16 images in, fp16 MFMA arithmetic with fp32
+        accumulation, fp16 logits out); bf16 (16-bit activations, fp32 master weights /
+        statistics / accumulation) for bf16 input, for fp16 input in training, and under
+        autocast (train.py:269's AMP)."""
+        if x.dtype == torch.float16 and not train:
+            return torch.float16
         if x.dtype in (torch.bfloat16, torch.float16):
             return torch.bfloat16
         if torch.is_autocast_enabled("cuda"):
@@ -368,7 +371,7 @@ class FastSCNN(nn.Module):
         N, _, H, W = x.shape
         if H < 32 or W < 32:
             raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
-        dt = self._compute_dtype(x)
+        dt = self._compute_dtype(x, train)
         x = self._input(x)
         if train and N < 2:
             # the reference raises from the PPM 1x1 BatchNorm in train mode (SURVEY §0 trap 5)
@@ -414,7 +417,7 @@ class FastSCNN(nn.Module):
         N, _, H, W = x.shape
         if H < 32 or W < 32:
             raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
-        dt = self._compute_dtype(x)
+        dt = self._compute_dtype(x, False)
         x = self._input(x)
         plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), False)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
@@ -458,7 +461,7 @@ class FastSCNN(nn.Module):
         if N < 2:
             raise ValueError("Expected more than 1 value per channel when training, got input "
                              "size torch.Size([1, 32, 1, 1])")
-        dt = self._compute_dtype(x)
+        dt = self._compute_dtype(x, True)
         x = self._input(x)
         target = target.to(torch.int64).contiguous()
         from . import loss as _loss
