@@ -85,6 +85,7 @@ SIGNATURES = {
     "fscnn_pw_gemm": (c_int, [c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp,
                               c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "fscnn_pw_wgrad_slab_floats": (c_ll, [c_int, c_int, c_int]),
+    "fscnn_pw_gemm_stats_parts": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "fscnn_pw_wgrad": (c_int, [c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int,
                                c_vp]),
     "fscnn_bn_finalize": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_float,

@@ -510,6 +510,12 @@ int fscnn_dw3x3_wgrad(const void* x, const void* dy, int dtype, int N, int H, in
   return dw_wgrad_reduce(slab, dw_wgrad_parts(N, a.Ho, a.Wo, C, dtype, stride), C, dw, S(stream));
 }
 
+int fscnn_pw_gemm_stats_parts(int M, int N, int K, int lda, int ldc, int dtype) {
+  GemmArgs a{};
+  static float dummy;  // only the presence of the statistics pointer matters
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = K; a.ldc = ldc; a.part = &dummy;
+  return gemm_nt_parts(a, dtype);
+}
 int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                   int b_trans, const float* scale, const float* shift, const void* R, int ldr,
                   int relu, void* C, int ldc, float* stats_part, int dtype, void* stream) {

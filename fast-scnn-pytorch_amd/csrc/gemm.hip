@@ -473,6 +473,21 @@ static int pick_nt(int N) {
 
 int gemm_parts(int M) { return cdiv(M, G_BM); }
 
+// the streaming kernel takes every shape it supports (FSCNN_GEMM_STREAM=0: tiled kernel only)
+static bool use_stream(const GemmArgs& a, int dtype) {
+  static const bool stream_on = [] {
+    const char* e = getenv("FSCNN_GEMM_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return stream_on && gemm_stream_ok(a, dtype);
+}
+
+// BN partial records one gemm_nt call writes (part / bpart): one per 128-row tile, or one per
+// streaming workgroup of a column group; always <= gemm_parts(M)
+int gemm_nt_parts(const GemmArgs& a, int dtype) {
+  return use_stream(a, dtype) ? gemm_stream_parts(a, dtype) : gemm_parts(a.M);
+}
+
 template <typename T, bool BT, bool BS, bool AT = false, bool AX = false>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
@@ -523,16 +538,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     set_error("gemm_nt: BN-backward A transform needs z, a plain B and K %% %d == 0", V);
     return E_UNSUPPORTED;
   }
-  static const bool stream_on = [] {
-    const char* e = getenv("FSCNN_GEMM_STREAM");
-    return !(e && e[0] == '0');
-  }();
   const bool at = a.a_scale != nullptr;
   if (at && (!a.a_shift || a.b_trans || a.bpart || a.K > G_ATMAX || a.K % V)) {
     set_error("gemm_nt: lazy BN on A needs a plain GEMM with K <= %d, K %% %d == 0", G_ATMAX, V);
     return E_UNSUPPORTED;
   }
-  if (stream_on && !at && !ax && gemm_stream_ok(a, dtype)) return gemm_stream(a, dtype, st);
   const bool bs = a.bpart != nullptr;
   if (bs && (a.part || !a.bz || !a.bmean || !a.binvstd || !a.bscale || !a.bshift ||
              (a.bmode != 0 && a.bmode != 2) || a.ldbz % V)) {
@@ -545,6 +555,7 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     set_error("gemm_nt: fused BN-backward partials need a non-transposed B");
     return E_UNSUPPORTED;
   }
+  if (use_stream(a, dtype)) return gemm_stream(a, dtype, st);
   if (dtype == DT_F16) {  // inference plans only: plain forward GEMMs
     if (a.b_trans || bs || at || ax || a.part) {
       set_error("gemm_nt: fp16 arithmetic is inference-only");

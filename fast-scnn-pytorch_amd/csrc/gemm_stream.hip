@@ -1,26 +1,38 @@
-// Streaming pointwise GEMM for the eval forward: C[m][n] = epi(sum_k A[m][k] * W[n][k]).
-// Same contract as gemm_nt (kernels.hpp GemmArgs, b_trans = 0, no statistics) for the 1x1 convs
-// whose whole weight slice fits in LDS: every K <= 128 fp32 / <= 256 bf16 conv of
-// models/fast_scnn.py (:73 DSConv pw, :103 expand, :124-128 PPM, :198/:202 FFM, :230 classifier).
+// Streaming pointwise GEMM: C[m][n] = epi(sum_k A[m][k] * W[n][k]) for every 1x1 conv whose
+// weight slice fits in LDS (K <= 128 fp32 / <= 256 bf16-fp16): models/fast_scnn.py :73 DSConv pw,
+// :103 expand, :124-128 PPM, :198/:202 FFM, :230 classifier, and the dgrads of those shapes
+// (the executor's dgrad reads a per-step transposed weight copy, so it is the same NT GEMM).
 //
-// Why a second kernel: at M = 262,144 pixels and K = 128 the tiled gemm_nt spends as long in its
-// LDS-staged A tile and epilogue as in MFMA.  Here
+// Same contract as gemm_nt (kernels.hpp GemmArgs).  Why a second kernel: at M = 262,144 pixels
+// and K = 64-128 the tiled gemm_nt spends as long in its LDS-staged A tile and block-wide
+// epilogue as in MFMA.  Here
 //   * a workgroup owns one column group (16*NT output channels) and keeps that group's weights
 //     [16*NT][K] in LDS for its whole life (loaded once);
 //   * each wave streams its own 32-pixel chunks straight from HBM into registers (lane (li, lq)
 //     loads pixel li's k-vector lq of every k-step: one 16-B load per MFMA operand), with no
-//     workgroup barrier in the loop;
+//     workgroup barrier in the loop; the next chunk's loads are in flight during this chunk's
+//     MFMAs (register double buffer), and tail masks / the lazy BN are applied at the use site;
 //   * the MFMA operands are swapped (weights as the A operand), so each lane's accumulator holds
-//     4 CONSECUTIVE output channels of one pixel: the epilogue (BN fold, bias, residual, ReLU)
-//     runs in registers and stores 16-B (fp32) / 8-B (bf16) NHWC vectors directly.
+//     4 CONSECUTIVE output channels of one pixel: the epilogue runs in registers and stores
+//     16-B (fp32) / 8-B (16-bit) NHWC vectors directly.
+// Training forms (template flags):
+//   AT  the A operand is the raw conv output z of a BN+ReLU that is never stored; the GEMM
+//       consumes relu(fmaf(z, a_scale[k], a_shift[k])) (bn_apply's arithmetic, bit-identical);
+//   ST  per-channel BN statistics of the output: each lane keeps shifted sums (shift = the
+//       channel's value at the wave's first pixel, broadcast) over its pixels; at the end the
+//       lanes (xor butterfly, fixed order) and the 4 waves (Chan merge, fixed order) are folded
+//       into ONE (mean, M2, count) record per workgroup -> part[bi][3][N] (bi < bpg, the
+//       workgroup's index within its column group; gemm_stream_parts reports bpg);
+//   BS  dgrad producing the dy of a BN: per-channel sum(g*mask), sum(g*mask*xhat) of the stored
+//       (rounded) output, the mask recomputed from that BN's z -> bpart[bi][2][N].
 // The k summation order inside a 16x16xK MFMA step matches gemm_nt (4-element k quads for fp32,
-// 8-element for bf16, steps in increasing k), so results agree with it to rounding of the
-// accumulation order within the hardware MFMA.
+// 8-element for 16-bit, steps in increasing k).
 #include "kernels.hpp"
 
 namespace fscnn {
 
-constexpr int GS_MW = 32;  // pixels per wave chunk (2 x 16-row MFMA tiles)
+constexpr int GS_MW = 32;     // pixels per wave chunk (2 x 16-row MFMA tiles)
+constexpr int GS_KMAX = 256;  // largest K of a lazily normalised (AT) A operand
 
 template <typename T>
 struct GsMma;
@@ -42,7 +54,6 @@ struct GsMma<bf16> {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, xv, acc, 0, 0, 0);
   }
 };
-
 template <>
 struct GsMma<f16> {
   static __device__ __forceinline__ void run(const uint4& w, const uint4& x, f32x4& acc) {
@@ -71,15 +82,28 @@ __device__ __forceinline__ uint4 gs_tail(uint4 v, int valid) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// NT: 16-column MFMA tiles per group; KS: k-steps (16 fp32 / 32 bf16 k each) covering K
-template <typename T, int NT, int KS, bool TAIL>
+// sum over the 16 lanes li of a 16-lane row (xor butterfly: every lane ends with the same sum)
+__device__ __forceinline__ float gs_rowsum(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+// NT: 16-column MFMA tiles per group; KS: k-steps (16 fp32 / 32 16-bit k each) covering K
+template <typename T, int NT, int KS, bool TAIL, bool AT, bool ST, bool BS>
 __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg) {
   constexpr int V = VecW<T>::V;     // elements per 16-B vector
   constexpr int KV = 4 * KS;        // 16-B vectors per weight row (4 per k-step)
+  constexpr int KP = KV * V;        // K padded to whole k-steps
   constexpr int WST = KV + 1;       // padded LDS row stride (vectors): conflict-free b128 reads
   constexpr int BN = 16 * NT;
+  constexpr bool SUMS = ST || BS;
   extern __shared__ __attribute__((aligned(16))) uint4 s_w[];  // [BN][WST]
   float* s_sc = reinterpret_cast<float*>(s_w + BN * WST);       // [BN] scale, [BN] shift
+  float* s_at = s_sc + 2 * BN;                                  // AT: [GS_KMAX] scale, shift
+  float* s_bc = s_at + (AT ? 2 * GS_KMAX : 0);                  // BS: [4][BN] mean/istd/sc/sh
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -91,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   const T* A = (const T*)a.A;
   const T* B = (const T*)a.B;
 
-  // ---- weights of the group -> LDS (zero rows n >= N, zero k >= K) ---------------------------
+  // ---- weights of the group -> LDS (zero rows n >= N, zero k >= K), per-column tables -------
   for (int i = tid; i < BN * KV; i += 256) {
     const int r = i / KV, v = i - r * KV;
     const int n = n0 + r, k = v * V;
@@ -104,15 +128,46 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     const int n = n0 + i < a.N ? n0 + i : 0;
     s_sc[i] = a.scale ? a.scale[n] : 1.f;
     s_sc[BN + i] = a.shift ? a.shift[n] : 0.f;
+    if constexpr (BS) {
+      // ReLU mask of that BN recomputed as fmaf(z, scale, shift) > 0 (mode 2); mode 0 (no
+      // ReLU) uses scale 0, shift 1 so both are the same select
+      const bool m2 = a.bmode == 2;
+      s_bc[i] = a.bmean[n];
+      s_bc[BN + i] = a.binvstd[n];
+      s_bc[2 * BN + i] = m2 ? a.bscale[n] : 0.f;
+      s_bc[3 * BN + i] = m2 ? a.bshift[n] : 1.f;
+    }
+  }
+  if constexpr (AT) {
+    for (int k = tid; k < KP; k += 256) {
+      s_at[k] = k < a.K ? a.a_scale[k] : 0.f;
+      s_at[GS_KMAX + k] = k < a.K ? a.a_shift[k] : 0.f;
+    }
   }
   __syncthreads();
 
   const int nchunks = cdiv(a.M, GS_MW);
   const int wstride = bpg * 4;
   int c = bi * 4 + wave;
-  if (c >= nchunks) return;
 
-  // k-vector (4*s + lq) of pixel rows li, 16 + li of the chunk -> x[mt][s]
+  // sums of channels n0 + 16nt + 4lq + r over this lane's pixels (ST: shifted by shf)
+  float s1[SUMS ? NT : 1][4], s2[SUMS ? NT : 1][4], shf[ST ? NT : 1][4];
+  float cnt = 0.f;
+  if constexpr (SUMS) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[nt][r] = 0.f; s2[nt][r] = 0.f; }
+  }
+  if constexpr (ST) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) shf[nt][r] = 0.f;
+  }
+  bool first = true;
+
+  // k-vector (4*s + lq) of pixel rows li, 16 + li of the chunk -> r[mt][s] (raw, clamped loads)
   uint4 xa[2][KS];
   auto loadx = [&](int chunk, uint4 (&r)[2][KS]) {
     const bool cok = chunk < nchunks;
@@ -127,13 +182,20 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
         r[mt][s] = *reinterpret_cast<const uint4*>(A + (ok ? (size_t)m * a.lda + k : 0));
       }
     }
-    // zero invalid rows / the K tail (selects after all loads are in flight)
+  };
+  // at the use site: lazy BN+ReLU (AT), then the row / K-tail zeroing
+  auto prep = [&](int chunk, uint4 (&r)[2][KS]) {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int m = chunk * GS_MW + mt * 16 + li;
-      const bool mok = cok && m < a.M;
+      const bool mok = m < a.M;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) r[mt][s] = gs_tail<T>(r[mt][s], mok ? a.K - (4 * s + lq) * V : 0);
+      for (int s = 0; s < KS; ++s) {
+        const int k = (4 * s + lq) * V;
+        uint4 v = r[mt][s];
+        if constexpr (AT) v = bnrelu_vec<T>(v, s_at + k, s_at + GS_KMAX + k);
+        r[mt][s] = gs_tail<T>(v, mok ? a.K - k : 0);
+      }
     }
   };
 
@@ -145,10 +207,13 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   // s's loads.
   constexpr bool PF = KS <= 4;
   uint4 xn[2][PF ? KS : 1];
-  if constexpr (PF) loadx(c, xa);
+  if constexpr (PF) {
+    if (c < nchunks) loadx(c, xa);
+  }
   for (; c < nchunks; c += wstride) {
-    if constexpr (PF) loadx(c + wstride, xn);  // clamped / zeroed past the end
+    if constexpr (PF) loadx(c + wstride, xn);  // clamped past the end
     else loadx(c, xa);
+    prep(c, xa);
     f32x4 acc[2][NT];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -158,7 +223,9 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     // chunk (cheap ds_read_b128) instead of being hoisted into NT*KS*4 registers
     int wb = li * WST + lq;
     asm volatile("" : "+v"(wb));
-    const float* ssc = s_sc + (wb - li * WST - lq);  // same laundering for the epilogue table
+    const int wz = wb - li * WST - lq;  // 0, opaque to the compiler
+    const float* ssc = s_sc + wz;       // same laundering for the epilogue tables
+    const float* sbc = s_bc + wz;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
@@ -170,6 +237,18 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     }
     // ---- epilogue: lane holds channels n0 + 16nt + 4lq + r of pixel m ------------------------
     if constexpr (!TAIL) {  // whole 4-channel vectors, 16-B aligned rows (checked on the host)
+      if constexpr (ST) {
+        if (first) {  // per-channel shift: the value at the wave's first pixel (lane li = 0)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            const int nl = nt * 16 + 4 * lq;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              shf[nt][r] = __shfl(acc[0][nt][r] * ssc[nl + r] + ssc[BN + nl + r], lane & 48);
+          }
+          first = false;
+        }
+      }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const int m = c * GS_MW + mt * 16 + li;
@@ -180,6 +259,13 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) ld4v(Rp + mr * a.ldr + n0 + nt * 16 + 4 * lq, rv[nt]);
         }
+        float zv[BS ? NT : 1][4];
+        if constexpr (BS) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            ld4v((const T*)a.bz + mr * a.ldbz + n0 + nt * 16 + 4 * lq, zv[nt]);
+        }
+        if constexpr (SUMS) cnt += mok ? 1.f : 0.f;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const int nl = nt * 16 + 4 * lq;
@@ -190,13 +276,33 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[mt][nt][r] * scv[r] + shv[r];
+            if constexpr (ST) {  // statistics of the unrounded value (gemm_nt's convention)
+              const float d = mok ? v - shf[nt][r] : 0.f;
+              s1[nt][r] += d;
+              s2[nt][r] += d * d;
+            }
             if (Rp) v += rv[nt][r];
             o[r] = a.relu ? fmaxf(v, 0.f) : v;
           }
           if (mok) st4v(Cp + mr * a.ldc + n0 + nl, o);
+          if constexpr (BS) {  // partials of the value as stored, masked by that BN's ReLU
+            const float4 bm = *reinterpret_cast<const float4*>(sbc + nl);
+            const float4 bv = *reinterpret_cast<const float4*>(sbc + BN + nl);
+            const float4 bs = *reinterpret_cast<const float4*>(sbc + 2 * BN + nl);
+            const float4 bh = *reinterpret_cast<const float4*>(sbc + 3 * BN + nl);
+            const float bmv[4] = {bm.x, bm.y, bm.z, bm.w}, biv[4] = {bv.x, bv.y, bv.z, bv.w};
+            const float bsv[4] = {bs.x, bs.y, bs.z, bs.w}, bhv[4] = {bh.x, bh.y, bh.z, bh.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float gv = round_as<T>(o[r]);
+              gv = (mok && fmaf(zv[nt][r], bsv[r], bhv[r]) > 0.f) ? gv : 0.f;
+              s1[nt][r] += gv;
+              s2[nt][r] += gv * (zv[nt][r] - bmv[r]) * biv[r];
+            }
+          }
         }
       }
-    } else {  // column tail / unaligned rows (the 19-class classifier): scalar
+    } else {  // column tail / unaligned rows (the 19-class classifier): scalar, no statistics
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const int m = c * GS_MW + mt * 16 + li;
@@ -222,12 +328,70 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
         for (int s = 0; s < KS; ++s) xa[mt][s] = xn[mt][s];
     }
   }
+
+  if constexpr (SUMS) {
+    // ---- one record per workgroup: lanes (xor butterfly), then the 4 waves (fixed order) ----
+    cnt = gs_rowsum(cnt);  // pixels of this wave (every lane row covers the same pixels)
+    __syncthreads();       // every wave is done with s_w: reuse it as the reduction scratch
+    float* red = reinterpret_cast<float*>(s_w);  // [4 waves][3][BN]
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t1 = gs_rowsum(s1[nt][r]), t2 = gs_rowsum(s2[nt][r]);
+        if (li == 0) {
+          const int col = nt * 16 + 4 * lq + r;
+          if constexpr (ST) {  // (count, mean, M2) of the wave from its shifted sums
+            const float mean = cnt > 0.f ? shf[nt][r] + t1 / cnt : 0.f;
+            const float m2 = cnt > 0.f ? fmaxf(t2 - t1 * (t1 / cnt), 0.f) : 0.f;
+            red[(wave * 3 + 0) * BN + col] = cnt;
+            red[(wave * 3 + 1) * BN + col] = mean;
+            red[(wave * 3 + 2) * BN + col] = m2;
+          } else {
+            red[(wave * 3 + 0) * BN + col] = t1;
+            red[(wave * 3 + 1) * BN + col] = t2;
+          }
+        }
+      }
+    __syncthreads();
+    for (int col = tid; col < BN; col += 256) {
+      const int n = n0 + col;
+      if (n >= a.N) continue;
+      if constexpr (ST) {
+        float nn = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // Chan merge of the 4 waves, fixed order
+          const float nb = red[(w * 3 + 0) * BN + col];
+          if (nb <= 0.f) continue;
+          const float mb = red[(w * 3 + 1) * BN + col], qb = red[(w * 3 + 2) * BN + col];
+          const float tot = nn + nb, d = mb - mean;
+          mean += d * (nb / tot);
+          m2 += qb + d * d * (nn * nb / tot);
+          nn = tot;
+        }
+        float* rec = a.part + (size_t)bi * 3 * a.N;
+        rec[n] = mean;
+        rec[a.N + n] = m2;
+        rec[2 * a.N + n] = nn;
+      } else {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          t1 += red[(w * 3 + 0) * BN + col];
+          t2 += red[(w * 3 + 1) * BN + col];
+        }
+        float* rec = a.bpart + (size_t)bi * 2 * a.N;
+        rec[n] = t1;
+        rec[a.N + n] = t2;
+      }
+    }
+  }
 }
 
-static int gs_pick_nt(int N) {
+static int gs_pick_nt(int N, bool sums) {
   if (N <= 32) return 2;
   if (N <= 48) return 3;
-  if (N <= 64) return 4;
+  if (N <= 64 || sums) return 4;  // the statistics forms keep 2-3 x 4 x NT sum registers
   if (N % 96 == 0) return 6;
   return 8;
 }
@@ -236,65 +400,121 @@ static bool gs_tail_needed(const GemmArgs& a, int nt) {
   return a.N % (16 * nt) != 0 || a.ldc % 4 != 0 || (a.R && a.ldr % 4 != 0);
 }
 
+static size_t gs_lds(const GemmArgs& a, int nt, int ks) {
+  size_t b = (size_t)16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4;
+  if (a.a_scale) b += (size_t)2 * GS_KMAX * 4;
+  if (a.bpart) b += (size_t)4 * 16 * nt * 4;
+  return b;  // >= the end-of-kernel reduction scratch [4][3][16 nt] (aliases the weights)
+}
+
 bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   const int KC = dtype == DT_F32 ? 16 : 32;  // k per step
   const int ks = cdiv(a.K, KC);
-  if (a.part || a.bpart || a.b_trans) return false;
+  const bool sums = a.part || a.bpart;
+  if (a.b_trans || a.atab || (a.part && a.bpart)) return false;
+  if (a.part && a.R) return false;
+  // lazy BN on A: train-forward producers only (always with statistics)
+  if (a.a_scale && (!a.a_shift || !a.part || a.K > GS_KMAX)) return false;
+  if (dtype == DT_F16 && (sums || a.a_scale)) return false;
   if (!(ks == 1 || ks == 2 || ks == 3 || ks == 4 || ks == 6 || ks == 8)) return false;
-  const int nt = gs_pick_nt(a.N);
-  if (gs_tail_needed(a, nt) && nt != 2) return false;  // scalar-tail variant only for N <= 32
-  const size_t lds = (size_t)16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4;
-  if (lds > 72 * 1024) return false;
+  if (sums && ks > 4) return false;  // keep the statistics forms within 256 VGPRs
+  const int nt = gs_pick_nt(a.N, sums);
+  if (a.bpart && dtype == DT_F32 && nt == 4 && ks > 2) return false;  // would spill
+  if (gs_tail_needed(a, nt) && (nt != 2 || sums)) return false;  // scalar tail: N <= 32 only
+  if (a.bpart && (!a.bz || a.ldbz % 4 || (a.bmode != 0 && a.bmode != 2))) return false;
+  if (gs_lds(a, nt, ks) > 72 * 1024) return false;
   return a.M >= 4096;  // tiny GEMMs (PPM bins): loading a weight slice per block does not pay
 }
 
-
-template <typename T, int NT, bool TAIL>
-static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int bpg,
-                         hipStream_t st) {
-  switch (ks) {
-    case 1: gemm_stream_kernel<T, NT, 1, TAIL><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 2: gemm_stream_kernel<T, NT, 2, TAIL><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 3: gemm_stream_kernel<T, NT, 3, TAIL><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 4: gemm_stream_kernel<T, NT, 4, TAIL><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 6: gemm_stream_kernel<T, NT, 6, TAIL><<<grid, 256, lds, st>>>(a, bpg); break;
-    default: gemm_stream_kernel<T, NT, 8, TAIL><<<grid, 256, lds, st>>>(a, bpg); break;
-  }
-}
-
-template <typename T>
-static void gs_launch(const GemmArgs& a, hipStream_t st) {
-  constexpr int KC = 4 * VecW<T>::V;
-  const int ks = cdiv(a.K, KC);
-  const int nt = gs_pick_nt(a.N);
+// workgroups per column group = the record count of the statistics forms
+static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
+  const int KC = dtype == DT_F32 ? 16 : 32;
+  ks = cdiv(a.K, KC);
+  nt = gs_pick_nt(a.N, a.part || a.bpart);
   const int groups = cdiv(a.N, 16 * nt);
-  const size_t lds = (size_t)16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4;
+  lds = gs_lds(a, nt, ks);
   const int nchunks = cdiv(a.M, GS_MW);
   // resident workgroups: LDS-limited (160 KB / CU), at most 2 per CU (measured: 3-4 slower)
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
   int bpg = cdiv(256 * per_cu, groups);
   bpg = (bpg + 7) / 8 * 8;
-  const int need = cdiv(nchunks, 4);
+  const int need = cdiv(nchunks, 4);  // <= cdiv(M, 128) = gemm_parts(M): fits the record slots
   if (bpg > need) bpg = need;
   if (bpg < 1) bpg = 1;
-  dim3 grid((unsigned)(groups * bpg));
-  switch (nt) {
-    case 2:
-      if (gs_tail_needed(a, nt)) gs_launch_ks<T, 2, true>(a, ks, grid, lds, bpg, st);
-      else gs_launch_ks<T, 2, false>(a, ks, grid, lds, bpg, st);
+  return bpg;
+}
+
+int gemm_stream_parts(const GemmArgs& a, int dtype) {
+  int nt, ks;
+  size_t lds;
+  return gs_bpg(a, dtype, nt, ks, lds);
+}
+
+template <typename T, int NT, bool TAIL, bool AT, bool ST, bool BS>
+static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int bpg,
+                         hipStream_t st) {
+  constexpr bool SUMS = ST || BS;
+  switch (ks) {
+    case 1: gemm_stream_kernel<T, NT, 1, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
+    case 2: gemm_stream_kernel<T, NT, 2, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
+    case 3: gemm_stream_kernel<T, NT, 3, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
+    case 4: gemm_stream_kernel<T, NT, 4, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
+    case 6:
+      if constexpr (!SUMS) gemm_stream_kernel<T, NT, 6, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
       break;
-    case 3: gs_launch_ks<T, 3, false>(a, ks, grid, lds, bpg, st); break;
-    case 4: gs_launch_ks<T, 4, false>(a, ks, grid, lds, bpg, st); break;
-    case 6: gs_launch_ks<T, 6, false>(a, ks, grid, lds, bpg, st); break;
-    default: gs_launch_ks<T, 8, false>(a, ks, grid, lds, bpg, st); break;
+    default:
+      if constexpr (!SUMS) gemm_stream_kernel<T, NT, 8, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      break;
   }
 }
 
+template <typename T, bool AT, bool ST, bool BS>
+static void gs_launch_nt(const GemmArgs& a, int nt, int ks, dim3 grid, size_t lds, int bpg,
+                         hipStream_t st) {
+  constexpr bool SUMS = ST || BS;
+  switch (nt) {
+    case 2:
+      if (!SUMS && gs_tail_needed(a, nt)) gs_launch_ks<T, 2, true, AT, false, false>(a, ks, grid, lds, bpg, st);
+      else gs_launch_ks<T, 2, false, AT, ST, BS>(a, ks, grid, lds, bpg, st);
+      break;
+    case 3: gs_launch_ks<T, 3, false, AT, ST, BS>(a, ks, grid, lds, bpg, st); break;
+    case 4: gs_launch_ks<T, 4, false, AT, ST, BS>(a, ks, grid, lds, bpg, st); break;
+    case 6:
+      if constexpr (!SUMS) gs_launch_ks<T, 6, false, AT, false, false>(a, ks, grid, lds, bpg, st);
+      break;
+    default:
+      if constexpr (!SUMS) gs_launch_ks<T, 8, false, AT, false, false>(a, ks, grid, lds, bpg, st);
+      break;
+  }
+}
+
+template <typename T>
+static void gs_launch(const GemmArgs& a, int dtype, hipStream_t st) {
+  int nt, ks;
+  size_t lds;
+  const int bpg = gs_bpg(a, dtype, nt, ks, lds);
+  const int groups = cdiv(a.N, 16 * nt);
+  dim3 grid((unsigned)(groups * bpg));
+  const bool at = a.a_scale != nullptr;
+  if (a.bpart) gs_launch_nt<T, false, false, true>(a, nt, ks, grid, lds, bpg, st);
+  else if (a.part && at) gs_launch_nt<T, true, true, false>(a, nt, ks, grid, lds, bpg, st);
+  else if (a.part) gs_launch_nt<T, false, true, false>(a, nt, ks, grid, lds, bpg, st);
+  else gs_launch_nt<T, false, false, false>(a, nt, ks, grid, lds, bpg, st);
+}
+
 int gemm_stream(const GemmArgs& a, int dtype, hipStream_t st) {
-  if (dtype == DT_F32) gs_launch<float>(a, st);
-  else if (dtype == DT_F16) gs_launch<f16>(a, st);
-  else gs_launch<bf16>(a, st);
+  if (dtype == DT_F32) {
+    gs_launch<float>(a, dtype, st);
+  } else if (dtype == DT_F16) {
+    if (a.part || a.bpart || a.a_scale) {
+      set_error("gemm_stream: fp16 arithmetic is inference-only");
+      return E_UNSUPPORTED;
+    }
+    gs_launch<f16>(a, dtype, st);
+  } else {
+    gs_launch<bf16>(a, dtype, st);
+  }
   return check_launch("gemm_stream");
 }
 

@@ -282,7 +282,9 @@ int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st);
 int gemm_parts(int M);
 int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st);
 bool gemm_stream_ok(const GemmArgs& a, int dtype);
-int gemm_stream(const GemmArgs& a, int dtype, hipStream_t st);  // eval-form gemm_nt (gemm_stream.hip)
+int gemm_stream(const GemmArgs& a, int dtype, hipStream_t st);  // streaming gemm_nt (gemm_stream.hip)
+int gemm_stream_parts(const GemmArgs& a, int dtype);  // its workgroups per column group
+int gemm_nt_parts(const GemmArgs& a, int dtype);      // BN records gemm_nt(a) writes
 int gemm_tn_splits(int M, int N, int K);
 int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st);
 // slab is consumed (folded in place)

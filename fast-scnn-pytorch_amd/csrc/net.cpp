@@ -551,9 +551,10 @@ struct Exec {
   static In raw(const void* p, int ld) { return {p, ld, nullptr, nullptr}; }
 
   // ---- BN glue -----------------------------------------------------------------------
-  int finalize(const Unit& u, const BnL& bn) {
+  // np: records the producer wrote (<= u.nparts slots); 0: all slots
+  int finalize(const Unit& u, const BnL& bn, int np = 0) {
     BnFinalizeArgs f{};
-    f.part = Wf(u.part); f.P = u.nparts; f.C = u.C;
+    f.part = Wf(u.part); f.P = np > 0 ? np : u.nparts; f.C = u.C;
     f.gamma = P(bn.g); f.beta = P(bn.b);
     f.rmean = r.R + bn.rm; f.rvar = r.R + bn.rv;
     f.nbt = r.NBT ? r.NBT + bn.nbt : nullptr;
@@ -594,8 +595,9 @@ struct Exec {
     g.scale = nullptr; g.shift = P(c.b);
     g.C = W(u.z); g.ldc = u.C;
     g.part = Wf(u.part);
+    const int np = gemm_nt_parts(g, dt);
     TRY(gemm_nt(g, dt, r.st));
-    TRY(finalize(u, *bn));
+    TRY(finalize(u, *bn, np));
     return u.lazy ? OK : apply(u, relu, res, ldres);
   }
   int dw(const Unit& u, const ConvL& c, const BnL& bn, In x, int H, int Wd, int Ho, int Wo,
@@ -718,13 +720,15 @@ struct Exec {
         g.a_scale = fin.sc; g.a_shift = fin.sh;
         g.B = Wg(net.ffm_low); g.ldb = 128; g.shift = P(net.ffm_low.b);
         g.C = W(pl.flow.z); g.ldc = 128; g.part = Wf(pl.flow.part);
+        int np = gemm_nt_parts(g, dt);
         TRY(gemm_nt(g, dt, r.st));
-        TRY(finalize(pl.flow, net.ffm_blow));
+        TRY(finalize(pl.flow, net.ffm_blow, np));
         g.K = 64; g.A = W(pl.l2pw.a); g.lda = 64; g.B = Wg(net.ffm_high); g.ldb = 64;
         g.a_scale = g.a_shift = nullptr;
         g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z); g.part = Wf(pl.fhigh.part);
+        np = gemm_nt_parts(g, dt);
         TRY(gemm_nt(g, dt, r.st));
-        TRY(finalize(pl.fhigh, net.ffm_bhigh));
+        TRY(finalize(pl.fhigh, net.ffm_bhigh, np));
         BnApplyArgs a{};
         a.M = pl.flow.M; a.C = 128;
         a.z = W(pl.flow.z); a.ldz = 128; a.scale = Wf(pl.flow.scale); a.shift = Wf(pl.flow.shift);
@@ -951,12 +955,15 @@ struct Exec {
     g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
-    if (bt.u && train) set_btarget(g, bt);
+    if (bt.u && train) {
+      set_btarget(g, bt);
+      bt.u->bparts = gemm_nt_parts(g, dt);
+    }
     return gemm_nt(g, dt, r.st);
   }
   BTarget relu_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 2; return t; }
   BTarget plain_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 0; return t; }
-  static int pre(const Unit& u) { return gemm_parts((int)u.M); }
+  static int pre(const Unit& u) { return u.bparts; }
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
   int dw_bwd(const ConvL& c, int C, const void* dz, In X, int H, int Wd, int Ho, int Wo,
              int stride, void* dX) {

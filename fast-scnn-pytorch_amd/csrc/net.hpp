@@ -64,7 +64,10 @@ struct Unit {
   int C = 0, ld = 0;
   size_t z = 0, a = 0;      // raw conv output / activation (same in eval)
   size_t part = 0;          // BN partial records
-  int nparts = 0;
+  int nparts = 0;           // record slots (gemm_parts(M) for GEMM producers: an upper bound)
+  // records the dgrad producing this unit's dy wrote with fused BN-backward partials (set when
+  // that dgrad is issued, a pure function of its shape; 0: none, the reduce pass runs)
+  mutable int bparts = 0;
   size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
   size_t ga = 0;            // backward: grad wrt a (bwd workspace)
   int ga_ld = 0;

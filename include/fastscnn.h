@@ -211,7 +211,11 @@ int fscnn_dw3x3_dgrad(const void* dy, int dtype, int N, int H, int W, int C, int
 long long fscnn_dw3x3_wgrad_slab_floats(int N, int H, int W, int C, int stride, int dtype);
 int fscnn_dw3x3_wgrad(const void* x, const void* dy, int dtype, int N, int H, int W, int C,
                       int stride, float* slab, float* dw, void* stream);
-/* C[M][N] = act((A[M][K] . B^T) * scale + shift (+ R)); B is [N][K] (b_trans=0) or [K][N] */
+/* C[M][N] = act((A[M][K] . B^T) * scale + shift (+ R)); B is [N][K] (b_trans=0) or [K][N].
+ * stats_part (train BN statistics of the output, before R / relu): room for ceil(M/128)
+ * records [P][3][N]; the call writes fscnn_pw_gemm_stats_parts(...) of them (pass that count as
+ * P to fscnn_bn_finalize). */
+int fscnn_pw_gemm_stats_parts(int M, int N, int K, int lda, int ldc, int dtype);
 int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                   int b_trans, const float* scale, const float* shift, const void* R, int ldr,
                   int relu, void* C, int ldc, float* stats_part, int dtype, void* stream);

@@ -61,6 +61,25 @@ def oracle_bf16_emulated(sd, x, nc):
         F.conv2d = oc
 
 
+def oracle_half_emulated(sd, x, nc, dtype=torch.float16):
+    """Oracle forward as fp16 (or bf16) autocast runs it (test_specific_images.py:121,
+    train.py:269): every conv's input, weights and output, every BatchNorm and interpolate output
+    rounded to ``dtype``.  Its distance from the fp32 oracle is the error half precision itself
+    implies for a weight set (cfg5 golden weights: fp16 max |d| 6.8e-2, argmax 98.84 %)."""
+    import torch.nn.functional as F
+    from oracle import fast_scnn_ref as ref
+    q = lambda v: v.to(dtype).float()  # noqa: E731
+    oc, ob, oi = F.conv2d, F.batch_norm, F.interpolate
+    F.conv2d = lambda a, w, b=None, *r, **k: q(oc(q(a), q(w), b, *r, **k))
+    F.batch_norm = lambda *a, **k: q(ob(*a, **k))
+    F.interpolate = lambda *a, **k: q(oi(*a, **k))
+    try:
+        with torch.no_grad():
+            return ref.forward(sd, q(x), nc)[0][0]
+    finally:
+        F.conv2d, F.batch_norm, F.interpolate = oc, ob, oi
+
+
 def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True):
     """One train step (forward, CE(ignore -1), backward) of the oracle: fp64 when ``emulate`` is
     False, else fp32 with every conv input / weight / output rounded to bf16 — and, because

@@ -189,17 +189,24 @@ def test_pw_gemm_residual_in_place(dt, M, N, K):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_gemm_bn_statistics(dt):
-    M, N, K = 3001, 96, 64
+@pytest.mark.parametrize("M,N,K", [(3001, 96, 64), (20001, 48, 32), (70000, 64, 64)])
+def test_gemm_bn_statistics(dt, M, N, K):
+    """Tiled (M < 4096: one record per 128-row tile) and streaming (one shifted-sum record per
+    workgroup) statistics forms; the call reports how many records it writes."""
     A = rnd(M, K, seed=20) + 3.0  # large mean: catches E[x^2]-E[x]^2 cancellation
     B = rnd(N, K, seed=21, scale=0.2)
     z = A.to(dt).float() @ B.to(dt).float().t()
-    parts = (M + 127) // 128
-    part = torch.empty(parts * 3 * N, dtype=torch.float32, device=DEV)
+    slots = (M + 127) // 128
+    parts = _lib.load().fscnn_pw_gemm_stats_parts(M, N, K, K, N, _lib.dtype_code(dt))
+    assert 1 <= parts <= slots
+    part = torch.full((slots * 3 * N,), float("nan"), dtype=torch.float32, device=DEV)
     C = torch.empty(M, N, dtype=dt, device=DEV)
     Ad, Bd = A.to(dt).to(DEV), B.to(dt).to(DEV)
     _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(Ad), K, _lib.ptr(Bd),
               K, 0, None, None, None, 0, 0, _lib.ptr(C), N, _lib.ptr(part), _lib.dtype_code(dt), S())
+    sync()
+    close(C.float(), z, TOL[dt] * (10 if dt == torch.float32 else 1))
+    assert torch.isfinite(part[:parts * 3 * N]).all()  # every reported record written
     gamma, beta = (rnd(N, seed=22).abs() + 0.5).to(DEV), rnd(N, seed=23).to(DEV)
     rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
     nbt = torch.zeros(1, dtype=torch.int64, device=DEV)

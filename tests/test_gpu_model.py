@@ -185,6 +185,31 @@ def test_train_fp32_bnrand_vs_oracle():
     _check_grads(m, gref, 19)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 256, 512), (2, 3, 512, 1024)])
+def test_train_fp32_streaming_sizes_vs_oracle(shape):
+    """Sizes where the 1x1 convs of the LearningToDownsample, the first bottleneck and the FFM
+    take the streaming GEMM (M >= 4096 pixels): its per-workgroup BN statistics records, the lazy
+    BN+ReLU of its A operand and the fused BN-backward partials of its dgrads, against the fp64
+    oracle under the same contract as the golden cases (running statistics included)."""
+    sd = portable_sd(19, variant="bnrand")
+    g = {"shape": np.array(shape), "num_classes": np.int64(19), "seed_w": np.int64(0),
+         "seed_x": np.int64(5), "seed_t": np.int64(6), "ignore_frac": np.float64(0.05),
+         "drop_seed": np.int64(99), "variant": np.array("bnrand"), "aux": np.int64(0)}
+    m = make_model(sd, 19).train()
+    m._dropout_seed = 99
+    from fast_scnn_pytorch_amd.loss import cross_entropy
+    x, t = golden_input(g), golden_target(g)
+    loss = cross_entropy(m(x.to(DEV))[0], t.to(DEV))
+    loss.backward()
+    lref, gref, stats = oracle_train(sd, x, t, 19, 99)
+    assert abs(loss.item() - lref) < 1e-5 * max(1.0, abs(lref))
+    _check_grads(m, gref, 19)
+    msd = m.state_dict()
+    for k, v in stats.items():
+        np.testing.assert_allclose(msd[k].cpu().double().numpy(), v.detach().double().numpy(),
+                                   rtol=1e-4, atol=1e-5, err_msg=k)
+
+
 def test_sgd_step_matches_torch_semantics():
     g = load_golden("train_c19")
     m, _ = _hip_train_step(g)
