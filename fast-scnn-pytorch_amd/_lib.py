@@ -64,6 +64,9 @@ SIGNATURES = {
     "fscnn_prof_begin": (c_int, [c_int, c_int]),
     "fscnn_prof_end": (c_int, [ctypes.POINTER(ctypes.c_double), P_ll, ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_double)]),
+    "fscnn_prof_launch": (c_int, [c_ll, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_float),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(c_char_p)]),
     "fscnn_prof_kind_name": (c_char_p, [c_int]),
     "fscnn_ce_parts": (c_ll, [c_int, c_ll]),
     "fscnn_ce_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp, c_vp]),

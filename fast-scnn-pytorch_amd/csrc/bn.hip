@@ -9,11 +9,9 @@
 //        bn_apply normalises (+ residual / second branch, + ReLU).
 // backward: bn_bwd_reduce (per-block sums of dy_r and dy_r*xhat) -> bn_bwd_finalize
 //        (dgamma, dbeta into the gradient arena + coefficients) -> bn_bwd_apply (dz).
-#include "kernels.hpp"
+#include "bn_finish.hpp"
 
 namespace fscnn {
-
-constexpr float BN_EPS = 1e-5f;
 
 // ---- eval fold of every BN in one launch ------------------------------------------------------
 
@@ -137,23 +135,7 @@ __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q
     s1 += sh[1][t][cx];
     s2 += sh[2][t][cx];
   }
-  const double mu = n > 0.0 ? s1 / n : 0.0;
-  const double m2 = n > 0.0 ? fmax(s2 - n * mu * mu, 0.0) : 0.0;
-  const double mean = mu + (a.bias ? (double)a.bias[c] : 0.0);
-  const double var = n > 0 ? m2 / n : 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)BN_EPS));
-  const float scale = a.gamma[c] * invstd;
-  a.mean[c] = (float)mean;
-  a.invstd[c] = invstd;
-  a.scale[c] = scale;
-  a.shift[c] = a.beta[c] - (float)mean * scale;
-  if (a.rmean) {
-    const float m = a.momentum;
-    a.rmean[c] = (1.f - m) * a.rmean[c] + m * (float)mean;
-    const float unb = n > 1 ? (float)(m2 / (n - 1.0)) : (float)var;
-    a.rvar[c] = (1.f - m) * a.rvar[c] + m * unb;
-  }
-  if (a.nbt && c == 0) a.nbt[0] += 1;
+  bn_fwd_finish(a, c, n, s1, s2);
 }
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
@@ -434,23 +416,7 @@ __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, 
     s1 += sh[0][t][cx];
     s2 += sh[1][t][cx];
   }
-  if (dbeta) dbeta[c] = (float)s1;
-  if (dgamma) dgamma[c] = (float)s2;
-  const float c0 = (float)(s1 / count), c1 = (float)(s2 / count);
-  coef[c] = c0;
-  coef[C + c] = c1;
-  if (t.tab) {  // dz = scale*(dy_r - c0 - (z - mean)*invstd*c1) = al*dy_r + gz*z + be
-    const float sc = t.scale[c];
-    const float gz = -sc * c1 * t.invstd[c];
-    float4 v;
-    v.x = sc;
-    v.y = -sc * c0 - gz * t.mean[c];
-    v.z = gz;
-    v.w = t.relu ? sc : 0.f;
-    float* e = t.tab + (size_t)c * BWDX_STRIDE;
-    *reinterpret_cast<float4*>(e) = v;
-    e[4] = t.relu ? t.shift[c] : 1.f;
-  }
+  bn_bwd_finish(c, C, s1, s2, count, dgamma, dbeta, coef, t);
 }
 
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* part, int Q, int C,

@@ -31,9 +31,13 @@ int check_launch(const char* what) {
 
 // ---- launch profiler --------------------------------------------------------------------
 int g_prof_kind = PK_NONE;
+const char* g_prof_tag = "";
 namespace {
 struct ProfState {
   std::vector<hipEvent_t> ev;  // pairs
+  std::vector<int> kind;       // per recorded launch
+  std::vector<std::string> tag;
+  std::vector<double> lbytes, lflops;
   size_t used = 0;
   double bytes = 0, flops = 0;
   long long launches = 0;
@@ -45,10 +49,14 @@ void prof_start(hipStream_t st) {
   if (g_prof.used + 2 > g_prof.ev.size()) { g_prof.overflow = true; return; }
   (void)hipEventRecord(g_prof.ev[g_prof.used], st);
 }
-void prof_stop(hipStream_t st, double bytes, double flops) {
+void prof_stop(hipStream_t st, int kind, double bytes, double flops) {
   if (g_prof.used + 2 > g_prof.ev.size()) return;
   (void)hipEventRecord(g_prof.ev[g_prof.used + 1], st);
   g_prof.used += 2;
+  g_prof.kind.push_back(kind);
+  g_prof.tag.emplace_back(g_prof_tag ? g_prof_tag : "");
+  g_prof.lbytes.push_back(bytes);
+  g_prof.lflops.push_back(flops);
   g_prof.bytes += bytes;
   g_prof.flops += flops;
   g_prof.launches++;
@@ -59,7 +67,11 @@ void prof_stop(hipStream_t st, double bytes, double flops) {
 using namespace fscnn;
 
 extern "C" int fscnn_prof_begin(int kind, int max_launches) {
-  if (kind <= PK_NONE || kind >= PK_COUNT || max_launches <= 0) {
+  if ((kind <= PK_NONE || kind >= PK_COUNT) && kind != PK_ALL) {
+    set_error("fscnn_prof_begin: bad kind %d", kind);
+    return E_INVALID;
+  }
+  if (max_launches <= 0) {
     set_error("fscnn_prof_begin: bad kind %d", kind);
     return E_INVALID;
   }
@@ -70,6 +82,7 @@ extern "C" int fscnn_prof_begin(int kind, int max_launches) {
     g_prof.ev.push_back(e);
   }
   g_prof.used = 0; g_prof.bytes = 0; g_prof.flops = 0; g_prof.launches = 0;
+  g_prof.kind.clear(); g_prof.tag.clear(); g_prof.lbytes.clear(); g_prof.lflops.clear();
   g_prof.overflow = false;
   g_prof_kind = kind;
   return OK;
@@ -94,6 +107,27 @@ extern "C" int fscnn_prof_end(double* total_ms, long long* launches, double* byt
   if (bytes) *bytes = g_prof.bytes;
   if (flops) *flops = g_prof.flops;
   if (g_prof.overflow) { set_error("fscnn_prof_end: event pool overflow"); return E_INVALID; }
+  return OK;
+}
+
+// One recorded launch of the last fscnn_prof_begin / _end window (after _end): its kind, kernel
+// time, algorithmic bytes / flops and the executor's layer label.
+extern "C" int fscnn_prof_launch(long long i, int* kind, float* ms, double* bytes, double* flops,
+                                 const char** tag) {
+  if (i < 0 || (size_t)i >= g_prof.kind.size()) {
+    set_error("fscnn_prof_launch: index %lld out of range (%zu recorded)", i, g_prof.kind.size());
+    return E_INVALID;
+  }
+  float t = 0;
+  if (hipEventElapsedTime(&t, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]) != hipSuccess) {
+    set_error("fscnn_prof_launch: event query failed");
+    return E_HIP;
+  }
+  if (kind) *kind = g_prof.kind[i];
+  if (ms) *ms = t;
+  if (bytes) *bytes = g_prof.lbytes[i];
+  if (flops) *flops = g_prof.lflops[i];
+  if (tag) *tag = g_prof.tag[i].c_str();  // valid until the next fscnn_prof_begin
   return OK;
 }
 

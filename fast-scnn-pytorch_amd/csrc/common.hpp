@@ -352,19 +352,23 @@ enum ProfKind : int {
   PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_CONV0_WGRAD, PK_BN_BWD_RED, PK_BN_FIN,
   PK_COUNT
 };
+constexpr int PK_ALL = 100;  // record every kind (per-launch layer report)
 extern int g_prof_kind;  // kind being recorded (PK_NONE = off)
+extern const char* g_prof_tag;  // layer the executor is issuing (per-launch report label)
 void prof_start(hipStream_t st);
-void prof_stop(hipStream_t st, double bytes, double flops);
+void prof_stop(hipStream_t st, int kind, double bytes, double flops);
 struct ProfScope {
   bool on;
+  int kind;
   hipStream_t st;
   double bytes, flops;
-  ProfScope(int kind, hipStream_t s, double b, double f)
-      : on(g_prof_kind == kind), st(s), bytes(b), flops(f) {
+  ProfScope(int k, hipStream_t s, double b, double f)
+      : on(g_prof_kind == k || (g_prof_kind == PK_ALL && k != PK_NONE)), kind(k), st(s), bytes(b),
+        flops(f) {
     if (on) prof_start(st);
   }
   ~ProfScope() {
-    if (on) prof_stop(st, bytes, flops);
+    if (on) prof_stop(st, kind, bytes, flops);
   }
 };
 

@@ -508,6 +508,9 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   }
 }
 
+static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool ax, bool bs,
+                         hipStream_t st);
+
 int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) {
@@ -531,9 +534,6 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   const bool ax = a.atab != nullptr;
-  ProfScope ps(PK_GEMM_NT, st,
-               E * (M * K * (ax ? 2 : 1) + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
-               2.0 * M * N * K);
   if (ax && (!a.az || a.a_scale || a.b_trans || a.K % V)) {
     set_error("gemm_nt: BN-backward A transform needs z, a plain B and K %% %d == 0", V);
     return E_UNSUPPORTED;
@@ -555,7 +555,34 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     set_error("gemm_nt: fused BN-backward partials need a non-transposed B");
     return E_UNSUPPORTED;
   }
-  if (use_stream(a, dtype)) return gemm_stream(a, dtype, st);
+  if (a.tail.counters && !a.part && !a.bpart) {
+    set_error("gemm_nt: a BN finish needs statistics records (part or bpart)");
+    return E_INVALID;
+  }
+  const bool stream = use_stream(a, dtype);
+  int rc;
+  {
+    ProfScope ps(PK_GEMM_NT, st,
+                 E * (M * K * (ax ? 2 : 1) + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
+                 2.0 * M * N * K);
+    rc = stream ? gemm_stream(a, dtype, st)  // finishes the BN in-kernel (last workgroup)
+                : gemm_nt_tiled(a, dtype, nt, at, ax, bs, st);
+  }
+  if (rc || stream || !a.tail.counters) return rc;
+  // tiled path: the BN finish as its own (fold + finalize) launch over the per-tile records
+  if (a.part) {
+    BnFinalizeArgs f = a.tail.fwd;
+    f.part = a.part; f.P = gemm_parts(a.M); f.C = a.N; f.counters = a.tail.counters;
+    return bn_finalize(f, st);
+  }
+  if (a.bpart)
+    return bn_bwd_finalize(a.bpart, gemm_parts(a.M), a.N, a.tail.count, a.tail.dgamma,
+                           a.tail.dbeta, a.tail.coef, st, a.tail.counters, a.tail.tab);
+  return OK;
+}
+
+static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool ax, bool bs,
+                         hipStream_t st) {
   if (dtype == DT_F16) {  // inference plans only: plain forward GEMMs
     if (a.b_trans || bs || at || ax || a.part) {
       set_error("gemm_nt: fp16 arithmetic is inference-only");

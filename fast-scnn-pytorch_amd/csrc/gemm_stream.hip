@@ -27,7 +27,7 @@
 //       (rounded) output, the mask recomputed from that BN's z -> bpart[bi][2][N].
 // The k summation order inside a 16x16xK MFMA step matches gemm_nt (4-element k quads for fp32,
 // 8-element for 16-bit, steps in increasing k).
-#include "kernels.hpp"
+#include "bn_finish.hpp"
 
 namespace fscnn {
 
@@ -91,6 +91,104 @@ __device__ __forceinline__ float gs_rowsum(float v) {
   return v;
 }
 
+// In-kernel BN finish (GemmArgs::tail).  Two arrival levels keep every fold one batch of loads
+// deep (a single finisher walking all bpg <= 512 records was a chain of ~25 dependent sc1 round
+// trips): workgroups arrive in teams of GS_TEAM; a team's last arriver folds the team's records
+// into the team's first slot (in place, write-through) and arrives on the column group's
+// counter; the group's last arriver folds the team records and finishes each channel with the
+// finalize kernels' arithmetic (bn_finish.hpp).  Folds are fp64 sums in fixed order (thread
+// slice sl takes records sl, sl + S, ... in increasing order; slices summed in order).
+constexpr int GS_TEAM = 16;
+constexpr int GS_CTR_TEAMS = 64;  // counters: [0, 64) groups, then 32 teams per group
+
+template <bool FWD>
+__device__ inline void gs_fold(const GemmArgs& a, int n0, int BN, int first, int count, int stride,
+                               double (&sum)[3]) {
+  __shared__ double s_f[3][256];
+  const int tid = threadIdx.x;
+  const int S = 256 / BN;
+  const int col = tid % BN, sl = tid / BN;
+  const int n = n0 + col;
+  const int N = a.N;
+  const float* base = FWD ? a.part : a.bpart;
+  constexpr int R = FWD ? 3 : 2;
+  constexpr int U = FWD ? 8 : 4;  // records per thread per batch (all loads issued before the sums)
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+  if (sl < S && n < N) {
+    for (int i0 = sl; i0 < count; i0 += U * S) {
+      float v[U][R];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * S;
+        const float* rec = base + (size_t)(first + (i < count ? i : i0) * stride) * R * N;
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[u][j] = ld_wt(rec + (size_t)j * N + n);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + u * S >= count) break;
+        if constexpr (FWD) {  // (mean, M2, count) -> (n, n*mean, M2 + n*mean^2)
+          const double cn = v[u][2], m = v[u][0];
+          t0 += cn;
+          t1 += cn * m;
+          t2 += (double)v[u][1] + cn * m * m;
+        } else {
+          t1 += v[u][0];
+          t2 += v[u][1];
+        }
+      }
+    }
+  }
+  s_f[0][tid] = t0;
+  s_f[1][tid] = t1;
+  s_f[2][tid] = t2;
+  __syncthreads();
+  sum[0] = sum[1] = sum[2] = 0.0;
+  if (sl == 0) {
+    for (int j = 0; j < S; ++j) {
+      sum[0] += s_f[0][j * BN + col];
+      sum[1] += s_f[1][j * BN + col];
+      sum[2] += s_f[2][j * BN + col];
+    }
+  }
+  __syncthreads();  // s_f reusable by the next fold
+}
+
+template <bool FWD>
+__device__ inline void gs_finish(const GemmArgs& a, int g, int bi, int n0, int BN, int bpg) {
+  unsigned* ctr = a.tail.counters;
+  const int team = bi / GS_TEAM, nteam = cdiv(bpg, GS_TEAM);
+  const int tsize = min(GS_TEAM, bpg - team * GS_TEAM);
+  const int tid = threadIdx.x, col = tid % BN, n = n0 + col;
+  const bool owner = tid < BN && n < a.N;  // slice 0 holds the folded sums
+  if (!arrive_last(ctr + GS_CTR_TEAMS + g * 32 + team, (unsigned)tsize)) return;
+  double s[3];
+  gs_fold<FWD>(a, n0, BN, team * GS_TEAM, tsize, 1, s);
+  if (owner) {  // the team record replaces slot team * GS_TEAM (every other reader is done)
+    const int N = a.N;
+    if constexpr (FWD) {
+      float* rec = a.part + (size_t)team * GS_TEAM * 3 * N;
+      const double mean = s[0] > 0.0 ? s[1] / s[0] : 0.0;
+      st_wt(rec + n, (float)mean);
+      st_wt(rec + N + n, s[0] > 0.0 ? (float)fmax(s[2] - s[0] * mean * mean, 0.0) : 0.f);
+      st_wt(rec + 2 * N + n, (float)s[0]);
+    } else {
+      float* rec = a.bpart + (size_t)team * GS_TEAM * 2 * N;
+      st_wt(rec + n, (float)s[1]);
+      st_wt(rec + N + n, (float)s[2]);
+    }
+  }
+  reset_counter(ctr + GS_CTR_TEAMS + g * 32 + team);
+  if (!arrive_last(ctr + g, (unsigned)nteam)) return;
+  gs_fold<FWD>(a, n0, BN, 0, nteam, GS_TEAM, s);
+  if (owner) {
+    if constexpr (FWD) bn_fwd_finish(a.tail.fwd, n, s[0], s[1], s[2]);
+    else bn_bwd_finish(n, a.N, s[1], s[2], a.tail.count, a.tail.dgamma, a.tail.dbeta,
+                       a.tail.coef, a.tail.tab);
+  }
+  reset_counter(ctr + g);
+}
+
 // NT: 16-column MFMA tiles per group; KS: k-steps (16 fp32 / 32 16-bit k each) covering K
 template <typename T, int NT, int KS, bool TAIL, bool AT, bool ST, bool BS>
 __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg) {
@@ -104,6 +202,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   float* s_sc = reinterpret_cast<float*>(s_w + BN * WST);       // [BN] scale, [BN] shift
   float* s_at = s_sc + 2 * BN;                                  // AT: [GS_KMAX] scale, shift
   float* s_bc = s_at + (AT ? 2 * GS_KMAX : 0);                  // BS: [4][BN] mean/istd/sc/sh
+  float* s_shf = s_bc + (BS ? 4 * BN : 0);                       // ST: [4 waves][BN] shifts
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -151,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   int c = bi * 4 + wave;
 
   // sums of channels n0 + 16nt + 4lq + r over this lane's pixels (ST: shifted by shf)
-  float s1[SUMS ? NT : 1][4], s2[SUMS ? NT : 1][4], shf[ST ? NT : 1][4];
+  float s1[SUMS ? NT : 1][4], s2[SUMS ? NT : 1][4];
   float cnt = 0.f;
   if constexpr (SUMS) {
 #pragma unroll
@@ -159,11 +258,10 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 #pragma unroll
       for (int r = 0; r < 4; ++r) { s1[nt][r] = 0.f; s2[nt][r] = 0.f; }
   }
+  // ST shift of each channel: its value at the wave's first pixel, kept in LDS (s_shf[wave])
+  float* wshf = s_shf + wave * BN;
   if constexpr (ST) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) shf[nt][r] = 0.f;
+    for (int i = lane; i < BN; i += 64) wshf[i] = 0.f;
   }
   bool first = true;
 
@@ -239,13 +337,15 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     if constexpr (!TAIL) {  // whole 4-channel vectors, 16-B aligned rows (checked on the host)
       if constexpr (ST) {
         if (first) {  // per-channel shift: the value at the wave's first pixel (lane li = 0)
+          if (li == 0) {
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) {
-            const int nl = nt * 16 + 4 * lq;
+            for (int nt = 0; nt < NT; ++nt) {
+              const int nl = nt * 16 + 4 * lq;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              shf[nt][r] = __shfl(acc[0][nt][r] * ssc[nl + r] + ssc[BN + nl + r], lane & 48);
+              for (int r = 0; r < 4; ++r) wshf[nl + r] = acc[0][nt][r] * ssc[nl + r] + ssc[BN + nl + r];
+            }
           }
+          __builtin_amdgcn_wave_barrier();
           first = false;
         }
       }
@@ -272,12 +372,17 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
           const float4 sc = *reinterpret_cast<const float4*>(ssc + nl);
           const float4 sh = *reinterpret_cast<const float4*>(ssc + BN + nl);
           const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+          float shf[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (ST) {
+            const float4 t = *reinterpret_cast<const float4*>(wshf + wz + nl);
+            shf[0] = t.x; shf[1] = t.y; shf[2] = t.z; shf[3] = t.w;
+          }
           float o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[mt][nt][r] * scv[r] + shv[r];
             if constexpr (ST) {  // statistics of the unrounded value (gemm_nt's convention)
-              const float d = mok ? v - shf[nt][r] : 0.f;
+              const float d = mok ? v - shf[r] : 0.f;
               s1[nt][r] += d;
               s2[nt][r] += d * d;
             }
@@ -342,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
         if (li == 0) {
           const int col = nt * 16 + 4 * lq + r;
           if constexpr (ST) {  // (count, mean, M2) of the wave from its shifted sums
-            const float mean = cnt > 0.f ? shf[nt][r] + t1 / cnt : 0.f;
+            const float mean = cnt > 0.f ? wshf[col] + t1 / cnt : 0.f;
             const float m2 = cnt > 0.f ? fmaxf(t2 - t1 * (t1 / cnt), 0.f) : 0.f;
             red[(wave * 3 + 0) * BN + col] = cnt;
             red[(wave * 3 + 1) * BN + col] = mean;
@@ -369,10 +474,10 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
           m2 += qb + d * d * (nn * nb / tot);
           nn = tot;
         }
-        float* rec = a.part + (size_t)bi * 3 * a.N;
-        rec[n] = mean;
-        rec[a.N + n] = m2;
-        rec[2 * a.N + n] = nn;
+        float* rec = a.part + (size_t)bi * 3 * a.N;  // write-through: read by the finisher
+        st_wt(rec + n, mean);
+        st_wt(rec + a.N + n, m2);
+        st_wt(rec + 2 * a.N + n, nn);
       } else {
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll
@@ -381,19 +486,24 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
           t2 += red[(w * 3 + 1) * BN + col];
         }
         float* rec = a.bpart + (size_t)bi * 2 * a.N;
-        rec[n] = t1;
-        rec[a.N + n] = t2;
+        st_wt(rec + n, t1);
+        st_wt(rec + a.N + n, t2);
       }
     }
+    // ---- in-kernel finish by the column group's last workgroup (no finalize launch) ---------
+    if (a.tail.counters) gs_finish<ST>(a, g, bi, n0, BN, bpg);
   }
 }
 
-static int gs_pick_nt(int N, bool sums) {
+// column tile: the dgrad partial sums also hold a z row (NT <= 4); the forward statistics fit
+// NT = 6 (NT = 8 spills)
+static int gs_pick_nt(const GemmArgs& a) {
+  const int N = a.N;
   if (N <= 32) return 2;
   if (N <= 48) return 3;
-  if (N <= 64 || sums) return 4;  // the statistics forms keep 2-3 x 4 x NT sum registers
+  if (N <= 64 || a.bpart) return 4;
   if (N % 96 == 0) return 6;
-  return 8;
+  return a.part ? 4 : 8;
 }
 
 static bool gs_tail_needed(const GemmArgs& a, int nt) {
@@ -404,6 +514,7 @@ static size_t gs_lds(const GemmArgs& a, int nt, int ks) {
   size_t b = (size_t)16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4;
   if (a.a_scale) b += (size_t)2 * GS_KMAX * 4;
   if (a.bpart) b += (size_t)4 * 16 * nt * 4;
+  if (a.part) b += (size_t)4 * 16 * nt * 4;
   return b;  // >= the end-of-kernel reduction scratch [4][3][16 nt] (aliases the weights)
 }
 
@@ -418,11 +529,14 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   if (dtype == DT_F16 && (sums || a.a_scale)) return false;
   if (!(ks == 1 || ks == 2 || ks == 3 || ks == 4 || ks == 6 || ks == 8)) return false;
   if (sums && ks > 4) return false;  // keep the statistics forms within 256 VGPRs
-  const int nt = gs_pick_nt(a.N, sums);
+  const int nt = gs_pick_nt(a);
+  if (a.part && nt > 4 && ks > 2) return false;
   if (a.bpart && dtype == DT_F32 && nt == 4 && ks > 2) return false;  // would spill
   if (gs_tail_needed(a, nt) && (nt != 2 || sums)) return false;  // scalar tail: N <= 32 only
   if (a.bpart && (!a.bz || a.ldbz % 4 || (a.bmode != 0 && a.bmode != 2))) return false;
   if (gs_lds(a, nt, ks) > 72 * 1024) return false;
+  // in-kernel BN finish: group counters [0, 64), 32 team counters per group after them
+  if (a.tail.counters && GS_CTR_TEAMS + 32 * cdiv(a.N, 16 * nt) > BN_COUNTERS) return false;
   return a.M >= 4096;  // tiny GEMMs (PPM bins): loading a weight slice per block does not pay
 }
 
@@ -430,17 +544,22 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
 static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   const int KC = dtype == DT_F32 ? 16 : 32;
   ks = cdiv(a.K, KC);
-  nt = gs_pick_nt(a.N, a.part || a.bpart);
+  nt = gs_pick_nt(a);
   const int groups = cdiv(a.N, 16 * nt);
   lds = gs_lds(a, nt, ks);
   const int nchunks = cdiv(a.M, GS_MW);
   // resident workgroups: LDS-limited (160 KB / CU), at most 2 per CU (measured: 3-4 slower)
+  static const int cap = [] {  // FSCNN_GS_PER_CU: tuning override of the residency cap
+    const char* e = getenv("FSCNN_GS_PER_CU");
+    return e ? atoi(e) : 2;
+  }();
   int per_cu = (int)((160 * 1024) / (lds + 1024));
-  per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
+  per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
   int bpg = cdiv(256 * per_cu, groups);
   bpg = (bpg + 7) / 8 * 8;
   const int need = cdiv(nchunks, 4);  // <= cdiv(M, 128) = gemm_parts(M): fits the record slots
   if (bpg > need) bpg = need;
+  if (bpg > GS_TEAM * 32) bpg = GS_TEAM * 32;  // the finish's team counters (32 per group)
   if (bpg < 1) bpg = 1;
   return bpg;
 }
@@ -455,11 +574,16 @@ template <typename T, int NT, bool TAIL, bool AT, bool ST, bool BS>
 static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int bpg,
                          hipStream_t st) {
   constexpr bool SUMS = ST || BS;
+  constexpr bool WIDE = SUMS && NT > 4;  // wide statistics tiles: K <= 2 k-steps only
   switch (ks) {
     case 1: gemm_stream_kernel<T, NT, 1, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
     case 2: gemm_stream_kernel<T, NT, 2, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 3: gemm_stream_kernel<T, NT, 3, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 4: gemm_stream_kernel<T, NT, 4, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
+    case 3:
+      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 3, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      break;
+    case 4:
+      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 4, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      break;
     case 6:
       if constexpr (!SUMS) gemm_stream_kernel<T, NT, 6, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
       break;
@@ -481,7 +605,7 @@ static void gs_launch_nt(const GemmArgs& a, int nt, int ks, dim3 grid, size_t ld
     case 3: gs_launch_ks<T, 3, false, AT, ST, BS>(a, ks, grid, lds, bpg, st); break;
     case 4: gs_launch_ks<T, 4, false, AT, ST, BS>(a, ks, grid, lds, bpg, st); break;
     case 6:
-      if constexpr (!SUMS) gs_launch_ks<T, 6, false, AT, false, false>(a, ks, grid, lds, bpg, st);
+      if constexpr (!BS) gs_launch_ks<T, 6, false, AT, ST, false>(a, ks, grid, lds, bpg, st);
       break;
     default:
       if constexpr (!SUMS) gs_launch_ks<T, 8, false, AT, false, false>(a, ks, grid, lds, bpg, st);
@@ -497,6 +621,10 @@ static void gs_launch(const GemmArgs& a, int dtype, hipStream_t st) {
   const int groups = cdiv(a.N, 16 * nt);
   dim3 grid((unsigned)(groups * bpg));
   const bool at = a.a_scale != nullptr;
+  if constexpr (std::is_same<T, f16>::value) {  // inference only (checked by the caller)
+    gs_launch_nt<T, false, false, false>(a, nt, ks, grid, lds, bpg, st);
+    return;
+  }
   if (a.bpart) gs_launch_nt<T, false, false, true>(a, nt, ks, grid, lds, bpg, st);
   else if (a.part && at) gs_launch_nt<T, true, true, false>(a, nt, ks, grid, lds, bpg, st);
   else if (a.part) gs_launch_nt<T, false, true, false>(a, nt, ks, grid, lds, bpg, st);

@@ -56,6 +56,50 @@ struct DwBwdArgs {
   const float* x_shift = nullptr;
 };
 
+struct BnFinalizeArgs {
+  float* part;        // [P][3][C] (mean, M2, count); consumed (folded in place)
+  int P, C;
+  const float* gamma;
+  const float* beta;
+  float* rmean;       // running stats, updated in place (or null)
+  float* rvar;
+  long long* nbt;     // num_batches_tracked (or null)
+  float momentum;
+  const float* bias;  // conv bias to add to the batch mean (stats taken before the bias) or null
+  float* mean;        // [C] saved for backward
+  float* invstd;      // [C]
+  float* scale;       // [C] gamma*invstd
+  float* shift;       // [C] beta - mean*scale
+  unsigned* counters = nullptr;  // >= cdiv(C,64) zeroed arrival counters: one-launch fold+finalize
+};
+
+struct BnBwdTab {
+  float* tab = nullptr;
+  const float* scale = nullptr;
+  const float* shift = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  int relu = 0;
+};
+
+// In-kernel BatchNorm finish of a GEMM producer: the last-arriving workgroup of each column
+// group folds that group's records and writes the finished per-channel values, so no separate
+// finalize launch sits between producer and consumer.  Forward (GemmArgs::part): fwd's gamma ..
+// shift (part / P / C / counters are the GEMM's own).  Backward (GemmArgs::bpart): dgamma /
+// dbeta into the gradient arena, the apply coefficients coef [2][C] and, when tab.tab is set,
+// the BN-backward operand table.  When gemm_nt takes its tiled path it runs the separate
+// finalize itself, so callers see the same result either way.
+constexpr int BN_COUNTERS = 512;  // arrival counters per direction (zeroed each step)
+struct BnTail {
+  unsigned* counters = nullptr;  // BN_COUNTERS zeroed counters; null: no finish (records only)
+  BnFinalizeArgs fwd{};
+  double count = 0.0;
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+  float* coef = nullptr;
+  BnBwdTab tab{};
+};
+
 struct GemmArgs {
   int M, N, K;
   const void* A;
@@ -87,6 +131,7 @@ struct GemmArgs {
   // stored): A is dy, az the saved pre-BN tensor [M][K] (ld K), atab [K][BWDX_STRIDE]
   const void* az = nullptr;
   const float* atab = nullptr;
+  BnTail tail{};        // in-kernel finish of the BN whose records this GEMM writes
 };
 
 struct GemmTnArgs {
@@ -120,22 +165,6 @@ struct FoldTable {
   FoldEntry e[MAX_FOLD];
 };
 
-struct BnFinalizeArgs {
-  float* part;        // [P][3][C] (mean, M2, count); consumed (folded in place)
-  int P, C;
-  const float* gamma;
-  const float* beta;
-  float* rmean;       // running stats, updated in place (or null)
-  float* rvar;
-  long long* nbt;     // num_batches_tracked (or null)
-  float momentum;
-  const float* bias;  // conv bias to add to the batch mean (stats taken before the bias) or null
-  float* mean;        // [C] saved for backward
-  float* invstd;      // [C]
-  float* scale;       // [C] gamma*invstd
-  float* shift;       // [C] beta - mean*scale
-  unsigned* counters = nullptr;  // >= cdiv(C,64) zeroed arrival counters: one-launch fold+finalize
-};
 
 struct BnApplyArgs {
   long long M;
@@ -318,14 +347,6 @@ int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
 int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);
 // tab (optional): the per-channel operand-transform table of common.hpp bwdx_apply, built from
 // the forward BN (scale, shift, mean, invstd; relu: the ReLU mask is recomputed from z)
-struct BnBwdTab {
-  float* tab = nullptr;
-  const float* scale = nullptr;
-  const float* shift = nullptr;
-  const float* mean = nullptr;
-  const float* invstd = nullptr;
-  int relu = 0;
-};
 int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, float* dbeta,
                     float* coef, hipStream_t st, unsigned* counters = nullptr,
                     const BnBwdTab& tab = BnBwdTab());

@@ -268,6 +268,22 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.aux_drop = train ? A.get((size_t)M2 * 32 * E) : pl.aux0.a;
     pl.aux_logits = A.get((size_t)M2 * pl.Cp * E);
   }
+  // labels: models/fast_scnn.py module paths
+  pl.c0.name = "learning_to_downsample.conv";
+  pl.l1dw.name = "learning_to_downsample.dsconv1.dw"; pl.l1pw.name = "learning_to_downsample.dsconv1.pw";
+  pl.l2dw.name = "learning_to_downsample.dsconv2.dw"; pl.l2pw.name = "learning_to_downsample.dsconv2.pw";
+  for (int i = 0; i < 9; ++i) {
+    const std::string b = "global_feature_extractor.bottleneck" + std::to_string(i / 3 + 1) + "." +
+                          std::to_string(i % 3);
+    pl.lbe[i].name = b + ".expand"; pl.lbd[i].name = b + ".dw"; pl.lbp[i].name = b + ".project";
+  }
+  for (int i = 0; i < 4; ++i) pl.ppk[i].name = "global_feature_extractor.ppm.conv" + std::to_string(i + 1);
+  pl.po.name = "global_feature_extractor.ppm.out";
+  pl.fdw.name = "feature_fusion.dwconv"; pl.flow.name = "feature_fusion.conv_lower_res";
+  pl.fhigh.name = "feature_fusion.conv_higher_res";
+  pl.c1dw.name = "classifier.dsconv1.dw"; pl.c1pw.name = "classifier.dsconv1.pw";
+  pl.c2dw.name = "classifier.dsconv2.dw"; pl.c2pw.name = "classifier.dsconv2.pw";
+  pl.aux0.name = "auxlayer";
   if (train) {
     pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
@@ -276,8 +292,8 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.seed_slot = A.get(64);
     // arrival counters of the one-launch BN fold+finalize (forward and backward), zeroed by the
     // step's weights_prep launch and left zero by every launch that uses them
-    pl.fcnt = A.get(2 * 64 * 4);
-    pl.bcnt = pl.fcnt + 64 * 4;
+    pl.fcnt = A.get(2 * BN_COUNTERS * 4);
+    pl.bcnt = pl.fcnt + BN_COUNTERS * 4;
   }
   if (train && lazy_bn_enabled()) {
     // BN+ReLU outputs whose only consumers are GEMM / depthwise operands (and the wgrads reading
@@ -308,6 +324,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   for (int i = 0; i < 4; ++i) nu("ppk" + std::to_string(i), pl.ppk[i]);
   nu("po", pl.po); nu("fdw", pl.fdw); nu("flow", pl.flow); nu("fhigh", pl.fhigh);
   nu("c1dw", pl.c1dw); nu("c1pw", pl.c1pw); nu("c2dw", pl.c2dw); nu("c2pw", pl.c2pw);
+  if (net.aux) nu("aux0", pl.aux0);
   nm("concat", pl.concat, M5, 256, 256, 0);
   nm("up_low", pl.up_low, M2, 128, 128, 0);
   nm("f", pl.f, M2, 128, 128, 0);
@@ -443,6 +460,7 @@ namespace {
 // fused BN-backward partials: the dgrad GEMM producing the dy of unit `u` emits its records
 struct BTarget {
   const Unit* u = nullptr;
+  const BnL* bn = nullptr;
   int mode = 0;  // 0 no ReLU, 2 relu_z (mask recomputed from z)
 };
 
@@ -492,8 +510,9 @@ struct Exec {
       add(net.ppm_o); add(net.ffm_low); add(net.ffm_high);
       add(net.cls1.pw); add(net.cls2.pw); add(net.cls_out);
       if (net.aux) { add(net.aux0); add(net.aux4); }
-      PrepJob& z = t.j[t.n++];  // BN arrival counters (fcnt, bcnt: 2 x 64 uint32)
-      z.src = 0; z.dst = (long long)(pl.fcnt / E); z.R = 1; z.Cc = (int)(2 * 64 * 4 / E); z.ld = 0;
+      PrepJob& z = t.j[t.n++];  // BN arrival counters (fcnt, bcnt: 2 x BN_COUNTERS uint32)
+      z.src = 0; z.dst = (long long)(pl.fcnt / E); z.R = 1; z.Cc = (int)(2 * BN_COUNTERS * 4 / E);
+      z.ld = 0;
       z.trans = 2;
     }
     if (!t.n) return OK;
@@ -551,10 +570,9 @@ struct Exec {
   static In raw(const void* p, int ld) { return {p, ld, nullptr, nullptr}; }
 
   // ---- BN glue -----------------------------------------------------------------------
-  // np: records the producer wrote (<= u.nparts slots); 0: all slots
-  int finalize(const Unit& u, const BnL& bn, int np = 0) {
+  BnFinalizeArgs fin_args(const Unit& u, const BnL& bn) const {
     BnFinalizeArgs f{};
-    f.part = Wf(u.part); f.P = np > 0 ? np : u.nparts; f.C = u.C;
+    f.part = Wf(u.part); f.P = u.nparts; f.C = u.C;
     f.gamma = P(bn.g); f.beta = P(bn.b);
     f.rmean = r.R + bn.rm; f.rvar = r.R + bn.rv;
     f.nbt = r.NBT ? r.NBT + bn.nbt : nullptr;
@@ -562,7 +580,17 @@ struct Exec {
     f.bias = nullptr;
     f.mean = Wf(u.mean); f.invstd = Wf(u.invstd); f.scale = Wf(u.scale); f.shift = Wf(u.shift);
     f.counters = (unsigned*)W(pl.fcnt);  // one launch (fold + last-arriver finalize)
-    return bn_finalize(f, r.st);
+    return f;
+  }
+  int finalize(const Unit& u, const BnL& bn) {
+    g_prof_tag = u.name.c_str();
+    return bn_finalize(fin_args(u, bn), r.st);
+  }
+  // a GEMM producer finishes its BN itself (gemm_nt: in-kernel, or its own finalize launch)
+  void gemm_fin(GemmArgs& g, const Unit& u, const BnL& bn) const {
+    g.part = Wf(u.part);
+    g.tail.counters = (unsigned*)W(pl.fcnt);
+    g.tail.fwd = fin_args(u, bn);
   }
   int apply(const Unit& u, bool relu, const void* res = nullptr, int ldres = 0) {
     BnApplyArgs a{};
@@ -579,6 +607,7 @@ struct Exec {
   // pointwise conv on X [M][K] (ld ldx); eval: fused BN(+res,+relu); train: stats → apply
   int pw(const Unit& u, const ConvL& c, const BnL* bn, In x, bool relu,
          const void* res = nullptr, int ldres = 0) {
+    g_prof_tag = u.name.c_str();
     GemmArgs g{};
     const int K = c.cin * c.k * c.k;  // 1x1 convs; the aux 3x3 runs on its im2col columns
     g.M = (int)u.M; g.N = c.cout; g.K = K;
@@ -594,14 +623,13 @@ struct Exec {
     }
     g.scale = nullptr; g.shift = P(c.b);
     g.C = W(u.z); g.ldc = u.C;
-    g.part = Wf(u.part);
-    const int np = gemm_nt_parts(g, dt);
+    gemm_fin(g, u, *bn);
     TRY(gemm_nt(g, dt, r.st));
-    TRY(finalize(u, *bn, np));
     return u.lazy ? OK : apply(u, relu, res, ldres);
   }
   int dw(const Unit& u, const ConvL& c, const BnL& bn, In x, int H, int Wd, int Ho, int Wo,
          int stride) {
+    g_prof_tag = u.name.c_str();
     DwArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = u.C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
     d.x = x.p; d.w = P(c.w); d.in_scale = x.sc; d.in_shift = x.sh;
@@ -649,8 +677,10 @@ struct Exec {
   // ================================ forward ================================================
   int forward() {
     const int N = pl.N;
+    g_prof_tag = "weights_prep";
     TRY(prep_weights());
     if (!train) TRY(fold_all());
+    g_prof_tag = pl.c0.name.c_str();
     // ---- LearningToDownsample ----
     {
       Conv0Args c{};
@@ -687,6 +717,7 @@ struct Exec {
     }
     // ---- PPM ----
     {
+      g_prof_tag = "global_feature_extractor.ppm.pool";
       PoolArgs p{};
       p.N = N; p.H = pl.H5; p.W = pl.W5; p.C = 128; p.x = W(pl.concat); p.ldx = 256;
       p.pooled = W(pl.pooled);
@@ -696,6 +727,7 @@ struct Exec {
         const void* xin = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
         TRY(pw(pl.ppk[i], net.ppm_c[i], &net.ppm_b[i], raw(xin, 128), true));
       }
+      g_prof_tag = "global_feature_extractor.ppm.upsample";
       PpmUpArgs u{};
       u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = W(pl.feats_a);
       u.y = W(pl.concat); u.ldy = 256; u.coff = 128;
@@ -704,6 +736,7 @@ struct Exec {
     }
     // ---- FFM ----
     {
+      g_prof_tag = "feature_fusion.upsample";
       UpArgs u{};
       u.N = N; u.Hi = pl.H5; u.Wi = pl.W5; u.C = 128; u.Ho = pl.H3; u.Wo = pl.W3;
       u.x = W(pl.po.a); u.ldx = 128; u.y = W(pl.up_low); u.ldy = 128;
@@ -714,21 +747,21 @@ struct Exec {
         TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, raw(W(pl.l2pw.a), 64), false));
         TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, act(pl.fdw), true, W(pl.f), 128));
       } else {
+        g_prof_tag = pl.flow.name.c_str();
         GemmArgs g{};
         const In fin = act(pl.fdw);
         g.M = (int)pl.flow.M; g.N = 128; g.K = 128; g.A = fin.p; g.lda = fin.ld;
         g.a_scale = fin.sc; g.a_shift = fin.sh;
         g.B = Wg(net.ffm_low); g.ldb = 128; g.shift = P(net.ffm_low.b);
-        g.C = W(pl.flow.z); g.ldc = 128; g.part = Wf(pl.flow.part);
-        int np = gemm_nt_parts(g, dt);
+        g.C = W(pl.flow.z); g.ldc = 128;
+        gemm_fin(g, pl.flow, net.ffm_blow);
         TRY(gemm_nt(g, dt, r.st));
-        TRY(finalize(pl.flow, net.ffm_blow, np));
+        g_prof_tag = pl.fhigh.name.c_str();
         g.K = 64; g.A = W(pl.l2pw.a); g.lda = 64; g.B = Wg(net.ffm_high); g.ldb = 64;
         g.a_scale = g.a_shift = nullptr;
-        g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z); g.part = Wf(pl.fhigh.part);
-        np = gemm_nt_parts(g, dt);
+        g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z);
+        gemm_fin(g, pl.fhigh, net.ffm_bhigh);
         TRY(gemm_nt(g, dt, r.st));
-        TRY(finalize(pl.fhigh, net.ffm_bhigh, np));
         BnApplyArgs a{};
         a.M = pl.flow.M; a.C = 128;
         a.z = W(pl.flow.z); a.ldz = 128; a.scale = Wf(pl.flow.scale); a.shift = Wf(pl.flow.shift);
@@ -751,6 +784,7 @@ struct Exec {
       TRY(dropout(d, dt, r.st));
       cls_in = W(pl.drop);
     }
+    g_prof_tag = "classifier.conv";
     {
       GemmArgs g{};
       g.M = (int)pl.c2pw.M; g.N = net.num_classes; g.K = 128; g.A = cls_in; g.lda = 128;
@@ -765,6 +799,7 @@ struct Exec {
         set_error("forward_loss needs a training plan");
         return E_INVALID;
       }
+      g_prof_tag = "head (upsample + cross entropy)";
       CeHeadArgs h{};
       h.N = N; h.C = net.num_classes; h.Hl = pl.H3; h.Wl = pl.W3; h.H = pl.H; h.W = pl.W;
       h.logits = W(pl.logits); h.ldl = pl.Cp; h.target = r.target; h.ignore_index = r.ignore_index;
@@ -772,6 +807,7 @@ struct Exec {
       return ce_head(h, r.loss2, dt, r.st);
     }
     // ---- final bilinear (align_corners) to NCHW ----
+    g_prof_tag = "head (upsample)";
     UpArgs u{};
     if (r.labels) {  // eval.py:45 / demo.py:48: only torch.argmax(outputs[0], 1) is consumed
       u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
@@ -814,6 +850,7 @@ struct Exec {
   // aux head backward from d(aux_out); its input gradient is added into l2pw.ga (which the FFM
   // high-res dgrad has written and bottleneck 1's expand dgrad later accumulates into)
   int backward_aux() {
+    g_prof_tag = "auxlayer (backward)";
     const int N = pl.N, C = net.num_classes;
     const Unit& u = pl.aux0;
     void* dz = Bw(pl.dz);
@@ -840,7 +877,7 @@ struct Exec {
       TRY(dropout(d, dt, r.st));
     }
     Dz d;
-    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, 0, dz, d));
+    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, dz, d));
     TRY(pw_bwd(net.aux0, u.M, d, raw(W(pl.aux_col), 576), Bw(pl.aux_dcol), 576));
     Col2ImArgs cc{};
     cc.N = N; cc.H = pl.H3; cc.W = pl.W3; cc.C = 64; cc.dcol = Bw(pl.aux_dcol); cc.ldcol = 576;
@@ -849,9 +886,9 @@ struct Exec {
   }
 
   // ================================ backward ===============================================
-  // BN backward of unit u: dy = u.ga (ld u.ga_ld), mask = relu output (or null) → dz scratch
-  // P_pre > 0: the producer of dy (a dgrad GEMM with bpart set) already wrote P_pre partial
-  // records into bnpart, so the reduce pass is skipped.
+  // BN backward of unit u: dy = u.ga (ld u.ga_ld), mask = relu output (or null) → dz scratch.
+  // u.bdone: the dgrad that produced dy already reduced and finished this BN (coef / dgamma /
+  // dbeta written, set_btarget), so only the apply runs.
   // dz operand of a conv backward: a materialised tensor, or dy + z + transform table
   struct Dz {
     const void* p;
@@ -860,40 +897,10 @@ struct Exec {
     const float* tab;
   };
   static Dz plain(const void* p, int ld) { return {p, ld, nullptr, nullptr}; }
-  // fused form (fuse_bnbwd_enabled): reduce + finalize only; the consumers apply it on load
-  // streaming: the consumer is a bandwidth-efficient streaming kernel (conv0's wgrad)
-  int bn_bwd_x(const Unit& u, const BnL& bn, const void* dy, int lddy, bool relu_z, int P_pre,
-               void* dz, Dz& out, bool streaming = false) {
-    const int mode = fuse_bnbwd_mode();
-    if (!train || mode == 0 || (mode == 1 && !streaming)) {
-      TRY(bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, relu_z, P_pre));
-      out = plain(dz, u.C);
-      return OK;
-    }
-    BnBwdArgs b{};
-    b.M = u.M; b.C = u.C;
-    b.dy = dy; b.lddy = lddy; b.mask = nullptr; b.ldmask = 0;
-    b.z = W(u.z); b.ldz = u.C;
-    b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
-    b.shift = Wf(u.shift); b.relu_z = relu_z;
-    b.part = (float*)Bw(pl.bnpart);
-    int P = P_pre;
-    if (!P) {
-      TRY(bn_bwd_reduce(b, dt, r.st));
-      int rpb;
-      P = bn_bwd_parts(u.M, u.C, dt, &rpb);
-    }
-    BnBwdTab tb;
-    tb.tab = (float*)Bw(pl.xtab);
-    tb.scale = Wf(u.scale); tb.shift = Wf(u.shift); tb.mean = Wf(u.mean); tb.invstd = Wf(u.invstd);
-    tb.relu = relu_z;
-    TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b),
-                        (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb));
-    out = {dy, lddy, W(u.z), tb.tab};
-    return OK;
-  }
-  int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
-             int ldmask, void* dz, bool relu_z = false, int P_pre = 0) {
+  // reduce + finalize of u's BN backward unless its dy producer did both
+  int bn_bwd_stats(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
+                   int ldmask, bool relu_z, const BnBwdTab& tb) {
+    if (u.bdone) return OK;
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
     b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
@@ -901,29 +908,67 @@ struct Exec {
     b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
     b.shift = Wf(u.shift); b.relu_z = relu_z;
     b.part = (float*)Bw(pl.bnpart);
-    int P = P_pre;
-    if (!P) {
-      TRY(bn_bwd_reduce(b, dt, r.st));
-      int rpb;
-      P = bn_bwd_parts(u.M, u.C, dt, &rpb);
+    TRY(bn_bwd_reduce(b, dt, r.st));
+    int rpb;
+    const int P = bn_bwd_parts(u.M, u.C, dt, &rpb);
+    return bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b),
+                           (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb);
+  }
+  // fused form (fuse_bnbwd_mode): reduce + finalize only; the consumers apply it on load
+  // streaming: the consumer is a bandwidth-efficient streaming kernel (conv0's wgrad)
+  int bn_bwd_x(const Unit& u, const BnL& bn, const void* dy, int lddy, bool relu_z, void* dz,
+               Dz& out, bool streaming = false) {
+    g_prof_tag = u.name.c_str();
+    const int mode = fuse_bnbwd_mode();
+    if (!train || mode == 0 || (mode == 1 && !streaming)) {
+      TRY(bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, relu_z));
+      out = plain(dz, u.C);
+      return OK;
     }
-    float* coef = (float*)Bw(pl.coef);
-    TRY(bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b), coef, r.st,
-                        (unsigned*)W(pl.bcnt)));
-    b.coef = coef;
+    const BnBwdTab tb = bwd_tab(u, relu_z);
+    TRY(bn_bwd_stats(u, bn, dy, lddy, nullptr, 0, relu_z, tb));
+    out = {dy, lddy, W(u.z), tb.tab};
+    return OK;
+  }
+  int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
+             int ldmask, void* dz, bool relu_z = false) {
+    g_prof_tag = u.name.c_str();
+    TRY(bn_bwd_stats(u, bn, dy, lddy, mask, ldmask, relu_z, BnBwdTab()));
+    BnBwdArgs b{};
+    b.M = u.M; b.C = u.C;
+    b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
+    b.z = W(u.z); b.ldz = u.C;
+    b.mean = Wf(u.mean); b.invstd = Wf(u.invstd); b.scale = Wf(u.scale);
+    b.shift = Wf(u.shift); b.relu_z = relu_z;
+    b.coef = (float*)Bw(pl.coef);
     b.dz = dz; b.lddz = u.C;
     return bn_bwd_apply(b, dt, r.st);
   }
   // BN whose output is relu(BN(z)) with no second branch: the ReLU mask is recomputed from z
-  int bn_bwd_relu(const Unit& u, const BnL& bn, const void* dy, int lddy, void* dz, int P_pre = 0) {
-    return bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, true, P_pre);
+  int bn_bwd_relu(const Unit& u, const BnL& bn, const void* dy, int lddy, void* dz) {
+    return bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, true);
   }
+  // the dgrad producing the dy of BN (u, bn) also reduces and finishes that BN's backward
+  // (gemm_nt: in-kernel, or its own finalize launch); its bn_bwd then only applies
   void set_btarget(GemmArgs& g, const BTarget& t) {
     const Unit& u = *t.u;
     g.bpart = (float*)Bw(pl.bnpart);
     g.bz = W(u.z); g.ldbz = u.C;
     g.bmean = Wf(u.mean); g.binvstd = Wf(u.invstd); g.bscale = Wf(u.scale); g.bshift = Wf(u.shift);
     g.bmode = t.mode;
+    g.tail.counters = (unsigned*)W(pl.bcnt);
+    g.tail.count = (double)u.M;
+    g.tail.dgamma = G(t.bn->g);
+    g.tail.dbeta = G(t.bn->b);
+    g.tail.coef = (float*)Bw(pl.coef);
+    if (fuse_bnbwd_mode() == 2) g.tail.tab = bwd_tab(u, t.mode == 2);
+  }
+  BnBwdTab bwd_tab(const Unit& u, bool relu) const {
+    BnBwdTab tb;
+    tb.tab = (float*)Bw(pl.xtab);
+    tb.scale = Wf(u.scale); tb.shift = Wf(u.shift); tb.mean = Wf(u.mean); tb.invstd = Wf(u.invstd);
+    tb.relu = relu;
+    return tb;
   }
   // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
   int pw_bwd(const ConvL& c, long long M, Dz dz, In X, void* dX, int lddx,
@@ -955,15 +1000,17 @@ struct Exec {
     g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
-    if (bt.u && train) {
-      set_btarget(g, bt);
-      bt.u->bparts = gemm_nt_parts(g, dt);
-    }
-    return gemm_nt(g, dt, r.st);
+    if (bt.u && train) set_btarget(g, bt);
+    TRY(gemm_nt(g, dt, r.st));
+    if (bt.u && train) bt.u->bdone = true;
+    return OK;
   }
-  BTarget relu_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 2; return t; }
-  BTarget plain_target(const Unit& u) { BTarget t; t.u = &u; t.mode = 0; return t; }
-  static int pre(const Unit& u) { return u.bparts; }
+  static BTarget relu_target(const Unit& u, const BnL& bn) {
+    BTarget t; t.u = &u; t.bn = &bn; t.mode = 2; return t;
+  }
+  static BTarget plain_target(const Unit& u, const BnL& bn) {
+    BTarget t; t.u = &u; t.bn = &bn; t.mode = 0; return t;
+  }
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
   int dw_bwd(const ConvL& c, int C, const void* dz, In X, int H, int Wd, int Ho, int Wo,
              int stride, void* dX) {
@@ -979,6 +1026,7 @@ struct Exec {
   }
 
   int backward_head() {
+    g_prof_tag = "head (backward) + classifier.conv";
     const int N = pl.N, C = net.num_classes;
     void* dz = Bw(pl.dz);
     if (r.gloss) {
@@ -1014,29 +1062,30 @@ struct Exec {
     }
     // classifier dsconv2, dsconv1
     Dz d;
-    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, 0, dz, d));
+    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz, d));
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
-               relu_target(pl.c2dw)));
-    TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz, pre(pl.c2dw)));
+               relu_target(pl.c2dw, net.cls2.bdw)));
+    TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz));
     TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
-    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, 0, dz, d));
+    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz, d));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
-               relu_target(pl.c1dw)));
-    TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz, pre(pl.c1dw)));
+               relu_target(pl.c1dw, net.cls1.bdw)));
+    TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz));
     TRY(dw_bwd(net.cls1.dw, 128, dz, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(dz, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
-               relu_target(pl.fdw)));
-    TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz, pre(pl.fdw)));
+               relu_target(pl.fdw, net.ffm_bdw)));
+    TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz));
     TRY(dw_bwd(net.ffm_dw, 128, dz, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(dz, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
     if (net.aux) TRY(backward_aux());
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
+    g_prof_tag = "feature_fusion.upsample (backward)";
     {
       AxisBwdArgs a{};
       a.n_o1 = (long long)N * pl.H3; a.n_o2 = 1; a.Lout = pl.W3; a.Lin = pl.W5; a.n_in = 128;
@@ -1052,12 +1101,13 @@ struct Exec {
       TRY(axis_bwd(b, DT_F32, dt, r.st));
     }
     // PPM out 1x1 (256→128) over the concat buffer
-    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, 0, dz, d));
+    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, dz, d));
     TRY(pw_bwd(net.ppm_o, pl.po.M, d, raw(W(pl.concat), 256), Bw(pl.g_concat), 256));
     {
       PpmUpArgs u{};
       u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = nullptr;
       u.y = Bw(pl.g_concat); u.ldy = 256; u.coff = 128;
+      g_prof_tag = "global_feature_extractor.ppm.upsample (backward)";
       TRY(ppm_up_bwd(u, Bw(pl.g_feats), dt, r.st));
       static const int base[4] = {0, 1, 5, 14};
       for (int i = 0; i < 4; ++i) {
@@ -1071,6 +1121,7 @@ struct Exec {
       PoolBwdArgs p{};
       p.N = N; p.H = pl.H5; p.W = pl.W5; p.C = 128; p.dpooled = Bw(pl.g_pooled);
       p.dx = Bw(pl.g_concat); p.lddx = 256; p.accumulate = 1;
+      g_prof_tag = "global_feature_extractor.ppm.pool (backward)";
       TRY(pyramid_pool_bwd(p, dt, r.st));
     }
     return OK;
@@ -1092,33 +1143,34 @@ struct Exec {
     // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
     // block: its dy is the PPM concat gradient)
     Dz d;
-    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, i < 8 ? pre(up) : 0, dz, d));
-    TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud)));
-    TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz, pre(ud)));
+    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz, d));
+    TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud, l.bd)));
+    TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz));
     TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
-    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, 0, dz, d));
+    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz, d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
     // the dgrad is the dy of the previous block's project BN (or of LTD.dsconv2's pw BN)
-    const BTarget bt = i == 0 ? relu_target(pl.l2pw) : plain_target(pl.lbp[i - 1]);
+    const BTarget bt = i == 0 ? relu_target(pl.l2pw, net.ltd2.bpw)
+                              : plain_target(pl.lbp[i - 1], net.lb[i - 1].bp);
     return pw_bwd(l.e, ue.M, d, raw(x, xld), gx, gxld, R, ldr, bt);
   }
 
   int backward_ltd() {
     void* dz = Bw(pl.dz);
     Dz d;
-    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, pre(pl.l2pw), dz, d));
+    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz, d));
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
-               relu_target(pl.l2dw)));
-    TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz, pre(pl.l2dw)));
+               relu_target(pl.l2dw, net.ltd2.bdw)));
+    TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz));
     TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
-    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, 0, dz, d));
+    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz, d));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
-               relu_target(pl.l1dw)));
-    TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz, pre(pl.l1dw)));
+               relu_target(pl.l1dw, net.ltd1.bdw)));
+    TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz));
     TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
-    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, 0, dz, d, true));
+    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz, d, true));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;

@@ -65,15 +65,16 @@ struct Unit {
   size_t z = 0, a = 0;      // raw conv output / activation (same in eval)
   size_t part = 0;          // BN partial records
   int nparts = 0;           // record slots (gemm_parts(M) for GEMM producers: an upper bound)
-  // records the dgrad producing this unit's dy wrote with fused BN-backward partials (set when
-  // that dgrad is issued, a pure function of its shape; 0: none, the reduce pass runs)
-  mutable int bparts = 0;
+  // the dgrad producing this unit's dy also reduces and finishes its BN backward (set when that
+  // dgrad is issued; fixed per plan): the BN backward then only applies
+  mutable bool bdone = false;
   size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
   size_t ga = 0;            // backward: grad wrt a (bwd workspace)
   int ga_ld = 0;
   // train: the BN+ReLU output is never stored; every consumer (forward GEMM / depthwise and the
   // backward wgrads) applies relu(fmaf(z, scale, shift)) to z while staging its operand
   bool lazy = false;
+  std::string name;         // reference module path (per-launch profile label)
 };
 
 struct GraphCache;
@@ -97,7 +98,7 @@ struct Plan {
   size_t wt = 0;                    // transposed weights (train plans), net.wt_total elements
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
-  size_t fcnt = 0, bcnt = 0;        // BN fold+finalize arrival counters (ws / bws), 64 each
+  size_t fcnt = 0, bcnt = 0;        // BN arrival counters (ws), BN_COUNTERS each
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,

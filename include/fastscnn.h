@@ -172,14 +172,18 @@ int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const fl
                         void* bws, unsigned long long dropout_seed, float dropout_p,
                         int stage_from, int stage_to, void* stream);
 
-/* ---- launch profiler (bench.py roofline) --------------------------------------------------
- * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 9 upsample,
- * 11 cross_entropy / fused loss head, 12 conv0_wgrad.
+/* ---- launch profiler (bench.py roofline, tools/layer_report.py) ----------------------------
+ * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 7 bn_apply,
+ * 8 bn_bwd (apply), 9 upsample, 10 upsample_bwd, 11 cross_entropy / fused loss head,
+ * 12 conv0_wgrad, 13 bn_bwd_reduce, 14 bn_finalize; 100 = every kind.
  * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
  * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes
- * and flops of those launches (SURVEY.md §8(d) formulas). */
+ * and flops of those launches (SURVEY.md §8(d) formulas); fscnn_prof_launch then returns launch
+ * i's kind, ms, bytes, flops and layer (reference module name; issue order). */
 int fscnn_prof_begin(int kind, int max_launches);
 int fscnn_prof_end(double* total_ms, long long* launches, double* bytes, double* flops);
+int fscnn_prof_launch(long long i, int* kind, float* ms, double* bytes, double* flops,
+                      const char** layer);
 const char* fscnn_prof_kind_name(int kind);
 
 /* ---- loss / optimizer ------------------------------------------------------------------- */

@@ -40,13 +40,26 @@ BOTTLENECKS = [
 class _Ctx:
     """Holds the parameters, the mode, and collects running-stat updates / intermediates."""
 
-    def __init__(self, sd, training, momentum, record):
+    def __init__(self, sd, training, momentum, record, relu_masks=None):
         self.sd = sd
         self.training = training
         self.momentum = momentum
         self.new_stats = {}
         self.record = record
         self.acts = {}
+        self.relu_masks = relu_masks or {}
+
+    def relu(self, x, name):
+        """F.relu at the ReLU following BN ``name``.  Test instrumentation: ``relu_masks[name]``
+        (a boolean NCHW tensor) replaces the sign test, so a test can evaluate the reference's
+        gradients under the mask another implementation took at near-tie pre-activations;
+        without it this is exactly F.relu.  record=True keeps the pre-activation."""
+        if self.record:
+            self.acts["pre:" + name] = x
+        m = self.relu_masks.get(name)
+        if m is None:
+            return F.relu(x)
+        return x * m.to(x.dtype)
 
     def p(self, key):
         return self.sd[key]
@@ -85,23 +98,23 @@ def _conv(ctx, x, key, stride=1, padding=0, groups=1, bias=False):
 def _conv_bn_relu(ctx, x, prefix, k, stride):
     """_ConvBNReLU: conv(bias=False, padding=0) → BN → ReLU (models/fast_scnn.py:49-61)."""
     x = _conv(ctx, x, prefix + ".conv.0", stride=stride, padding=0)
-    return F.relu(ctx.bn(x, prefix + ".conv.1"))
+    return ctx.relu(ctx.bn(x, prefix + ".conv.1"), prefix + ".conv.1")
 
 
 def _dsconv(ctx, x, prefix, stride):
     """_DSConv: dw3x3(s, p1) → BN → ReLU → pw → BN → ReLU (models/fast_scnn.py:64-79)."""
     c = x.shape[1]
     x = _conv(ctx, x, prefix + ".conv.0", stride=stride, padding=1, groups=c)
-    x = F.relu(ctx.bn(x, prefix + ".conv.1"))
+    x = ctx.relu(ctx.bn(x, prefix + ".conv.1"), prefix + ".conv.1")
     x = _conv(ctx, x, prefix + ".conv.3")
-    return F.relu(ctx.bn(x, prefix + ".conv.4"))
+    return ctx.relu(ctx.bn(x, prefix + ".conv.4"), prefix + ".conv.4")
 
 
 def _dwconv(ctx, x, prefix, stride):
     """_DWConv: dw3x3(s, p1) → BN → ReLU (models/fast_scnn.py:82-92)."""
     c = x.shape[1]
     x = _conv(ctx, x, prefix + ".conv.0", stride=stride, padding=1, groups=c)
-    return F.relu(ctx.bn(x, prefix + ".conv.1"))
+    return ctx.relu(ctx.bn(x, prefix + ".conv.1"), prefix + ".conv.1")
 
 
 def _bottleneck(ctx, x, prefix, cin, cout, stride):
@@ -156,15 +169,15 @@ def dropout_mask(seed, shape, p):
 
 
 def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
-            dropout_p=0.1, dropout_seed=None, record=False):
+            dropout_p=0.1, dropout_seed=None, record=False, relu_masks=None):
     """FastSCNN.forward (models/fast_scnn.py:33-46).
 
     Returns ``(outputs_tuple, new_running_stats, intermediates)``.  In training mode Dropout is
     applied with ``dropout_mask(dropout_seed, ...)`` when ``dropout_seed`` is given, else skipped
     (p treated as 0).  ``sd`` values may be fp32 or fp64 CPU tensors (leaf tensors with
-    requires_grad for gradient oracles).
+    requires_grad for gradient oracles).  ``relu_masks`` is test instrumentation (``_Ctx.relu``).
     """
-    ctx = _Ctx(sd, training, momentum, record)
+    ctx = _Ctx(sd, training, momentum, record, relu_masks)
     size = x.shape[2:]
     # LearningToDownsample (models/fast_scnn.py:148-161)
     h = _conv_bn_relu(ctx, x, "learning_to_downsample.conv", 3, 2)
@@ -187,7 +200,7 @@ def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
                  "feature_fusion.conv_lower_res.1")
     high = ctx.bn(_conv(ctx, hr, "feature_fusion.conv_higher_res.0", bias=True),
                   "feature_fusion.conv_higher_res.1")
-    f = F.relu(high + low)
+    f = ctx.relu(high + low, "feature_fusion")
     ctx.rec("ffm", f)
     # Classifer (models/fast_scnn.py:221-237)
     c = _dsconv(ctx, f, "classifier.dsconv1", 1)
@@ -203,7 +216,7 @@ def forward(sd, x, num_classes, training=False, aux=False, momentum=BN_MOMENTUM,
         # auxlayer (models/fast_scnn.py:24-31,42-45); its Dropout follows the same mask law with
         # seed+1 when active.
         a = F.conv2d(hr, ctx.p("auxlayer.0.weight"), None, padding=1)
-        a = F.relu(ctx.bn(a, "auxlayer.1"))
+        a = ctx.relu(ctx.bn(a, "auxlayer.1"), "auxlayer.1")
         if training and dropout_seed is not None and dropout_p > 0:
             keep = dropout_mask(dropout_seed + 1, tuple(a.shape), dropout_p).to(a.dtype)
             a = a * keep / (1.0 - dropout_p)

@@ -118,3 +118,64 @@ def argmax_agreement(logits, ref_argmax, ref_logits=None, margin_tol=1e-4):
         margin = (srt[:, -1] - srt[:, -2]).cpu().numpy()
         bad_confident = int(((~eq) & (margin > margin_tol)).sum())
     return float(eq.mean()), bad_confident
+
+
+# ReLU sites of the HIP plan (named plan units) -> the oracle's ReLU names (oracle/_Ctx.relu)
+def relu_sites(aux=False):
+    sites = [("c0", "learning_to_downsample.conv.conv.1"),
+             ("l1dw", "learning_to_downsample.dsconv1.conv.1"),
+             ("l1pw", "learning_to_downsample.dsconv1.conv.4"),
+             ("l2dw", "learning_to_downsample.dsconv2.conv.1"),
+             ("l2pw", "learning_to_downsample.dsconv2.conv.4")]
+    for i in range(9):
+        b = "global_feature_extractor.bottleneck%d.%d.block" % (i // 3 + 1, i % 3)
+        sites += [("lbe%d" % i, b + ".0.conv.1"), ("lbd%d" % i, b + ".1.conv.1")]
+    sites += [("ppk%d" % i, "global_feature_extractor.ppm.conv%d.conv.1" % (i + 1))
+              for i in range(4)]
+    sites += [("po", "global_feature_extractor.ppm.out.conv.1"),
+              ("fdw", "feature_fusion.dwconv.conv.1"), ("f", "feature_fusion"),
+              ("c1dw", "classifier.dsconv1.conv.1"), ("c1pw", "classifier.dsconv1.conv.4"),
+              ("c2dw", "classifier.dsconv2.conv.1"), ("c2pw", "classifier.dsconv2.conv.4")]
+    if aux:
+        sites.append(("aux0", "auxlayer.1"))
+    return sites
+
+
+def hip_relu_masks(m, pre_ref, aux=False):
+    """The ReLU masks the HIP forward of model ``m`` (run with ``m._keep_ws = True``) took at every
+    ReLU, as NCHW bool tensors keyed by oracle ReLU name.  Pre-activations are recomputed from the
+    unit's saved z / scale / shift exactly as the kernels evaluate them (fmaf(z, scale, shift) > 0:
+    the fp64 product of two fp32 values is exact, so its one-rounding sum has the fmaf's sign);
+    the FFM sum's mask is its stored output f > 0.  ``pre_ref``: the oracle's recorded
+    pre-activations (shapes)."""
+    out = {}
+    for unit, name in relu_sites(aux):
+        ref = pre_ref["pre:" + name]
+        N, C, H, W = ref.shape
+        if unit == "f":
+            pre = m.debug_buffer("f").double().cpu()
+        else:
+            z = m.debug_buffer(unit + ".z").double().cpu()
+            pre = z * m.debug_buffer(unit + ".scale").double().cpu() + \
+                m.debug_buffer(unit + ".shift").double().cpu()
+        if unit.startswith("ppk"):  # bin-major rows (bin = y * k + x, then n)
+            mask = (pre > 0).reshape(H, W, N, C).permute(2, 3, 0, 1)
+        else:
+            mask = (pre > 0).reshape(N, H, W, C).permute(0, 3, 1, 2)
+        out[name] = mask.contiguous()
+    return out
+
+
+def relu_flips(masks, pre_ref, tie=1e-5):
+    """Sites where the HIP mask differs from the oracle's sign test: (name, count, worst relative
+    |pre-activation| at a flip, relative to the channel's max |pre|).  Every flip of a correct
+    implementation sits at a near-tie (worst <= tie)."""
+    res = []
+    for name, mk in masks.items():
+        ref = pre_ref["pre:" + name].detach()
+        diff = mk != (ref > 0)
+        n = int(diff.sum())
+        if n:
+            scale = ref.abs().amax(dim=(0, 2, 3), keepdim=True).clamp_min(1e-30).expand_as(ref)
+            res.append((name, n, float((ref.abs() / scale)[diff].max())))
+    return res

@@ -189,6 +189,11 @@ def test_bf16_train_step_within_emulated_bf16_budget():
         a = named[k].grad.detach().double().cpu().flatten()
         b, e = g64[k].flatten(), gem[k].flatten()
         mine.append(a); truth.append(b); emu.append(e)
+        if k == "global_feature_extractor.ppm.conv1.conv.0.weight":
+            # its BN normalises N*1*1 = 2 values: xhat = +-1 and the BN backward
+            # dy - mean(dy) - xhat * mean(dy * xhat) is identically 0, so this gradient is zero
+            # in exact arithmetic and pure rounding noise in every precision (no ratio to take)
+            continue
         floor = 1e-3 * b.abs().max().item() * np.sqrt(b.numel()) + 1e-9
         ratios[k] = (a - b).norm().item() / ((e - b).norm().item() + floor)
     # BatchNorms over few values (the pool-1 / pool-2 PPM branches: N*1*1 = 2 and N*2*2 = 8

@@ -23,12 +23,16 @@ from models.fast_scnn import FastSCNN  # noqa: E402
 from oracle import fast_scnn_ref as ref  # noqa: E402
 
 
+DROP_SEED = 1234
+
+
 def oracle(sd, x, t, nc, p, dt):
     s = {k: (v.detach().clone().to(dt).requires_grad_(True)
              if v.is_floating_point() and "running" not in k else
              (v.to(dt) if v.is_floating_point() else v)) for k, v in sd.items()}
     outs, stats, acts = ref.forward(s, x.to(dt), nc, training=True,
-                                    dropout_seed=1234 if p > 0 else None, dropout_p=p, record=True)
+                                    dropout_seed=DROP_SEED if p > 0 else None, dropout_p=p,
+                                    record=True)
     for a in acts.values():
         a.retain_grad()
     loss = ref.cross_entropy(outs[0], t)
@@ -44,16 +48,25 @@ def rel(a, b):
     return (a.double().cpu() - b.double().cpu()).abs().max().item() / (b.abs().max().item() + 1e-30)
 
 
-def main(dtype=torch.float32, p=0.0, shape=(2, 3, 128, 256), nc=19):
-    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
-          arch.portable_state_dict(nc, seed=0, variant="bnrand").items()}
-    x = torch.from_numpy(portable_init.input_tensor(1, shape))
-    t = torch.from_numpy(portable_init.target_tensor(3, (shape[0],) + shape[2:], nc, 0.05))
+def main(dtype=torch.float32, p=0.0, shape=(2, 3, 128, 256), nc=19, case=None):
+    seed = 1234
+    if case:  # a golden train case: its weights, batch, targets and dropout seed
+        from helpers import golden_input, golden_sd, golden_target, load_golden
+        g = load_golden(case)
+        nc, sd, x, t = int(g["num_classes"]), golden_sd(g), golden_input(g), golden_target(g)
+        seed, p = int(g["drop_seed"]), 0.1
+    else:
+        sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+              arch.portable_state_dict(nc, seed=0, variant="bnrand").items()}
+        x = torch.from_numpy(portable_init.input_tensor(1, shape))
+        t = torch.from_numpy(portable_init.target_tensor(3, (shape[0],) + shape[2:], nc, 0.05))
+    global DROP_SEED
+    DROP_SEED = seed
     m = FastSCNN(nc)
     m.load_state_dict(sd)
     m = m.cuda().train()
     m.classifier.conv[0].p = p
-    m._dropout_seed = 1234
+    m._dropout_seed = seed
     m._keep_ws = True
     out = m(x.cuda().to(dtype))[0]
     loss = cross_entropy(out, t.cuda())
@@ -104,11 +117,14 @@ def main(dtype=torch.float32, p=0.0, shape=(2, 3, 128, 256), nc=19):
     print("mask flips vs oracle:", flips, "of", a.numel(), " min|a_ref| at flips",
           ra[(a > 0) != (ra > 0)].abs().max().item() if flips else 0)
     print("per-parameter grads (backward order): ours vs fp64 | oracle-fp32 vs fp64 (max-normalised)")
-    for k, *_ in list(reversed(arch.param_specs(nc)))[:24]:
+    for k, *_ in list(reversed(arch.param_specs(nc))):
         g = named[k].grad.detach().double().cpu()
         r = s64[k].grad
         print("  %-60s %.2e | %.2e" % (k, rel(g, r), rel(s32[k].grad, r)))
 
 
 if __name__ == "__main__":
-    main(torch.float32, 0.0)
+    if len(sys.argv) > 1:
+        main(torch.float32, case=sys.argv[1])
+    else:
+        main(torch.float32, 0.0)
