@@ -62,6 +62,19 @@ struct C0Mma<0> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
   }
 };
 
+// XCD-contiguous block order: linear blocks L = x (mod 8) share an XCD, so residue class x takes
+// the contiguous logical range [x*T/8, (x+1)*T/8) of (segment, row) in segment-fastest order.
+// Output row ho reads input rows 2ho..2ho+2, so row ho+1 re-reads row 2ho+2: with consecutive
+// rows on one XCD back to back that re-read is an L2 hit instead of a second HBM fetch.
+__device__ __forceinline__ void c0_tile(int& seg, int& row) {
+  const int gx = gridDim.x;
+  const long long T = (long long)gx * gridDim.y;
+  long long L = blockIdx.x + (long long)gx * blockIdx.y;
+  if ((T & 7) == 0) L = (L & 7) * (T >> 3) + (L >> 3);
+  seg = (int)(L % gx);
+  row = (int)(L / gx);
+}
+
 template <typename TO, int XB>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   // 16-bit output => MFMA operands in that dtype (the plan's compute dtype)
@@ -85,8 +98,9 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int wo0 = blockIdx.x * C0_TILE;
-  const int row = blockIdx.y;  // n * Ho + ho
+  int seg, row;  // row = n * Ho + ho
+  c0_tile(seg, row);
+  const int wo0 = seg * C0_TILE;
   const int n = row / a.Ho, ho = row - n * a.Ho;
   const int npx = min(C0_TILE, a.Wo - wo0);
 
@@ -266,7 +280,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
         for (int r = 0; r < 4; ++r) s_red[1][wave][16 * jt + 4 * lq + r] = sum[jt][r];
     __syncthreads();
     if (tid < C0_OUT) {
-      const size_t pi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+      const size_t pi = (size_t)row * gridDim.x + seg;
       float* rec = a.part + pi * 3 * C0_OUT;
       const int c = tid;
       rec[c] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
@@ -381,7 +395,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   }
   __syncthreads();
   if (wave == 0 && lq == 0) {
-    const size_t pi = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const size_t pi = (size_t)row * gridDim.x + seg;
     float* rec = a.part + pi * 3 * C0_OUT;
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -508,7 +522,10 @@ __global__ __launch_bounds__(256) void conv0_wgrad_kernel(Conv0WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+  // a contiguous run of row segments per workgroup: consecutive output rows share an input row
+  // (2ho+2), re-read from this CU's cache instead of HBM
+  const long long t_end = tiles * (blockIdx.x + 1) / gridDim.x;
+  for (long long t = tiles * blockIdx.x / gridDim.x; t < t_end; ++t) {
     const int seg = (int)(t % segs);
     const long long row = t / segs;  // n * Ho + ho
     const int n = (int)(row / a.Ho), ho = (int)(row - (long long)n * a.Ho);

@@ -265,53 +265,49 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   }
   bool first = true;
 
-  // k-vector (4*s + lq) of pixel rows li, 16 + li of the chunk -> r[mt][s] (raw, clamped loads)
-  uint4 xa[2][KS];
-  auto loadx = [&](int chunk, uint4 (&r)[2][KS]) {
+  // Software pipeline over K-halves: a chunk's k-steps are loaded as NH halves of KH steps
+  // (NH = 2 for the long fp32 K of 96-128: a whole chunk double-buffered would pass 256 VGPRs),
+  // and each half's loads are in flight while the previous half computes — the next chunk's
+  // first half during this chunk's last half (NH = 2) or during all of it (NH = 1).
+  constexpr int NH = KS > 4 ? 2 : 1;
+  constexpr int KH = KS / NH;
+  static_assert(KH * NH == KS, "k-steps split in equal halves");
+  // k-vector (4*s + lq), s in half h, of pixel rows li, 16 + li -> r[mt][j] (raw, clamped loads)
+  uint4 xa[2][KH], xn[2][KH];
+  auto loadx = [&](int chunk, int h, uint4 (&r)[2][KH]) {
     const bool cok = chunk < nchunks;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int m = chunk * GS_MW + mt * 16 + li;
       const bool mok = cok && m < a.M;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int k = (4 * s + lq) * V;
+      for (int j = 0; j < KH; ++j) {
+        const int k = (4 * (h * KH + j) + lq) * V;
         const bool ok = mok && k < a.K;
-        r[mt][s] = *reinterpret_cast<const uint4*>(A + (ok ? (size_t)m * a.lda + k : 0));
+        r[mt][j] = *reinterpret_cast<const uint4*>(A + (ok ? (size_t)m * a.lda + k : 0));
       }
     }
   };
   // at the use site: lazy BN+ReLU (AT), then the row / K-tail zeroing
-  auto prep = [&](int chunk, uint4 (&r)[2][KS]) {
+  auto prep = [&](int chunk, int h, uint4 (&r)[2][KH]) {
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int m = chunk * GS_MW + mt * 16 + li;
       const bool mok = m < a.M;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int k = (4 * s + lq) * V;
-        uint4 v = r[mt][s];
+      for (int j = 0; j < KH; ++j) {
+        const int k = (4 * (h * KH + j) + lq) * V;
+        uint4 v = r[mt][j];
         if constexpr (AT) v = bnrelu_vec<T>(v, s_at + k, s_at + GS_KMAX + k);
-        r[mt][s] = gs_tail<T>(v, mok ? a.K - k : 0);
+        r[mt][j] = gs_tail<T>(v, mok ? a.K - k : 0);
       }
     }
   };
 
   T* Cp = (T*)a.C;
   const T* Rp = (const T*)a.R;
-  // Small chunks (KS <= 4: 32 A registers or fewer) double-buffer the next chunk in registers;
-  // the big fp32 tiles do not (it would push them past 256 VGPRs): there the co-resident waves
-  // of a SIMD alternate their load and MFMA phases, and the MFMAs of step s wait only for step
-  // s's loads.
-  constexpr bool PF = KS <= 4;
-  uint4 xn[2][PF ? KS : 1];
-  if constexpr (PF) {
-    if (c < nchunks) loadx(c, xa);
-  }
+  if (c < nchunks) loadx(c, 0, xa);
   for (; c < nchunks; c += wstride) {
-    if constexpr (PF) loadx(c + wstride, xn);  // clamped past the end
-    else loadx(c, xa);
-    prep(c, xa);
     f32x4 acc[2][NT];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -324,14 +320,28 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     const int wz = wb - li * WST - lq;  // 0, opaque to the compiler
     const float* ssc = s_sc + wz;       // same laundering for the epilogue tables
     const float* sbc = s_bc + wz;
+    auto mma = [&](int h, uint4 (&r)[2][KH]) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+      for (int j = 0; j < KH; ++j) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const uint4 w = s_w[wb + nt * 16 * WST + 4 * s];
+        for (int nt = 0; nt < NT; ++nt) {
+          const uint4 w = s_w[wb + nt * 16 * WST + 4 * (h * KH + j)];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) GsMma<T>::run(w, xa[mt][s], acc[mt][nt]);
+          for (int mt = 0; mt < 2; ++mt) GsMma<T>::run(w, r[mt][j], acc[mt][nt]);
+        }
       }
+    };
+    if constexpr (NH == 1) {
+      loadx(c + wstride, 0, xn);  // clamped past the end
+      prep(c, 0, xa);
+      mma(0, xa);
+    } else {
+      loadx(c, 1, xn);
+      prep(c, 0, xa);
+      mma(0, xa);
+      loadx(c + wstride, 0, xa);
+      prep(c, 1, xn);
+      mma(1, xn);
     }
     // ---- epilogue: lane holds channels n0 + 16nt + 4lq + r of pixel m ------------------------
     if constexpr (!TAIL) {  // whole 4-channel vectors, 16-B aligned rows (checked on the host)
@@ -426,11 +436,11 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
         }
       }
     }
-    if constexpr (PF) {
+    if constexpr (NH == 1) {
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) xa[mt][s] = xn[mt][s];
+        for (int j = 0; j < KH; ++j) xa[mt][j] = xn[mt][j];
     }
   }
 
@@ -497,6 +507,198 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 
 // column tile: the dgrad partial sums also hold a z row (NT <= 4); the forward statistics fit
 // NT = 6 (NT = 8 spills)
+// ---- fp32 GEMMs on the bf16 matrix cores (inference plans) ---------------------------------
+// An fp32 value splits EXACTLY into three bf16 terms by truncation, f = f0 + f1 + f2 (each
+// term carries the next 8 of the 24 significand bits), so
+//   a.w = a0w0 + (a0w1 + a1w0) + (a0w2 + a1w1 + a2w0) + O(2^-23 |a||w|)
+// with the dropped terms (a1w2, a2w1, a2w2) below fp32's own product rounding.  Six
+// v_mfma_f32_16x16x32_bf16 per 32-k step (fp32 accumulation) replace eight 16x16x4 fp32 MFMAs
+// per 16-k step: 6 x 16 vs 16 x 32 cycles per 32 k, ~5x the fp32 matrix rate, which is what
+// bounds the K = 64-128 fp32 1x1 convs of the eval forward (fp32 MFMA: ~157 TFLOP/s).
+// Same tile scheme as gemm_stream_kernel; no training forms (statistics stay exact fp32).
+__device__ __forceinline__ void gs_split3(const uint4& lo4, const uint4& hi4, uint4 (&t)[3]) {
+  // 8 fp32 (k = 8lq .. 8lq+7 of one row) -> three bf16x8 vectors (truncation splits)
+  const uint32_t f[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+  uint32_t p0[8], p1[8], p2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t b0 = f[e] & 0xFFFF0000u;
+    const float r1 = __uint_as_float(f[e]) - __uint_as_float(b0);  // exact
+    const uint32_t b1 = __float_as_uint(r1) & 0xFFFF0000u;
+    const float r2 = r1 - __uint_as_float(b1);                       // exact, <= 8 bits
+    p0[e] = b0;
+    p1[e] = b1;
+    p2[e] = __float_as_uint(r2) & 0xFFFF0000u;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const uint32_t* p = j == 0 ? p0 : (j == 1 ? p1 : p2);
+    t[j] = make_uint4((p[0] >> 16) | p[1], (p[2] >> 16) | p[3], (p[4] >> 16) | p[5],
+                      (p[6] >> 16) | p[7]);
+  }
+}
+
+__device__ __forceinline__ void gs_mma_x3(const uint4 (&w)[3], const uint4 (&x)[3], f32x4& acc) {
+  i16x8 a[3], b[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    __builtin_memcpy(&a[j], &w[j], 16);
+    __builtin_memcpy(&b[j], &x[j], 16);
+  }
+  // smallest terms first
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+// KS: 32-k steps covering K (<= 4: K <= 128)
+template <int NT, int KS, bool TAIL>
+__global__ __launch_bounds__(256, 2) void gemm_stream_x3_kernel(GemmArgs a, int bpg) {
+  constexpr int KV = 4 * KS;   // bf16x8 vectors per weight row and plane
+  constexpr int WST = KV + 1;  // padded row stride
+  constexpr int BN = 16 * NT;
+  extern __shared__ __attribute__((aligned(16))) uint4 s_w[];  // [3][BN][WST]
+  float* s_sc = reinterpret_cast<float*>(s_w + 3 * BN * WST);   // [BN] scale, [BN] shift
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int g = blockIdx.x / bpg;
+  const int bi = blockIdx.x - g * bpg;
+  const int n0 = g * BN;
+  const float* A = (const float*)a.A;
+  const float* B = (const float*)a.B;
+  for (int i = tid; i < BN * KV; i += 256) {
+    const int r = i / KV, v = i - r * KV;
+    const int n = n0 + r, k = v * 8;
+    const bool ok = n < a.N && k < a.K;
+    const float* src = B + (ok ? (size_t)n * a.ldb + k : 0);
+    const uint4 lo4 = gs_tail<float>(*reinterpret_cast<const uint4*>(src), ok ? a.K - k : 0);
+    const uint4 hi4 = gs_tail<float>(*reinterpret_cast<const uint4*>(src + 4), ok ? a.K - k - 4 : 0);
+    uint4 t[3];
+    gs_split3(lo4, hi4, t);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) s_w[(j * BN + r) * WST + v] = t[j];
+  }
+  for (int i = tid; i < BN; i += 256) {
+    const int n = n0 + i < a.N ? n0 + i : 0;
+    s_sc[i] = a.scale ? a.scale[n] : 1.f;
+    s_sc[BN + i] = a.shift ? a.shift[n] : 0.f;
+  }
+  __syncthreads();
+
+  const int nchunks = cdiv(a.M, GS_MW);
+  const int wstride = bpg * 4;
+  int c = bi * 4 + wave;
+  // lane (li, lq) holds k = 32 s + 8 lq .. +7 of pixel rows li, 16 + li: two 16-B loads
+  uint4 xa[2][KS][2], xn[2][KS][2];
+  auto loadx = [&](int chunk, uint4 (&r)[2][KS][2]) {
+    const bool cok = chunk < nchunks;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int m = chunk * GS_MW + mt * 16 + li;
+      const bool mok = cok && m < a.M;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 32 * s + 8 * lq + 4 * h;
+          const bool ok = mok && k < a.K;
+          r[mt][s][h] = *reinterpret_cast<const uint4*>(A + (ok ? (size_t)m * a.lda + k : 0));
+        }
+    }
+  };
+  float* Cp = (float*)a.C;
+  const float* Rp = (const float*)a.R;
+  if (c < nchunks) loadx(c, xa);
+  for (; c < nchunks; c += wstride) {
+    loadx(c + wstride, xn);  // clamped past the end
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int wb = li * WST + lq;
+    asm volatile("" : "+v"(wb));
+    const float* ssc = s_sc + (wb - li * WST - lq);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      uint4 xs[2][3];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int m = c * GS_MW + mt * 16 + li;
+        const bool mok = m < a.M;
+        const int k = 32 * s + 8 * lq;
+        gs_split3(gs_tail<float>(xa[mt][s][0], mok ? a.K - k : 0),
+                  gs_tail<float>(xa[mt][s][1], mok ? a.K - k - 4 : 0), xs[mt]);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        uint4 w[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) w[j] = s_w[(j * BN + nt * 16) * WST + wb + 4 * s];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) gs_mma_x3(w, xs[mt], acc[mt][nt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int m = c * GS_MW + mt * 16 + li;
+      const bool mok = m < a.M;
+      const size_t mr = mok ? (size_t)m : 0;
+      if constexpr (!TAIL) {
+        float rv[NT][4];
+        if (Rp) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) ld4v(Rp + mr * a.ldr + n0 + nt * 16 + 4 * lq, rv[nt]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int nl = nt * 16 + 4 * lq;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[mt][nt][r] * ssc[nl + r] + ssc[BN + nl + r];
+            if (Rp) v += rv[nt][r];
+            o[r] = a.relu ? fmaxf(v, 0.f) : v;
+          }
+          if (mok) st4v(Cp + mr * a.ldc + n0 + nl, o);
+        }
+      } else {
+        if (!mok) continue;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int nl = nt * 16 + 4 * lq;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = n0 + nl + r;
+            if (n >= a.N) continue;
+            float v = acc[mt][nt][r] * ssc[nl + r] + ssc[BN + nl + r];
+            if (Rp) v += ld1(Rp + (size_t)m * a.ldr + n);
+            st1(Cp + (size_t)m * a.ldc + n, a.relu ? fmaxf(v, 0.f) : v);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) xa[mt][s][h] = xn[mt][s][h];
+  }
+}
+
+// eval-form fp32 GEMM on the bf16 matrix cores: FSCNN_F32_SPLIT=0 keeps exact fp32 MFMA
+static bool gs_x3_on() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_F32_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int gs_pick_nt(const GemmArgs& a) {
   const int N = a.N;
   if (N <= 32) return 2;
@@ -631,9 +833,50 @@ static void gs_launch(const GemmArgs& a, int dtype, hipStream_t st) {
   else gs_launch_nt<T, false, false, false>(a, nt, ks, grid, lds, bpg, st);
 }
 
+// fp32 eval GEMMs with K <= 128 on the bf16 matrix cores (gemm_stream_x3_kernel): the widest
+// column tile whose three weight planes fit 72 KB of LDS
+static bool gs_x3_launch(const GemmArgs& a, hipStream_t st) {
+  if (!gs_x3_on() || a.part || a.bpart || a.a_scale || a.K > 128) return false;
+  const int ks = cdiv(a.K, 32);
+  auto lds_of = [&](int nt) { return (size_t)3 * 16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4; };
+  int nt = gs_pick_nt(a);
+  while (nt > 2 && lds_of(nt) > 72 * 1024) nt = nt == 8 ? 4 : (nt == 6 ? 3 : 2);
+  if (lds_of(nt) > 72 * 1024) return false;
+  const bool tail = gs_tail_needed(a, nt);
+  if (tail && nt != 2) return false;
+  const size_t lds = lds_of(nt);
+  const int groups = cdiv(a.N, 16 * nt);
+  int per_cu = (int)((160 * 1024) / (lds + 1024));
+  per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
+  int bpg = cdiv(256 * per_cu, groups);
+  bpg = (bpg + 7) / 8 * 8;
+  const int need = cdiv(cdiv(a.M, GS_MW), 4);
+  if (bpg > need) bpg = need;
+  if (bpg < 1) bpg = 1;
+  const dim3 grid((unsigned)(groups * bpg));
+#define X3(NT, KS, TL) gemm_stream_x3_kernel<NT, KS, TL><<<grid, 256, lds, st>>>(a, bpg)
+#define X3K(NT, TL)                         \
+  switch (ks) {                             \
+    case 1: X3(NT, 1, TL); break;           \
+    case 2: X3(NT, 2, TL); break;           \
+    case 3: X3(NT, 3, TL); break;           \
+    default: X3(NT, 4, TL); break;          \
+  }
+  switch (nt) {
+    case 2: if (tail) { X3K(2, true) } else { X3K(2, false) } break;
+    case 3: X3K(3, false) break;
+    case 4: X3K(4, false) break;
+    case 6: X3K(6, false) break;
+    default: X3K(8, false) break;
+  }
+#undef X3K
+#undef X3
+  return true;
+}
+
 int gemm_stream(const GemmArgs& a, int dtype, hipStream_t st) {
   if (dtype == DT_F32) {
-    gs_launch<float>(a, dtype, st);
+    if (!gs_x3_launch(a, st)) gs_launch<float>(a, dtype, st);
   } else if (dtype == DT_F16) {
     if (a.part || a.bpart || a.a_scale) {
       set_error("gemm_stream: fp16 arithmetic is inference-only");
