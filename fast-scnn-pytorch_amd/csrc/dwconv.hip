@@ -133,7 +133,7 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
 }
 
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
-template <typename T, int S, bool FLIP, bool IT>
+template <typename T, int S, bool FLIP, bool IT, bool BR = false>
 __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
   __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
@@ -214,6 +214,60 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
       }
     }
   }
+  if constexpr (BR) {
+    // ---- stride-1 dgrad: BN-backward partial sums of the stored dx (it is that BN's dy) -----
+    const BnBwdPart& b = a.bs;
+    const bool m2 = b.mode == 2;
+    float bm[4], bi[4], bsc[4], bsh[4], s1[4], s2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bm[j] = b.mean[c0 + j];
+      bi[j] = b.invstd[c0 + j];
+      bsc[j] = m2 ? b.scale[c0 + j] : 0.f;  // mode 0: mask fmaf(z, 0, 1) > 0 always
+      bsh[j] = m2 ? b.shift[c0 + j] : 1.f;
+      s1[j] = s2[j] = 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < G::HS; ++r) {
+      float z[G::WS][4];  // one output row of z per batch of loads
+#pragma unroll
+      for (int p = 0; p < G::WS; ++p) {
+        const bool ok = r < nrow && p < ncol;
+        const size_t pix = ok ? ((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0 + p : 0;
+        quad_ld((const T*)b.z + pix * a.C + c0, z[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < G::WS; ++p) {
+        const bool ok = r < nrow && p < ncol;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float gv = round_as<T>(acc[r][p][j]);
+          gv = (ok && fmaf(z[p][j], bsc[j], bsh[j]) > 0.f) ? gv : 0.f;
+          s1[j] += gv;
+          s2[j] += gv * (z[p][j] - bm[j]) * bi[j];
+        }
+      }
+      asm volatile("" ::: "memory");  // next row's z loads after this row's use
+    }
+    // the G pixel groups in fixed order, one record per workgroup
+    float* rec = b.part + ((size_t)bz * gridDim.y + by) * 2 * a.C;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s_red[(grp * QB + q) * 4 + j] = pass ? s2[j] : s1[j];
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = 0.f;
+          for (int g2 = 0; g2 < G::G; ++g2) t += s_red[(g2 * QB + q) * 4 + j];
+          rec[(size_t)pass * a.C + c0 + j] = t;
+        }
+      }
+    }
+    return;
+  }
   if (a.part == nullptr) return;
   // ---- per-channel (mean, M2, count) over the tile (train-mode BN statistics) ---------------
   const int trows = min(G::TH, a.Ho - th0), tcols = min(G::TW, a.Wo - tw0);
@@ -281,7 +335,7 @@ int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
   return (int)(g.y * g.z);
 }
 
-template <bool FLIP, bool IT>
+template <bool FLIP, bool IT, bool BR = false>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   int cbv;
@@ -299,6 +353,11 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     if (a.stride == 1) dw_fwd_kernel<f16, 1, false, false><<<grid, nthr, 0, st>>>(a, cbv);
     else dw_fwd_kernel<f16, 2, false, false><<<grid, nthr, 0, st>>>(a, cbv);
     return check_launch("dw_fwd");
+  }
+  if constexpr (BR) {  // stride-1 dgrad with BN-backward partials
+    if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, true><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<bf16, 1, true, false, true><<<grid, nthr, 0, st>>>(a, cbv);
+    return check_launch("dw_dgrad");
   }
   if (dtype == DT_F32) {
     if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
@@ -339,8 +398,8 @@ static void dw_block_shape(int C, int V, int& bx, int& by) {
 // stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even):
 //   row h0   <- dy row h0/2 (kh=1);  row h0+1 <- dy rows h0/2+1 (kh=0) and h0/2 (kh=2)
 //   col w0+q <- dy cols w0/2 + (q+1-kw)/2 for the kw of matching parity
-template <typename T>
-__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
+template <typename T, bool BR>
+__global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
   int bx, by, bz;
@@ -352,7 +411,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   const int h0 = (bz - n * nb) * 2;
   const int w0 = (by * BY + ty) * 4;
   const bool active = cv < CV && w0 < a.W;
-  if (!active) return;
+  if (!BR && !active) return;  // (BR: every thread joins the workgroup reduction)
   const int cvc = active ? cv : 0;
   float wt[9][V];
   const float* wp = a.w + (size_t)cvc * V * 9;
@@ -397,11 +456,78 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
-    if (h0 + r >= a.H) continue;
+    if (!active || h0 + r >= a.H) continue;
     T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + (size_t)cv * V;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (w0 + q < a.W) stv(db + (size_t)q * a.C, acc[r][q]);
+  }
+  if constexpr (BR) {
+    // ---- BN-backward partial sums of the stored dx (the dy of that BN), one record per
+    // workgroup: the BY column groups of a channel vector summed in fixed order
+    __shared__ float s_br[256 * 2 * V];
+    __shared__ float s_bc[4][64 * V];  // mean, invstd, mask scale, mask shift of the channels
+    const BnBwdPart& b = a.bs;
+    const bool m2 = b.mode == 2;
+    const int cb = cvc * V;
+    {
+      const int c0b = bx * BX * V;
+      for (int i = ty * BX + tx; i < BX * V; i += BX * BY) {
+        const int c = min(c0b + i, a.C - 1);
+        s_bc[0][i] = b.mean[c];
+        s_bc[1][i] = b.invstd[c];
+        s_bc[2][i] = m2 ? b.scale[c] : 0.f;  // mode 0: mask fmaf(z, 0, 1) > 0 always
+        s_bc[3][i] = m2 ? b.shift[c] : 1.f;
+      }
+    }
+    __syncthreads();
+    float s1[V], s2[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
+    // one dx row (4 pixels) per batch of z loads: keeps the live set within the register budget
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      float z[4][V];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = active && h0 + r < a.H && w0 + q < a.W;
+        const size_t pix = ok ? ((size_t)n * a.H + h0 + r) * a.W + w0 + q : 0;
+        ldv((const T*)b.z + pix * a.C + cb, z[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = active && h0 + r < a.H && w0 + q < a.W;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int cl = tx * V + j;
+          float gv = round_as<T>(acc[r][q][j]);
+          gv = (ok && fmaf(z[q][j], s_bc[2][cl], s_bc[3][cl]) > 0.f) ? gv : 0.f;
+          s1[j] += gv;
+          s2[j] += gv * (z[q][j] - s_bc[0][cl]) * s_bc[1][cl];
+        }
+      }
+      asm volatile("" ::: "memory");  // keep the second row's z loads after the first's use
+    }
+    const int t = ty * BX + tx;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      s_br[t * 2 * V + j] = s1[j];
+      s_br[t * 2 * V + V + j] = s2[j];
+    }
+    __syncthreads();
+    if (ty == 0 && cv < CV) {
+      float* rec = b.part + ((size_t)bz * gridDim.y + by) * 2 * a.C;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float t1 = 0.f, t2 = 0.f;
+        for (int y = 0; y < BY; ++y) {
+          t1 += s_br[(y * BX + tx) * 2 * V + j];
+          t2 += s_br[(y * BX + tx) * 2 * V + V + j];
+        }
+        rec[cb + j] = t1;
+        rec[a.C + cb + j] = t2;
+      }
+    }
   }
 }
 
@@ -410,19 +536,43 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   ProfScope ps(PK_DW_DGRAD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
+  const bool br = a.bs.part != nullptr;
+  if (br && (!a.bs.z || !a.bs.mean || !a.bs.invstd || (a.bs.mode == 2 && (!a.bs.scale || !a.bs.shift)))) {
+    set_error("dw_dgrad: inconsistent BN-backward partial arguments");
+    return E_INVALID;
+  }
   if (a.stride == 1) {
     // correlation of dy with the flipped taps, same geometry as the forward
     DwArgs f{};
     f.N = a.N; f.H = a.Ho; f.W = a.Wo; f.C = a.C; f.Ho = a.H; f.Wo = a.W; f.stride = 1;
     f.x = a.dy; f.w = a.w; f.y = a.dx;
-    return dw_launch_fwd<true, false>(f, dtype, st);
+    f.bs = a.bs;
+    return br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
   }
   int bx, by;
   dw_block_shape(a.C, V, bx, by);
   dim3 grid(cdiv(a.C / V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
-  if (dtype == DT_F32) dw_dgrad_s2_kernel<float><<<grid, block, 0, st>>>(a);
-  else dw_dgrad_s2_kernel<bf16><<<grid, block, 0, st>>>(a);
+  if (dtype == DT_F32) {
+    if (br) dw_dgrad_s2_kernel<float, true><<<grid, block, 0, st>>>(a);
+    else dw_dgrad_s2_kernel<float, false><<<grid, block, 0, st>>>(a);
+  } else {
+    if (br) dw_dgrad_s2_kernel<bf16, true><<<grid, block, 0, st>>>(a);
+    else dw_dgrad_s2_kernel<bf16, false><<<grid, block, 0, st>>>(a);
+  }
   return check_launch("dw_dgrad");
+}
+
+// workgroups of the dgrad launch = its BnBwdPart record count (H, W: dx = the dw's input)
+int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
+  const int V = dtype == DT_F32 ? 4 : 8;
+  if (stride == 1) {
+    int cbv;
+    const dim3 g = dw_grid(N, H, W, C, V, 1, cbv);
+    return (int)(g.y * g.z);
+  }
+  int bx, by;
+  dw_block_shape(C, V, bx, by);
+  return cdiv(W, by * 4) * N * ((H + 1) / 2);
 }
 
 // ---- weight gradient: per-workgroup partial [part][9][C] --------------------------------------

@@ -31,6 +31,19 @@ struct Conv0WgradArgs {
   const float* tab = nullptr;
 };
 
+// BatchNorm-backward partial sums of a dgrad's OUTPUT, when that output is the dy of a BN
+// (the mirror of GemmArgs::bpart): per workgroup, s1[c] = sum g*mask, s2[c] = sum
+// g*mask*(z-mean)*invstd of the stored (rounded) output g, the mask recomputed from that BN's z
+struct BnBwdPart {
+  float* part = nullptr;        // [P][2][C] or null
+  const void* z = nullptr;      // that BN's pre-BN tensor, NHWC with ld C
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* scale = nullptr;  // forward BN affine (mode 2: mask = fmaf(z, scale, shift) > 0)
+  const float* shift = nullptr;
+  int mode = 0;                  // 0 no ReLU, 2 relu_z
+};
+
 struct DwArgs {
   int N, H, W, C, Ho, Wo, stride;
   const void* x;   // NHWC [N,H,W,C] (input activation)
@@ -43,6 +56,7 @@ struct DwArgs {
   // lazily applied BN+ReLU of x (train: x is the producer's raw conv output z) or null
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
+  BnBwdPart bs{};  // stride-1 dgrad (the flipped forward): BN-backward partials of y
 };
 
 struct DwBwdArgs {
@@ -54,6 +68,7 @@ struct DwBwdArgs {
   float* slab;      // [parts][9][C] (wgrad)
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
   const float* x_shift = nullptr;
+  BnBwdPart bs{};  // dgrad: BN-backward partials of dx (dw_dgrad_parts records)
 };
 
 struct BnFinalizeArgs {
@@ -304,6 +319,7 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
+int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride);  // BnBwdPart records
 int dw_wgrad_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st);
 int dw_wgrad_reduce(float* slab, int P, int C, float* dw, hipStream_t st);

@@ -158,6 +158,15 @@ struct Alloc {
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
 
+// FSCNN_DW_BNRED=0: depthwise dgrads do not fold the next BN's backward reduce (own pass)
+static bool dw_bnred_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_DW_BNRED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Where a BN-backward dz is formed: by bn_bwd_apply (materialised), or by its consumers while
 // they stage their operand (common.hpp bwdx_apply).  Measured on MI355X (cfg3): the streaming
 // conv0 wgrad absorbs the extra z read at ~5.4 TB/s (c0's 800 MB apply, 189 us, becomes +49 us),
@@ -421,6 +430,18 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     for (int i = 0; i < 4; ++i) bn_upd(pl.ppk[i]);
     bn_upd(pl.po); bn_upd(pl.fdw); bn_upd(pl.flow); bn_upd(pl.c1dw); bn_upd(pl.c1pw);
     if (net.aux) bn_upd(pl.aux0);
+    // depthwise dgrads producing a BN's dy write dw_dgrad_parts records (Executor::dw_bwd)
+    auto dw_upd = [&](int H, int W, int Cc, int stride) {
+      const size_t s = (size_t)dw_dgrad_parts(N, H, W, Cc, dtype, stride) * 2 * Cc;
+      if (s > bnp) bnp = s;
+    };
+    dw_upd(pl.H1, pl.W1, 32, 2); dw_upd(pl.H2, pl.W2, 48, 2);
+    for (int i = 0; i < 9; ++i) {
+      const int Hin = i == 0 ? pl.H3 : (i <= 3 ? pl.H4 : pl.H5);
+      const int Win = i == 0 ? pl.W3 : (i <= 3 ? pl.W4 : pl.W5);
+      dw_upd(Hin, Win, net.lb[i].cin * 6, net.lb[i].stride);
+    }
+    dw_upd(pl.H3, pl.W3, 128, 1);
     pl.bnpart = B.get(bnp * 4);
     pl.coef = B.get(2 * 1024 * 4);
     pl.xtab = B.get((size_t)1024 * BWDX_STRIDE * 4);
@@ -901,6 +922,9 @@ struct Exec {
   int bn_bwd_stats(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
                    int ldmask, bool relu_z, const BnBwdTab& tb) {
     if (u.bdone) return OK;
+    if (u.bparts > 0)  // the depthwise dgrad that produced dy wrote the partial records
+      return bn_bwd_finalize((float*)Bw(pl.bnpart), u.bparts, u.C, (double)u.M, G(bn.g),
+                             G(bn.b), (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb);
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
     b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
@@ -1012,8 +1036,10 @@ struct Exec {
     BTarget t; t.u = &u; t.bn = &bn; t.mode = 0; return t;
   }
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
+  // bt: the BN whose dy the dgrad produces — its reduce pass is folded into the dgrad (records
+  // in bnpart; that BN's backward then only finalizes and applies)
   int dw_bwd(const ConvL& c, int C, const void* dz, In X, int H, int Wd, int Ho, int Wo,
-             int stride, void* dX) {
+             int stride, void* dX, BTarget bt = BTarget()) {
     DwBwdArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
     d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz; d.w = P(c.w); d.dx = dX;
@@ -1022,7 +1048,18 @@ struct Exec {
     if (!d.slab) return slab_oom();
     TRY(dw_wgrad(d, dt, r.st));
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
-    return dw_dgrad(d, dt, r.st);
+    const bool br = bt.u && train && dw_bnred_enabled();
+    if (br) {
+      const Unit& u = *bt.u;
+      d.bs.part = (float*)Bw(pl.bnpart);
+      d.bs.z = W(u.z);
+      d.bs.mean = Wf(u.mean); d.bs.invstd = Wf(u.invstd);
+      d.bs.scale = Wf(u.scale); d.bs.shift = Wf(u.shift);
+      d.bs.mode = bt.mode;
+    }
+    TRY(dw_dgrad(d, dt, r.st));
+    if (br) bt.u->bparts = dw_dgrad_parts(pl.N, H, Wd, C, dt, stride);
+    return OK;
   }
 
   int backward_head() {
@@ -1066,7 +1103,8 @@ struct Exec {
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw, net.cls2.bdw)));
     TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz));
-    TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga)));
+    TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
+               relu_target(pl.c1pw, net.cls1.bpw)));
     TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz, d));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw, net.cls1.bdw)));
@@ -1146,7 +1184,7 @@ struct Exec {
     TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz, d));
     TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud, l.bd)));
     TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz));
-    TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga)));
+    TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue, l.be)));
     TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz, d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
@@ -1164,12 +1202,14 @@ struct Exec {
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw, net.ltd2.bdw)));
     TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz));
-    TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga)));
+    TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
+               relu_target(pl.l1pw, net.ltd1.bpw)));
     TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz, d));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
     TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz));
-    TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga)));
+    TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
+               relu_target(pl.c0, net.b0)));
     TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz, d, true));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype;

@@ -68,6 +68,9 @@ struct Unit {
   // the dgrad producing this unit's dy also reduces and finishes its BN backward (set when that
   // dgrad is issued; fixed per plan): the BN backward then only applies
   mutable bool bdone = false;
+  // the depthwise dgrad producing this unit's dy wrote bparts BN-backward partial records (the
+  // reduce pass is skipped; set when that dgrad is issued, fixed per plan)
+  mutable int bparts = 0;
   size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
   size_t ga = 0;            // backward: grad wrt a (bwd workspace)
   int ga_ld = 0;
