@@ -89,10 +89,13 @@ __device__ __forceinline__ void dw_tile(int& cx, int& cy, int& cz) {
 // IT: x is the raw conv output z of a BatchNorm+ReLU that is never stored (train); the staged
 // value is relu(fmaf(z, isc[c], ish[c])) (bn_apply's arithmetic), padding stays zero.  A thread's
 // vectors all belong to one channel vector (lv = tid % cbv), so its V pairs are loaded once.
-template <typename T, int S, bool IT>
+// BX: x is a BN's dy and the staged value is that BN's dz = bwdx_apply(dy, z, tab) (the dz is
+// never stored; z = xz, same layout as x), padding stays zero.
+template <typename T, int S, bool IT, bool BX = false>
 __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, int C, int n,
                                          int hi0, int wi0, int cvbase, int cbv, int tid, int nthr,
-                                         const float* isc, const float* ish) {
+                                         const float* isc, const float* ish,
+                                         const T* xz = nullptr, const float* xtab = nullptr) {
   using G = DwTile<T, S>;
   constexpr int V = VecW<T>::V;
   float sc[IT ? V : 1], sh[IT ? V : 1];
@@ -104,7 +107,9 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
       sh[j] = ish[cb + j];
     }
   }
-  uint4 raw[G::LPT];
+  BwdXCoef<T> bx;
+  if constexpr (BX) bx.load(xtab, (cvbase + tid % cbv) * V);
+  uint4 raw[G::LPT], rz[BX ? G::LPT : 1];
 #pragma unroll
   for (int k = 0; k < G::LPT; ++k) {
     const int i = tid + k * nthr;
@@ -114,18 +119,20 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
     const bool ok = pix < G::IR * G::IC && hi >= 0 && hi < H && wi >= 0 && wi < W;
     const size_t off = ok ? (((size_t)n * H + hi) * W + wi) * C + (size_t)(cvbase + lv) * V : 0;
     raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(x + off));
+    if constexpr (BX) rz[k] = *reinterpret_cast<const uint4*>(xz + off);
   }
 #pragma unroll
   for (int k = 0; k < G::LPT; ++k) {
     const int i = tid + k * nthr;
     if (i < G::IR * G::IC * cbv) {
       uint4 v = raw[k];
-      if constexpr (IT) {
+      if constexpr (IT || BX) {
         const int pix = i / cbv;
         const int r = pix / G::IC, col = pix - r * G::IC;
         const int hi = hi0 + r, wi = wi0 + col;
         const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
-        v = sel4(ok, bnrelu_vec<T>(v, sc, sh));
+        if constexpr (IT) v = sel4(ok, bnrelu_vec<T>(v, sc, sh));
+        if constexpr (BX) v = sel4(ok, bwdx_apply<T>(v, rz[k], bx.al, bx.be, bx.gz, bx.sc, bx.sh));
       }
       s_in[i] = v;
     }
@@ -133,7 +140,7 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
 }
 
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
-template <typename T, int S, bool FLIP, bool IT, bool BR = false>
+template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool BX = false>
 __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
   __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
@@ -148,8 +155,9 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   const int n = bz / tiles_h;
   const int th0 = (bz - n * tiles_h) * G::TH, tw0 = by * G::TW;
   const int c0 = bx * cbv * VecW<T>::V + q * 4;  // first channel of the thread's quad
-  dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv,
-                     cbv, tid, nthr, a.in_scale, a.in_shift);
+  dw_stage<T, S, IT, BX>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
+                         bx * cbv, cbv, tid, nthr, a.in_scale, a.in_shift, (const T*)a.xz,
+                         a.xtab);
   float wt[9][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -335,7 +343,7 @@ int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
   return (int)(g.y * g.z);
 }
 
-template <bool FLIP, bool IT, bool BR = false>
+template <bool FLIP, bool IT, bool BR = false, bool BX = false>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   int cbv;
@@ -354,9 +362,9 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     else dw_fwd_kernel<f16, 2, false, false><<<grid, nthr, 0, st>>>(a, cbv);
     return check_launch("dw_fwd");
   }
-  if constexpr (BR) {  // stride-1 dgrad with BN-backward partials
-    if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, true><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<bf16, 1, true, false, true><<<grid, nthr, 0, st>>>(a, cbv);
+  if constexpr (BR || BX) {  // stride-1 dgrad with BN-backward partials / operand transform
+    if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX><<<grid, nthr, 0, st>>>(a, cbv);
+    else dw_fwd_kernel<bf16, 1, true, false, BR, BX><<<grid, nthr, 0, st>>>(a, cbv);
     return check_launch("dw_dgrad");
   }
   if (dtype == DT_F32) {
@@ -398,8 +406,8 @@ static void dw_block_shape(int C, int V, int& bx, int& by) {
 // stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even):
 //   row h0   <- dy row h0/2 (kh=1);  row h0+1 <- dy rows h0/2+1 (kh=0) and h0/2 (kh=2)
 //   col w0+q <- dy cols w0/2 + (q+1-kw)/2 for the kw of matching parity
-template <typename T, bool BR>
-__global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
+template <typename T, bool BR, bool XF = false>
+__global__ __launch_bounds__(256, (BR || XF) ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
   int bx, by, bz;
@@ -427,6 +435,9 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
 #pragma unroll
       for (int j = 0; j < V; ++j) acc[r][q][j] = 0.f;
   const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cvc * V;
+  const T* zb = (const T*)a.dyz + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cvc * V;
+  BwdXCoef<T> bxc;  // XF: dy is a BN's dy, the kernel forms that BN's dz on load
+  if constexpr (XF) bxc.load(a.dytab, cvc * V);
   const int hb = h0 / 2, wb = w0 / 2;
 #pragma unroll
   for (int dr = 0; dr < 2; ++dr) {       // dy rows hb, hb+1
@@ -436,7 +447,14 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
       const int wo = wb + dc;
       const bool ok = active && ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
       float g[V];
-      ldv(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * a.C, g);
+      const size_t goff = (ok ? (size_t)ho * a.Wo + wo : 0) * a.C;
+      if constexpr (XF) {  // dz = bwdx_apply(dy, z) (rounded to T like a stored dz)
+        const uint4 dv = *reinterpret_cast<const uint4*>(gb + goff);
+        const uint4 zv = *reinterpret_cast<const uint4*>(zb + goff);
+        unpackv(bwdx_apply<T>(dv, zv, bxc.al, bxc.be, bxc.gz, bxc.sc, bxc.sh), g);
+      } else {
+        ldv(gb + goff, g);
+      }
 #pragma unroll
       for (int j = 0; j < V; ++j) g[j] = ok ? g[j] : 0.f;
 #pragma unroll
@@ -515,18 +533,15 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
       s_br[t * 2 * V + V + j] = s2[j];
     }
     __syncthreads();
-    if (ty == 0 && cv < CV) {
-      float* rec = b.part + ((size_t)bz * gridDim.y + by) * 2 * a.C;
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float t1 = 0.f, t2 = 0.f;
-        for (int y = 0; y < BY; ++y) {
-          t1 += s_br[(y * BX + tx) * 2 * V + j];
-          t2 += s_br[(y * BX + tx) * 2 * V + V + j];
-        }
-        rec[cb + j] = t1;
-        rec[a.C + cb + j] = t2;
-      }
+    // every thread sums whole (channel, s1|s2) columns over the BY column groups (fixed order):
+    // a single row of reducers would walk BY = 64 rows alone for C = 32
+    float* rec = b.part + ((size_t)bz * gridDim.y + by) * 2 * a.C;
+    for (int col = t; col < BX * 2 * V; col += BX * BY) {
+      const int x = col / (2 * V), j2 = col - x * 2 * V;
+      if (bx * BX + x >= CV) continue;
+      float sum = 0.f;
+      for (int y = 0; y < BY; ++y) sum += s_br[(y * BX + x) * 2 * V + j2];
+      rec[(j2 < V ? 0 : a.C) + (size_t)(bx * BX + x) * V + (j2 < V ? j2 : j2 - V)] = sum;
     }
   }
 }
@@ -535,8 +550,14 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
-  ProfScope ps(PK_DW_DGRAD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
-  const bool br = a.bs.part != nullptr;
+  const bool br = a.bs.part != nullptr;  // + a read of the next BN's z (dx-sized)
+  const bool xf = a.dytab != nullptr;    // + a read of this BN's z (dy-sized)
+  ProfScope ps(PK_DW_DGRAD, st, E * (in_el * (br ? 2 : 1) + out_el * (xf ? 2 : 1)) + 36.0 * a.C,
+               18.0 * out_el);
+  if (xf && !a.dyz) {
+    set_error("dw_dgrad: BN-backward operand transform needs z");
+    return E_INVALID;
+  }
   if (br && (!a.bs.z || !a.bs.mean || !a.bs.invstd || (a.bs.mode == 2 && (!a.bs.scale || !a.bs.shift)))) {
     set_error("dw_dgrad: inconsistent BN-backward partial arguments");
     return E_INVALID;
@@ -547,18 +568,27 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     f.N = a.N; f.H = a.Ho; f.W = a.Wo; f.C = a.C; f.Ho = a.H; f.Wo = a.W; f.stride = 1;
     f.x = a.dy; f.w = a.w; f.y = a.dx;
     f.bs = a.bs;
+    f.xz = a.dyz; f.xtab = a.dytab;
+    if (xf) return br ? dw_launch_fwd<true, false, true, true>(f, dtype, st)
+                      : dw_launch_fwd<true, false, false, true>(f, dtype, st);
     return br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
   }
   int bx, by;
   dw_block_shape(a.C, V, bx, by);
   dim3 grid(cdiv(a.C / V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
-  if (dtype == DT_F32) {
-    if (br) dw_dgrad_s2_kernel<float, true><<<grid, block, 0, st>>>(a);
-    else dw_dgrad_s2_kernel<float, false><<<grid, block, 0, st>>>(a);
-  } else {
-    if (br) dw_dgrad_s2_kernel<bf16, true><<<grid, block, 0, st>>>(a);
-    else dw_dgrad_s2_kernel<bf16, false><<<grid, block, 0, st>>>(a);
-  }
+#define DWD2(T)                                                                   \
+  do {                                                                            \
+    if (xf) {                                                                     \
+      if (br) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(a);       \
+      else dw_dgrad_s2_kernel<T, false, true><<<grid, block, 0, st>>>(a);         \
+    } else {                                                                      \
+      if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(a);             \
+      else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(a);               \
+    }                                                                             \
+  } while (0)
+  if (dtype == DT_F32) DWD2(float);
+  else DWD2(bf16);
+#undef DWD2
   return check_launch("dw_dgrad");
 }
 
@@ -577,7 +607,7 @@ int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
 
 // ---- weight gradient: per-workgroup partial [part][9][C] --------------------------------------
 // grid: x = channel chunk, y = groups of tpb column tiles, z = N * row bands; part = (z, y).
-template <typename T, int S, bool IT>
+template <typename T, int S, bool IT, bool BX = false>
 __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, int tpb) {
   using G = DwTile<T, S>;
   __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
@@ -600,6 +630,16 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
+  // BX: the quad's BN-backward operand coefficients (al, be, gz, mask scale, mask shift)
+  float wx[BX ? 5 : 1][4];
+  if constexpr (BX) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 t = *reinterpret_cast<const float4*>(a.dytab + (size_t)(c0 + j) * BWDX_STRIDE);
+      wx[0][j] = t.x; wx[1][j] = t.y; wx[2][j] = t.z; wx[3][j] = t.w;
+      wx[4][j] = a.dytab[(size_t)(c0 + j) * BWDX_STRIDE + 4];
+    }
+  }
   const int tw_lo = by * tpb, tw_hi = min(tiles_w, tw_lo + tpb);
   for (int twi = tw_lo; twi < tw_hi; ++twi) {
     const int tw0 = twi * G::TW;
@@ -608,6 +648,7 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
     // dy of the thread's outputs (clamped + selected), issued with the tile loads
     float g[G::HS][G::WS][4];
     const T* gb = (const T*)a.dy + c0;
+    float zq[BX ? G::HS : 1][BX ? G::WS : 1][4];
 #pragma unroll
     for (int r = 0; r < G::HS; ++r)
 #pragma unroll
@@ -615,8 +656,22 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
         const bool ok = r < nrow && p < ncol;
         const size_t off = ok ? (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0 + p) * a.C : 0;
         quad_ld(gb + off, g[r][p]);
+        if constexpr (BX) quad_ld((const T*)a.dyz + c0 + off, zq[r][p]);
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) g[r][p][j] = ok ? g[r][p][j] : 0.f;
+    for (int r = 0; r < G::HS; ++r)
+#pragma unroll
+      for (int p = 0; p < G::WS; ++p) {
+        const bool ok = r < nrow && p < ncol;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = g[r][p][j];
+          if constexpr (BX) {  // dz = bwdx_apply(dy, z), rounded to T like a stored dz
+            const float gv = fmaf(zq[r][p][j], wx[3][j], wx[4][j]) > 0.f ? v : 0.f;
+            v = round_as<T>(fmaf(wx[0][j], gv, fmaf(wx[2][j], zq[r][p][j], wx[1][j])));
+          }
+          g[r][p][j] = ok ? v : 0.f;
+        }
       }
     __syncthreads();  // previous tile's LDS reads are done
     dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv,
@@ -689,12 +744,22 @@ int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const int tpb = dw_wgrad_tpb(a.N, a.Ho, a.Wo, a.C, V, a.stride, grid, cbv);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
-  ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el), 18.0 * out_el);
+  const bool bx = a.dytab != nullptr;
+  ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el * (bx ? 2 : 1)), 18.0 * out_el);
+  if (bx && !a.dyz) {
+    set_error("dw_wgrad: BN-backward operand transform needs z");
+    return E_INVALID;
+  }
   const int nthr = cbv * 32;
-#define DWW_LAUNCH(T, S)                                                              \
-  do {                                                                                \
-    if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, 0, st>>>(a, cbv, tpb);   \
-    else dw_wgrad_kernel<T, S, false><<<grid, nthr, 0, st>>>(a, cbv, tpb);            \
+#define DWW_LAUNCH(T, S)                                                                  \
+  do {                                                                                    \
+    if (bx) {                                                                             \
+      if (a.x_scale) dw_wgrad_kernel<T, S, true, true><<<grid, nthr, 0, st>>>(a, cbv, tpb); \
+      else dw_wgrad_kernel<T, S, false, true><<<grid, nthr, 0, st>>>(a, cbv, tpb);        \
+    } else {                                                                              \
+      if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, 0, st>>>(a, cbv, tpb);     \
+      else dw_wgrad_kernel<T, S, false><<<grid, nthr, 0, st>>>(a, cbv, tpb);              \
+    }                                                                                     \
   } while (0)
   if (dtype == DT_F32) {
     if (a.stride == 1) DWW_LAUNCH(float, 1);

@@ -57,6 +57,10 @@ struct DwArgs {
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
   BnBwdPart bs{};  // stride-1 dgrad (the flipped forward): BN-backward partials of y
+  // stride-1 dgrad: x is a BN's dy whose dz is never stored; the staged value is
+  // bwdx_apply(x, xz, xtab) (common.hpp), xz that BN's pre-BN tensor (ld C), or null
+  const void* xz = nullptr;
+  const float* xtab = nullptr;
 };
 
 struct DwBwdArgs {
@@ -69,6 +73,9 @@ struct DwBwdArgs {
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
   const float* x_shift = nullptr;
   BnBwdPart bs{};  // dgrad: BN-backward partials of dx (dw_dgrad_parts records)
+  // dy is a BN's dy whose dz is never stored: wgrad and dgrad read bwdx_apply(dy, dyz, dytab)
+  const void* dyz = nullptr;
+  const float* dytab = nullptr;
 };
 
 struct BnFinalizeArgs {

@@ -158,6 +158,19 @@ struct Alloc {
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
 
+// FSCNN_DW_BNBWD=1: the depthwise wgrad / dgrad form a dw BN's dz from (dy, z) on load instead
+// of reading a materialised dz.  Off by default: measured on MI355X (cfg3 step, 30 steps) 7.48
+// vs 7.28 ms — the two consumers' extra z reads and their higher register use cost more than
+// the apply pass they replace.  (FSCNN_DW_BNRED, the reduce folded into the dgrad, is the
+// opposite: 7.52 off vs 7.48 on with BNBWD; 7.41 vs 7.28 without.)
+static bool dw_bx_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_DW_BNBWD");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // FSCNN_DW_BNRED=0: depthwise dgrads do not fold the next BN's backward reduce (own pass)
 static bool dw_bnred_enabled() {
   static const bool on = [] {
@@ -985,7 +998,9 @@ struct Exec {
     g.tail.dgamma = G(t.bn->g);
     g.tail.dbeta = G(t.bn->b);
     g.tail.coef = (float*)Bw(pl.coef);
-    if (fuse_bnbwd_mode() == 2) g.tail.tab = bwd_tab(u, t.mode == 2);
+    // the operand table too: a fused consumer (depthwise, or every pointwise one in mode 2)
+    // reads it instead of a materialised dz
+    g.tail.tab = bwd_tab(u, t.mode == 2);
   }
   BnBwdTab bwd_tab(const Unit& u, bool relu) const {
     BnBwdTab tb;
@@ -1038,11 +1053,17 @@ struct Exec {
   // dw conv backward given dz [M][C]: wgrad into G, dgrad into dX
   // bt: the BN whose dy the dgrad produces — its reduce pass is folded into the dgrad (records
   // in bnpart; that BN's backward then only finalizes and applies)
-  int dw_bwd(const ConvL& c, int C, const void* dz, In X, int H, int Wd, int Ho, int Wo,
+  // dz: this dw's BN-backward output, materialised or as (dy, z, table) applied on load
+  int dw_bwd(const ConvL& c, int C, Dz dz, In X, int H, int Wd, int Ho, int Wo,
              int stride, void* dX, BTarget bt = BTarget()) {
+    if (dz.ld != C) {
+      set_error("dw_bwd: strided dz (ld %d, C %d) not supported", dz.ld, C);
+      return E_UNSUPPORTED;
+    }
     DwBwdArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
-    d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz; d.w = P(c.w); d.dx = dX;
+    d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz.p; d.w = P(c.w); d.dx = dX;
+    d.dyz = dz.z; d.dytab = dz.tab;
     const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
     d.slab = slab_alloc((size_t)S * 9 * C);
     if (!d.slab) return slab_oom();
@@ -1102,22 +1123,22 @@ struct Exec {
     TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz, d));
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw, net.cls2.bdw)));
-    TRY(bn_bwd_relu(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, dz));
-    TRY(dw_bwd(net.cls2.dw, 128, dz, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
+    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz, d, dw_bx_enabled()));
+    TRY(dw_bwd(net.cls2.dw, 128, d, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
                relu_target(pl.c1pw, net.cls1.bpw)));
     TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz, d));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw, net.cls1.bdw)));
-    TRY(bn_bwd_relu(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, dz));
-    TRY(dw_bwd(net.cls1.dw, 128, dz, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
+    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz, d, dw_bx_enabled()));
+    TRY(dw_bwd(net.cls1.dw, 128, d, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(dz, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw, net.ffm_bdw)));
-    TRY(bn_bwd_relu(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, dz));
-    TRY(dw_bwd(net.ffm_dw, 128, dz, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
+    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz, d, dw_bx_enabled()));
+    TRY(dw_bwd(net.ffm_dw, 128, d, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(dz, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
@@ -1183,8 +1204,8 @@ struct Exec {
     Dz d;
     TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz, d));
     TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud, l.bd)));
-    TRY(bn_bwd_relu(ud, l.bd, Bw(ud.ga), e, dz));
-    TRY(dw_bwd(l.d, e, dz, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue, l.be)));
+    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz, d, dw_bx_enabled()));
+    TRY(dw_bwd(l.d, e, d, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue, l.be)));
     TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz, d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
@@ -1201,14 +1222,14 @@ struct Exec {
     TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz, d));
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw, net.ltd2.bdw)));
-    TRY(bn_bwd_relu(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, dz));
-    TRY(dw_bwd(net.ltd2.dw, 48, dz, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
+    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz, d, dw_bx_enabled()));
+    TRY(dw_bwd(net.ltd2.dw, 48, d, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
                relu_target(pl.l1pw, net.ltd1.bpw)));
     TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz, d));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
-    TRY(bn_bwd_relu(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, dz));
-    TRY(dw_bwd(net.ltd1.dw, 32, dz, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
+    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz, d, dw_bx_enabled()));
+    TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
                relu_target(pl.c0, net.b0)));
     TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz, d, true));
     Conv0WgradArgs c{};
