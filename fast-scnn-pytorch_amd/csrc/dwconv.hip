@@ -143,8 +143,10 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
 template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool BX = false>
 __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
-  __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
-  __shared__ float s_red[256 * 4];
+  // LDS sized per launch (dw_shm): the staged tile of cbv channel vectors + the reduction rows
+  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
+  uint4* s_in = s_dyn;
+  float* s_red = reinterpret_cast<float*>(s_dyn + G::IR * G::IC * cbv);
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int QB = cbv * G::QPV;                 // quads per workgroup
   const int q = tid % QB, grp = tid / QB;
@@ -324,6 +326,13 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   }
 }
 
+// dynamic LDS of the tile kernels: the haloed input tile of cbv vectors + 4 floats per thread
+template <typename T, int S>
+static size_t dw_shm(int cbv) {
+  using G = DwTile<T, S>;
+  return (size_t)G::IR * G::IC * cbv * 16 + (size_t)cbv * 32 * 16;
+}
+
 static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv) {
   cbv = dw_cbv(C / V);
   int TH, TW;
@@ -358,21 +367,21 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
       set_error("dw: fp16 arithmetic is inference-only");
       return E_UNSUPPORTED;
     }
-    if (a.stride == 1) dw_fwd_kernel<f16, 1, false, false><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<f16, 2, false, false><<<grid, nthr, 0, st>>>(a, cbv);
+    if (a.stride == 1) dw_fwd_kernel<f16, 1, false, false><<<grid, nthr, dw_shm<f16, 1>(cbv), st>>>(a, cbv);
+    else dw_fwd_kernel<f16, 2, false, false><<<grid, nthr, dw_shm<f16, 2>(cbv), st>>>(a, cbv);
     return check_launch("dw_fwd");
   }
   if constexpr (BR || BX) {  // stride-1 dgrad with BN-backward partials / operand transform
-    if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<bf16, 1, true, false, BR, BX><<<grid, nthr, 0, st>>>(a, cbv);
+    if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
+    else dw_fwd_kernel<bf16, 1, true, false, BR, BX><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
     return check_launch("dw_dgrad");
   }
   if (dtype == DT_F32) {
-    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<float, 2, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
+    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
+    else dw_fwd_kernel<float, 2, FLIP, IT><<<grid, nthr, dw_shm<float, 2>(cbv), st>>>(a, cbv);
   } else {
-    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
-    else dw_fwd_kernel<bf16, 2, FLIP, IT><<<grid, nthr, 0, st>>>(a, cbv);
+    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP, IT><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
+    else dw_fwd_kernel<bf16, 2, FLIP, IT><<<grid, nthr, dw_shm<bf16, 2>(cbv), st>>>(a, cbv);
   }
   return check_launch("dw_fwd");
 }
@@ -610,7 +619,7 @@ int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
 template <typename T, int S, bool IT, bool BX = false>
 __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, int tpb) {
   using G = DwTile<T, S>;
-  __shared__ uint4 s_in[G::IR * G::IC * DWL_CB];
+  extern __shared__ __attribute__((aligned(16))) uint4 s_in[];  // [IR*IC*cbv] (dw_shm)
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int QB = cbv * G::QPV;
   const int q = tid % QB, grp = tid / QB;
@@ -754,11 +763,11 @@ int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
 #define DWW_LAUNCH(T, S)                                                                  \
   do {                                                                                    \
     if (bx) {                                                                             \
-      if (a.x_scale) dw_wgrad_kernel<T, S, true, true><<<grid, nthr, 0, st>>>(a, cbv, tpb); \
-      else dw_wgrad_kernel<T, S, false, true><<<grid, nthr, 0, st>>>(a, cbv, tpb);        \
+      if (a.x_scale) dw_wgrad_kernel<T, S, true, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb); \
+      else dw_wgrad_kernel<T, S, false, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);        \
     } else {                                                                              \
-      if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, 0, st>>>(a, cbv, tpb);     \
-      else dw_wgrad_kernel<T, S, false><<<grid, nthr, 0, st>>>(a, cbv, tpb);              \
+      if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);     \
+      else dw_wgrad_kernel<T, S, false><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);              \
     }                                                                                     \
   } while (0)
   if (dtype == DT_F32) {
