@@ -219,6 +219,7 @@ int fscnn_plan_create(const fscnn_net* net, int N, int H, int W, int dtype, int 
   int rc = plan_build(net->net, N, H, W, dtype, train, p->plan);
   if (rc) { delete p; return rc; }
   p->plan.graphs = make_graph_cache();
+  p->plan.side = make_side_stream();
   *out = p;
   return OK;
 }

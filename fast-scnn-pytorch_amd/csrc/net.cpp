@@ -397,6 +397,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     upd(pl.po); upd(pl.fdw); upd(pl.flow); upd(pl.c1dw); upd(pl.c1pw);
     if (net.aux) upd(pl.aux0);
     pl.dz = B.get((size_t)max_mc * E);
+    pl.dz2 = B.get((size_t)max_mc * E);  // ping-pong: a wgrad on the side stream may still read dz
     // weight-gradient partial slabs: the reductions of a backward stage are deferred to one
     // multi-job launch pair (Exec::flush_reduce), so every job keeps its own slab until then;
     // the arena holds the whole step's (sum over jobs, 64-float aligned each)
@@ -483,6 +484,44 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
 // ======================================================================================
 // execution
 // ======================================================================================
+// The backward's weight gradients (gemm_tn, colsum, depthwise / conv0 wgrad) only feed the
+// deferred slab reduction at the end of their stage, so they run on a second stream, beside
+// the dgrad -> BN-backward chain that carries the critical path: many of those launches are
+// latency-bound and leave HBM idle.  Dependencies are events: fork (the wgrad's operands and
+// slab are ready), the dz ping-pong buffer it read (released before that buffer is rewritten),
+// and join (before the stage's slab reduction).  FSCNN_SIDE_STREAM=0 keeps one stream.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, buf[2] = {nullptr, nullptr};
+  bool ready = false, failed = false;
+  bool init() {
+    if (ready || failed) return ready;
+    failed = true;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
+    hipEvent_t* ev[4] = {&fork, &join, &buf[0], &buf[1]};
+    for (auto* e : ev)
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
+    ready = true;
+    failed = false;
+    return true;
+  }
+  ~SideStream() {
+    hipEvent_t ev[4] = {fork, join, buf[0], buf[1]};
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+std::shared_ptr<SideStream> make_side_stream() { return std::make_shared<SideStream>(); }
+
+static bool side_stream_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_SIDE_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 namespace {
 
 #define TRY(x)                 \
@@ -510,6 +549,54 @@ struct Exec {
   Exec(const Plan& p, const RunArgs& ra)
       : pl(p), net(*p.net), r(ra), ws((char*)ra.ws), bws((char*)ra.bws), dt(p.dtype),
         E(p.dtype == DT_F32 ? 4 : 2), train(p.train != 0) {}
+
+  // ---- side stream for the weight gradients (backward only; see SideStream) ----------------
+  SideStream* side = nullptr;
+  bool pend[2] = {false, false};
+  int dzk = 0;
+  void use_side() {
+    if (train && side_stream_enabled() && pl.side && pl.side->init()) side = pl.side.get();
+  }
+  hipStream_t wst() const { return side ? side->s : r.st; }
+  int fork() {  // everything enqueued on the main stream so far happens before the side's next
+    if (!side) return OK;
+    if (hipEventRecord(side->fork, r.st) != hipSuccess ||
+        hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess) {
+      set_error("side stream: fork failed");
+      return E_HIP;
+    }
+    return OK;
+  }
+  int release(const void* p) {  // the side's work so far is the last reader of buffer p
+    if (!side) return OK;
+    const int k = p == Bw(pl.dz) ? 0 : (p == Bw(pl.dz2) ? 1 : -1);
+    if (k < 0) return OK;
+    if (hipEventRecord(side->buf[k], side->s) != hipSuccess) {
+      set_error("side stream: event record failed");
+      return E_HIP;
+    }
+    pend[k] = true;
+    return OK;
+  }
+  void* dz_buf() {  // the next BN-backward output buffer, once no side reader is left on it
+    const int k = dzk;
+    dzk ^= 1;
+    if (side && pend[k]) {
+      (void)hipStreamWaitEvent(r.st, side->buf[k], 0);
+      pend[k] = false;
+    }
+    return Bw(k ? pl.dz2 : pl.dz);
+  }
+  int join() {
+    if (!side) return OK;
+    if (hipEventRecord(side->join, side->s) != hipSuccess ||
+        hipStreamWaitEvent(r.st, side->join, 0) != hipSuccess) {
+      set_error("side stream: join failed");
+      return E_HIP;
+    }
+    pend[0] = pend[1] = false;
+    return OK;
+  }
 
   void* W(size_t off) const { return ws + off; }
   void* Bw(size_t off) const { return bws + off; }
@@ -580,6 +667,7 @@ struct Exec {
   }
   // slabs are reused only by kernels enqueued after these launches (same stream)
   int flush_reduce() {
+    TRY(join());  // every wgrad slab of the table is written
     const int rc = reduce_slabs_multi(red, r.st);
     red = RedTable();
     slab_top = 0;
@@ -887,7 +975,6 @@ struct Exec {
     g_prof_tag = "auxlayer (backward)";
     const int N = pl.N, C = net.num_classes;
     const Unit& u = pl.aux0;
-    void* dz = Bw(pl.dz);
     AxisBwdArgs a{};
     a.n_o1 = (long long)N * C * pl.H; a.n_o2 = 1; a.Lout = pl.W; a.Lin = pl.W3; a.n_in = 1;
     a.g = r.daux; a.g_s1 = pl.W; a.g_s2 = 0; a.g_idx = 1; a.g_in = 0;
@@ -911,7 +998,7 @@ struct Exec {
       TRY(dropout(d, dt, r.st));
     }
     Dz d;
-    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, dz, d));
+    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, dz_buf(), d));
     TRY(pw_bwd(net.aux0, u.M, d, raw(W(pl.aux_col), 576), Bw(pl.aux_dcol), 576));
     Col2ImArgs cc{};
     cc.N = N; cc.H = pl.H3; cc.W = pl.W3; cc.C = 64; cc.dcol = Bw(pl.aux_dcol); cc.ldcol = 576;
@@ -1020,7 +1107,11 @@ struct Exec {
     int S = gemm_tn_splits((int)M, c.cout, K);
     t.slab = slab_alloc((size_t)S * c.cout * K);
     if (!t.slab) return slab_oom();
-    TRY(gemm_tn(t, S, dt, r.st));
+    // an operand table (fused BN-backward) is shared scratch the main stream rewrites for the
+    // next BN: such a wgrad stays on the main stream
+    const hipStream_t ws2 = dz.tab ? r.st : wst();
+    if (!dz.tab) TRY(fork());
+    TRY(gemm_tn(t, S, dt, ws2));
     TRY(defer_reduce(t.slab, S, (long long)c.cout * K, G(c.w), 0));
     if (c.b >= 0) {
       float* part = slab_alloc((size_t)colsum_parts((int)M) * c.cout);
@@ -1029,9 +1120,10 @@ struct Exec {
         set_error("pw_bwd: bias gradient of a fused BN-backward operand");
         return E_UNSUPPORTED;
       }
-      TRY(colsum(dz.p, (int)M, c.cout, dz.ld, part, dt, r.st));
+      TRY(colsum(dz.p, (int)M, c.cout, dz.ld, part, dt, ws2));
       TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
+    if (!dz.tab) TRY(release(dz.p));
     if (!dX) return OK;
     GemmArgs g{};
     g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
@@ -1067,7 +1159,10 @@ struct Exec {
     const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
     d.slab = slab_alloc((size_t)S * 9 * C);
     if (!d.slab) return slab_oom();
-    TRY(dw_wgrad(d, dt, r.st));
+    const hipStream_t ws2 = dz.tab ? r.st : wst();  // (see pw_bwd)
+    if (!dz.tab) TRY(fork());
+    TRY(dw_wgrad(d, dt, ws2));
+    if (!dz.tab) TRY(release(dz.p));
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
     const bool br = bt.u && train && dw_bnred_enabled();
     if (br) {
@@ -1086,7 +1181,6 @@ struct Exec {
   int backward_head() {
     g_prof_tag = "head (backward) + classifier.conv";
     const int N = pl.N, C = net.num_classes;
-    void* dz = Bw(pl.dz);
     if (r.gloss) {
       // fused head: the low-res logits gradient was gathered in the forward; scale by dL/dloss / count
       TRY(ce_head_scale(Wf(pl.g_raw), Bw(pl.g_logits), pl.c2pw.M, C, pl.Cp, r.gloss, r.loss2, dt,
@@ -1120,28 +1214,30 @@ struct Exec {
     }
     // classifier dsconv2, dsconv1
     Dz d;
-    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz, d));
+    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz_buf(), d));
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw, net.cls2.bdw)));
-    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz, d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz_buf(), d, dw_bx_enabled()));
     TRY(dw_bwd(net.cls2.dw, 128, d, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
                relu_target(pl.c1pw, net.cls1.bpw)));
-    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz, d));
+    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz_buf(), d));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw, net.cls1.bdw)));
-    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz, d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz_buf(), d, dw_bx_enabled()));
     TRY(dw_bwd(net.cls1.dw, 128, d, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
-    TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(dz, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
+    void* zl = dz_buf();
+    TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, zl));
+    TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(zl, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw, net.ffm_bdw)));
-    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz, d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz_buf(), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ffm_dw, 128, d, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
-    TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, dz));
-    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(dz, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
+    void* zh = dz_buf();
+    TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, zh));
+    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(zh, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
     if (net.aux) TRY(backward_aux());
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     g_prof_tag = "feature_fusion.upsample (backward)";
@@ -1160,7 +1256,7 @@ struct Exec {
       TRY(axis_bwd(b, DT_F32, dt, r.st));
     }
     // PPM out 1x1 (256→128) over the concat buffer
-    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, dz, d));
+    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, dz_buf(), d));
     TRY(pw_bwd(net.ppm_o, pl.po.M, d, raw(W(pl.concat), 256), Bw(pl.g_concat), 256));
     {
       PpmUpArgs u{};
@@ -1172,9 +1268,10 @@ struct Exec {
       for (int i = 0; i < 4; ++i) {
         const Unit& u4 = pl.ppk[i];
         size_t off = (size_t)base[i] * N;
+        void* zp = dz_buf();
         TRY(bn_bwd(u4, net.ppm_b[i], (char*)Bw(pl.g_feats) + off * 32 * E, 32,
-                   (char*)W(pl.feats_a) + off * 32 * E, 32, dz));
-        TRY(pw_bwd(net.ppm_c[i], u4.M, plain(dz, 32), raw((char*)W(pl.pooled) + off * 128 * E, 128),
+                   (char*)W(pl.feats_a) + off * 32 * E, 32, zp));
+        TRY(pw_bwd(net.ppm_c[i], u4.M, plain(zp, 32), raw((char*)W(pl.pooled) + off * 128 * E, 128),
                    (char*)Bw(pl.g_pooled) + off * 128 * E, 128));
       }
       PoolBwdArgs p{};
@@ -1188,7 +1285,6 @@ struct Exec {
 
   int backward_block(int i) {
     const LbL& l = net.lb[i];
-    void* dz = Bw(pl.dz);
     const Unit &ue = pl.lbe[i], &ud = pl.lbd[i], &up = pl.lbp[i];
     int Hin = i == 0 ? pl.H3 : (i <= 3 ? pl.H4 : pl.H5);
     int Win = i == 0 ? pl.W3 : (i <= 3 ? pl.W4 : pl.W5);
@@ -1202,11 +1298,11 @@ struct Exec {
     // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
     // block: its dy is the PPM concat gradient)
     Dz d;
-    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz, d));
+    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz_buf(), d));
     TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud, l.bd)));
-    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz, d, dw_bx_enabled()));
+    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz_buf(), d, dw_bx_enabled()));
     TRY(dw_bwd(l.d, e, d, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue, l.be)));
-    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz, d));
+    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz_buf(), d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
@@ -1217,21 +1313,20 @@ struct Exec {
   }
 
   int backward_ltd() {
-    void* dz = Bw(pl.dz);
     Dz d;
-    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz, d));
+    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz_buf(), d));
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw, net.ltd2.bdw)));
-    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz, d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz_buf(), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ltd2.dw, 48, d, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
                relu_target(pl.l1pw, net.ltd1.bpw)));
-    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz, d));
+    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz_buf(), d));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
-    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz, d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
                relu_target(pl.c0, net.b0)));
-    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz, d, true));
+    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz_buf(), d, true));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
@@ -1239,7 +1334,9 @@ struct Exec {
     c.dz = d.p; c.zz = d.z; c.tab = d.tab; c.slab = slab_alloc((size_t)S * 864);
     c.rows_per_block = 8;
     if (!c.slab) return slab_oom();
-    TRY(conv0_wgrad(c, dt, r.st));
+    TRY(fork());
+    TRY(conv0_wgrad(c, dt, wst()));
+    TRY(release(d.p));
     return defer_reduce(c.slab, S, 864, G(net.c0.w), 0);
   }
 };
@@ -1272,6 +1369,7 @@ struct GraphCache {
 };
 
 std::shared_ptr<GraphCache> make_graph_cache() { return std::make_shared<GraphCache>(); }
+
 
 namespace {
 
@@ -1413,6 +1511,7 @@ int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to)
     RunArgs rr = r;
     rr.st = st;
     Exec ex(pl, rr);
+    ex.use_side();
     for (int s = stage_from; s <= stage_to; ++s) {
       switch (s) {
         case 0: TRY(ex.backward_head()); break;

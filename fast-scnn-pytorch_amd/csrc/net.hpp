@@ -81,6 +81,7 @@ struct Unit {
 };
 
 struct GraphCache;
+struct SideStream;
 
 struct Plan {
   const Net* net = nullptr;
@@ -105,16 +106,19 @@ struct Plan {
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
-         g_aux = 0, g_auxlog = 0, aux_dcol = 0, xtab = 0;
+         g_aux = 0, g_auxlog = 0, aux_dcol = 0, xtab = 0, dz2 = 0;
   // named buffers for debugging / stage-level parity: name -> (offset, rows, cols, ld, in_bws)
   struct Named { std::string name; size_t off; long long rows; int cols, ld, bws; };
   std::vector<Named> named;
   // captured hipGraphs of whole forward / backward-stage calls, keyed by their arguments
   std::shared_ptr<GraphCache> graphs;
+  // second stream for the weight-gradient launches of the backward (created on first use)
+  std::shared_ptr<SideStream> side;
 };
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl);
 std::shared_ptr<GraphCache> make_graph_cache();
+std::shared_ptr<SideStream> make_side_stream();
 
 struct RunArgs {
   const void* x; int x_dtype;     // NCHW input image
