@@ -189,6 +189,48 @@ __device__ __forceinline__ void reset_counter(unsigned* ctr) {
     __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- fp32 products on the bf16 matrix cores (eval GEMMs; gemm_stream.hip, gemm.hip) --------
+// An fp32 value splits exactly into three bf16 terms by truncation, f = f0 + f1 + f2; with the
+// same k permutation in both operands, six v_mfma_f32_16x16x32_bf16 give a.w to fp32 accuracy
+// (the dropped a1w2 + a2w1 + a2w2 are below fp32's own product rounding).
+__device__ __forceinline__ void gs_split3(const uint4& lo4, const uint4& hi4, uint4 (&t)[3]) {
+  // 8 fp32 (k = 8lq .. 8lq+7 of one row) -> three bf16x8 vectors (truncation splits)
+  const uint32_t f[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+  uint32_t p0[8], p1[8], p2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t b0 = f[e] & 0xFFFF0000u;
+    const float r1 = __uint_as_float(f[e]) - __uint_as_float(b0);  // exact
+    const uint32_t b1 = __float_as_uint(r1) & 0xFFFF0000u;
+    const float r2 = r1 - __uint_as_float(b1);                       // exact, <= 8 bits
+    p0[e] = b0;
+    p1[e] = b1;
+    p2[e] = __float_as_uint(r2) & 0xFFFF0000u;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const uint32_t* p = j == 0 ? p0 : (j == 1 ? p1 : p2);
+    t[j] = make_uint4((p[0] >> 16) | p[1], (p[2] >> 16) | p[3], (p[4] >> 16) | p[5],
+                      (p[6] >> 16) | p[7]);
+  }
+}
+
+__device__ __forceinline__ void gs_mma_x3(const uint4 (&w)[3], const uint4 (&x)[3], f32x4& acc) {
+  i16x8 a[3], b[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    __builtin_memcpy(&a[j], &w[j], 16);
+    __builtin_memcpy(&b[j], &x[j], 16);
+  }
+  // smallest terms first
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
 // ---- 4-element vectors (16 B fp32 / 8 B bf16) ------------------------------------------------
 __device__ __forceinline__ void st4v(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);

@@ -97,7 +97,10 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
   }
 }
 
-template <typename T, int NT, bool BT, bool BS, bool AT, bool AX = false>
+// X3 (fp32 eval GEMMs): the MFMA step runs on the bf16 matrix cores with exact three-way
+// splits of both operands (common.hpp gs_split3 / gs_mma_x3) — lane lq's two fp32 vectors of a
+// 32-k chunk (k = 4lq.., 16+4lq..) form its 8 bf16 k-slots, the same permutation in A and B
+template <typename T, int NT, bool BT, bool BS, bool AT, bool AX = false, bool X3 = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -249,18 +252,35 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   for (int c = 0; c < nchunks; ++c) {
     const int buf = nbuf == 2 ? (c & 1) : 0;
     if (c + 1 < nchunks) load_chunk(c + 1);
+    if constexpr (X3) {
+      uint4 a3[2][3];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int vv = lq + 4 * h;
-      uint4 af[2], bfv[NT];
+      for (int mt = 0; mt < 2; ++mt) {
+        const uint4* ar = sA(buf) + (wave * 32 + mt * 16 + li) * G_VPAD + lq;
+        gs_split3(ar[0], ar[4], a3[mt]);
+      }
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) af[mt] = sA(buf)[(wave * 32 + mt * 16 + li) * G_VPAD + vv];
+      for (int nt = 0; nt < NT; ++nt) {
+        const uint4* br = sB(buf) + (nt * 16 + li) * G_VPAD + lq;
+        uint4 b3[3];
+        gs_split3(br[0], br[4], b3);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB(buf)[(nt * 16 + li) * G_VPAD + vv];
+        for (int mt = 0; mt < 2; ++mt) gs_mma_x3(a3[mt], b3, acc[mt][nt]);
+      }
+    } else {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int h = 0; h < 2; ++h) {
+        const int vv = lq + 4 * h;
+        uint4 af[2], bfv[NT];
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
+        for (int mt = 0; mt < 2; ++mt) af[mt] = sA(buf)[(wave * 32 + mt * 16 + li) * G_VPAD + vv];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB(buf)[(nt * 16 + li) * G_VPAD + vv];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
+      }
     }
     if (c + 1 < nchunks) {
       if (nbuf == 1) __syncthreads();  // every wave's MFMA reads of this chunk are done
@@ -488,7 +508,7 @@ int gemm_nt_parts(const GemmArgs& a, int dtype) {
   return use_stream(a, dtype) ? gemm_stream_parts(a, dtype) : gemm_parts(a.M);
 }
 
-template <typename T, bool BT, bool BS, bool AT = false, bool AX = false>
+template <typename T, bool BT, bool BS, bool AT = false, bool AX = false, bool X3 = false>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   constexpr int V = VecW<T>::V;
@@ -500,11 +520,11 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS, AT, AX><<<grid, 256, shm, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
   }
 }
 
@@ -592,7 +612,12 @@ static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool ax,
     return check_launch("gemm_nt");
   }
   if (dtype == DT_F32) {
-    if (a.b_trans) launch_nt<float, true, false>(a, nt, st);
+    static const bool x3 = [] {  // FSCNN_F32_SPLIT=0: exact fp32 MFMA (gemm_stream.hip)
+      const char* e = getenv("FSCNN_F32_SPLIT");
+      return !(e && e[0] == '0');
+    }();
+    if (x3 && !a.b_trans && !ax && !bs && !at && !a.part) launch_nt<float, false, false, false, false, true>(a, nt, st);
+    else if (a.b_trans) launch_nt<float, true, false>(a, nt, st);
     else if (ax) { if (bs) launch_nt<float, false, true, false, true>(a, nt, st);
                    else launch_nt<float, false, false, false, true>(a, nt, st); }
     else if (bs) launch_nt<float, false, true>(a, nt, st);

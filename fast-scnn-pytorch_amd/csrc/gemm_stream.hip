@@ -516,44 +516,6 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 // per 16-k step: 6 x 16 vs 16 x 32 cycles per 32 k, ~5x the fp32 matrix rate, which is what
 // bounds the K = 64-128 fp32 1x1 convs of the eval forward (fp32 MFMA: ~157 TFLOP/s).
 // Same tile scheme as gemm_stream_kernel; no training forms (statistics stay exact fp32).
-__device__ __forceinline__ void gs_split3(const uint4& lo4, const uint4& hi4, uint4 (&t)[3]) {
-  // 8 fp32 (k = 8lq .. 8lq+7 of one row) -> three bf16x8 vectors (truncation splits)
-  const uint32_t f[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-  uint32_t p0[8], p1[8], p2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint32_t b0 = f[e] & 0xFFFF0000u;
-    const float r1 = __uint_as_float(f[e]) - __uint_as_float(b0);  // exact
-    const uint32_t b1 = __float_as_uint(r1) & 0xFFFF0000u;
-    const float r2 = r1 - __uint_as_float(b1);                       // exact, <= 8 bits
-    p0[e] = b0;
-    p1[e] = b1;
-    p2[e] = __float_as_uint(r2) & 0xFFFF0000u;
-  }
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const uint32_t* p = j == 0 ? p0 : (j == 1 ? p1 : p2);
-    t[j] = make_uint4((p[0] >> 16) | p[1], (p[2] >> 16) | p[3], (p[4] >> 16) | p[5],
-                      (p[6] >> 16) | p[7]);
-  }
-}
-
-__device__ __forceinline__ void gs_mma_x3(const uint4 (&w)[3], const uint4 (&x)[3], f32x4& acc) {
-  i16x8 a[3], b[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    __builtin_memcpy(&a[j], &w[j], 16);
-    __builtin_memcpy(&b[j], &x[j], 16);
-  }
-  // smallest terms first
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
-}
-
 // KS: 32-k steps covering K (<= 4: K <= 128)
 template <int NT, int KS, bool TAIL>
 __global__ __launch_bounds__(256, 2) void gemm_stream_x3_kernel(GemmArgs a, int bpg) {
