@@ -34,7 +34,7 @@ MFMA_PEAK_TFS = {"bf16": 2500.0, "fp32": 157.3}
 # flops of SURVEY.md §8(d) for its launch shape (csrc/*.hip ProfScope), DESIGN.md §3
 PROF_KINDS = {1: "conv0_fwd", 2: "dw_fwd", 3: "dw_dgrad", 4: "dw_wgrad", 5: "gemm_nt",
               6: "gemm_tn", 7: "bn_apply", 8: "bn_bwd_apply", 9: "upsample", 11: "ce_head",
-              12: "conv0_wgrad", 13: "bn_bwd_reduce", 14: "bn_finalize"}
+              12: "conv0_wgrad", 13: "bn_bwd_reduce", 14: "bn_finalize", 15: "ppm_branches"}
 
 
 def parse():

@@ -135,7 +135,7 @@ extern "C" const char* fscnn_prof_kind_name(int kind) {
   static const char* names[PK_COUNT] = {"none", "conv0_fwd", "dw_fwd", "dw_dgrad", "dw_wgrad",
                                         "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
                                         "upsample_bwd", "cross_entropy", "conv0_wgrad",
-                                        "bn_bwd_reduce", "bn_finalize"};
+                                        "bn_bwd_reduce", "bn_finalize", "ppm_branches"};
   return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
 }
 

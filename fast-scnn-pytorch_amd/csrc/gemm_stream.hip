@@ -32,7 +32,7 @@
 namespace fscnn {
 
 constexpr int GS_MW = 32;     // pixels per wave chunk (2 x 16-row MFMA tiles)
-constexpr int GS_KMAX = 256;  // largest K of a lazily normalised (AT) A operand
+constexpr int GS_KMAX = 576;  // largest K of a lazily normalised (AT) A operand
 
 template <typename T>
 struct GsMma;
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   constexpr bool SUMS = ST || BS;
   extern __shared__ __attribute__((aligned(16))) uint4 s_w[];  // [BN][WST]
   float* s_sc = reinterpret_cast<float*>(s_w + BN * WST);       // [BN] scale, [BN] shift
-  float* s_at = s_sc + 2 * BN;                                  // AT: [GS_KMAX] scale, shift
-  float* s_bc = s_at + (AT ? 2 * GS_KMAX : 0);                  // BS: [4][BN] mean/istd/sc/sh
+  float* s_at = s_sc + 2 * BN;                                  // AT: [KP] scale, [KP] shift
+  float* s_bc = s_at + (AT ? 2 * KP : 0);                       // BS: [4][BN] mean/istd/sc/sh
   float* s_shf = s_bc + (BS ? 4 * BN : 0);                       // ST: [4 waves][BN] shifts
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   if constexpr (AT) {
     for (int k = tid; k < KP; k += 256) {
       s_at[k] = k < a.K ? a.a_scale[k] : 0.f;
-      s_at[GS_KMAX + k] = k < a.K ? a.a_shift[k] : 0.f;
+      s_at[KP + k] = k < a.K ? a.a_shift[k] : 0.f;
     }
   }
   __syncthreads();
@@ -265,13 +265,14 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   }
   bool first = true;
 
-  // Software pipeline over K-halves: a chunk's k-steps are loaded as NH halves of KH steps
-  // (NH = 2 for the long fp32 K of 96-128: a whole chunk double-buffered would pass 256 VGPRs),
-  // and each half's loads are in flight while the previous half computes — the next chunk's
-  // first half during this chunk's last half (NH = 2) or during all of it (NH = 1).
-  constexpr int NH = KS > 4 ? 2 : 1;
+  // Software pipeline over K-parts: a chunk's k-steps are loaded as NH parts of KH steps (a
+  // whole chunk double-buffered would pass 256 VGPRs for K > 4 steps), and each part's loads are
+  // in flight while the previous part computes — the next chunk's first part during this
+  // chunk's last part (NH > 1) or during all of it (NH = 1).  Even parts live in xa, odd in xn.
+  constexpr int NH =
+      KS <= 4 ? 1 : (KS <= 8 ? 2 : (KS == 12 ? (BS ? 4 : 2) : (KS == 16 ? 4 : 6)));
   constexpr int KH = KS / NH;
-  static_assert(KH * NH == KS, "k-steps split in equal halves");
+  static_assert(KH * NH == KS && (NH == 1 || NH % 2 == 0), "k-steps split in an even part count");
   // k-vector (4*s + lq), s in half h, of pixel rows li, 16 + li -> r[mt][j] (raw, clamped loads)
   uint4 xa[2][KH], xn[2][KH];
   auto loadx = [&](int chunk, int h, uint4 (&r)[2][KH]) {
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
       for (int j = 0; j < KH; ++j) {
         const int k = (4 * (h * KH + j) + lq) * V;
         uint4 v = r[mt][j];
-        if constexpr (AT) v = bnrelu_vec<T>(v, s_at + k, s_at + GS_KMAX + k);
+        if constexpr (AT) v = bnrelu_vec<T>(v, s_at + k, s_at + KP + k);
         r[mt][j] = gs_tail<T>(v, mok ? a.K - k : 0);
       }
     }
@@ -336,12 +337,16 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
       prep(c, 0, xa);
       mma(0, xa);
     } else {
-      loadx(c, 1, xn);
-      prep(c, 0, xa);
-      mma(0, xa);
-      loadx(c + wstride, 0, xa);
-      prep(c, 1, xn);
-      mma(1, xn);
+#pragma unroll
+      for (int h = 0; h < NH; h += 2) {
+        loadx(c, h + 1, xn);
+        prep(c, h, xa);
+        mma(h, xa);
+        if (h + 2 < NH) loadx(c, h + 2, xa);
+        else loadx(c + wstride, 0, xa);  // clamped past the end
+        prep(c, h + 1, xn);
+        mma(h + 1, xn);
+      }
     }
     // ---- epilogue: lane holds channels n0 + 16nt + 4lq + r of pixel m ------------------------
     if constexpr (!TAIL) {  // whole 4-channel vectors, 16-B aligned rows (checked on the host)
@@ -661,9 +666,10 @@ static bool gs_x3_on() {
   return on;
 }
 
-static int gs_pick_nt(const GemmArgs& a) {
+static int gs_pick_nt(const GemmArgs& a, int ks) {
   const int N = a.N;
   if (N <= 32) return 2;
+  if (ks > 8) return N % 64 == 0 ? 4 : (N % 48 == 0 ? 3 : 4);  // deep K: weights [<=64][K] in LDS
   if (N <= 48) return 3;
   if (N <= 64 || a.bpart) return 4;
   if (N % 96 == 0) return 6;
@@ -674,9 +680,9 @@ static bool gs_tail_needed(const GemmArgs& a, int nt) {
   return a.N % (16 * nt) != 0 || a.ldc % 4 != 0 || (a.R && a.ldr % 4 != 0);
 }
 
-static size_t gs_lds(const GemmArgs& a, int nt, int ks) {
+static size_t gs_lds(const GemmArgs& a, int nt, int ks, int kc) {
   size_t b = (size_t)16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4;
-  if (a.a_scale) b += (size_t)2 * GS_KMAX * 4;
+  if (a.a_scale) b += (size_t)2 * ks * kc * 4;
   if (a.bpart) b += (size_t)4 * 16 * nt * 4;
   if (a.part) b += (size_t)4 * 16 * nt * 4;
   return b;  // >= the end-of-kernel reduction scratch [4][3][16 nt] (aliases the weights)
@@ -691,26 +697,54 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   // lazy BN on A: train-forward producers only (always with statistics)
   if (a.a_scale && (!a.a_shift || !a.part || a.K > GS_KMAX)) return false;
   if (dtype == DT_F16 && (sums || a.a_scale)) return false;
-  if (!(ks == 1 || ks == 2 || ks == 3 || ks == 4 || ks == 6 || ks == 8)) return false;
-  if (sums && ks > 4) return false;  // keep the statistics forms within 256 VGPRs
-  const int nt = gs_pick_nt(a);
+  // deep K (K = 384 / 512 / 576 16-bit: the projects and the expand dgrads) streams the chunk
+  // in 2-6 register parts against a <= 64-column weight slice of up to 75 KB
+  static const bool deep_on = [] {  // FSCNN_GS_DEEP=0: deep-K shapes take the tiled kernel (A/B)
+    const char* e = getenv("FSCNN_GS_DEEP");
+    return !(e && e[0] == '0');
+  }();
+  const bool deep = ks == 12 || ks == 16 || ks == 18;
+  if (deep && (dtype == DT_F32 || !deep_on)) return false;
+  // (measured: at M <= 65536 each wave streams one or two chunks and the part-by-part load chain
+  //  is slower than the tiled kernel; at M = 262,144, e.g. bottleneck1.0's expand dgrad, 10% faster)
+  if (deep && a.M < 131072) return false;
+  if (!(ks == 1 || ks == 2 || ks == 3 || ks == 4 || ks == 6 || ks == 8 || deep)) return false;
+  const int nt = gs_pick_nt(a, ks);
+  // keep the statistics forms within 256 VGPRs (measured: these would spill)
+  if (sums && ks > 4 && nt > 4) return false;
+  if (sums && nt == 4 && ks > 12) return false;
   if (a.part && nt > 4 && ks > 2) return false;
   if (a.bpart && dtype == DT_F32 && nt == 4 && ks > 2) return false;  // would spill
   if (gs_tail_needed(a, nt) && (nt != 2 || sums)) return false;  // scalar tail: N <= 32 only
   if (a.bpart && (!a.bz || a.ldbz % 4 || (a.bmode != 0 && a.bmode != 2))) return false;
-  if (gs_lds(a, nt, ks) > 72 * 1024) return false;
+  // two resident workgroups per CU (160 KB LDS, 1 KB reserved each)
+  if (gs_lds(a, nt, ks, KC) > (deep ? 80 * 1024 - 1024 : 72 * 1024)) return false;
   // in-kernel BN finish: group counters [0, 64), 32 team counters per group after them
   if (a.tail.counters && GS_CTR_TEAMS + 32 * cdiv(a.N, 16 * nt) > BN_COUNTERS) return false;
   return a.M >= 4096;  // tiny GEMMs (PPM bins): loading a weight slice per block does not pay
+}
+
+// workgroups per column group for `slots` resident workgroups shared by `groups` column groups:
+// a multiple of 8 (XCD-aligned), and (FSCNN_GS_ROUND=1, tuning) rounded down so the grid fits
+// one residency round
+static int gs_fill_bpg(int slots, int groups) {
+  static const int mode = [] {
+    const char* e = getenv("FSCNN_GS_ROUND");
+    return e ? atoi(e) : 0;
+  }();
+  int bpg = cdiv(slots, groups);
+  if (mode == 1 && slots / groups >= 8) bpg = slots / groups / 8 * 8;
+  else bpg = (bpg + 7) / 8 * 8;
+  return bpg;
 }
 
 // workgroups per column group = the record count of the statistics forms
 static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   const int KC = dtype == DT_F32 ? 16 : 32;
   ks = cdiv(a.K, KC);
-  nt = gs_pick_nt(a);
+  nt = gs_pick_nt(a, ks);
   const int groups = cdiv(a.N, 16 * nt);
-  lds = gs_lds(a, nt, ks);
+  lds = gs_lds(a, nt, ks, KC);
   const int nchunks = cdiv(a.M, GS_MW);
   // resident workgroups: LDS-limited (160 KB / CU), at most 2 per CU (measured: 3-4 slower)
   static const int cap = [] {  // FSCNN_GS_PER_CU: tuning override of the residency cap
@@ -719,8 +753,7 @@ static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   }();
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
-  int bpg = cdiv(256 * per_cu, groups);
-  bpg = (bpg + 7) / 8 * 8;
+  int bpg = gs_fill_bpg(256 * per_cu, groups);
   const int need = cdiv(nchunks, 4);  // <= cdiv(M, 128) = gemm_parts(M): fits the record slots
   if (bpg > need) bpg = need;
   if (bpg > GS_TEAM * 32) bpg = GS_TEAM * 32;  // the finish's team counters (32 per group)
@@ -739,6 +772,7 @@ static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int b
                          hipStream_t st) {
   constexpr bool SUMS = ST || BS;
   constexpr bool WIDE = SUMS && NT > 4;  // wide statistics tiles: K <= 2 k-steps only
+  constexpr bool DEEP = sizeof(T) == 2 && NT <= 4 && !TAIL;
   switch (ks) {
     case 1: gemm_stream_kernel<T, NT, 1, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
     case 2: gemm_stream_kernel<T, NT, 2, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
@@ -749,10 +783,17 @@ static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int b
       if constexpr (!WIDE) gemm_stream_kernel<T, NT, 4, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
       break;
     case 6:
-      if constexpr (!SUMS) gemm_stream_kernel<T, NT, 6, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 6, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
       break;
-    default:
-      if constexpr (!SUMS) gemm_stream_kernel<T, NT, 8, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+    case 8:
+      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 8, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      break;
+    default:  // deep K: 16-bit, <= 4 column tiles, no scalar tail
+      if constexpr (DEEP) {
+        if (ks == 12) gemm_stream_kernel<T, NT, 12, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+        else if (ks == 16) gemm_stream_kernel<T, NT, 16, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+        else gemm_stream_kernel<T, NT, 18, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      }
       break;
   }
 }
@@ -801,7 +842,7 @@ static bool gs_x3_launch(const GemmArgs& a, hipStream_t st) {
   if (!gs_x3_on() || a.part || a.bpart || a.a_scale || a.K > 128) return false;
   const int ks = cdiv(a.K, 32);
   auto lds_of = [&](int nt) { return (size_t)3 * 16 * nt * (4 * ks + 1) * 16 + (size_t)2 * 16 * nt * 4; };
-  int nt = gs_pick_nt(a);
+  int nt = gs_pick_nt(a, ks);
   while (nt > 2 && lds_of(nt) > 72 * 1024) nt = nt == 8 ? 4 : (nt == 6 ? 3 : 2);
   if (lds_of(nt) > 72 * 1024) return false;
   const bool tail = gs_tail_needed(a, nt);
@@ -810,8 +851,7 @@ static bool gs_x3_launch(const GemmArgs& a, hipStream_t st) {
   const int groups = cdiv(a.N, 16 * nt);
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
-  int bpg = cdiv(256 * per_cu, groups);
-  bpg = (bpg + 7) / 8 * 8;
+  int bpg = gs_fill_bpg(256 * per_cu, groups);
   const int need = cdiv(cdiv(a.M, GS_MW), 4);
   if (bpg > need) bpg = need;
   if (bpg < 1) bpg = 1;

@@ -253,6 +253,36 @@ struct PpmUpArgs {
   void* y; int ldy; int coff;
 };
 
+// PPM branch convs of the training step, one workgroup per branch (ppm.hip)
+struct PpmBranchFwd {
+  BnFinalizeArgs f;  // gamma / beta / running statistics -> mean / invstd / scale / shift
+  const void* x;     // pooled rows [M][K]
+  const void* w;     // [32][K], storage type
+  void* z;           // [M][32] conv output
+  void* y;           // relu(BN(z)) [M][ldy]
+  int ldy, M;
+};
+struct PpmFwdArgs {
+  PpmBranchFwd b[4];
+  int nb, K, C;
+};
+struct PpmBranchBwd {
+  const void* dy; int lddy;  // gradient of y
+  const void* y; int ldy;    // forward output (its ReLU mask)
+  const void* z;             // [M][32]
+  const float *mean, *invstd, *scale;
+  const void* x;             // pooled rows [M][K]
+  const void* w;             // [32][K], storage type
+  float *dgamma, *dbeta;     // [32]
+  float* dw;                 // [32][K] fp32, stored
+  void* dx;                  // [M][K]
+  int M;
+};
+struct PpmBwdArgs {
+  PpmBranchBwd b[4];
+  int nb, K, C;
+};
+
 struct CeArgs {
   int N, C;
   long long HW;
@@ -387,6 +417,10 @@ int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st);
 int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st);
 int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st);
 int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st);
+
+bool ppm_branches_ok(int maxM, int K, int dtype);
+int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st);
+int ppm_branches_bwd(const PpmBwdArgs& a, int dtype, hipStream_t st);
 
 int ce_parts(int N, long long HW);
 int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st);

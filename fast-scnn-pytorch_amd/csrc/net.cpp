@@ -459,6 +459,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.bnpart = B.get(bnp * 4);
     pl.coef = B.get(2 * 1024 * 4);
     pl.xtab = B.get((size_t)1024 * BWDX_STRIDE * 4);
+    pl.xtab2 = B.get((size_t)1024 * BWDX_STRIDE * 4);
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
     pl.bws_bytes = B.top;
     auto gu = [&](const std::string& n, const Unit& u) {
@@ -492,13 +493,14 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
 // and join (before the stage's slab reduction).  FSCNN_SIDE_STREAM=0 keeps one stream.
 struct SideStream {
   hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, buf[2] = {nullptr, nullptr};
+  // buf[k]: last side read of dz buffer k; buf[2 + k]: of operand table k
+  hipEvent_t fork = nullptr, join = nullptr, buf[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ready = false, failed = false;
   bool init() {
     if (ready || failed) return ready;
     failed = true;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
-    hipEvent_t* ev[4] = {&fork, &join, &buf[0], &buf[1]};
+    hipEvent_t* ev[6] = {&fork, &join, &buf[0], &buf[1], &buf[2], &buf[3]};
     for (auto* e : ev)
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
     ready = true;
@@ -506,7 +508,7 @@ struct SideStream {
     return true;
   }
   ~SideStream() {
-    hipEvent_t ev[4] = {fork, join, buf[0], buf[1]};
+    hipEvent_t ev[6] = {fork, join, buf[0], buf[1], buf[2], buf[3]};
     for (auto e : ev)
       if (e) (void)hipEventDestroy(e);
     if (s) (void)hipStreamDestroy(s);
@@ -552,12 +554,20 @@ struct Exec {
 
   // ---- side stream for the weight gradients (backward only; see SideStream) ----------------
   SideStream* side = nullptr;
-  bool pend[2] = {false, false};
+  bool pend[4] = {false, false, false, false};  // (indexed as SideStream::buf)
   int dzk = 0;
   void use_side() {
     if (train && side_stream_enabled() && pl.side && pl.side->init()) side = pl.side.get();
   }
   hipStream_t wst() const { return side ? side->s : r.st; }
+  // the PPM branches as one fused launch each way (ppm.hip; FSCNN_PPM_FUSED=0: general kernels)
+  bool ppm_fused() const {
+    static const bool on = [] {
+      const char* e = getenv("FSCNN_PPM_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    return on && train && ppm_branches_ok((int)pl.ppk[3].M, 128, dt);
+  }
   int fork() {  // everything enqueued on the main stream so far happens before the side's next
     if (!side) return OK;
     if (hipEventRecord(side->fork, r.st) != hipSuccess ||
@@ -567,24 +577,41 @@ struct Exec {
     }
     return OK;
   }
-  int release(const void* p) {  // the side's work so far is the last reader of buffer p
+  // the side's work so far is the last reader of dz buffer k, or (fused) of operand table k
+  int release(const void* p, const float* tab = nullptr) {
     if (!side) return OK;
-    const int k = p == Bw(pl.dz) ? 0 : (p == Bw(pl.dz2) ? 1 : -1);
-    if (k < 0) return OK;
-    if (hipEventRecord(side->buf[k], side->s) != hipSuccess) {
+    int i = -1;
+    if (tab)
+      i = (const void*)tab == Bw(pl.xtab) ? 2 : ((const void*)tab == Bw(pl.xtab2) ? 3 : -1);
+    else
+      i = p == Bw(pl.dz) ? 0 : (p == Bw(pl.dz2) ? 1 : -1);
+    if (i < 0) return OK;
+    if (hipEventRecord(side->buf[i], side->s) != hipSuccess) {
       set_error("side stream: event record failed");
       return E_HIP;
     }
-    pend[k] = true;
+    pend[i] = true;
     return OK;
   }
-  void* dz_buf() {  // the next BN-backward output buffer, once no side reader is left on it
-    const int k = dzk;
-    dzk ^= 1;
-    if (side && pend[k]) {
-      (void)hipStreamWaitEvent(r.st, side->buf[k], 0);
-      pend[k] = false;
+  void wait_buf(int i) {
+    if (side && pend[i]) {
+      (void)hipStreamWaitEvent(r.st, side->buf[i], 0);
+      pend[i] = false;
     }
+  }
+  // operand table of pair dzk (the next BN backward's), once no side reader is left on it
+  int next_tab() {
+    wait_buf(2 + dzk);
+    return dzk;
+  }
+  // the next BN-backward output buffer (its operand table: xtab of the same pair, see bwd_tab)
+  int curk = 0;
+  void* dz_buf() {
+    const int k = dzk;
+    wait_buf(k);
+    wait_buf(2 + k);
+    dzk ^= 1;
+    curk = k;
     return Bw(k ? pl.dz2 : pl.dz);
   }
   int join() {
@@ -594,7 +621,7 @@ struct Exec {
       set_error("side stream: join failed");
       return E_HIP;
     }
-    pend[0] = pend[1] = false;
+    for (bool& b : pend) b = false;
     return OK;
   }
 
@@ -850,9 +877,25 @@ struct Exec {
       p.pooled = W(pl.pooled);
       TRY(pyramid_pool(p, dt, r.st));
       static const int base[4] = {0, 1, 5, 14};
-      for (int i = 0; i < 4; ++i) {
-        const void* xin = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
-        TRY(pw(pl.ppk[i], net.ppm_c[i], &net.ppm_b[i], raw(xin, 128), true));
+      if (ppm_fused()) {
+        // the four branch convs + BN + ReLU in one launch (block-local batch statistics)
+        g_prof_tag = "global_feature_extractor.ppm.conv1-4";
+        PpmFwdArgs f{};
+        f.nb = 4; f.K = 128; f.C = 32;
+        for (int i = 0; i < 4; ++i) {
+          const Unit& u = pl.ppk[i];
+          PpmBranchFwd& b = f.b[i];
+          b.f = fin_args(u, net.ppm_b[i]);
+          b.x = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
+          b.w = Wg(net.ppm_c[i]);
+          b.z = W(u.z); b.y = W(u.a); b.ldy = u.ld; b.M = (int)u.M;
+        }
+        TRY(ppm_branches_fwd(f, dt, r.st));
+      } else {
+        for (int i = 0; i < 4; ++i) {
+          const void* xin = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
+          TRY(pw(pl.ppk[i], net.ppm_c[i], &net.ppm_b[i], raw(xin, 128), true));
+        }
       }
       g_prof_tag = "global_feature_extractor.ppm.upsample";
       PpmUpArgs u{};
@@ -1054,7 +1097,7 @@ struct Exec {
       out = plain(dz, u.C);
       return OK;
     }
-    const BnBwdTab tb = bwd_tab(u, relu_z);
+    const BnBwdTab tb = bwd_tab(u, relu_z, curk);  // the pair dz_buf() just handed out
     TRY(bn_bwd_stats(u, bn, dy, lddy, nullptr, 0, relu_z, tb));
     out = {dy, lddy, W(u.z), tb.tab};
     return OK;
@@ -1092,11 +1135,12 @@ struct Exec {
     g.tail.coef = (float*)Bw(pl.coef);
     // the operand table too: a fused consumer (depthwise, or every pointwise one in mode 2)
     // reads it instead of a materialised dz
-    g.tail.tab = bwd_tab(u, t.mode == 2);
+    // (pair dzk: the target's bn_bwd_x is the next BN backward and takes that same pair)
+    g.tail.tab = bwd_tab(u, t.mode == 2, next_tab());
   }
-  BnBwdTab bwd_tab(const Unit& u, bool relu) const {
+  BnBwdTab bwd_tab(const Unit& u, bool relu, int k) const {
     BnBwdTab tb;
-    tb.tab = (float*)Bw(pl.xtab);
+    tb.tab = (float*)Bw(k ? pl.xtab2 : pl.xtab);
     tb.scale = Wf(u.scale); tb.shift = Wf(u.shift); tb.mean = Wf(u.mean); tb.invstd = Wf(u.invstd);
     tb.relu = relu;
     return tb;
@@ -1112,10 +1156,8 @@ struct Exec {
     int S = gemm_tn_splits((int)M, c.cout, K);
     t.slab = slab_alloc((size_t)S * c.cout * K);
     if (!t.slab) return slab_oom();
-    // an operand table (fused BN-backward) is shared scratch the main stream rewrites for the
-    // next BN: such a wgrad stays on the main stream
-    const hipStream_t ws2 = dz.tab ? r.st : wst();
-    if (!dz.tab) TRY(fork());
+    TRY(fork());
+    const hipStream_t ws2 = wst();
     TRY(gemm_tn(t, S, dt, ws2));
     TRY(defer_reduce(t.slab, S, (long long)c.cout * K, G(c.w), 0));
     if (c.b >= 0) {
@@ -1128,7 +1170,7 @@ struct Exec {
       TRY(colsum(dz.p, (int)M, c.cout, dz.ld, part, dt, ws2));
       TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
-    if (!dz.tab) TRY(release(dz.p));
+    TRY(release(dz.p, dz.tab));
     if (!dX) return OK;
     GemmArgs g{};
     g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
@@ -1164,10 +1206,9 @@ struct Exec {
     const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
     d.slab = slab_alloc((size_t)S * 9 * C);
     if (!d.slab) return slab_oom();
-    const hipStream_t ws2 = dz.tab ? r.st : wst();  // (see pw_bwd)
-    if (!dz.tab) TRY(fork());
-    TRY(dw_wgrad(d, dt, ws2));
-    if (!dz.tab) TRY(release(dz.p));
+    TRY(fork());
+    TRY(dw_wgrad(d, dt, wst()));
+    TRY(release(dz.p, dz.tab));
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
     const bool br = bt.u && train && dw_bnred_enabled();
     if (br) {
@@ -1270,7 +1311,28 @@ struct Exec {
       g_prof_tag = "global_feature_extractor.ppm.upsample (backward)";
       TRY(ppm_up_bwd(u, Bw(pl.g_feats), dt, r.st));
       static const int base[4] = {0, 1, 5, 14};
-      for (int i = 0; i < 4; ++i) {
+      if (ppm_fused()) {
+        g_prof_tag = "global_feature_extractor.ppm.conv1-4 (backward)";
+        PpmBwdArgs f{};
+        f.nb = 4; f.K = 128; f.C = 32;
+        for (int i = 0; i < 4; ++i) {
+          const Unit& u4 = pl.ppk[i];
+          const size_t off = (size_t)base[i] * N;
+          PpmBranchBwd& b = f.b[i];
+          b.dy = (char*)Bw(pl.g_feats) + off * 32 * E; b.lddy = 32;
+          b.y = (char*)W(pl.feats_a) + off * 32 * E; b.ldy = 32;
+          b.z = W(u4.z);
+          b.mean = Wf(u4.mean); b.invstd = Wf(u4.invstd); b.scale = Wf(u4.scale);
+          b.x = (char*)W(pl.pooled) + off * 128 * E;
+          b.w = Wg(net.ppm_c[i]);
+          b.dgamma = G(net.ppm_b[i].g); b.dbeta = G(net.ppm_b[i].b);
+          b.dw = G(net.ppm_c[i].w);
+          b.dx = (char*)Bw(pl.g_pooled) + off * 128 * E;
+          b.M = (int)u4.M;
+        }
+        TRY(ppm_branches_bwd(f, dt, r.st));
+      }
+      for (int i = 0; i < 4 && !ppm_fused(); ++i) {
         const Unit& u4 = pl.ppk[i];
         size_t off = (size_t)base[i] * N;
         void* zp = dz_buf();
@@ -1341,7 +1403,7 @@ struct Exec {
     if (!c.slab) return slab_oom();
     TRY(fork());
     TRY(conv0_wgrad(c, dt, wst()));
-    TRY(release(d.p));
+    TRY(release(d.p, d.tab));
     return defer_reduce(c.slab, S, 864, G(net.c0.w), 0);
   }
 };

@@ -21,6 +21,12 @@ SHAPES = [  # (name, M, N, K)
     ("cls pw", 262144, 128, 128),
     ("ffm high", 262144, 128, 64),
     ("b1.0 proj dgrad", 65536, 384, 64),
+    ("b1 project", 65536, 64, 384),
+    ("b2.1 project", 16384, 96, 576),
+    ("b3.0 project", 16384, 128, 576),
+    ("b2.1 exp dgrad", 16384, 96, 576),
+    ("b1.0 exp dgrad", 262144, 64, 384),
+    ("ppm out", 16384, 128, 256),
 ]
 
 
