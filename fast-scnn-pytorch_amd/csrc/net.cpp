@@ -13,7 +13,9 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
+#include <vector>
 
 #include <cstdio>
 #include <cstring>
@@ -396,8 +398,19 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     for (int i = 0; i < 9; ++i) { upd(pl.lbe[i]); upd(pl.lbd[i]); upd(pl.lbp[i]); }
     upd(pl.po); upd(pl.fdw); upd(pl.flow); upd(pl.c1dw); upd(pl.c1pw);
     if (net.aux) upd(pl.aux0);
-    pl.dz = B.get((size_t)max_mc * E);
-    pl.dz2 = B.get((size_t)max_mc * E);  // ping-pong: a wgrad on the side stream may still read dz
+    // BN-backward outputs: one slot per unit per backward call (Exec::dz_buf), so a wgrad
+    // queued for the side stream never races a later rewrite
+    size_t dzs = 0;
+    auto dzu = [&](const Unit& u) { dzs += ((size_t)u.M * u.C * E + 255) / 256 * 256; };
+    dzu(pl.c0); dzu(pl.l1dw); dzu(pl.l1pw); dzu(pl.l2dw); dzu(pl.l2pw);
+    for (int i = 0; i < 9; ++i) { dzu(pl.lbe[i]); dzu(pl.lbd[i]); dzu(pl.lbp[i]); }
+    for (int i = 0; i < 4; ++i) dzu(pl.ppk[i]);
+    dzu(pl.po); dzu(pl.fdw); dzu(pl.flow); dzu(pl.fhigh); dzu(pl.c1dw); dzu(pl.c1pw);
+    dzu(pl.c2dw); dzu(pl.c2pw);
+    if (net.aux) dzu(pl.aux0);
+    (void)max_mc;
+    pl.dz_bytes = dzs;
+    pl.dz = B.get(dzs);
     // weight-gradient partial slabs: the reductions of a backward stage are deferred to one
     // multi-job launch pair (Exec::flush_reduce), so every job keeps its own slab until then;
     // the arena holds the whole step's (sum over jobs, 64-float aligned each)
@@ -458,8 +471,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     dw_upd(pl.H3, pl.W3, 128, 1);
     pl.bnpart = B.get(bnp * 4);
     pl.coef = B.get(2 * 1024 * 4);
-    pl.xtab = B.get((size_t)1024 * BWDX_STRIDE * 4);
-    pl.xtab2 = B.get((size_t)1024 * BWDX_STRIDE * 4);
+    pl.xtab = B.get((size_t)NTAB_SLOTS * 1024 * BWDX_STRIDE * 4);  // Exec::tab_slot
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
     pl.bws_bytes = B.top;
     auto gu = [&](const std::string& n, const Unit& u) {
@@ -488,19 +500,21 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
 // The backward's weight gradients (gemm_tn, colsum, depthwise / conv0 wgrad) only feed the
 // deferred slab reduction at the end of their stage, so they run on a second stream, beside
 // the dgrad -> BN-backward chain that carries the critical path: many of those launches are
-// latency-bound and leave HBM idle.  Dependencies are events: fork (the wgrad's operands and
-// slab are ready), the dz ping-pong buffer it read (released before that buffer is rewritten),
-// and join (before the stage's slab reduction).  FSCNN_SIDE_STREAM=0 keeps one stream.
+// latency-bound and leave HBM idle.  Every event recorded on a stream costs that stream ~7 us
+// of idle time on MI355X (measured: 61 such gaps = 0.43 ms of a 7.05 ms step), so events are
+// kept to one fork per wgrad launch (Exec::side_launch) and one join before the stage's slab
+// reduction: every BN-backward output dz and operand table a wgrad reads has its own slot in
+// the step's arenas (no reuse, so no release events; 7.08 -> 7.00 ms/step).
+// FSCNN_SIDE_STREAM=0 keeps one stream.
 struct SideStream {
   hipStream_t s = nullptr;
-  // buf[k]: last side read of dz buffer k; buf[2 + k]: of operand table k
-  hipEvent_t fork = nullptr, join = nullptr, buf[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t fork = nullptr, join = nullptr;
   bool ready = false, failed = false;
   bool init() {
     if (ready || failed) return ready;
     failed = true;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
-    hipEvent_t* ev[6] = {&fork, &join, &buf[0], &buf[1], &buf[2], &buf[3]};
+    hipEvent_t* ev[2] = {&fork, &join};
     for (auto* e : ev)
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
     ready = true;
@@ -508,7 +522,7 @@ struct SideStream {
     return true;
   }
   ~SideStream() {
-    hipEvent_t ev[6] = {fork, join, buf[0], buf[1], buf[2], buf[3]};
+    hipEvent_t ev[2] = {fork, join};
     for (auto e : ev)
       if (e) (void)hipEventDestroy(e);
     if (s) (void)hipStreamDestroy(s);
@@ -554,12 +568,10 @@ struct Exec {
 
   // ---- side stream for the weight gradients (backward only; see SideStream) ----------------
   SideStream* side = nullptr;
-  bool pend[4] = {false, false, false, false};  // (indexed as SideStream::buf)
-  int dzk = 0;
+  std::vector<std::function<int(hipStream_t)>> sideq;  // wgrads waiting for the next fork
   void use_side() {
     if (train && side_stream_enabled() && pl.side && pl.side->init()) side = pl.side.get();
   }
-  hipStream_t wst() const { return side ? side->s : r.st; }
   // the PPM branches as one fused launch each way (ppm.hip; FSCNN_PPM_FUSED=0: general kernels)
   bool ppm_fused() const {
     static const bool on = [] {
@@ -568,61 +580,70 @@ struct Exec {
     }();
     return on && train && ppm_branches_ok((int)pl.ppk[3].M, 128, dt);
   }
-  int fork() {  // everything enqueued on the main stream so far happens before the side's next
-    if (!side) return OK;
+  // a weight-gradient launch: queued for the side stream (issued by flush_side), or run now on
+  // the main stream without one
+  int side_launch(std::function<int(hipStream_t)> f) {
+    if (!side) return f(r.st);
+    const char* tag = g_prof_tag;  // the launch keeps its layer label (per-launch profile)
+    sideq.push_back([tag, f](hipStream_t s) {
+      const char* o = g_prof_tag;
+      g_prof_tag = tag;
+      const int rc = f(s);
+      g_prof_tag = o;
+      return rc;
+    });
+    // FSCNN_SIDE_BATCH=1: issue the queue only at the flush points (one fork per block) —
+    // measured slower (7.24 vs 7.00 ms/step): a wgrad started as soon as its dz exists fills the
+    // idle issue slots of the latency-bound dgrad chain, a delayed batch contends with the next
+    // block instead
+    static const bool batch = [] {
+      const char* e = getenv("FSCNN_SIDE_BATCH");
+      return e && e[0] == '1';
+    }();
+    return batch ? OK : flush_side();
+  }
+  // one fork: everything enqueued on the main stream so far happens before the queued wgrads
+  int flush_side() {
+    if (!side || sideq.empty()) return OK;
     if (hipEventRecord(side->fork, r.st) != hipSuccess ||
         hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess) {
       set_error("side stream: fork failed");
       return E_HIP;
     }
+    for (auto& f : sideq) TRY(f(side->s));
+    sideq.clear();
     return OK;
-  }
-  // the side's work so far is the last reader of dz buffer k, or (fused) of operand table k
-  int release(const void* p, const float* tab = nullptr) {
-    if (!side) return OK;
-    int i = -1;
-    if (tab)
-      i = (const void*)tab == Bw(pl.xtab) ? 2 : ((const void*)tab == Bw(pl.xtab2) ? 3 : -1);
-    else
-      i = p == Bw(pl.dz) ? 0 : (p == Bw(pl.dz2) ? 1 : -1);
-    if (i < 0) return OK;
-    if (hipEventRecord(side->buf[i], side->s) != hipSuccess) {
-      set_error("side stream: event record failed");
-      return E_HIP;
-    }
-    pend[i] = true;
-    return OK;
-  }
-  void wait_buf(int i) {
-    if (side && pend[i]) {
-      (void)hipStreamWaitEvent(r.st, side->buf[i], 0);
-      pend[i] = false;
-    }
-  }
-  // operand table of pair dzk (the next BN backward's), once no side reader is left on it
-  int next_tab() {
-    wait_buf(2 + dzk);
-    return dzk;
-  }
-  // the next BN-backward output buffer (its operand table: xtab of the same pair, see bwd_tab)
-  int curk = 0;
-  void* dz_buf() {
-    const int k = dzk;
-    wait_buf(k);
-    wait_buf(2 + k);
-    dzk ^= 1;
-    curk = k;
-    return Bw(k ? pl.dz2 : pl.dz);
   }
   int join() {
     if (!side) return OK;
+    TRY(flush_side());
     if (hipEventRecord(side->join, side->s) != hipSuccess ||
         hipStreamWaitEvent(r.st, side->join, 0) != hipSuccess) {
       set_error("side stream: join failed");
       return E_HIP;
     }
-    for (bool& b : pend) b = false;
     return OK;
+  }
+  // BN-backward output dz of unit u: its own slot of the step's dz arena (a queued wgrad may
+  // read it after the main stream has moved on)
+  size_t dz_top = 0;
+  void* dz_buf(const Unit& u) {
+    const size_t bytes = ((size_t)u.M * u.C * E + 255) / 256 * 256;
+    if (dz_top + bytes > pl.dz_bytes) return nullptr;
+    void* p = (char*)Bw(pl.dz) + dz_top;
+    dz_top += bytes;
+    return p;
+  }
+  // BN-backward operand table of unit u (written by its dy producer's BN finish, read by the
+  // consumers of the fused dz): one slot per unit
+  const Unit* tab_units[NTAB_SLOTS] = {};
+  int ntab = 0;
+  float* tab_slot(const Unit& u) {
+    for (int i = 0; i < ntab; ++i)
+      if (tab_units[i] == &u) return (float*)Bw(pl.xtab) + (size_t)i * 1024 * BWDX_STRIDE;
+    if (ntab == NTAB_SLOTS) return nullptr;
+    tab_units[ntab] = &u;
+    return (float*)Bw(pl.xtab) + (size_t)(ntab++) * 1024 * BWDX_STRIDE;
   }
 
   void* W(size_t off) const { return ws + off; }
@@ -1046,7 +1067,7 @@ struct Exec {
       TRY(dropout(d, dt, r.st));
     }
     Dz d;
-    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, dz_buf(), d));
+    TRY(bn_bwd_x(u, net.aux1, Bw(u.ga), 32, true, dz_buf(u), d));
     TRY(pw_bwd(net.aux0, u.M, d, raw(W(pl.aux_col), 576), Bw(pl.aux_dcol), 576));
     Col2ImArgs cc{};
     cc.N = N; cc.H = pl.H3; cc.W = pl.W3; cc.C = 64; cc.dcol = Bw(pl.aux_dcol); cc.ldcol = 576;
@@ -1097,7 +1118,7 @@ struct Exec {
       out = plain(dz, u.C);
       return OK;
     }
-    const BnBwdTab tb = bwd_tab(u, relu_z, curk);  // the pair dz_buf() just handed out
+    const BnBwdTab tb = bwd_tab(u, relu_z, tab_slot(u));  // written by u's dy producer
     TRY(bn_bwd_stats(u, bn, dy, lddy, nullptr, 0, relu_z, tb));
     out = {dy, lddy, W(u.z), tb.tab};
     return OK;
@@ -1105,6 +1126,10 @@ struct Exec {
   int bn_bwd(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
              int ldmask, void* dz, bool relu_z = false) {
     g_prof_tag = u.name.c_str();
+    if (!dz) {
+      set_error("backward: dz arena exhausted (%s)", u.name.c_str());
+      return E_INVALID;
+    }
     TRY(bn_bwd_stats(u, bn, dy, lddy, mask, ldmask, relu_z, BnBwdTab()));
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
@@ -1134,13 +1159,12 @@ struct Exec {
     g.tail.dbeta = G(t.bn->b);
     g.tail.coef = (float*)Bw(pl.coef);
     // the operand table too: a fused consumer (depthwise, or every pointwise one in mode 2)
-    // reads it instead of a materialised dz
-    // (pair dzk: the target's bn_bwd_x is the next BN backward and takes that same pair)
-    g.tail.tab = bwd_tab(u, t.mode == 2, next_tab());
+    // reads it instead of a materialised dz (the target's own slot, see bn_bwd_x)
+    g.tail.tab = bwd_tab(u, t.mode == 2, tab_slot(u));
   }
-  BnBwdTab bwd_tab(const Unit& u, bool relu, int k) const {
+  BnBwdTab bwd_tab(const Unit& u, bool relu, float* tab) const {
     BnBwdTab tb;
-    tb.tab = (float*)Bw(k ? pl.xtab2 : pl.xtab);
+    tb.tab = tab;
     tb.scale = Wf(u.scale); tb.shift = Wf(u.shift); tb.mean = Wf(u.mean); tb.invstd = Wf(u.invstd);
     tb.relu = relu;
     return tb;
@@ -1156,9 +1180,8 @@ struct Exec {
     int S = gemm_tn_splits((int)M, c.cout, K);
     t.slab = slab_alloc((size_t)S * c.cout * K);
     if (!t.slab) return slab_oom();
-    TRY(fork());
-    const hipStream_t ws2 = wst();
-    TRY(gemm_tn(t, S, dt, ws2));
+    const int dtc = dt;
+    TRY(side_launch([t, S, dtc](hipStream_t s) { return gemm_tn(t, S, dtc, s); }));
     TRY(defer_reduce(t.slab, S, (long long)c.cout * K, G(c.w), 0));
     if (c.b >= 0) {
       float* part = slab_alloc((size_t)colsum_parts((int)M) * c.cout);
@@ -1167,10 +1190,13 @@ struct Exec {
         set_error("pw_bwd: bias gradient of a fused BN-backward operand");
         return E_UNSUPPORTED;
       }
-      TRY(colsum(dz.p, (int)M, c.cout, dz.ld, part, dt, ws2));
+      const void* dp = dz.p;
+      const int Mi = (int)M, co = c.cout, ld = dz.ld;
+      TRY(side_launch([dp, Mi, co, ld, part, dtc](hipStream_t s) {
+        return colsum(dp, Mi, co, ld, part, dtc, s);
+      }));
       TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
-    TRY(release(dz.p, dz.tab));
     if (!dX) return OK;
     GemmArgs g{};
     g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
@@ -1206,9 +1232,11 @@ struct Exec {
     const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
     d.slab = slab_alloc((size_t)S * 9 * C);
     if (!d.slab) return slab_oom();
-    TRY(fork());
-    TRY(dw_wgrad(d, dt, wst()));
-    TRY(release(dz.p, dz.tab));
+    {
+      const DwBwdArgs dw = d;
+      const int dtc = dt;
+      TRY(side_launch([dw, dtc](hipStream_t s) { return dw_wgrad(dw, dtc, s); }));
+    }
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
     const bool br = bt.u && train && dw_bnred_enabled();
     if (br) {
@@ -1260,30 +1288,34 @@ struct Exec {
     }
     // classifier dsconv2, dsconv1
     Dz d;
-    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz_buf(), d));
+    TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz_buf(pl.c2pw), d));
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw, net.cls2.bdw)));
-    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz_buf(), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz_buf(pl.c2dw), d, dw_bx_enabled()));
     TRY(dw_bwd(net.cls2.dw, 128, d, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
                relu_target(pl.c1pw, net.cls1.bpw)));
-    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz_buf(), d));
+    TRY(flush_side());
+    TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz_buf(pl.c1pw), d));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw, net.cls1.bdw)));
-    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz_buf(), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz_buf(pl.c1dw), d, dw_bx_enabled()));
     TRY(dw_bwd(net.cls1.dw, 128, d, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
+    TRY(flush_side());
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
-    void* zl = dz_buf();
+    void* zl = dz_buf(pl.flow);
     TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, zl));
     TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(zl, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw, net.ffm_bdw)));
-    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz_buf(), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz_buf(pl.fdw), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ffm_dw, 128, d, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
-    void* zh = dz_buf();
+    TRY(flush_side());
+    void* zh = dz_buf(pl.fhigh);
     TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, zh));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(zh, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
+    TRY(flush_side());
     if (net.aux) TRY(backward_aux());
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
     g_prof_tag = "feature_fusion.upsample (backward)";
@@ -1302,8 +1334,9 @@ struct Exec {
       TRY(axis_bwd(b, DT_F32, dt, r.st));
     }
     // PPM out 1x1 (256→128) over the concat buffer
-    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, dz_buf(), d));
+    TRY(bn_bwd_x(pl.po, net.ppm_ob, Bw(pl.po.ga), 128, true, dz_buf(pl.po), d));
     TRY(pw_bwd(net.ppm_o, pl.po.M, d, raw(W(pl.concat), 256), Bw(pl.g_concat), 256));
+    TRY(flush_side());
     {
       PpmUpArgs u{};
       u.N = N; u.H = pl.H5; u.W = pl.W5; u.CF = 32; u.feats = nullptr;
@@ -1335,7 +1368,7 @@ struct Exec {
       for (int i = 0; i < 4 && !ppm_fused(); ++i) {
         const Unit& u4 = pl.ppk[i];
         size_t off = (size_t)base[i] * N;
-        void* zp = dz_buf();
+        void* zp = dz_buf(u4);
         TRY(bn_bwd(u4, net.ppm_b[i], (char*)Bw(pl.g_feats) + off * 32 * E, 32,
                    (char*)W(pl.feats_a) + off * 32 * E, 32, zp));
         TRY(pw_bwd(net.ppm_c[i], u4.M, plain(zp, 32), raw((char*)W(pl.pooled) + off * 128 * E, 128),
@@ -1365,35 +1398,38 @@ struct Exec {
     // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
     // block: its dy is the PPM concat gradient)
     Dz d;
-    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz_buf(), d));
+    TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz_buf(up), d));
     TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud, l.bd)));
-    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz_buf(), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz_buf(ud), d, dw_bx_enabled()));
     TRY(dw_bwd(l.d, e, d, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue, l.be)));
-    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz_buf(), d));
+    TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz_buf(ue), d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
     const void* R = shortcut ? Bw(up.ga) : (i == 0 ? gx : nullptr);
     int ldr = shortcut ? up.ga_ld : (i == 0 ? gxld : 0);
     // the dgrad is the dy of the previous block's project BN (or of LTD.dsconv2's pw BN)
     const BTarget bt = i == 0 ? relu_target(pl.l2pw, net.ltd2.bpw)
                               : plain_target(pl.lbp[i - 1], net.lb[i - 1].bp);
-    return pw_bwd(l.e, ue.M, d, raw(x, xld), gx, gxld, R, ldr, bt);
+    TRY(pw_bwd(l.e, ue.M, d, raw(x, xld), gx, gxld, R, ldr, bt));
+    return flush_side();  // the block's three wgrads behind one fork
   }
 
   int backward_ltd() {
     Dz d;
-    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz_buf(), d));
+    TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz_buf(pl.l2pw), d));
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw, net.ltd2.bdw)));
-    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz_buf(), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz_buf(pl.l2dw), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ltd2.dw, 48, d, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
                relu_target(pl.l1pw, net.ltd1.bpw)));
-    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz_buf(), d));
+    TRY(flush_side());
+    TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz_buf(pl.l1pw), d));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
-    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(pl.l1dw), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
                relu_target(pl.c0, net.b0)));
-    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz_buf(), d, true));
+    TRY(flush_side());
+    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz_buf(pl.c0), d, true));
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
@@ -1401,10 +1437,10 @@ struct Exec {
     c.dz = d.p; c.zz = d.z; c.tab = d.tab; c.slab = slab_alloc((size_t)S * 864);
     c.rows_per_block = 8;
     if (!c.slab) return slab_oom();
-    TRY(fork());
-    TRY(conv0_wgrad(c, dt, wst()));
-    TRY(release(d.p, d.tab));
-    return defer_reduce(c.slab, S, 864, G(net.c0.w), 0);
+    const int dtc = dt;
+    TRY(side_launch([c, dtc](hipStream_t s) { return conv0_wgrad(c, dtc, s); }));
+    TRY(defer_reduce(c.slab, S, 864, G(net.c0.w), 0));
+    return flush_side();
   }
 };
 

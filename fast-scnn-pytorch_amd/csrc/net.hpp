@@ -82,6 +82,7 @@ struct Unit {
 
 struct GraphCache;
 struct SideStream;
+constexpr int NTAB_SLOTS = 64;  // BN-backward operand tables per backward call (Exec::tab_slot)
 
 struct Plan {
   const Net* net = nullptr;
@@ -106,7 +107,8 @@ struct Plan {
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
-         g_aux = 0, g_auxlog = 0, aux_dcol = 0, xtab = 0, xtab2 = 0, dz2 = 0;
+         g_aux = 0, g_auxlog = 0, aux_dcol = 0, xtab = 0;
+  size_t dz_bytes = 0;             // the dz arena (one slot per unit, Exec::dz_buf)
   // named buffers for debugging / stage-level parity: name -> (offset, rows, cols, ld, in_bws)
   struct Named { std::string name; size_t off; long long rows; int cols, ld, bws; };
   std::vector<Named> named;
