@@ -672,6 +672,12 @@ static int gs_pick_nt(const GemmArgs& a, int ks) {
   if (ks > 8) return N % 64 == 0 ? 4 : (N % 48 == 0 ? 3 : 4);  // deep K: weights [<=64][K] in LDS
   if (N <= 48) return 3;
   if (N <= 64 || a.bpart) return 4;
+  static const bool st4 = [] {  // FSCNN_GS_ST4=0: statistics forms with K > 64 keep NT = 6 (A/B)
+    const char* e = getenv("FSCNN_GS_ST4");
+    return !(e && e[0] == '0');
+  }();
+  // statistics forms with ks > 2 cannot hold 6 column tiles in 256 VGPRs: 4 when N allows
+  if (st4 && a.part && ks > 2 && N % 64 == 0) return 4;
   if (N % 96 == 0) return 6;
   return a.part ? 4 : 8;
 }
@@ -707,7 +713,11 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   if (deep && (dtype == DT_F32 || !deep_on)) return false;
   // (measured: at M <= 65536 each wave streams one or two chunks and the part-by-part load chain
   //  is slower than the tiled kernel; at M = 262,144, e.g. bottleneck1.0's expand dgrad, 10% faster)
-  if (deep && a.M < 131072) return false;
+  static const int deep_min = [] {  // FSCNN_GS_DEEP_MIN: smallest M of a deep-K stream (A/B)
+    const char* e = getenv("FSCNN_GS_DEEP_MIN");
+    return e ? atoi(e) : 131072;
+  }();
+  if (deep && a.M < deep_min) return false;
   if (!(ks == 1 || ks == 2 || ks == 3 || ks == 4 || ks == 6 || ks == 8 || deep)) return false;
   const int nt = gs_pick_nt(a, ks);
   // keep the statistics forms within 256 VGPRs (measured: these would spill)
