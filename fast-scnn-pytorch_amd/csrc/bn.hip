@@ -510,4 +510,12 @@ int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
   return check_launch("bn_bwd_apply");
 }
 
+bool tail_ink_on(int bit) {
+  static const int mask = [] {
+    const char* e = getenv("FSCNN_TAIL_INK");
+    return e ? atoi(e) : 15;
+  }();
+  return (mask & bit) != 0;
+}
+
 }  // namespace fscnn

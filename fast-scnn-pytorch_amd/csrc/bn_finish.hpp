@@ -57,4 +57,135 @@ __device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2
   }
 }
 
+// ---- generic in-kernel finish over per-workgroup records ----------------------------------
+// For producers whose workgroup writes ONE record row p < P of records part[P][R][N] (R = 3:
+// mean, M2, count; R = 2: s1, s2) for a contiguous channel slice [c0, c0 + nc), stored with
+// write-through stores (st_wt).  Same protocol as the streaming GEMM's finish (common.hpp
+// arrive_last): workgroups arrive in teams of TS consecutive rows; a team's last arriver folds
+// the team's rows into the team's first row; the channel chunk's last team arriver folds the
+// team rows and finishes each channel with the finalize kernels' arithmetic.  Every fold is one
+// or two batches of loads deep (TS <= 2 * 8 * slices, nteam <= TAIL_TMAX).  fp64 sums in fixed
+// order: deterministic run to run.  Counters: ctr[chunk], ctr[TAIL_TEAM0 + chunk*TAIL_TMAX + team].
+constexpr int TAIL_TEAM0 = 64;
+constexpr int TAIL_TMAX = 32;
+__host__ __device__ inline int tail_team_size(int P) {
+  const int t = (P + TAIL_TMAX - 1) / TAIL_TMAX;
+  return t < 16 ? 16 : t;
+}
+// whether a producer with P record rows and `chunks` channel chunks fits the counter budget
+__host__ __device__ inline bool tail_fits(int P, int chunks) {
+  return P > 0 && P <= 64 * TAIL_TMAX && chunks <= (BN_COUNTERS - TAIL_TEAM0) / TAIL_TMAX &&
+         chunks <= TAIL_TEAM0;
+}
+constexpr int TAIL_CMAX = 1024;  // channels of the team-sum scratch (Plan::tsum)
+
+__device__ __forceinline__ void st_wt64(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt64(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// fold of `count` rows for channels [c0, c0 + nc) (nc <= workgroup size): TEAM = false reads
+// the float records part[first + i][R][N] (R = 3 forward (mean, M2, count), 2 backward);
+// TEAM = true reads the fp64 team sums tsum[i][3][N] (n, s1, s2).  Returns (n, s1, s2) sums in
+// the slice-0 threads (tid < nc).
+template <bool FWD, bool TEAM>
+__device__ inline void tail_fold(const float* part, const double* tsum, int N, int c0, int nc,
+                                 int first, int count, double* s_f, double (&sum)[3]) {
+  const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+  const int nthr = blockDim.x * blockDim.y * blockDim.z;  // <= 256, >= nc
+  const int S = nthr / nc;
+  const int col = tid % nc, sl = tid / nc;
+  const int n = c0 + col;
+  constexpr int R = TEAM ? 3 : (FWD ? 3 : 2);
+  constexpr int U = R == 3 ? 8 : 4;  // rows per thread per batch (all loads before the sums)
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+  if (sl < S && n < N) {
+    for (int i0 = sl; i0 < count; i0 += U * S) {
+      double v[U][R];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * S;
+        const int row = first + (i < count ? i : i0);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          if constexpr (TEAM) v[u][j] = ld_wt64(tsum + ((size_t)row * 3 + j) * N + n);
+          else v[u][j] = ld_wt(part + ((size_t)row * R + j) * N + n);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + u * S >= count) break;
+        if constexpr (TEAM) {
+          t0 += v[u][0];
+          t1 += v[u][1];
+          t2 += v[u][2];
+        } else if constexpr (FWD) {  // (mean, M2, count) -> (n, n*mean, M2 + n*mean^2)
+          const double cn = v[u][2], m = v[u][0];
+          t0 += cn;
+          t1 += cn * m;
+          t2 += v[u][1] + cn * m * m;
+        } else {
+          t1 += v[u][0];
+          t2 += v[u][1];
+        }
+      }
+    }
+  }
+  __syncthreads();  // s_f free (a previous fold's / the kernel's readers are done)
+  s_f[tid] = t0;
+  s_f[nthr + tid] = t1;
+  s_f[2 * nthr + tid] = t2;
+  __syncthreads();
+  sum[0] = sum[1] = sum[2] = 0.0;
+  if (sl == 0) {
+    for (int j = 0; j < S; ++j) {
+      sum[0] += s_f[j * nc + col];
+      sum[1] += s_f[nthr + j * nc + col];
+      sum[2] += s_f[2 * nthr + j * nc + col];
+    }
+  }
+}
+
+// every thread of the workgroup calls this after storing its record row p (st_wt); channel
+// slices wider than the workgroup are folded in passes of nthr channels.  The team sums stay
+// fp64 (t.tsum): a float team row would round the batch mean to fp32 before the final fold,
+// which is visible in x_hat wherever |mean| >> std.
+// lds: >= 3 * workgroup-size doubles of LDS the kernel no longer reads (aliased scratch, so
+// kernels that never finish in-kernel carry no extra LDS)
+template <bool FWD>
+__device__ inline void tail_finish(float* part, int P, int N, int p, int c0, int nc, int chunk,
+                                   const BnTail& t, double* lds) {
+  unsigned* ctr = t.counters;
+  const int TS = tail_team_size(P);
+  const int team = p / TS, nteam = (P + TS - 1) / TS;
+  const int tsize = min(TS, P - team * TS);
+  const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+  const int nthr = blockDim.x * blockDim.y * blockDim.z;
+  unsigned* tctr = ctr + TAIL_TEAM0 + chunk * TAIL_TMAX + team;
+  if (!arrive_last(tctr, (unsigned)tsize)) return;
+  for (int cb = 0; cb < nc; cb += nthr) {
+    const int ncb = min(nthr, nc - cb), n = c0 + cb + tid;
+    double s[3];
+    tail_fold<FWD, false>(part, nullptr, N, c0 + cb, ncb, team * TS, tsize, lds, s);
+    if (tid < ncb && n < N) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) st_wt64(t.tsum + ((size_t)team * 3 + j) * N + n, s[j]);
+    }
+  }
+  reset_counter(tctr);
+  if (!arrive_last(ctr + chunk, (unsigned)nteam)) return;
+  for (int cb = 0; cb < nc; cb += nthr) {
+    const int ncb = min(nthr, nc - cb), n = c0 + cb + tid;
+    double s[3];
+    tail_fold<FWD, true>(nullptr, t.tsum, N, c0 + cb, ncb, 0, nteam, lds, s);
+    if (tid < ncb && n < N) {
+      if constexpr (FWD) bn_fwd_finish(t.fwd, n, s[0], s[1], s[2]);
+      else bn_bwd_finish(n, N, s[1], s[2], t.count, t.dgamma, t.dbeta, t.coef, t.tab);
+    }
+  }
+  reset_counter(ctr + chunk);
+}
+
 }  // namespace fscnn

@@ -17,7 +17,7 @@
 //
 // Roofline: HBM-bound.  Algorithmic bytes per layer = e*(N*C*Hi*Wi + N*C*Ho*Wo) + 9*C*4,
 // flops = 18*N*C*Ho*Wo.
-#include "kernels.hpp"
+#include "bn_finish.hpp"
 
 namespace fscnn {
 
@@ -140,7 +140,9 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
 }
 
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
-template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool BX = false>
+// TL: the launch finishes its BN in the last workgroups (a.tail_ink; a separate instantiation so
+// the other launches keep their register budget)
+template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool BX = false, bool TL = false>
 __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
   // LDS sized per launch (dw_shm): the staged tile of cbv channel vectors + the reduction rows
@@ -272,10 +274,14 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
         for (int j = 0; j < 4; ++j) {
           float t = 0.f;
           for (int g2 = 0; g2 < G::G; ++g2) t += s_red[(g2 * QB + q) * 4 + j];
-          rec[(size_t)pass * a.C + c0 + j] = t;
+          st_wt(rec + (size_t)pass * a.C + c0 + j, t);
         }
       }
     }
+    if constexpr (TL)
+      tail_finish<false>(b.part, gridDim.y * gridDim.z, a.C, bz * gridDim.y + by,
+                         bx * cbv * VecW<T>::V, cbv * VecW<T>::V, bx, a.tail,
+                         reinterpret_cast<double*>(s_dyn));
     return;
   }
   if (a.part == nullptr) return;
@@ -319,11 +325,15 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
     for (int j = 0; j < 4; ++j) {
       float m2 = 0.f;
       for (int g = 0; g < G::G; ++g) m2 += s_red[(g * QB + q) * 4 + j];
-      rec[c0 + j] = mean[j];
-      rec[a.C + c0 + j] = m2;
-      rec[2 * a.C + c0 + j] = cnt;
+      st_wt(rec + c0 + j, mean[j]);
+      st_wt(rec + a.C + c0 + j, m2);
+      st_wt(rec + 2 * a.C + c0 + j, cnt);
     }
   }
+  if constexpr (TL)
+    tail_finish<true>(a.part, gridDim.y * gridDim.z, a.C, bz * gridDim.y + by,
+                      bx * cbv * VecW<T>::V, cbv * VecW<T>::V, bx, a.tail,
+                      reinterpret_cast<double*>(s_dyn));
 }
 
 // dynamic LDS of the tile kernels: the haloed input tile of cbv vectors + 4 floats per thread
@@ -372,9 +382,26 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     return check_launch("dw_fwd");
   }
   if constexpr (BR || BX) {  // stride-1 dgrad with BN-backward partials / operand transform
+    if constexpr (BR) {
+      if (a.tail_ink) {
+        if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX, true><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
+        else dw_fwd_kernel<bf16, 1, true, false, BR, BX, true><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
+        return check_launch("dw_dgrad");
+      }
+    }
     if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
     else dw_fwd_kernel<bf16, 1, true, false, BR, BX><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
     return check_launch("dw_dgrad");
+  }
+  if (!FLIP && a.tail_ink) {  // train forward with the in-kernel BN finish
+    if (dtype == DT_F32) {
+      if (a.stride == 1) dw_fwd_kernel<float, 1, false, IT, false, false, true><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
+      else dw_fwd_kernel<float, 2, false, IT, false, false, true><<<grid, nthr, dw_shm<float, 2>(cbv), st>>>(a, cbv);
+    } else {
+      if (a.stride == 1) dw_fwd_kernel<bf16, 1, false, IT, false, false, true><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
+      else dw_fwd_kernel<bf16, 2, false, IT, false, false, true><<<grid, nthr, dw_shm<bf16, 2>(cbv), st>>>(a, cbv);
+    }
+    return check_launch("dw_fwd");
   }
   if (dtype == DT_F32) {
     if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
@@ -400,7 +427,19 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     set_error("dw_fwd: in_scale without in_shift");
     return E_INVALID;
   }
-  return a.in_scale ? dw_launch_fwd<false, true>(a, dtype, st) : dw_launch_fwd<false, false>(a, dtype, st);
+  DwArgs b = a;
+  int P = 0;
+  if (a.part && a.tail.counters) {  // BN finish: in the kernel when the records fit its counters
+    int cbv;
+    const dim3 g = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
+    P = (int)(g.y * g.z);
+    b.tail_ink = tail_ink_on(2) && a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
+  }
+  const int rc = a.in_scale ? dw_launch_fwd<false, true>(b, dtype, st) : dw_launch_fwd<false, false>(b, dtype, st);
+  if (rc || !a.part || !a.tail.counters || b.tail_ink) return rc;
+  BnFinalizeArgs f = a.tail.fwd;
+  f.part = a.part; f.P = P; f.C = a.C; f.counters = a.tail.counters;
+  return bn_finalize(f, st);
 }
 
 static void dw_block_shape(int C, int V, int& bx, int& by) {
@@ -415,7 +454,7 @@ static void dw_block_shape(int C, int V, int& bx, int& by) {
 // stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even):
 //   row h0   <- dy row h0/2 (kh=1);  row h0+1 <- dy rows h0/2+1 (kh=0) and h0/2 (kh=2)
 //   col w0+q <- dy cols w0/2 + (q+1-kw)/2 for the kw of matching parity
-template <typename T, bool BR, bool XF = false>
+template <typename T, bool BR, bool XF = false, bool TL = false>
 __global__ __launch_bounds__(256, (BR || XF) ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
@@ -550,8 +589,12 @@ __global__ __launch_bounds__(256, (BR || XF) ? 2 : 3) void dw_dgrad_s2_kernel(Dw
       if (bx * BX + x >= CV) continue;
       float sum = 0.f;
       for (int y = 0; y < BY; ++y) sum += s_br[(y * BX + x) * 2 * V + j2];
-      rec[(j2 < V ? 0 : a.C) + (size_t)(bx * BX + x) * V + (j2 < V ? j2 : j2 - V)] = sum;
+      st_wt(rec + (j2 < V ? 0 : a.C) + (size_t)(bx * BX + x) * V + (j2 < V ? j2 : j2 - V), sum);
     }
+    if constexpr (TL)
+      tail_finish<false>(b.part, gridDim.y * gridDim.z, a.C, bz * gridDim.y + by, bx * BX * V,
+                         min(BX * V, a.C - bx * BX * V), bx, a.tail,
+                         reinterpret_cast<double*>(s_br));  // (>= 3 x 256 doubles)
   }
 }
 
@@ -571,6 +614,9 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     set_error("dw_dgrad: inconsistent BN-backward partial arguments");
     return E_INVALID;
   }
+  const bool fin = br && a.tail.counters;  // finish the bs.part BN (in the kernel when it fits)
+  int P = 0, rc;
+  bool ink = false;
   if (a.stride == 1) {
     // correlation of dy with the flipped taps, same geometry as the forward
     DwArgs f{};
@@ -578,27 +624,46 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     f.x = a.dy; f.w = a.w; f.y = a.dx;
     f.bs = a.bs;
     f.xz = a.dyz; f.xtab = a.dytab;
-    if (xf) return br ? dw_launch_fwd<true, false, true, true>(f, dtype, st)
-                      : dw_launch_fwd<true, false, false, true>(f, dtype, st);
-    return br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
-  }
-  int bx, by;
-  dw_block_shape(a.C, V, bx, by);
-  dim3 grid(cdiv(a.C / V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
+    if (fin) {
+      int cbv;
+      const dim3 g = dw_grid(a.N, a.H, a.W, a.C, V, 1, cbv);
+      P = (int)(g.y * g.z);
+      ink = tail_ink_on(4) && a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
+      f.tail = a.tail;
+      f.tail_ink = ink;
+    }
+    if (xf) rc = br ? dw_launch_fwd<true, false, true, true>(f, dtype, st)
+                    : dw_launch_fwd<true, false, false, true>(f, dtype, st);
+    else rc = br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
+  } else {
+    int bx, by;
+    dw_block_shape(a.C, V, bx, by);
+    dim3 grid(cdiv(a.C / V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
+    DwBwdArgs b = a;
+    if (fin) {
+      P = (int)(grid.y * grid.z);
+      ink = tail_ink_on(8) && a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)grid.x);
+      b.tail_ink = ink;
+    }
 #define DWD2(T)                                                                   \
   do {                                                                            \
     if (xf) {                                                                     \
-      if (br) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(a);       \
-      else dw_dgrad_s2_kernel<T, false, true><<<grid, block, 0, st>>>(a);         \
+      if (br) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(b);       \
+      else dw_dgrad_s2_kernel<T, false, true><<<grid, block, 0, st>>>(b);         \
     } else {                                                                      \
-      if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(a);             \
-      else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(a);               \
+      if (br && ink) dw_dgrad_s2_kernel<T, true, false, true><<<grid, block, 0, st>>>(b); \
+      else if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b);        \
+      else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b);               \
     }                                                                             \
   } while (0)
-  if (dtype == DT_F32) DWD2(float);
-  else DWD2(bf16);
+    if (dtype == DT_F32) DWD2(float);
+    else DWD2(bf16);
 #undef DWD2
-  return check_launch("dw_dgrad");
+    rc = check_launch("dw_dgrad");
+  }
+  if (rc || !fin || ink) return rc;
+  return bn_bwd_finalize(a.bs.part, P, a.C, a.tail.count, a.tail.dgamma, a.tail.dbeta,
+                         a.tail.coef, st, a.tail.counters, a.tail.tab);
 }
 
 // workgroups of the dgrad launch = its BnBwdPart record count (H, W: dx = the dw's input)

@@ -18,7 +18,7 @@
 // fp32 storage uses v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulate); bf16 storage
 // uses v_mfma_f32_16x16x32_bf16 with f32 accumulation.  Roofline: MFMA-bound only when the
 // tile's K and N are large; most Fast-SCNN 1x1 convs are HBM-bound.
-#include "kernels.hpp"
+#include "bn_finish.hpp"
 
 namespace fscnn {
 
@@ -100,7 +100,10 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
 // X3 (fp32 eval GEMMs): the MFMA step runs on the bf16 matrix cores with exact three-way
 // splits of both operands (common.hpp gs_split3 / gs_mma_x3) — lane lq's two fp32 vectors of a
 // 32-k chunk (k = 4lq.., 16+4lq..) form its 8 bf16 k-slots, the same permutation in A and B
-template <typename T, int NT, bool BT, bool BS, bool AT, bool AX = false, bool X3 = false>
+// TL: the launch finishes its BN in its last workgroups (a.tail_ink; a separate instantiation so
+// the other launches keep their register budget)
+template <typename T, int NT, bool BT, bool BS, bool AT, bool AX = false, bool X3 = false,
+          bool TL = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -422,9 +425,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         t2 += red[RG * BN + g2 * BN + tid];
       }
       float* rec = a.bpart + (size_t)tm * 2 * a.N;
-      rec[n0 + tid] = t1;
-      rec[a.N + n0 + tid] = t2;
+      st_wt(rec + n0 + tid, t1);
+      st_wt(rec + a.N + n0 + tid, t2);
     }
+    if constexpr (TL)
+      tail_finish<false>(a.bpart, cdiv(a.M, G_BM), a.N, tm, n0, min(BN, a.N - n0), tn, a.tail,
+                         reinterpret_cast<double*>(s_dyn));
     return;  // a dgrad output never carries forward statistics (acc dies with the epilogue)
   }
   if (a.part == nullptr) return;
@@ -475,12 +481,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
     for (int nt = 0; nt < NT; ++nt) {
       int col = nt * 16 + li, n = n0 + col;
       if (n < a.N) {
-        rec[n] = mean_c[nt];
-        rec[a.N + n] = s_red[0][col] + s_red[1][col] + s_red[2][col] + s_red[3][col];
-        rec[2 * a.N + n] = (float)valid_rows;
+        st_wt(rec + n, mean_c[nt]);
+        st_wt(rec + a.N + n, s_red[0][col] + s_red[1][col] + s_red[2][col] + s_red[3][col]);
+        st_wt(rec + 2 * a.N + n, (float)valid_rows);
       }
     }
   }
+  if constexpr (TL)
+    tail_finish<true>(a.part, cdiv(a.M, G_BM), a.N, tm, n0, min(BN, a.N - n0), tn, a.tail,
+                      reinterpret_cast<double*>(s_dyn));
 }
 
 static int pick_nt(int N) {
@@ -519,6 +528,18 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   const size_t red = (size_t)2 * 256 * V * 4;  // bwd-BN column reduction (2 x RG x BN floats)
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
+  if constexpr (!BT && !AX && !X3) {
+    if (a.tail_ink) {
+      switch (nt) {
+        case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 4: gemm_nt_kernel<T, 4, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 6: gemm_nt_kernel<T, 6, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
+        default: gemm_nt_kernel<T, 8, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
+      }
+      return;
+    }
+  }
   switch (nt) {
     case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
     case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
@@ -580,15 +601,20 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     return E_INVALID;
   }
   const bool stream = use_stream(a, dtype);
+  // tiled path: the BN finish runs in the kernel's last workgroups (bn_finish.hpp tail_finish)
+  // when the records fit its counters; otherwise as its own fold + finalize launch below
+  GemmArgs b = a;
+  b.tail_ink = !stream && a.tail.counters && tail_ink_on(1) && !a.b_trans && !ax &&
+               a.tail.tsum && a.N <= TAIL_CMAX && tail_fits(gemm_parts(a.M), cdiv(a.N, 16 * nt));
   int rc;
   {
     ProfScope ps(PK_GEMM_NT, st,
                  E * (M * K * (ax ? 2 : 1) + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
                  2.0 * M * N * K);
     rc = stream ? gemm_stream(a, dtype, st)  // finishes the BN in-kernel (last workgroup)
-                : gemm_nt_tiled(a, dtype, nt, at, ax, bs, st);
+                : gemm_nt_tiled(b, dtype, nt, at, ax, bs, st);
   }
-  if (rc || stream || !a.tail.counters) return rc;
+  if (rc || stream || !a.tail.counters || b.tail_ink) return rc;
   // tiled path: the BN finish as its own (fold + finalize) launch over the per-tile records
   if (a.part) {
     BnFinalizeArgs f = a.tail.fwd;

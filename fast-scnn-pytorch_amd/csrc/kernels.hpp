@@ -31,53 +31,6 @@ struct Conv0WgradArgs {
   const float* tab = nullptr;
 };
 
-// BatchNorm-backward partial sums of a dgrad's OUTPUT, when that output is the dy of a BN
-// (the mirror of GemmArgs::bpart): per workgroup, s1[c] = sum g*mask, s2[c] = sum
-// g*mask*(z-mean)*invstd of the stored (rounded) output g, the mask recomputed from that BN's z
-struct BnBwdPart {
-  float* part = nullptr;        // [P][2][C] or null
-  const void* z = nullptr;      // that BN's pre-BN tensor, NHWC with ld C
-  const float* mean = nullptr;
-  const float* invstd = nullptr;
-  const float* scale = nullptr;  // forward BN affine (mode 2: mask = fmaf(z, scale, shift) > 0)
-  const float* shift = nullptr;
-  int mode = 0;                  // 0 no ReLU, 2 relu_z
-};
-
-struct DwArgs {
-  int N, H, W, C, Ho, Wo, stride;
-  const void* x;   // NHWC [N,H,W,C] (input activation)
-  const float* w;  // [C][3][3] fp32 master weights
-  const float* scale;  // eval BN fold, or null
-  const float* shift;
-  int relu;
-  void* y;         // NHWC [N,Ho,Wo,C]
-  float* part;     // BN partial records [parts][3][C] or null
-  // lazily applied BN+ReLU of x (train: x is the producer's raw conv output z) or null
-  const float* in_scale = nullptr;
-  const float* in_shift = nullptr;
-  BnBwdPart bs{};  // stride-1 dgrad (the flipped forward): BN-backward partials of y
-  // stride-1 dgrad: x is a BN's dy whose dz is never stored; the staged value is
-  // bwdx_apply(x, xz, xtab) (common.hpp), xz that BN's pre-BN tensor (ld C), or null
-  const void* xz = nullptr;
-  const float* xtab = nullptr;
-};
-
-struct DwBwdArgs {
-  int N, H, W, C, Ho, Wo, stride;
-  const void* x;    // forward input activation (wgrad)
-  const void* dy;   // NHWC [N,Ho,Wo,C]
-  const float* w;   // [C][9]
-  void* dx;         // NHWC [N,H,W,C] (dgrad)
-  float* slab;      // [parts][9][C] (wgrad)
-  const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
-  const float* x_shift = nullptr;
-  BnBwdPart bs{};  // dgrad: BN-backward partials of dx (dw_dgrad_parts records)
-  // dy is a BN's dy whose dz is never stored: wgrad and dgrad read bwdx_apply(dy, dyz, dytab)
-  const void* dyz = nullptr;
-  const float* dytab = nullptr;
-};
-
 struct BnFinalizeArgs {
   float* part;        // [P][3][C] (mean, M2, count); consumed (folded in place)
   int P, C;
@@ -120,6 +73,63 @@ struct BnTail {
   float* dbeta = nullptr;
   float* coef = nullptr;
   BnBwdTab tab{};
+  // fp64 team sums of the generic in-kernel finish (bn_finish.hpp tail_finish), >= TAIL_TMAX *
+  // 3 * C doubles; null: that finish is not used (the producer falls back to a finalize launch)
+  double* tsum = nullptr;
+};
+
+// BatchNorm-backward partial sums of a dgrad's OUTPUT, when that output is the dy of a BN
+// (the mirror of GemmArgs::bpart): per workgroup, s1[c] = sum g*mask, s2[c] = sum
+// g*mask*(z-mean)*invstd of the stored (rounded) output g, the mask recomputed from that BN's z
+struct BnBwdPart {
+  float* part = nullptr;        // [P][2][C] or null
+  const void* z = nullptr;      // that BN's pre-BN tensor, NHWC with ld C
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* scale = nullptr;  // forward BN affine (mode 2: mask = fmaf(z, scale, shift) > 0)
+  const float* shift = nullptr;
+  int mode = 0;                  // 0 no ReLU, 2 relu_z
+};
+
+struct DwArgs {
+  int N, H, W, C, Ho, Wo, stride;
+  const void* x;   // NHWC [N,H,W,C] (input activation)
+  const float* w;  // [C][3][3] fp32 master weights
+  const float* scale;  // eval BN fold, or null
+  const float* shift;
+  int relu;
+  void* y;         // NHWC [N,Ho,Wo,C]
+  float* part;     // BN partial records [parts][3][C] or null
+  // lazily applied BN+ReLU of x (train: x is the producer's raw conv output z) or null
+  const float* in_scale = nullptr;
+  const float* in_shift = nullptr;
+  BnBwdPart bs{};  // stride-1 dgrad (the flipped forward): BN-backward partials of y
+  // stride-1 dgrad: x is a BN's dy whose dz is never stored; the staged value is
+  // bwdx_apply(x, xz, xtab) (common.hpp), xz that BN's pre-BN tensor (ld C), or null
+  const void* xz = nullptr;
+  const float* xtab = nullptr;
+  // BN finish of the records this launch writes (part: forward statistics; bs.part: stride-1
+  // dgrad partials): tail.counters set -> dw_fwd finishes the BN, in the kernel's last
+  // workgroups when the records fit (tail_ink, set by the launcher) or as its own launch
+  BnTail tail{};
+  int tail_ink = 0;
+};
+
+struct DwBwdArgs {
+  int N, H, W, C, Ho, Wo, stride;
+  const void* x;    // forward input activation (wgrad)
+  const void* dy;   // NHWC [N,Ho,Wo,C]
+  const float* w;   // [C][9]
+  void* dx;         // NHWC [N,H,W,C] (dgrad)
+  float* slab;      // [parts][9][C] (wgrad)
+  const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
+  const float* x_shift = nullptr;
+  BnBwdPart bs{};  // dgrad: BN-backward partials of dx (dw_dgrad_parts records)
+  // dy is a BN's dy whose dz is never stored: wgrad and dgrad read bwdx_apply(dy, dyz, dytab)
+  const void* dyz = nullptr;
+  const float* dytab = nullptr;
+  BnTail tail{};     // dgrad: finish of the bs.part BN (see DwArgs::tail)
+  int tail_ink = 0;
 };
 
 struct GemmArgs {
@@ -154,6 +164,7 @@ struct GemmArgs {
   const void* az = nullptr;
   const float* atab = nullptr;
   BnTail tail{};        // in-kernel finish of the BN whose records this GEMM writes
+  int tail_ink = 0;     // (set by the launcher) the tiled kernel runs the finish itself (tail_finish)
 };
 
 struct GemmTnArgs {
@@ -395,6 +406,9 @@ int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStrea
 
 int bn_fold(const FoldTable& t, hipStream_t st);
 int bn_finalize(const BnFinalizeArgs& a, hipStream_t st);
+// FSCNN_TAIL_INK bitmask of the producers that finish their BN in-kernel (A/B, bisection):
+// 1 tiled gemm_nt, 2 depthwise forward, 4 depthwise stride-1 dgrad, 8 stride-2 dgrad
+bool tail_ink_on(int bit);
 int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st);
 int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
 int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);

@@ -10,6 +10,7 @@
 // eval : BN folded into every producer's epilogue (one bn_fold launch per forward)
 // train: producer writes raw z + per-block statistics → bn_finalize → bn_apply (+res / ReLU)
 #include "net.hpp"
+#include "bn_finish.hpp"
 
 #include <cstdlib>
 #include <cstring>
@@ -327,6 +328,8 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     for (int i = 0; i < 9; ++i) pl.lbe[i].lazy = pl.lbd[i].lazy = true;
     pl.fdw.lazy = pl.c1dw.lazy = pl.c1pw.lazy = pl.c2dw.lazy = true;
   }
+  // fp64 team sums of the in-kernel BN finishes (last, so the activation offsets above do not move)
+  if (train) pl.tsum = A.get((size_t)TAIL_TMAX * 3 * TAIL_CMAX * 8);
   pl.ws_bytes = A.top;
   auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
     pl.named.push_back({n, off, rows, cols, ld, bws});
@@ -766,6 +769,7 @@ struct Exec {
     g.part = Wf(u.part);
     g.tail.counters = (unsigned*)W(pl.fcnt);
     g.tail.fwd = fin_args(u, bn);
+    g.tail.tsum = (double*)W(pl.tsum);
   }
   int apply(const Unit& u, bool relu, const void* res = nullptr, int ldres = 0) {
     BnApplyArgs a{};
@@ -817,8 +821,10 @@ struct Exec {
       return dw_fwd(d, dt, r.st);
     }
     d.relu = 0; d.y = W(u.z); d.part = Wf(u.part);
+    d.tail.counters = (unsigned*)W(pl.fcnt);  // dw_fwd finishes the BN (in-kernel when it fits)
+    d.tail.fwd = fin_args(u, bn);
+    d.tail.tsum = (double*)W(pl.tsum);
     TRY(dw_fwd(d, dt, r.st));
-    TRY(finalize(u, bn));
     return u.lazy ? OK : apply(u, true);
   }
 
@@ -1091,9 +1097,6 @@ struct Exec {
   int bn_bwd_stats(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
                    int ldmask, bool relu_z, const BnBwdTab& tb) {
     if (u.bdone) return OK;
-    if (u.bparts > 0)  // the depthwise dgrad that produced dy wrote the partial records
-      return bn_bwd_finalize((float*)Bw(pl.bnpart), u.bparts, u.C, (double)u.M, G(bn.g),
-                             G(bn.b), (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb);
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
     b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
@@ -1154,6 +1157,7 @@ struct Exec {
     g.bmean = Wf(u.mean); g.binvstd = Wf(u.invstd); g.bscale = Wf(u.scale); g.bshift = Wf(u.shift);
     g.bmode = t.mode;
     g.tail.counters = (unsigned*)W(pl.bcnt);
+    g.tail.tsum = (double*)W(pl.tsum);
     g.tail.count = (double)u.M;
     g.tail.dgamma = G(t.bn->g);
     g.tail.dbeta = G(t.bn->b);
@@ -1246,9 +1250,18 @@ struct Exec {
       d.bs.mean = Wf(u.mean); d.bs.invstd = Wf(u.invstd);
       d.bs.scale = Wf(u.scale); d.bs.shift = Wf(u.shift);
       d.bs.mode = bt.mode;
+      // and finishes that BN's backward (dgamma, dbeta, coefficients, operand table): in the
+      // kernel's last workgroups when its records fit the counters, else its own launch
+      d.tail.counters = (unsigned*)W(pl.bcnt);
+      d.tail.tsum = (double*)W(pl.tsum);
+      d.tail.count = (double)u.M;
+      d.tail.dgamma = G(bt.bn->g);
+      d.tail.dbeta = G(bt.bn->b);
+      d.tail.coef = (float*)Bw(pl.coef);
+      d.tail.tab = bwd_tab(u, bt.mode == 2, tab_slot(u));
     }
     TRY(dw_dgrad(d, dt, r.st));
-    if (br) bt.u->bparts = dw_dgrad_parts(pl.N, H, Wd, C, dt, stride);
+    if (br) bt.u->bdone = true;
     return OK;
   }
 

