@@ -292,6 +292,7 @@ struct PpmBranchBwd {
 struct PpmBwdArgs {
   PpmBranchBwd b[4];
   int nb, K, C;
+  int wg0[5] = {0, 0, 0, 0, 0};  // (set by the launcher) first workgroup of each branch
 };
 
 struct CeArgs {

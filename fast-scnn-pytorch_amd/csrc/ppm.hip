@@ -12,6 +12,8 @@
 // to the storage type before both GEMMs read it (bn_bwd_apply).
 #include "bn_finish.hpp"
 
+#include <algorithm>
+
 namespace fscnn {
 
 constexpr int PPM_T = 512;  // threads: 16 row slices x 32 channels
@@ -43,10 +45,22 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_kernel(PpmFwdArgs a) {
   const T* X = (const T*)b.x;
   T* Z = (T*)b.z;
   const float* wr = s_w + n * (K + 1);
+  // (a chunk of 8 k-vectors is loaded before its FMAs: the row walk is a chain of load
+  //  round trips otherwise — the loop trip counts are runtime values)
   for (int m = sl; m < M; m += 16) {
     const T* xr = X + (size_t)m * K;
     float acc = 0.f;
-    for (int k = 0; k < K; k += V) {
+    int k = 0;
+    for (; k + 8 * V <= K; k += 8 * V) {
+      float xv[8][V];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) ldv(xr + k + u * V, xv[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc = fmaf(xv[u][j], wr[k + u * V + j], acc);
+    }
+    for (; k < K; k += V) {
       float xv[V];
       ldv(xr + k, xv);
 #pragma unroll
@@ -82,9 +96,16 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_kernel(PpmFwdArgs a) {
     st1(Y + (size_t)m * b.ldy + n, fmaxf(fmaf(round_as<T>(s_z[m * PPM_C + n]), sc, sh), 0.f));
 }
 
+// G workgroups per branch (a.wg0): each recomputes the branch's BN-backward sums and dz (tiny,
+// block-local, identical arithmetic in every workgroup) and then owns a 1/G slice of the weight
+// gradient's k and of the input gradient's rows — one workgroup per branch was LDS-bound on the
+// 288-row branch's dx (2 LDS reads per FMA on one CU)
 template <typename T>
 __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
-  const PpmBranchBwd& b = a.b[blockIdx.x];
+  int bi = 0;
+  while (bi + 1 < a.nb && (int)blockIdx.x >= a.wg0[bi + 1]) ++bi;
+  const int gpart = blockIdx.x - a.wg0[bi], NG = a.wg0[bi + 1] - a.wg0[bi];
+  const PpmBranchBwd& b = a.b[bi];
   const int K = a.K, M = b.M, tid = threadIdx.x;
   const int n = tid & 31, sl = tid >> 5;
   constexpr int DZ = PPM_C + 1;  // padded dz row
@@ -100,13 +121,32 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
   const T* Z = (const T*)b.z;
   const float mean = b.mean[n], istd = b.invstd[n], scale = b.scale[n];
   // BN backward sums: dy masked by the forward ReLU (y > 0), xhat of the stored z
+  // the slice's rows are loaded once, 4 rows per batch of loads, and kept for the dz pass
+  constexpr int RMAX = 32;  // rows per slice held in registers (M <= 16 * RMAX)
+  float gr[RMAX], xr[RMAX];
   double t1 = 0.0, t2 = 0.0;
-  for (int m = sl; m < M; m += 16) {
-    const float g = ld1(G + (size_t)m * b.lddy + n);
-    const float gv = ld1(Y + (size_t)m * b.ldy + n) > 0.f ? g : 0.f;
-    const float xh = (ld1(Z + (size_t)m * PPM_C + n) - mean) * istd;
-    t1 += gv;
-    t2 += (double)gv * xh;
+  const int nr = M > sl ? (M - sl + 15) / 16 : 0;
+#pragma unroll
+  for (int i0 = 0; i0 < RMAX; i0 += 4) {
+    if (i0 >= nr) continue;
+    float g4[4], y4[4], z4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = sl + 16 * (i0 + u < nr ? i0 + u : 0);
+      g4[u] = ld1(G + (size_t)m * b.lddy + n);
+      y4[u] = ld1(Y + (size_t)m * b.ldy + n);
+      z4[u] = ld1(Z + (size_t)m * PPM_C + n);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = i0 + u < nr;
+      const float gv = (ok && y4[u] > 0.f) ? g4[u] : 0.f;
+      const float xh = (z4[u] - mean) * istd;
+      gr[i0 + u] = gv;
+      xr[i0 + u] = xh;
+      t1 += gv;
+      t2 += (double)gv * xh;
+    }
   }
   s_r[0][tid] = t1;
   s_r[1][tid] = t2;
@@ -117,25 +157,36 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
       s1 += s_r[0][j * PPM_C + tid];
       s2 += s_r[1][j * PPM_C + tid];
     }
-    bn_bwd_finish(tid, PPM_C, s1, s2, (double)M, b.dgamma, b.dbeta, s_cf, BnBwdTab());
+    bn_bwd_finish(tid, PPM_C, s1, s2, (double)M, gpart == 0 ? b.dgamma : nullptr,
+                  gpart == 0 ? b.dbeta : nullptr, s_cf, BnBwdTab());
   }
   __syncthreads();
   const float c0 = s_cf[n], c1 = s_cf[PPM_C + n];
-  for (int m = sl; m < M; m += 16) {
-    const float g = ld1(G + (size_t)m * b.lddy + n);
-    const float gv = ld1(Y + (size_t)m * b.ldy + n) > 0.f ? g : 0.f;
-    const float xh = (ld1(Z + (size_t)m * PPM_C + n) - mean) * istd;
-    s_dz[m * DZ + n] = round_as<T>(scale * (gv - c0 - xh * c1));
+#pragma unroll
+  for (int i = 0; i < RMAX; ++i) {
+    if (i >= nr) continue;
+    s_dz[(sl + 16 * i) * DZ + n] = round_as<T>(scale * (gr[i] - c0 - xr[i] * c1));
   }
   __syncthreads();
   // weight gradient dW[c][k] = sum_m dz[m][c] x[m][k]: thread (k, 8-channel group), m ascending
   const T* X = (const T*)b.x;
-  for (int p = tid; p < K * (PPM_C / 8); p += PPM_T) {
-    const int k = p % K, cg = p / K;
+  const int kb = K * gpart / NG, ke = K * (gpart + 1) / NG, KS = ke - kb;
+  for (int p = tid; p < KS * (PPM_C / 8); p += PPM_T) {
+    const int k = kb + p % KS, cg = p / KS;
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int m = 0; m < M; ++m) {
+    int m = 0;
+    for (; m + 16 <= M; m += 16) {  // 16 loads in flight, then the FMAs in ascending m
+      float xv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) xv[u] = ld1(X + (size_t)(m + u) * K + k);
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(s_dz[(m + u) * DZ + cg * 8 + j], xv[u], acc[j]);
+    }
+    for (; m < M; ++m) {
       const float xv = ld1(X + (size_t)m * K + k);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = fmaf(s_dz[m * DZ + cg * 8 + j], xv, acc[j]);
@@ -145,7 +196,8 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
   }
   // input gradient dx[m][k] = sum_c dz[m][c] W[c][k]
   T* DX = (T*)b.dx;
-  for (int p = tid; p < M * K; p += PPM_T) {
+  const int mb = M * gpart / NG, me = M * (gpart + 1) / NG;
+  for (int p = mb * K + tid; p < me * K; p += PPM_T) {
     const int m = p / K, k = p - m * K;
     float acc = 0.f;
 #pragma unroll 8
@@ -155,7 +207,7 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
 }
 
 static bool ppm_check(int nb, int K, int C, int maxM, int dtype) {
-  if (nb < 1 || nb > 4 || C != PPM_C || K < 8 || K % 8 || K > 1024 || maxM < 1 ||
+  if (nb < 1 || nb > 4 || C != PPM_C || K < 8 || K % 8 || K > 1024 || maxM < 1 || maxM > 512 ||
       ppm_branch_lds(maxM, K) > 150 * 1024 || (dtype != DT_F32 && dtype != DT_BF16)) {
     set_error("ppm_branches: nb=%d K=%d C=%d M=%d dtype=%d not supported", nb, K, C, maxM, dtype);
     return false;
@@ -164,7 +216,8 @@ static bool ppm_check(int nb, int K, int C, int maxM, int dtype) {
 }
 
 bool ppm_branches_ok(int maxM, int K, int dtype) {
-  return ppm_branch_lds(maxM, K) <= 150 * 1024 && K >= 8 && K % 8 == 0 && K <= 1024 &&
+  // maxM <= 16 slices x 32 rows: the backward keeps a slice's rows in registers
+  return maxM <= 512 && ppm_branch_lds(maxM, K) <= 150 * 1024 && K >= 8 && K % 8 == 0 && K <= 1024 &&
          (dtype == DT_F32 || dtype == DT_BF16);
 }
 
@@ -191,8 +244,12 @@ int ppm_branches_bwd(const PpmBwdArgs& a, int dtype, hipStream_t st) {
   for (int i = 0; i < a.nb; ++i) rows += a.b[i].M;
   ProfScope ps(PK_PPM, st, rows * (2.0 * a.K + 3.0 * PPM_C) * (dtype == DT_F32 ? 4 : 2),
                4.0 * a.K * PPM_C * rows);
-  if (dtype == DT_F32) ppm_bwd_kernel<float><<<a.nb, PPM_T, lds, st>>>(a);
-  else ppm_bwd_kernel<bf16><<<a.nb, PPM_T, lds, st>>>(a);
+  PpmBwdArgs b = a;
+  b.wg0[0] = 0;
+  for (int i = 0; i < a.nb; ++i) b.wg0[i + 1] = b.wg0[i] + std::max(1, std::min(16, a.b[i].M / 32));
+  const int nwg = b.wg0[a.nb];
+  if (dtype == DT_F32) ppm_bwd_kernel<float><<<nwg, PPM_T, lds, st>>>(b);
+  else ppm_bwd_kernel<bf16><<<nwg, PPM_T, lds, st>>>(b);
   return check_launch("ppm_branches_bwd");
 }
 
