@@ -148,23 +148,32 @@ __device__ inline void tail_fold(const float* part, const double* tsum, int N, i
   }
 }
 
-// every thread of the workgroup calls this after storing its record row p (st_wt); channel
-// slices wider than the workgroup are folded in passes of nthr channels.  The team sums stay
-// fp64 (t.tsum): a float team row would round the batch mean to fp32 before the final fold,
-// which is visible in x_hat wherever |mean| >> std.
+// First half, every workgroup after its record stores (st_wt): true in the team's last arriver.
+// Producers that store a large output tile call it BEFORE those stores, so the arrival's vmcnt(0)
+// drain covers only the records.
+__device__ inline bool tail_arrive(int P, int p, int chunk, const BnTail& t) {
+  const int TS = tail_team_size(P);
+  const int team = p / TS;
+  const int tsize = min(TS, P - team * TS);
+  return arrive_last(t.counters + TAIL_TEAM0 + chunk * TAIL_TMAX + team, (unsigned)tsize);
+}
+
+// Second half, in a team's last arriver (every thread of it): fold the team's rows into its fp64
+// team sums, arrive on the chunk, and (chunk's last team) finish every channel.  Channel slices
+// wider than the workgroup are folded in passes of nthr channels.  The team sums stay fp64
+// (t.tsum): a float team row would round the batch mean to fp32 before the final fold, which is
+// visible in x_hat wherever |mean| >> std.
 // lds: >= 3 * workgroup-size doubles of LDS the kernel no longer reads (aliased scratch, so
 // kernels that never finish in-kernel carry no extra LDS)
 template <bool FWD>
-__device__ inline void tail_finish(float* part, int P, int N, int p, int c0, int nc, int chunk,
-                                   const BnTail& t, double* lds) {
+__device__ inline void tail_complete(float* part, int P, int N, int p, int c0, int nc, int chunk,
+                                     const BnTail& t, double* lds) {
   unsigned* ctr = t.counters;
   const int TS = tail_team_size(P);
   const int team = p / TS, nteam = (P + TS - 1) / TS;
   const int tsize = min(TS, P - team * TS);
   const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
   const int nthr = blockDim.x * blockDim.y * blockDim.z;
-  unsigned* tctr = ctr + TAIL_TEAM0 + chunk * TAIL_TMAX + team;
-  if (!arrive_last(tctr, (unsigned)tsize)) return;
   for (int cb = 0; cb < nc; cb += nthr) {
     const int ncb = min(nthr, nc - cb), n = c0 + cb + tid;
     double s[3];
@@ -174,7 +183,7 @@ __device__ inline void tail_finish(float* part, int P, int N, int p, int c0, int
       for (int j = 0; j < 3; ++j) st_wt64(t.tsum + ((size_t)team * 3 + j) * N + n, s[j]);
     }
   }
-  reset_counter(tctr);
+  reset_counter(ctr + TAIL_TEAM0 + chunk * TAIL_TMAX + team);
   if (!arrive_last(ctr + chunk, (unsigned)nteam)) return;
   for (int cb = 0; cb < nc; cb += nthr) {
     const int ncb = min(nthr, nc - cb), n = c0 + cb + tid;
@@ -186,6 +195,13 @@ __device__ inline void tail_finish(float* part, int P, int N, int p, int c0, int
     }
   }
   reset_counter(ctr + chunk);
+}
+
+// both halves, for producers whose records are their last stores
+template <bool FWD>
+__device__ inline void tail_finish(float* part, int P, int N, int p, int c0, int nc, int chunk,
+                                   const BnTail& t, double* lds) {
+  if (tail_arrive(P, p, chunk, t)) tail_complete<FWD>(part, P, N, p, c0, nc, chunk, t, lds);
 }
 
 }  // namespace fscnn
