@@ -19,6 +19,8 @@
 // flops = 18*N*C*Ho*Wo.
 #include "bn_finish.hpp"
 
+#include <optional>
+
 namespace fscnn {
 
 constexpr int DWL_CB = 8;  // max 16-B channel vectors per workgroup (128 B per pixel)
@@ -422,7 +424,9 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   }
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
-  ProfScope ps(PK_DW_FWD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
+  // (closed before a separate finalize launch: profiler scopes do not nest)
+  std::optional<ProfScope> ps;
+  ps.emplace(PK_DW_FWD, st, E * (in_el + out_el) + 36.0 * a.C, 18.0 * out_el);
   if (a.in_scale && !a.in_shift) {
     set_error("dw_fwd: in_scale without in_shift");
     return E_INVALID;
@@ -437,6 +441,7 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   }
   const int rc = a.in_scale ? dw_launch_fwd<false, true>(b, dtype, st) : dw_launch_fwd<false, false>(b, dtype, st);
   if (rc || !a.part || !a.tail.counters || b.tail_ink) return rc;
+  ps.reset();
   BnFinalizeArgs f = a.tail.fwd;
   f.part = a.part; f.P = P; f.C = a.C; f.counters = a.tail.counters;
   return bn_finalize(f, st);
@@ -604,8 +609,9 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   const bool br = a.bs.part != nullptr;  // + a read of the next BN's z (dx-sized)
   const bool xf = a.dytab != nullptr;    // + a read of this BN's z (dy-sized)
-  ProfScope ps(PK_DW_DGRAD, st, E * (in_el * (br ? 2 : 1) + out_el * (xf ? 2 : 1)) + 36.0 * a.C,
-               18.0 * out_el);
+  std::optional<ProfScope> ps;  // (closed before a separate finalize launch)
+  ps.emplace(PK_DW_DGRAD, st, E * (in_el * (br ? 2 : 1) + out_el * (xf ? 2 : 1)) + 36.0 * a.C,
+             18.0 * out_el);
   if (xf && !a.dyz) {
     set_error("dw_dgrad: BN-backward operand transform needs z");
     return E_INVALID;
@@ -662,6 +668,7 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     rc = check_launch("dw_dgrad");
   }
   if (rc || !fin || ink) return rc;
+  ps.reset();
   return bn_bwd_finalize(a.bs.part, P, a.C, a.tail.count, a.tail.dgamma, a.tail.dbeta,
                          a.tail.coef, st, a.tail.counters, a.tail.tab);
 }
