@@ -20,6 +20,9 @@ namespace fscnn {
 constexpr int HD_T = 256;
 constexpr int HD_CMAX = 32;
 constexpr int HD_TMAX = 2048;  // max full-res row width whose targets are staged in LDS
+constexpr float HD_LOG2E = 1.4426950408889634f;
+constexpr float HD_LN2 = 0.6931471805599453f;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int hd_first_ge(int i, int Lin, int Lout, float sc) {
   int lo = 0, hi = Lout;
@@ -62,15 +65,17 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
       const int j = jr % (HD_T + 1), r = jr / (HD_T + 1);
       const int col = min(cb + j, Wl - 1);
       const int row = r ? hl1 : hl;
+      // staged in log2 units (x log2 e): the softmax below runs on v_exp_f32 (2^x) directly
       s_L[(r * (HD_T + 1) + j) * SL + c] =
-          c < Cm ? ld1(lg + ((size_t)row * Wl + col) * ldl + c) : 0.f;
+          c < Cm ? ld1(lg + ((size_t)row * Wl + col) * ldl + c) * HD_LOG2E : 0.f;
     }
     __syncthreads();
     const int t = cb + tid;
     const bool active = t < Wl;
-    float acc00[CT], acc01[CT], acc10[CT], acc11[CT];
+    // a0[c] = (acc00, acc01): own row, columns t / t+1; a1[c] = (acc10, acc11): row hl+1
+    f32x2 a0[CT], a1[CT];
 #pragma unroll
-    for (int c = 0; c < CT; ++c) acc00[c] = acc01[c] = acc10[c] = acc11[c] = 0.f;
+    for (int c = 0; c < CT; ++c) a0[c] = a1[c] = f32x2{0.f, 0.f};
     // the full-resolution target rows are loaded by the whole workgroup with coalesced int64
     // loads (next row prefetched into registers during the current row) and kept in LDS as int8
     // class indices (-1 = ignored); all threads run the row loop (inactive columns: no pixels)
@@ -102,11 +107,20 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
       }
       if (active) {
         const Lerp lh = ac_lerp(h, Hl, H, sh);
-        float v0[CT], v1[CT];
+        // class pairs (v_pk_* f32): v0 / v1 = the row-interpolated low-res logits of columns
+        // t / t+1 (log2 units), padded to an even class count with zeros
+        constexpr int CP = (CT + 1) / 2;
+        f32x2 v0[CP], v1[CP];
+        const f32x2 h0 = {lh.l0, lh.l0}, h1 = {lh.l1, lh.l1};
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          v0[c] = lh.l0 * L0[c] + lh.l1 * L1[c];
-          v1[c] = lh.l0 * L0[SL + c] + lh.l1 * L1[SL + c];
+        for (int p = 0; p < CP; ++p) {
+          const int c = 2 * p, c1 = c + 1 < CT ? c + 1 : c;
+          const f32x2 l00 = {L0[c], c + 1 < CT ? L0[c1] : 0.f};
+          const f32x2 l10 = {L1[c], c + 1 < CT ? L1[c1] : 0.f};
+          const f32x2 l01 = {L0[SL + c], c + 1 < CT ? L0[SL + c1] : 0.f};
+          const f32x2 l11 = {L1[SL + c], c + 1 < CT ? L1[SL + c1] : 0.f};
+          v0[p] = __builtin_elementwise_fma(h1, l10, h0 * l00);
+          v1[p] = __builtin_elementwise_fma(h1, l11, h0 * l01);
         }
         const long long* trow = tgt + (size_t)h * W;
         for (int w = w_lo; w < w_hi; ++w) {
@@ -119,37 +133,56 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
             ti = (tg != a.ignore_index && tg >= 0 && tg < Cm) ? (int)tg : -1;
           }
           const bool valid = ti >= 0;
-          float e[CT];
+          const f32x2 w0 = {lw.l0, lw.l0}, w1 = {lw.l1, lw.l1};
+          f32x2 e[CP];
           float mx = -INFINITY, lt = 0.f;
 #pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            e[c] = lw.l0 * v0[c] + lw.l1 * v1[c];
-            if (c < Cm) mx = fmaxf(mx, e[c]);
-            lt = (c == ti) ? e[c] : lt;
+          for (int p = 0; p < CP; ++p) {
+            e[p] = __builtin_elementwise_fma(w1, v1[p], w0 * v0[p]);
+            if (2 * p < Cm) mx = fmaxf(mx, e[p].x);
+            if (2 * p + 1 < Cm) mx = fmaxf(mx, e[p].y);
+            lt = (2 * p == ti) ? e[p].x : lt;
+            lt = (2 * p + 1 == ti) ? e[p].y : lt;
           }
           float se = 0.f;
 #pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            e[c] = c < Cm ? __expf(e[c] - mx) : 0.f;  // v_exp_f32 path; loss uses accurate logf
-            se += e[c];
+          for (int p = 0; p < CP; ++p) {  // v_exp_f32 (2^x); the loss keeps an accurate logf
+            e[p].x = 2 * p < Cm ? __builtin_amdgcn_exp2f(e[p].x - mx) : 0.f;
+            e[p].y = 2 * p + 1 < Cm ? __builtin_amdgcn_exp2f(e[p].y - mx) : 0.f;
+            se += e[p].x;
+            se += e[p].y;
           }
           const float inv = valid ? __builtin_amdgcn_rcpf(se) : 0.f;  // v_rcp_f32 (1 ulp)
           if (valid) {
-            loss += mx + logf(se) - lt;
+            loss += (mx - lt) * HD_LN2 + logf(se);
             cnt += 1.f;
           }
-          const float k00 = lh.l0 * lw.l0, k01 = lh.l0 * lw.l1;
-          const float k10 = lh.l1 * lw.l0, k11 = lh.l1 * lw.l1;
+          // the four tap products as two packed pairs (v_pk_fma_f32: (00, 01) and (10, 11))
+          const f32x2 k0 = {lh.l0 * lw.l0, lh.l0 * lw.l1};
+          const f32x2 k1 = {lh.l1 * lw.l0, lh.l1 * lw.l1};
+          const f32x2 iv = {inv, inv};
 #pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            const float g = e[c] * inv - ((valid && c == ti) ? 1.f : 0.f);
-            acc00[c] += k00 * g;
-            acc01[c] += k01 * g;
-            acc10[c] += k10 * g;
-            acc11[c] += k11 * g;
+          for (int p = 0; p < CP; ++p) {
+            const f32x2 oh = {(valid && 2 * p == ti) ? 1.f : 0.f, (valid && 2 * p + 1 == ti) ? 1.f : 0.f};
+            const f32x2 g = e[p] * iv - oh;
+            const f32x2 gx = {g.x, g.x}, gy = {g.y, g.y};
+            a0[2 * p] = __builtin_elementwise_fma(k0, gx, a0[2 * p]);
+            a1[2 * p] = __builtin_elementwise_fma(k1, gx, a1[2 * p]);
+            if (2 * p + 1 < CT) {
+              a0[2 * p + 1] = __builtin_elementwise_fma(k0, gy, a0[2 * p + 1]);
+              a1[2 * p + 1] = __builtin_elementwise_fma(k1, gy, a1[2 * p + 1]);
+            }
           }
         }
       }
+    }
+    float acc00[CT], acc01[CT], acc10[CT], acc11[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      acc00[c] = a0[c].x;
+      acc01[c] = a0[c].y;
+      acc10[c] = a1[c].x;
+      acc11[c] = a1[c].y;
     }
     if (active) {
       if (t == Wl - 1) {  // i1(w) == i0(w) on the last column: both taps are column t
