@@ -12,11 +12,13 @@ import json
 import os
 import sys
 
-FAMILIES = {  # bench.py PROF_KINDS names -> kernel-name substrings
-    "conv0_fwd": ["conv0_fwd_kernel"], "dw_fwd": ["dw_fwd_kernel<", "false>"],
-    "dw_dgrad": ["dw_dgrad_s2_kernel"], "dw_wgrad": ["dw_wgrad_kernel"],
-    "gemm_nt": ["gemm_nt_kernel"], "gemm_tn": ["gemm_tn_kernel"], "ce_head": ["ce_head_kernel"],
-    "conv0_wgrad": ["conv0_wgrad_kernel"],
+# bench.py PROF_KINDS names -> alternatives, each a list of kernel-name substrings that must all
+# match (gemm_nt is the launcher's family: the tiled kernel and the streaming kernel it picks)
+FAMILIES = {
+    "conv0_fwd": [["conv0_fwd_kernel"]], "dw_fwd": [["dw_fwd_kernel<", "false>"]],
+    "dw_dgrad": [["dw_dgrad_s2_kernel"]], "dw_wgrad": [["dw_wgrad_kernel"]],
+    "gemm_nt": [["gemm_nt_kernel"], ["gemm_stream_kernel"]], "gemm_tn": [["gemm_tn_kernel"]],
+    "ce_head": [["ce_head_kernel"]], "conv0_wgrad": [["conv0_wgrad_kernel"]],
 }
 
 
@@ -78,8 +80,8 @@ def main():
         name = e["name"].replace("void fscnn::", "").replace("fscnn::", "")
         print("%-58s %10.2f %10.2f %8s" % (name[:58], rd / 1e6, wr / 1e6,
                                            "%.0f" % (100 * act / wc) if wc else "-"))
-        for f, keys in FAMILIES.items():
-            if all(k in e["name"] for k in keys):
+        for f, alts in FAMILIES.items():
+            if any(all(k in e["name"] for k in keys) for keys in alts):
                 fam[f]["n"] += 1
                 fam[f]["fetch"] += rd
                 fam[f]["write"] += wr
