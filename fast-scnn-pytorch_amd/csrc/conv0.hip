@@ -451,7 +451,9 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
 // end and one [864] partial per workgroup is written (reduced in fixed order by reduce_slabs).
 // HBM-bound: the x strip and the dZ tile are read once.
 constexpr int CW_TP = 256;  // pixels per tile
-constexpr int CW_MAXP = 1024;  // max workgroups (partials)
+// max workgroups (partials): one residency round of the bf16 BN-backward-on-load variant (141
+// VGPRs: 3 workgroups per CU x 256 CUs); 1024 left a second round one third full
+constexpr int CW_MAXP = 768;
 
 template <typename T>
 struct CwOps;
