@@ -334,6 +334,10 @@ struct DropArgs {
   float p;
   const uint64_t* seed_ptr = nullptr;  // device slot holding the seed (graph-replayable), or null
   uint64_t seed_add = 0;               // mask seed = seed + seed_add (aux head Dropout: +1)
+  // x is the raw conv output z of a BN+ReLU that is never stored: the kernel drops out
+  // relu(fmaf(z, x_scale[c], x_shift[c])) (bn_apply's arithmetic), or null
+  const float* x_scale = nullptr;
+  const float* x_shift = nullptr;
 };
 
 // aux head 3x3 conv as im2col + GEMM (aux.hip): col[m][c*9 + kh*3 + kw], pad 1, stride 1

@@ -500,6 +500,11 @@ __global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr) 
   const uint64_t seed = (a.seed_ptr ? *a.seed_ptr : a.seed) + a.seed_add;
   float v[V];
   ldv((const T*)a.x + (size_t)pix * a.ldx + cv * V, v);
+  if (a.x_scale) {  // lazy BN+ReLU of the producer's z (the activation itself is never stored)
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+      v[j] = round_as<T>(fmaxf(fmaf(v[j], a.x_scale[cv * V + j], a.x_shift[cv * V + j]), 0.f));
+  }
   const float s = 1.f / (1.f - a.p);
 #pragma unroll
   for (int j = 0; j < V; ++j) {

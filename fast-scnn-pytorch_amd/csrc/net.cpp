@@ -784,8 +784,9 @@ struct Exec {
 
   // ---- conv + BN (+ReLU) producers -------------------------------------------------------
   // pointwise conv on X [M][K] (ld ldx); eval: fused BN(+res,+relu); train: stats → apply
+  // store_out = false (train): the BN+ReLU output is applied by its only consumer instead
   int pw(const Unit& u, const ConvL& c, const BnL* bn, In x, bool relu,
-         const void* res = nullptr, int ldres = 0) {
+         const void* res = nullptr, int ldres = 0, bool store_out = true) {
     g_prof_tag = u.name.c_str();
     GemmArgs g{};
     const int K = c.cin * c.k * c.k;  // 1x1 convs; the aux 3x3 runs on its im2col columns
@@ -804,7 +805,7 @@ struct Exec {
     g.C = W(u.z); g.ldc = u.C;
     gemm_fin(g, u, *bn);
     TRY(gemm_nt(g, dt, r.st));
-    return u.lazy ? OK : apply(u, relu, res, ldres);
+    return (u.lazy || !store_out) ? OK : apply(u, relu, res, ldres);
   }
   int dw(const Unit& u, const ConvL& c, const BnL& bn, In x, int H, int Wd, int Ho, int Wo,
          int stride) {
@@ -971,11 +972,15 @@ struct Exec {
     TRY(dw(pl.c1dw, net.cls1.dw, net.cls1.bdw, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
     TRY(pw(pl.c1pw, net.cls1.pw, &net.cls1.bpw, act(pl.c1dw), true));
     TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1));
-    TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, act(pl.c2dw), true));
+    // train with Dropout: the dsconv2 pw BN+ReLU output is only read by the dropout, which
+    // applies the BN itself (c2pw.a is never stored: one 128-channel write + read fewer)
+    const bool drop_fused = train && r.dropout_p > 0.f;
+    TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, act(pl.c2dw), true, nullptr, 0, !drop_fused));
     const void* cls_in = W(pl.c2pw.a);
-    if (train && r.dropout_p > 0.f) {
+    if (drop_fused) {
       DropArgs d{};
-      d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = W(pl.c2pw.a); d.ldx = 128;
+      d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = W(pl.c2pw.z); d.ldx = 128;
+      d.x_scale = Wf(pl.c2pw.scale); d.x_shift = Wf(pl.c2pw.shift);
       d.y = W(pl.drop); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
       d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
       TRY(dropout(d, dt, r.st));
