@@ -228,20 +228,23 @@ int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st) {
 // MODE: 0 = no ReLU, 1 = mask tensor (y > 0), 2 = relu_z (mask recomputed from z).  The mode is
 // a template parameter and rows past the end are clamped + zero-weighted, so a batch's loads are
 // issued back to back with no branch (a branch between loads and use forces vmcnt(0) waits).
-template <typename T, int MODE>
+// PAIR (mask mode): a second BN on the same dy and mask (BnBwdArgs::z2): its sum of dy_r*xhat2
+// comes from the same pass (dy and the mask read once); its sum of dy_r is the first BN's
+template <typename T, int MODE, bool PAIR = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   constexpr int V = VecW<T>::V;
+  constexpr int NS = PAIR ? 3 : 2;  // sums per channel: s1, s2 (, s3)
   const int CV = a.C / V;
   // block = (channel vectors along x, row groups along y)
   const int cv = blockIdx.x * blockDim.x + threadIdx.x;
   const int BX = blockDim.x, BY = blockDim.y;
-  extern __shared__ float red[];  // [BY][BX*V*2]
-  float s1[V], s2[V];
+  extern __shared__ float red[];  // [BY][BX*V*NS]
+  float s1[V], s2[V], s3[PAIR ? V : 1];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; if constexpr (PAIR) s3[j] = 0.f; }
   if (cv < CV) {
     const int c = cv * V;
-    float mu[V], is[V], fs[V], fb[V];
+    float mu[V], is[V], fs[V], fb[V], mu2[PAIR ? V : 1], is2[PAIR ? V : 1];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       mu[j] = a.mean[c + j];
@@ -250,12 +253,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
         fs[j] = a.scale[c + j];
         fb[j] = a.shift[c + j];
       }
+      if constexpr (PAIR) {
+        mu2[j] = a.mean2[c + j];
+        is2[j] = a.invstd2[c + j];
+      }
     }
     const long long mb = (long long)blockIdx.y * a.rows_per_block;
     const long long me = min(a.M, mb + a.rows_per_block);
     constexpr int U = 4;  // rows per batch (8 measured slower: 256 VGPRs, occupancy 2)
     for (long long m0 = mb + threadIdx.y; m0 < me; m0 += U * BY) {
-      float g[U][V], z[U][V], mk[U][V];
+      float g[U][V], z[U][V], mk[U][V], z2[PAIR ? U : 1][V];
       float ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -265,6 +272,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
         ldv((const T*)a.dy + m * a.lddy + c, g[u]);
         ldv((const T*)a.z + m * a.ldz + c, z[u]);
         if (MODE == 1) ldv((const T*)a.mask + m * a.ldmask + c, mk[u]);
+        if constexpr (PAIR) ldv((const T*)a.z2 + m * a.ldz + c, z2[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -275,26 +283,34 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
           if (MODE == 2) gv = fmaf(z[u][j], fs[j], fb[j]) > 0.f ? gv : 0.f;
           s1[j] += gv;
           s2[j] += gv * (z[u][j] - mu[j]) * is[j];
+          if constexpr (PAIR) s3[j] += gv * (z2[u][j] - mu2[j]) * is2[j];
         }
     }
   }
 #pragma unroll
   for (int j = 0; j < V; ++j) {
-    red[(threadIdx.y * BX + threadIdx.x) * 2 * V + j] = s1[j];
-    red[(threadIdx.y * BX + threadIdx.x) * 2 * V + V + j] = s2[j];
+    red[(threadIdx.y * BX + threadIdx.x) * NS * V + j] = s1[j];
+    red[(threadIdx.y * BX + threadIdx.x) * NS * V + V + j] = s2[j];
+    if constexpr (PAIR) red[(threadIdx.y * BX + threadIdx.x) * NS * V + 2 * V + j] = s3[j];
   }
   __syncthreads();
   if (threadIdx.y == 0 && cv < CV) {
     float* rec = a.part + (size_t)blockIdx.y * 2 * a.C;
+    float* rec2 = PAIR ? a.part2 + (size_t)blockIdx.y * 2 * a.C : nullptr;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      float t1 = 0.f, t2 = 0.f;
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
       for (int k = 0; k < BY; ++k) {
-        t1 += red[(k * BX + threadIdx.x) * 2 * V + j];
-        t2 += red[(k * BX + threadIdx.x) * 2 * V + V + j];
+        t1 += red[(k * BX + threadIdx.x) * NS * V + j];
+        t2 += red[(k * BX + threadIdx.x) * NS * V + V + j];
+        if constexpr (PAIR) t3 += red[(k * BX + threadIdx.x) * NS * V + 2 * V + j];
       }
       rec[cv * V + j] = t1;
       rec[a.C + cv * V + j] = t2;
+      if constexpr (PAIR) {
+        rec2[cv * V + j] = t1;
+        rec2[a.C + cv * V + j] = t3;
+      }
     }
   }
 }
@@ -327,8 +343,17 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
   BnBwdArgs b = a;
   b.rows_per_block = rpb;
   dim3 grid(cdiv(a.C / V, bx), P), block(bx, by);
-  size_t shm = (size_t)bx * by * V * 2 * sizeof(float);
+  size_t shm = (size_t)bx * by * V * (a.z2 ? 3 : 2) * sizeof(float);
   const int mode = b.relu_z ? 2 : (b.mask ? 1 : 0);
+  if (a.z2) {  // paired BNs (mask mode)
+    if (mode != 1 || !a.part2 || !a.mean2 || !a.invstd2) {
+      set_error("bn_bwd_reduce: a paired BN needs the mask mode and its own records / statistics");
+      return E_INVALID;
+    }
+    if (dtype == DT_F32) bn_bwd_reduce_kernel<float, 1, true><<<grid, block, shm, st>>>(b);
+    else bn_bwd_reduce_kernel<bf16, 1, true><<<grid, block, shm, st>>>(b);
+    return check_launch("bn_bwd_reduce");
+  }
 #define BN_RED(T, M) bn_bwd_reduce_kernel<T, M><<<grid, block, shm, st>>>(b)
   if (dtype == DT_F32) {
     if (mode == 0) BN_RED(float, 0); else if (mode == 1) BN_RED(float, 1); else BN_RED(float, 2);
@@ -455,7 +480,7 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
 }
 
 // dz = scale * (dy_r - coef0 - xhat * coef1)   (train);  dz = scale * dy_r (eval: coef null)
-template <typename T, int MODE, bool TRAIN>
+template <typename T, int MODE, bool TRAIN, bool PAIR = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int CV = a.C / V;
@@ -465,10 +490,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const unsigned mu = i / (unsigned)CV;
   const int c = (int)(i - mu * (unsigned)CV) * V;
   const long long m = mu;
-  float g[V], z[V], mk[V], o[V];
+  float g[V], z[V], mk[V], o[V], z2[PAIR ? V : 1];
   ldv((const T*)a.dy + m * a.lddy + c, g);
   if (TRAIN || MODE == 2) ldv((const T*)a.z + m * a.ldz + c, z);
   if (MODE == 1) ldv((const T*)a.mask + m * a.ldmask + c, mk);
+  if constexpr (PAIR) {  // second BN on the same dy and mask (train, mask mode)
+    ldv((const T*)a.z2 + m * a.ldz + c, z2);
+    float o2[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float gv = mk[j] > 0.f ? g[j] : 0.f;
+      const float xh = (z2[j] - a.mean2[c + j]) * a.invstd2[c + j];
+      o2[j] = a.scale2[c + j] * (gv - a.coef2[c + j] - xh * a.coef2[a.C + c + j]);
+    }
+    stv((T*)a.dz2 + m * a.lddz + c, o2);
+  }
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     float gv = g[j];
@@ -502,6 +538,16 @@ int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
   int V = dtype == DT_F32 ? 4 : 8;
   long long total = a.M * (a.C / V);
   unsigned grid = (unsigned)((total + 255) / 256);
+  if (a.z2) {  // paired BNs: train, mask mode
+    if (!a.mask || !a.coef || !a.coef2 || !a.dz2 || !a.mean2 || !a.invstd2 || !a.scale2) {
+      set_error("bn_bwd_apply: a paired BN needs the mask mode, both coefficient sets and dz2");
+      return E_INVALID;
+    }
+    ProfScope ps(PK_BN_BWD, st, (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * 6, 0.0);
+    if (dtype == DT_F32) bn_bwd_apply_kernel<float, 1, true, true><<<grid, 256, 0, st>>>(a);
+    else bn_bwd_apply_kernel<bf16, 1, true, true><<<grid, 256, 0, st>>>(a);
+    return check_launch("bn_bwd_apply");
+  }
   ProfScope ps(PK_BN_BWD, st,
                (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * (2 + (a.coef || a.relu_z ? 1 : 0) + (a.mask ? 1 : 0)),
                0.0);

@@ -225,6 +225,14 @@ struct BnBwdArgs {
   // apply
   const float* coef;              // [2][C]: mean(dy_r), mean(dy_r*xhat) (train) — null in eval
   void* dz; int lddz;
+  // a second BN with the same dy and mask (FeatureFusionModule: relu(BN_l(z_l) + BN_h(z_h))):
+  // z2 / mean2 / invstd2 / scale2 [C], records part2 [P][2][C] (its s1 equals the first BN's),
+  // coef2 and dz2 (ld lddz) — one pass reads dy and the mask once for both BNs (mask mode only)
+  const void* z2 = nullptr;
+  const float* mean2 = nullptr; const float* invstd2 = nullptr; const float* scale2 = nullptr;
+  float* part2 = nullptr;
+  const float* coef2 = nullptr;
+  void* dz2 = nullptr;
 };
 
 struct UpArgs {

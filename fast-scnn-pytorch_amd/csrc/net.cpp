@@ -472,7 +472,13 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
       dw_upd(Hin, Win, net.lb[i].cin * 6, net.lb[i].stride);
     }
     dw_upd(pl.H3, pl.W3, 128, 1);
+    {  // the FFM pair (Exec::bn_bwd_pair) keeps both BNs' records side by side
+      int rpb;
+      const size_t s = (size_t)2 * bn_bwd_parts(pl.flow.M, 128, dtype, &rpb) * 2 * 128;
+      if (s > bnp) bnp = s;
+    }
     pl.bnpart = B.get(bnp * 4);
+    pl.bnpart_floats = bnp;
     pl.coef = B.get(2 * 1024 * 4);
     pl.xtab = B.get((size_t)NTAB_SLOTS * 1024 * BWDX_STRIDE * 4);  // Exec::tab_slot
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
@@ -532,6 +538,15 @@ struct SideStream {
   }
 };
 std::shared_ptr<SideStream> make_side_stream() { return std::make_shared<SideStream>(); }
+
+// FSCNN_FFM_PAIR=0: the FFM's two BN backwards as separate reduce / apply passes (A/B)
+static bool ffm_pair_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_FFM_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 static bool side_stream_enabled() {
   static const bool on = [] {
@@ -1149,6 +1164,38 @@ struct Exec {
     b.dz = dz; b.lddz = u.C;
     return bn_bwd_apply(b, dt, r.st);
   }
+  // the FeatureFusionModule's two BNs, f = relu(BN_l(z_l) + BN_h(z_h)) (models/fast_scnn.py
+  // :207-218): the same dy (g_f) and ReLU mask (f) for both, so one reduce pass and one apply
+  // pass read them once (the reduce's sum of dy_r is shared; the finishes stay per BN)
+  int bn_bwd_pair(const Unit& u1, const BnL& bn1, const Unit& u2, const BnL& bn2, const void* dy,
+                  int lddy, const void* mask, int ldmask, void* dz1, void* dz2) {
+    g_prof_tag = "feature_fusion (BN backward, both branches)";
+    int rpb;
+    const int P = bn_bwd_parts(u1.M, u1.C, dt, &rpb);
+    if (!dz1 || !dz2 || u1.M != u2.M || u1.C != u2.C || 4 * u1.C > 2048 ||
+        (size_t)P * 4 * u1.C > pl.bnpart_floats) {
+      set_error("bn_bwd_pair: units do not pair or the record arena is too small");
+      return E_INVALID;
+    }
+    BnBwdArgs b{};
+    b.M = u1.M; b.C = u1.C;
+    b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
+    b.z = W(u1.z); b.ldz = u1.C;
+    b.mean = Wf(u1.mean); b.invstd = Wf(u1.invstd); b.scale = Wf(u1.scale); b.shift = Wf(u1.shift);
+    b.z2 = W(u2.z); b.mean2 = Wf(u2.mean); b.invstd2 = Wf(u2.invstd); b.scale2 = Wf(u2.scale);
+    b.part = (float*)Bw(pl.bnpart);
+    b.part2 = b.part + (size_t)P * 2 * u1.C;
+    TRY(bn_bwd_reduce(b, dt, r.st));
+    float* coef = (float*)Bw(pl.coef);
+    float* coef2 = coef + 2 * u1.C;
+    TRY(bn_bwd_finalize(b.part, P, u1.C, (double)u1.M, G(bn1.g), G(bn1.b), coef, r.st,
+                        (unsigned*)W(pl.bcnt), BnBwdTab()));
+    TRY(bn_bwd_finalize(b.part2, P, u2.C, (double)u2.M, G(bn2.g), G(bn2.b), coef2, r.st,
+                        (unsigned*)W(pl.bcnt), BnBwdTab()));
+    b.coef = coef; b.coef2 = coef2;
+    b.dz = dz1; b.dz2 = dz2; b.lddz = u1.C;
+    return bn_bwd_apply(b, dt, r.st);
+  }
   // BN whose output is relu(BN(z)) with no second branch: the ReLU mask is recomputed from z
   int bn_bwd_relu(const Unit& u, const BnL& bn, const void* dy, int lddy, void* dz) {
     return bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, true);
@@ -1323,15 +1370,20 @@ struct Exec {
     // (low branch first so the low 1x1 dgrad can hand its BN-backward partials straight to
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     void* zl = dz_buf(pl.flow);
-    TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, zl));
+    void* zh = dz_buf(pl.fhigh);
+    const bool pair = ffm_pair_enabled();
+    if (pair)  // both branch BNs in one reduce and one apply (same dy g_f and mask f)
+      TRY(bn_bwd_pair(pl.flow, net.ffm_blow, pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f),
+                      128, zl, zh));
+    else
+      TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, zl));
     TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(zl, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw, net.ffm_bdw)));
     TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz_buf(pl.fdw), d, dw_bx_enabled()));
     TRY(dw_bwd(net.ffm_dw, 128, d, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
     TRY(flush_side());
-    void* zh = dz_buf(pl.fhigh);
-    TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, zh));
+    if (!pair) TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, zh));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(zh, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
     TRY(flush_side());
     if (net.aux) TRY(backward_aux());
