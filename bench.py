@@ -252,9 +252,10 @@ def main():
     barrier()
 
     # ---- timed region: K steps; HIP events bracket the dominant family's launches in the last
-    # quarter of the timed steps (timing events on every launch of every step would add ~0.4 ms
-    # of event packets to a 60-launch family; the events are created before the region)
-    nprof = max(1, args.steps // 4)
+    # tenth of the timed steps (each timing event costs its stream ~7 us of idle time on MI355X:
+    # ~0.7 ms per profiled step for the 52-launch gemm_nt family, so profiling a quarter of the
+    # steps inflated ms_per_step by ~0.12 ms; the events are created before the region)
+    nprof = max(1, args.steps // 10)
     _lib.check(lib.fscnn_prof_begin(kind, 512 * nprof), "fscnn_prof_begin")
     ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
     _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
