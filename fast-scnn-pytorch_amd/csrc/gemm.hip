@@ -570,7 +570,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   int nt = pick_nt(a.N);
   // small-M problems (the 16 K-row bottleneck3 / bottleneck2 projects): split the columns
   // further so the grid covers the 256 CUs (the A tile is then read twice, from L2)
-  if ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < 256 && (nt == 8 || nt == 6 || nt == 4))
+  static const int min_tiles = [] {  // FSCNN_GEMM_MIN_TILES: grid size below which NT halves
+    const char* e = getenv("FSCNN_GEMM_MIN_TILES");
+    return e ? atoi(e) : 256;
+  }();
+  while ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < min_tiles && (nt == 8 || nt == 6 || nt == 4))
     nt /= 2;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
