@@ -610,10 +610,14 @@ struct Exec {
       g_prof_tag = o;
       return rc;
     });
-    // FSCNN_SIDE_BATCH=1: issue the queue only at the flush points (one fork per block) —
-    // measured slower (7.24 vs 7.00 ms/step): a wgrad started as soon as its dz exists fills the
-    // idle issue slots of the latency-bound dgrad chain, a delayed batch contends with the next
-    // block instead
+    return OK;
+  }
+  // the wgrads of one conv (gemm_tn + bias colsum, or the depthwise wgrad) behind one fork.
+  // FSCNN_SIDE_BATCH=1: issue the queue only at the flush points (one fork per block) —
+  // measured slower (7.24 vs 7.00 ms/step): a wgrad started as soon as its dz exists fills the
+  // idle issue slots of the latency-bound dgrad chain, a delayed batch contends with the next
+  // block instead
+  int flush_conv() {
     static const bool batch = [] {
       const char* e = getenv("FSCNN_SIDE_BATCH");
       return e && e[0] == '1';
@@ -1253,6 +1257,7 @@ struct Exec {
       }));
       TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
+    TRY(flush_conv());
     if (!dX) return OK;
     GemmArgs g{};
     g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
@@ -1292,6 +1297,7 @@ struct Exec {
       const DwBwdArgs dw = d;
       const int dtc = dt;
       TRY(side_launch([dw, dtc](hipStream_t s) { return dw_wgrad(dw, dtc, s); }));
+      TRY(flush_conv());
     }
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
     const bool br = bt.u && train && dw_bnred_enabled();
