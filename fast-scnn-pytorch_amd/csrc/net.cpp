@@ -327,6 +327,9 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.c0.lazy = pl.l1dw.lazy = pl.l1pw.lazy = pl.l2dw.lazy = true;
     for (int i = 0; i < 9; ++i) pl.lbe[i].lazy = pl.lbd[i].lazy = true;
     pl.fdw.lazy = pl.c1dw.lazy = pl.c1pw.lazy = pl.c2dw.lazy = true;
+    // LearningToDownsample's output: read by bottleneck1.0's expand and the FFM's high-res
+    // branch (both GEMM operands) — unless the aux head's im2col reads it as well
+    if (!net.aux) pl.l2pw.lazy = true;
   }
   // fp64 team sums of the in-kernel BN finishes (last, so the activation offsets above do not move)
   if (train) pl.tsum = A.get((size_t)TAIL_TMAX * 3 * TAIL_CMAX * 8);
@@ -907,7 +910,7 @@ struct Exec {
     for (int i = 0; i < 9; ++i) {
       const LbL& l = net.lb[i];
       int Ho = dwout(Hc, l.stride), Wo = dwout(Wc, l.stride);
-      TRY(pw(pl.lbe[i], l.e, &l.be, raw(x, xld), true));
+      TRY(pw(pl.lbe[i], l.e, &l.be, i == 0 ? act(pl.l2pw) : raw(x, xld), true));
       TRY(dw(pl.lbd[i], l.d, l.bd, act(pl.lbe[i]), Hc, Wc, Ho, Wo, l.stride));
       bool shortcut = l.stride == 1 && l.cin == l.cout;
       TRY(pw(pl.lbp[i], l.p, &l.bp, act(pl.lbd[i]), false, shortcut ? x : nullptr,
@@ -974,8 +977,9 @@ struct Exec {
         gemm_fin(g, pl.flow, net.ffm_blow);
         TRY(gemm_nt(g, dt, r.st));
         g_prof_tag = pl.fhigh.name.c_str();
-        g.K = 64; g.A = W(pl.l2pw.a); g.lda = 64; g.B = Wg(net.ffm_high); g.ldb = 64;
-        g.a_scale = g.a_shift = nullptr;
+        const In hin = act(pl.l2pw);
+        g.K = 64; g.A = hin.p; g.lda = hin.ld; g.B = Wg(net.ffm_high); g.ldb = 64;
+        g.a_scale = hin.sc; g.a_shift = hin.sh;
         g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z);
         gemm_fin(g, pl.fhigh, net.ffm_bhigh);
         TRY(gemm_nt(g, dt, r.st));
@@ -1390,7 +1394,7 @@ struct Exec {
                Bw(pl.g_up)));
     TRY(flush_side());
     if (!pair) TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, zh));
-    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(zh, 128), raw(W(pl.l2pw.a), 64), Bw(pl.l2pw.ga), 64));
+    TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(zh, 128), act(pl.l2pw), Bw(pl.l2pw.ga), 64));
     TRY(flush_side());
     if (net.aux) TRY(backward_aux());
     // upsample (x4, ac) backward: W pass then H pass → grad of ppm.out activation
@@ -1485,7 +1489,7 @@ struct Exec {
     // the dgrad is the dy of the previous block's project BN (or of LTD.dsconv2's pw BN)
     const BTarget bt = i == 0 ? relu_target(pl.l2pw, net.ltd2.bpw)
                               : plain_target(pl.lbp[i - 1], net.lb[i - 1].bp);
-    TRY(pw_bwd(l.e, ue.M, d, raw(x, xld), gx, gxld, R, ldr, bt));
+    TRY(pw_bwd(l.e, ue.M, d, i == 0 ? act(pl.l2pw) : raw(x, xld), gx, gxld, R, ldr, bt));
     return flush_side();  // the block's three wgrads behind one fork
   }
 
