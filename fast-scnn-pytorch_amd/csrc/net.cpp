@@ -567,6 +567,8 @@ namespace {
     if (rc__) return rc__;     \
   } while (0)
 
+bool graphs_enabled();
+
 // fused BN-backward partials: the dgrad GEMM producing the dy of unit `u` emits its records
 struct BTarget {
   const Unit* u = nullptr;
@@ -671,6 +673,11 @@ struct Exec {
     return (float*)Bw(pl.xtab) + (size_t)(ntab++) * 1024 * BWDX_STRIDE;
   }
 
+  // the dropout seed: a device slot only when the launches may be captured into a hipGraph
+  // (replays must see a new seed); otherwise a kernel argument (no set_u64 launch per step)
+  const uint64_t* seed_ptr() const {
+    return graphs_enabled() ? reinterpret_cast<const uint64_t*>(W(pl.seed_slot)) : nullptr;
+  }
   void* W(size_t off) const { return ws + off; }
   void* Bw(size_t off) const { return bws + off; }
   float* Wf(size_t off) const { return (float*)(ws + off); }
@@ -1005,7 +1012,7 @@ struct Exec {
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = W(pl.c2pw.z); d.ldx = 128;
       d.x_scale = Wf(pl.c2pw.scale); d.x_shift = Wf(pl.c2pw.shift);
       d.y = W(pl.drop); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
-      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
+      d.seed_ptr = seed_ptr();
       TRY(dropout(d, dt, r.st));
       cls_in = W(pl.drop);
     }
@@ -1057,7 +1064,7 @@ struct Exec {
       DropArgs d{};
       d.N = pl.N; d.H = pl.H3; d.W = pl.W3; d.C = 32; d.x = W(u.a); d.ldx = 32;
       d.y = W(pl.aux_drop); d.ldy = 32; d.seed = r.seed; d.p = r.dropout_p; d.seed_add = 1;
-      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
+      d.seed_ptr = seed_ptr();
       TRY(dropout(d, dt, r.st));
       ain = W(pl.aux_drop);
     }
@@ -1097,7 +1104,7 @@ struct Exec {
       DropArgs d{};
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 32; d.x = Bw(pl.g_aux); d.ldx = 32;
       d.y = Bw(u.ga); d.ldy = 32; d.seed = r.seed; d.p = r.dropout_p; d.seed_add = 1;
-      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
+      d.seed_ptr = seed_ptr();
       TRY(dropout(d, dt, r.st));
     }
     Dz d;
@@ -1358,7 +1365,7 @@ struct Exec {
       DropArgs d{};
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = Bw(pl.g_drop); d.ldx = 128;
       d.y = Bw(pl.c2pw.ga); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;
-      d.seed_ptr = reinterpret_cast<const uint64_t*>(W(pl.seed_slot));
+      d.seed_ptr = seed_ptr();
       TRY(dropout(d, dt, r.st));
     }
     // classifier dsconv2, dsconv1
@@ -1664,7 +1671,7 @@ int net_forward(const Plan& pl, const RunArgs& r) {
     set_error("fscnn_forward: this net has the aux head; use fscnn_forward_aux");
     return E_INVALID;
   }
-  if (pl.train && r.dropout_p > 0.f)  // read by the dropout kernels (outside any graph)
+  if (pl.train && r.dropout_p > 0.f && graphs_enabled())  // read by the dropout kernels
     TRY(set_u64(reinterpret_cast<uint64_t*>((char*)r.ws + pl.seed_slot), r.seed, r.st));
   return run_graphed(pl, run_key(0, 0, 0, r), r.st, [&](hipStream_t st) -> int {
     RunArgs rr = r;
