@@ -112,9 +112,10 @@ def prof(lib, kind, fn, max_launches):
 
 
 def cpu_baseline(args):
-    """Oracle restatement (port) timed on this host's cores on bounded samples: one train step
-    (the metric's unit), the cfg2 forward (8 x 3 x 1024 x 2048, eval) beside forward_fp32, and the
-    cfg1 forward (1 x 3 x 768 x 768, the demo.py path)."""
+    """Oracle restatement (port) timed on this host's cores on bounded samples: the train step
+    (the metric's unit, at cfg3's own 8 x 3 x 1024 x 2048), the cfg2 forward (8 x 3 x 1024 x 2048,
+    eval) beside forward_fp32, the cfg1 forward (1 x 3 x 768 x 768, the demo.py path) and the cfg5
+    forward (32 x 3 x 480 x 640, 2 classes; fp32 — the CPU has no fp16 arithmetic path)."""
     import numpy as np
     import torch
     from fast_scnn_pytorch_amd import arch, portable_init
@@ -148,7 +149,17 @@ def cpu_baseline(args):
         out["forward_cfg1"] = {"value": round(1 / med, 3), "unit": "images/s",
                                "ms_per_image": round(1e3 * med, 2),
                                "sample": "eval fp32 1x3x768x768 (demo.py path), median of %d" % n}
-    nb = 2
+        del x1
+        sd5 = {k: torch.from_numpy(np.asarray(v)) for k, v in
+               arch.portable_state_dict(2, seed=0).items()}
+        x5 = torch.from_numpy(portable_init.input_tensor(1, (32, 3, 480, 640)))
+        med, n = timed(lambda: ref.forward(sd5, x5, 2), 3, 6.0)
+        out["forward_cfg5"] = {"value": round(32 / med, 3), "unit": "images/s",
+                               "ms_per_batch": round(1e3 * med, 1),
+                               "sample": "eval fp32 32x3x480x640, 2 classes, median of %d after "
+                                         "1 warm-up" % n}
+        del x5, sd5
+    nb = args.batch
     for k, v in sd.items():
         if v.is_floating_point() and "running" not in k:
             v.requires_grad_(True)
@@ -162,7 +173,7 @@ def cpu_baseline(args):
         outs, _, _ = ref.forward(sd, x, args.classes, training=True, dropout_seed=5)
         ref.cross_entropy(outs[0], t).backward()
 
-    med, n = timed(step, 3, 25.0)
+    med, n = timed(step, 2, 20.0)
     res = {"value": round(nb / med, 4), "unit": "images/s", "cores": threads, "kind": "port",
            "sample": "oracle/fast_scnn_ref.py train step (fwd+CE+bwd, fp32) on %d x 3 x %d x %d, "
                      "median of %d after 1 warm-up, torch CPU %d threads"
@@ -321,6 +332,9 @@ def main():
     }
     if census:
         result["kernel_ms_per_step_census"] = census
+        result["census_note"] = ("HIP-event kernel time per family over one profiled step each; "
+                                 "the families overlap on two streams and every event idles its "
+                                 "stream ~7 us, so the sum is not a breakdown of ms_per_step")
 
     # forward-only inference (rank 0, N=1 only): cfg2 fp32 (north-star forward target), cfg1
     # (demo.py: 1 x 3 x 768 x 768, latency) and cfg5 (TuSimple 32 x 3 x 480 x 640, C=2)

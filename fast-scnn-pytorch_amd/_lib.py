@@ -41,7 +41,6 @@ SIGNATURES = {
     "fscnn_remap_labels": (c_int, [c_vp, c_ll, c_vp, c_int, c_int, c_ll, c_vp, c_vp]),
     "fscnn_ohem_prob": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_float, c_vp, c_vp,
                                 c_vp]),
-    "fscnn_kth_smallest": (c_int, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp]),
     "fscnn_ohem_threshold": (c_int, [c_vp, c_ll, c_vp, c_ll, c_float, c_vp, c_vp, c_vp]),
     "fscnn_ce_weighted_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp]),

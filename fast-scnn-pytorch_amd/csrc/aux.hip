@@ -91,6 +91,7 @@ int col2im3(const Col2ImArgs& a, int dtype, hipStream_t st) {
   }
   const unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) col2im3_kernel<float><<<grid, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) col2im3_kernel<f16><<<grid, 256, 0, st>>>(a);
   else col2im3_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("col2im3");
 }

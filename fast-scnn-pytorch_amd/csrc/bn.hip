@@ -217,6 +217,7 @@ int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st) {
                0.0);
   unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) bn_apply_kernel<float><<<grid, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) bn_apply_kernel<f16><<<grid, 256, 0, st>>>(a);
   else bn_apply_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("bn_apply");
 }
@@ -351,12 +352,15 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
       return E_INVALID;
     }
     if (dtype == DT_F32) bn_bwd_reduce_kernel<float, 1, true><<<grid, block, shm, st>>>(b);
+    else if (dtype == DT_F16) bn_bwd_reduce_kernel<f16, 1, true><<<grid, block, shm, st>>>(b);
     else bn_bwd_reduce_kernel<bf16, 1, true><<<grid, block, shm, st>>>(b);
     return check_launch("bn_bwd_reduce");
   }
 #define BN_RED(T, M) bn_bwd_reduce_kernel<T, M><<<grid, block, shm, st>>>(b)
   if (dtype == DT_F32) {
     if (mode == 0) BN_RED(float, 0); else if (mode == 1) BN_RED(float, 1); else BN_RED(float, 2);
+  } else if (dtype == DT_F16) {
+    if (mode == 0) BN_RED(f16, 0); else if (mode == 1) BN_RED(f16, 1); else BN_RED(f16, 2);
   } else {
     if (mode == 0) BN_RED(bf16, 0); else if (mode == 1) BN_RED(bf16, 1); else BN_RED(bf16, 2);
   }
@@ -545,6 +549,7 @@ int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
     }
     ProfScope ps(PK_BN_BWD, st, (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * 6, 0.0);
     if (dtype == DT_F32) bn_bwd_apply_kernel<float, 1, true, true><<<grid, 256, 0, st>>>(a);
+    else if (dtype == DT_F16) bn_bwd_apply_kernel<f16, 1, true, true><<<grid, 256, 0, st>>>(a);
     else bn_bwd_apply_kernel<bf16, 1, true, true><<<grid, 256, 0, st>>>(a);
     return check_launch("bn_bwd_apply");
   }
@@ -552,16 +557,10 @@ int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
                (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * (2 + (a.coef || a.relu_z ? 1 : 0) + (a.mask ? 1 : 0)),
                0.0);
   if (dtype == DT_F32) bn_bwd_apply_launch<float>(a, grid, st);
+  else if (dtype == DT_F16) bn_bwd_apply_launch<f16>(a, grid, st);
   else bn_bwd_apply_launch<bf16>(a, grid, st);
   return check_launch("bn_bwd_apply");
 }
 
-bool tail_ink_on(int bit) {
-  static const int mask = [] {
-    const char* e = getenv("FSCNN_TAIL_INK");
-    return e ? atoi(e) : 15;
-  }();
-  return (mask & bit) != 0;
-}
 
 }  // namespace fscnn

@@ -31,7 +31,7 @@ int check_launch(const char* what) {
 
 // ---- launch profiler --------------------------------------------------------------------
 int g_prof_kind = PK_NONE;
-const char* g_prof_tag = "";
+thread_local const char* g_prof_tag = "";
 namespace {
 struct ProfState {
   std::vector<hipEvent_t> ev;  // pairs
@@ -362,15 +362,6 @@ int fscnn_ohem_prob(const void* logits, int dtype, const long long* target, int 
   CeArgs a{};
   a.N = N; a.C = C; a.HW = HW; a.logits = logits; a.target = target; a.ignore_index = ignore_index;
   return ohem_prob(a, thresh, prob, counts, dtype, S(stream));
-}
-
-int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* hist, float* out,
-                       void* stream) {
-  if (!values || !hist || !out) {
-    set_error("fscnn_kth_smallest: null argument");
-    return E_INVALID;
-  }
-  return kth_smallest(values, n, k, hist, out, S(stream));
 }
 
 int fscnn_ohem_threshold(const float* prob, long long n, const unsigned long long* counts,

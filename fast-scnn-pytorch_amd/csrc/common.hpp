@@ -277,13 +277,13 @@ __device__ __forceinline__ uint4 bnrelu_vec(const uint4& t, const float* sc, con
     return make_uint4(w[0], w[1], w[2], w[3]);
   } else {
     float v[8];
-    unpackv(t, v);
+    unpack<T>(t, v);
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float a = fmaxf(fmaf(v[2 * i], sc[2 * i], sh[2 * i]), 0.f);
       const float b = fmaxf(fmaf(v[2 * i + 1], sc[2 * i + 1], sh[2 * i + 1]), 0.f);
-      w[i] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+      w[i] = (uint32_t)s16_from<T>(a) | ((uint32_t)s16_from<T>(b) << 16);
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -329,8 +329,8 @@ __device__ __forceinline__ uint4 bwdx_apply(const uint4& dy, const uint4& z, con
                                             const float* sh) {
   constexpr int V = VecW<T>::V;
   float g[V], zz[V], o[V];
-  unpackv(dy, g);
-  unpackv(z, zz);
+  unpack<T>(dy, g);
+  unpack<T>(z, zz);
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const float gv = fmaf(zz[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
@@ -396,7 +396,9 @@ enum ProfKind : int {
 };
 constexpr int PK_ALL = 100;  // record every kind (per-launch layer report)
 extern int g_prof_kind;  // kind being recorded (PK_NONE = off)
-extern const char* g_prof_tag;  // layer the executor is issuing (per-launch report label)
+// layer the executor is issuing (per-launch report label); per thread: DataParallel replicas
+// (train.py:170-171) run the executor from one worker thread per device
+extern thread_local const char* g_prof_tag;
 void prof_start(hipStream_t st);
 void prof_stop(hipStream_t st, int kind, double bytes, double flops);
 struct ProfScope {

@@ -424,11 +424,7 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
     if (a.x_bf16 == 2) conv0_fwd_kernel<float, 2><<<grid, 256, 0, st>>>(a);
     else if (a.x_bf16) conv0_fwd_kernel<float, 1><<<grid, 256, 0, st>>>(a);
     else conv0_fwd_kernel<float, 0><<<grid, 256, 0, st>>>(a);
-  } else if (y_dtype == DT_F16) {  // inference plans only (no statistics)
-    if (a.part) {
-      set_error("conv0_fwd: fp16 arithmetic is inference-only");
-      return E_UNSUPPORTED;
-    }
+  } else if (y_dtype == DT_F16) {
     if (a.x_bf16 == 2) conv0_fwd_kernel<f16, 2><<<grid, 256, 0, st>>>(a);
     else if (a.x_bf16) conv0_fwd_kernel<f16, 1><<<grid, 256, 0, st>>>(a);
     else conv0_fwd_kernel<f16, 0><<<grid, 256, 0, st>>>(a);
@@ -487,6 +483,17 @@ struct CwOps<bf16> {
   }
 };
 
+template <>
+struct CwOps<f16> {
+  static constexpr int LD = CW_TP + 8;
+  static __device__ __forceinline__ void mma(const f16* a, const f16* b, f32x4& acc) {
+    h16x8 av, bv;
+    __builtin_memcpy(&av, a, 16);
+    __builtin_memcpy(&bv, b, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+  }
+};
+
 template <typename T>
 __device__ __forceinline__ T cw_cvt(float v);
 template <>
@@ -495,6 +502,12 @@ template <>
 __device__ __forceinline__ bf16 cw_cvt<bf16>(float v) {
   bf16 r;
   r.x = f2bf(v);
+  return r;
+}
+template <>
+__device__ __forceinline__ f16 cw_cvt<f16>(float v) {
+  f16 r;
+  r.x = f2h(v);
   return r;
 }
 
@@ -648,6 +661,7 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
     }                                                                                 \
   } while (0)
   if (dz_dtype == DT_F32) CW_LAUNCH(float);
+  else if (dz_dtype == DT_F16) CW_LAUNCH(f16);
   else CW_LAUNCH(bf16);
 #undef CW_LAUNCH
   return check_launch("conv0_wgrad");

@@ -91,13 +91,10 @@ __device__ __forceinline__ void dw_tile(int& cx, int& cy, int& cz) {
 // IT: x is the raw conv output z of a BatchNorm+ReLU that is never stored (train); the staged
 // value is relu(fmaf(z, isc[c], ish[c])) (bn_apply's arithmetic), padding stays zero.  A thread's
 // vectors all belong to one channel vector (lv = tid % cbv), so its V pairs are loaded once.
-// BX: x is a BN's dy and the staged value is that BN's dz = bwdx_apply(dy, z, tab) (the dz is
-// never stored; z = xz, same layout as x), padding stays zero.
-template <typename T, int S, bool IT, bool BX = false>
+template <typename T, int S, bool IT>
 __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, int C, int n,
                                          int hi0, int wi0, int cvbase, int cbv, int tid, int nthr,
-                                         const float* isc, const float* ish,
-                                         const T* xz = nullptr, const float* xtab = nullptr) {
+                                         const float* isc, const float* ish) {
   using G = DwTile<T, S>;
   constexpr int V = VecW<T>::V;
   float sc[IT ? V : 1], sh[IT ? V : 1];
@@ -109,9 +106,7 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
       sh[j] = ish[cb + j];
     }
   }
-  BwdXCoef<T> bx;
-  if constexpr (BX) bx.load(xtab, (cvbase + tid % cbv) * V);
-  uint4 raw[G::LPT], rz[BX ? G::LPT : 1];
+  uint4 raw[G::LPT];
 #pragma unroll
   for (int k = 0; k < G::LPT; ++k) {
     const int i = tid + k * nthr;
@@ -121,20 +116,18 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
     const bool ok = pix < G::IR * G::IC && hi >= 0 && hi < H && wi >= 0 && wi < W;
     const size_t off = ok ? (((size_t)n * H + hi) * W + wi) * C + (size_t)(cvbase + lv) * V : 0;
     raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(x + off));
-    if constexpr (BX) rz[k] = *reinterpret_cast<const uint4*>(xz + off);
   }
 #pragma unroll
   for (int k = 0; k < G::LPT; ++k) {
     const int i = tid + k * nthr;
     if (i < G::IR * G::IC * cbv) {
       uint4 v = raw[k];
-      if constexpr (IT || BX) {
+      if constexpr (IT) {
         const int pix = i / cbv;
         const int r = pix / G::IC, col = pix - r * G::IC;
         const int hi = hi0 + r, wi = wi0 + col;
         const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
-        if constexpr (IT) v = sel4(ok, bnrelu_vec<T>(v, sc, sh));
-        if constexpr (BX) v = sel4(ok, bwdx_apply<T>(v, rz[k], bx.al, bx.be, bx.gz, bx.sc, bx.sh));
+        v = sel4(ok, bnrelu_vec<T>(v, sc, sh));
       }
       s_in[i] = v;
     }
@@ -144,7 +137,7 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
 // TL: the launch finishes its BN in the last workgroups (a.tail_ink; a separate instantiation so
 // the other launches keep their register budget)
-template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool BX = false, bool TL = false>
+template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool TL = false>
 __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
   // LDS sized per launch (dw_shm): the staged tile of cbv channel vectors + the reduction rows
@@ -161,9 +154,8 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   const int n = bz / tiles_h;
   const int th0 = (bz - n * tiles_h) * G::TH, tw0 = by * G::TW;
   const int c0 = bx * cbv * VecW<T>::V + q * 4;  // first channel of the thread's quad
-  dw_stage<T, S, IT, BX>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
-                         bx * cbv, cbv, tid, nthr, a.in_scale, a.in_shift, (const T*)a.xz,
-                         a.xtab);
+  dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
+                     bx * cbv, cbv, tid, nthr, a.in_scale, a.in_shift);
   float wt[9][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -364,7 +356,23 @@ int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
   return (int)(g.y * g.z);
 }
 
-template <bool FLIP, bool IT, bool BR = false, bool BX = false>
+template <typename T, bool FLIP, bool IT, bool BR>
+static void dw_launch_fwd_t(const DwArgs& a, dim3 grid, int nthr, int cbv, hipStream_t st) {
+  if constexpr (BR) {  // stride-1 dgrad with BN-backward partials
+    if (a.tail_ink) dw_fwd_kernel<T, 1, true, false, true, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
+    else dw_fwd_kernel<T, 1, true, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
+    return;
+  }
+  if (!FLIP && a.tail_ink) {  // train forward with the in-kernel BN finish
+    if (a.stride == 1) dw_fwd_kernel<T, 1, false, IT, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
+    else dw_fwd_kernel<T, 2, false, IT, false, true><<<grid, nthr, dw_shm<T, 2>(cbv), st>>>(a, cbv);
+    return;
+  }
+  if (a.stride == 1) dw_fwd_kernel<T, 1, FLIP, IT><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
+  else dw_fwd_kernel<T, 2, FLIP, IT><<<grid, nthr, dw_shm<T, 2>(cbv), st>>>(a, cbv);
+}
+
+template <bool FLIP, bool IT, bool BR = false>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   int cbv;
@@ -374,45 +382,10 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   const int nthr = cbv * 32;  // = quads * groups for both dtypes
-  if (dtype == DT_F16) {  // inference plans only
-    if (FLIP || IT) {
-      set_error("dw: fp16 arithmetic is inference-only");
-      return E_UNSUPPORTED;
-    }
-    if (a.stride == 1) dw_fwd_kernel<f16, 1, false, false><<<grid, nthr, dw_shm<f16, 1>(cbv), st>>>(a, cbv);
-    else dw_fwd_kernel<f16, 2, false, false><<<grid, nthr, dw_shm<f16, 2>(cbv), st>>>(a, cbv);
-    return check_launch("dw_fwd");
-  }
-  if constexpr (BR || BX) {  // stride-1 dgrad with BN-backward partials / operand transform
-    if constexpr (BR) {
-      if (a.tail_ink) {
-        if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX, true><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
-        else dw_fwd_kernel<bf16, 1, true, false, BR, BX, true><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
-        return check_launch("dw_dgrad");
-      }
-    }
-    if (dtype == DT_F32) dw_fwd_kernel<float, 1, true, false, BR, BX><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
-    else dw_fwd_kernel<bf16, 1, true, false, BR, BX><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
-    return check_launch("dw_dgrad");
-  }
-  if (!FLIP && a.tail_ink) {  // train forward with the in-kernel BN finish
-    if (dtype == DT_F32) {
-      if (a.stride == 1) dw_fwd_kernel<float, 1, false, IT, false, false, true><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
-      else dw_fwd_kernel<float, 2, false, IT, false, false, true><<<grid, nthr, dw_shm<float, 2>(cbv), st>>>(a, cbv);
-    } else {
-      if (a.stride == 1) dw_fwd_kernel<bf16, 1, false, IT, false, false, true><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
-      else dw_fwd_kernel<bf16, 2, false, IT, false, false, true><<<grid, nthr, dw_shm<bf16, 2>(cbv), st>>>(a, cbv);
-    }
-    return check_launch("dw_fwd");
-  }
-  if (dtype == DT_F32) {
-    if (a.stride == 1) dw_fwd_kernel<float, 1, FLIP, IT><<<grid, nthr, dw_shm<float, 1>(cbv), st>>>(a, cbv);
-    else dw_fwd_kernel<float, 2, FLIP, IT><<<grid, nthr, dw_shm<float, 2>(cbv), st>>>(a, cbv);
-  } else {
-    if (a.stride == 1) dw_fwd_kernel<bf16, 1, FLIP, IT><<<grid, nthr, dw_shm<bf16, 1>(cbv), st>>>(a, cbv);
-    else dw_fwd_kernel<bf16, 2, FLIP, IT><<<grid, nthr, dw_shm<bf16, 2>(cbv), st>>>(a, cbv);
-  }
-  return check_launch("dw_fwd");
+  if (dtype == DT_F32) dw_launch_fwd_t<float, FLIP, IT, BR>(a, grid, nthr, cbv, st);
+  else if (dtype == DT_F16) dw_launch_fwd_t<f16, FLIP, IT, BR>(a, grid, nthr, cbv, st);
+  else dw_launch_fwd_t<bf16, FLIP, IT, BR>(a, grid, nthr, cbv, st);
+  return check_launch(FLIP ? "dw_dgrad" : "dw_fwd");
 }
 
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
@@ -437,7 +410,7 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     int cbv;
     const dim3 g = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
     P = (int)(g.y * g.z);
-    b.tail_ink = tail_ink_on(2) && a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
+    b.tail_ink = a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
   }
   const int rc = a.in_scale ? dw_launch_fwd<false, true>(b, dtype, st) : dw_launch_fwd<false, false>(b, dtype, st);
   if (rc || !a.part || !a.tail.counters || b.tail_ink) return rc;
@@ -459,8 +432,8 @@ static void dw_block_shape(int C, int V, int& bx, int& by) {
 // stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even):
 //   row h0   <- dy row h0/2 (kh=1);  row h0+1 <- dy rows h0/2+1 (kh=0) and h0/2 (kh=2)
 //   col w0+q <- dy cols w0/2 + (q+1-kw)/2 for the kw of matching parity
-template <typename T, bool BR, bool XF = false, bool TL = false>
-__global__ __launch_bounds__(256, (BR || XF) ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
+template <typename T, bool BR, bool TL = false>
+__global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
   constexpr int V = VecW<T>::V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
   int bx, by, bz;
@@ -488,9 +461,6 @@ __global__ __launch_bounds__(256, (BR || XF) ? 2 : 3) void dw_dgrad_s2_kernel(Dw
 #pragma unroll
       for (int j = 0; j < V; ++j) acc[r][q][j] = 0.f;
   const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cvc * V;
-  const T* zb = (const T*)a.dyz + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cvc * V;
-  BwdXCoef<T> bxc;  // XF: dy is a BN's dy, the kernel forms that BN's dz on load
-  if constexpr (XF) bxc.load(a.dytab, cvc * V);
   const int hb = h0 / 2, wb = w0 / 2;
 #pragma unroll
   for (int dr = 0; dr < 2; ++dr) {       // dy rows hb, hb+1
@@ -501,13 +471,7 @@ __global__ __launch_bounds__(256, (BR || XF) ? 2 : 3) void dw_dgrad_s2_kernel(Dw
       const bool ok = active && ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
       float g[V];
       const size_t goff = (ok ? (size_t)ho * a.Wo + wo : 0) * a.C;
-      if constexpr (XF) {  // dz = bwdx_apply(dy, z) (rounded to T like a stored dz)
-        const uint4 dv = *reinterpret_cast<const uint4*>(gb + goff);
-        const uint4 zv = *reinterpret_cast<const uint4*>(zb + goff);
-        unpackv(bwdx_apply<T>(dv, zv, bxc.al, bxc.be, bxc.gz, bxc.sc, bxc.sh), g);
-      } else {
-        ldv(gb + goff, g);
-      }
+      ldv(gb + goff, g);
 #pragma unroll
       for (int j = 0; j < V; ++j) g[j] = ok ? g[j] : 0.f;
 #pragma unroll
@@ -608,14 +572,8 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
   const bool br = a.bs.part != nullptr;  // + a read of the next BN's z (dx-sized)
-  const bool xf = a.dytab != nullptr;    // + a read of this BN's z (dy-sized)
   std::optional<ProfScope> ps;  // (closed before a separate finalize launch)
-  ps.emplace(PK_DW_DGRAD, st, E * (in_el * (br ? 2 : 1) + out_el * (xf ? 2 : 1)) + 36.0 * a.C,
-             18.0 * out_el);
-  if (xf && !a.dyz) {
-    set_error("dw_dgrad: BN-backward operand transform needs z");
-    return E_INVALID;
-  }
+  ps.emplace(PK_DW_DGRAD, st, E * (in_el * (br ? 2 : 1) + out_el) + 36.0 * a.C, 18.0 * out_el);
   if (br && (!a.bs.z || !a.bs.mean || !a.bs.invstd || (a.bs.mode == 2 && (!a.bs.scale || !a.bs.shift)))) {
     set_error("dw_dgrad: inconsistent BN-backward partial arguments");
     return E_INVALID;
@@ -629,18 +587,15 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     f.N = a.N; f.H = a.Ho; f.W = a.Wo; f.C = a.C; f.Ho = a.H; f.Wo = a.W; f.stride = 1;
     f.x = a.dy; f.w = a.w; f.y = a.dx;
     f.bs = a.bs;
-    f.xz = a.dyz; f.xtab = a.dytab;
     if (fin) {
       int cbv;
       const dim3 g = dw_grid(a.N, a.H, a.W, a.C, V, 1, cbv);
       P = (int)(g.y * g.z);
-      ink = tail_ink_on(4) && a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
+      ink = a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
       f.tail = a.tail;
       f.tail_ink = ink;
     }
-    if (xf) rc = br ? dw_launch_fwd<true, false, true, true>(f, dtype, st)
-                    : dw_launch_fwd<true, false, false, true>(f, dtype, st);
-    else rc = br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
+    rc = br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
   } else {
     int bx, by;
     dw_block_shape(a.C, V, bx, by);
@@ -648,21 +603,17 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     DwBwdArgs b = a;
     if (fin) {
       P = (int)(grid.y * grid.z);
-      ink = tail_ink_on(8) && a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)grid.x);
+      ink = a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)grid.x);
       b.tail_ink = ink;
     }
-#define DWD2(T)                                                                   \
-  do {                                                                            \
-    if (xf) {                                                                     \
-      if (br) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(b);       \
-      else dw_dgrad_s2_kernel<T, false, true><<<grid, block, 0, st>>>(b);         \
-    } else {                                                                      \
-      if (br && ink) dw_dgrad_s2_kernel<T, true, false, true><<<grid, block, 0, st>>>(b); \
-      else if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b);        \
-      else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b);               \
-    }                                                                             \
+#define DWD2(T)                                                                 \
+  do {                                                                          \
+    if (br && ink) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(b); \
+    else if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b);        \
+    else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b);               \
   } while (0)
     if (dtype == DT_F32) DWD2(float);
+    else if (dtype == DT_F16) DWD2(f16);
     else DWD2(bf16);
 #undef DWD2
     rc = check_launch("dw_dgrad");
@@ -688,7 +639,7 @@ int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
 
 // ---- weight gradient: per-workgroup partial [part][9][C] --------------------------------------
 // grid: x = channel chunk, y = groups of tpb column tiles, z = N * row bands; part = (z, y).
-template <typename T, int S, bool IT, bool BX = false>
+template <typename T, int S, bool IT>
 __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, int tpb) {
   using G = DwTile<T, S>;
   extern __shared__ __attribute__((aligned(16))) uint4 s_in[];  // [IR*IC*cbv] (dw_shm)
@@ -711,16 +662,6 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[t][j] = 0.f;
-  // BX: the quad's BN-backward operand coefficients (al, be, gz, mask scale, mask shift)
-  float wx[BX ? 5 : 1][4];
-  if constexpr (BX) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 t = *reinterpret_cast<const float4*>(a.dytab + (size_t)(c0 + j) * BWDX_STRIDE);
-      wx[0][j] = t.x; wx[1][j] = t.y; wx[2][j] = t.z; wx[3][j] = t.w;
-      wx[4][j] = a.dytab[(size_t)(c0 + j) * BWDX_STRIDE + 4];
-    }
-  }
   const int tw_lo = by * tpb, tw_hi = min(tiles_w, tw_lo + tpb);
   for (int twi = tw_lo; twi < tw_hi; ++twi) {
     const int tw0 = twi * G::TW;
@@ -729,7 +670,6 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
     // dy of the thread's outputs (clamped + selected), issued with the tile loads
     float g[G::HS][G::WS][4];
     const T* gb = (const T*)a.dy + c0;
-    float zq[BX ? G::HS : 1][BX ? G::WS : 1][4];
 #pragma unroll
     for (int r = 0; r < G::HS; ++r)
 #pragma unroll
@@ -737,7 +677,6 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
         const bool ok = r < nrow && p < ncol;
         const size_t off = ok ? (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0 + p) * a.C : 0;
         quad_ld(gb + off, g[r][p]);
-        if constexpr (BX) quad_ld((const T*)a.dyz + c0 + off, zq[r][p]);
       }
 #pragma unroll
     for (int r = 0; r < G::HS; ++r)
@@ -745,14 +684,7 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwBwdArgs a, int cbv, 
       for (int p = 0; p < G::WS; ++p) {
         const bool ok = r < nrow && p < ncol;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v = g[r][p][j];
-          if constexpr (BX) {  // dz = bwdx_apply(dy, z), rounded to T like a stored dz
-            const float gv = fmaf(zq[r][p][j], wx[3][j], wx[4][j]) > 0.f ? v : 0.f;
-            v = round_as<T>(fmaf(wx[0][j], gv, fmaf(wx[2][j], zq[r][p][j], wx[1][j])));
-          }
-          g[r][p][j] = ok ? v : 0.f;
-        }
+        for (int j = 0; j < 4; ++j) g[r][p][j] = ok ? g[r][p][j] : 0.f;
       }
     __syncthreads();  // previous tile's LDS reads are done
     dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1, bx * cbv,
@@ -825,26 +757,19 @@ int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const int tpb = dw_wgrad_tpb(a.N, a.Ho, a.Wo, a.C, V, a.stride, grid, cbv);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double in_el = (double)a.N * a.C * a.H * a.W, out_el = (double)a.N * a.C * a.Ho * a.Wo;
-  const bool bx = a.dytab != nullptr;
-  ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el * (bx ? 2 : 1)), 18.0 * out_el);
-  if (bx && !a.dyz) {
-    set_error("dw_wgrad: BN-backward operand transform needs z");
-    return E_INVALID;
-  }
+  ProfScope ps(PK_DW_WGRAD, st, E * (in_el + out_el), 18.0 * out_el);
   const int nthr = cbv * 32;
-#define DWW_LAUNCH(T, S)                                                                  \
-  do {                                                                                    \
-    if (bx) {                                                                             \
-      if (a.x_scale) dw_wgrad_kernel<T, S, true, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb); \
-      else dw_wgrad_kernel<T, S, false, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);        \
-    } else {                                                                              \
-      if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);     \
-      else dw_wgrad_kernel<T, S, false><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);              \
-    }                                                                                     \
+#define DWW_LAUNCH(T, S)                                                                      \
+  do {                                                                                        \
+    if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb); \
+    else dw_wgrad_kernel<T, S, false><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);          \
   } while (0)
   if (dtype == DT_F32) {
     if (a.stride == 1) DWW_LAUNCH(float, 1);
     else DWW_LAUNCH(float, 2);
+  } else if (dtype == DT_F16) {
+    if (a.stride == 1) DWW_LAUNCH(f16, 1);
+    else DWW_LAUNCH(f16, 2);
   } else {
     if (a.stride == 1) DWW_LAUNCH(bf16, 1);
     else DWW_LAUNCH(bf16, 2);

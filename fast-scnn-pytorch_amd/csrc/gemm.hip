@@ -102,8 +102,7 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
 // 32-k chunk (k = 4lq.., 16+4lq..) form its 8 bf16 k-slots, the same permutation in A and B
 // TL: the launch finishes its BN in its last workgroups (a.tail_ink; a separate instantiation so
 // the other launches keep their register budget)
-template <typename T, int NT, bool BT, bool BS, bool AT, bool AX = false, bool X3 = false,
-          bool TL = false>
+template <typename T, int NT, bool BT, bool BS, bool AT, bool X3 = false, bool TL = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -141,7 +140,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int A_PER = G_BM * G_VROW / 256;            // 4
   constexpr int B_PER = (BN * G_VROW + 255) / 256;      // vectors per thread (non-trans)
   uint4 ra[A_PER];
-  uint4 raz[AX ? A_PER : 1];  // AX: the pre-BN z beside dy (A = bwdx_apply(dy, z))
   uint4 rb[BT ? 1 : B_PER];
   // transposed-B staging: KC rows (k) x BN cols (n) of scalars, held as raw 16-B vectors along n
   constexpr int BT_VEC = KC * BN / V;                   // vectors per chunk
@@ -161,8 +159,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       const bool ok = m < a.M && k < a.K;
       const size_t off = ok ? (size_t)m * a.lda + k : 0;
       ra[i] = *reinterpret_cast<const uint4*>(A + off);
-      if constexpr (AX)
-        raz[i] = *reinterpret_cast<const uint4*>((const T*)a.az + (ok ? (size_t)m * a.K + k : 0));
     }
     if (!BT) {
 #pragma unroll
@@ -189,14 +185,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // Tail masks (and the lazy BN+ReLU of A) are applied when a chunk is written to LDS, i.e. after
   // the current chunk's MFMAs: applying them right after issuing the loads made every wave wait
   // for the next chunk's loads before computing (no fetch/compute overlap).
-  // AX: a thread's A vectors all cover k = k0 + (tid & 7) * V, so one coefficient set per chunk
-  BwdXCoef<T> axc;
   auto store_chunk = [&](int buf, int c) {
     const int k0 = c * KC;
-    if constexpr (AX) {
-      const int kk = k0 + (tid & 7) * V;
-      axc.load(a.atab, kk < a.K ? kk : 0);
-    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int id = tid + 256 * i;
@@ -207,7 +197,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         const int kc = k < a.K ? k : 0;
         v = bnrelu_vec<T>(v, s_at + kc, s_at + G_ATMAX + kc);
       }
-      if constexpr (AX) v = bwdx_apply<T>(v, raz[i], axc.al, axc.be, axc.gz, axc.sc, axc.sh);
       sA(buf)[row * G_VPAD + vv] = zero_tail<T>(v, m < a.M ? a.K - k : 0);
     }
     if (!BT) {
@@ -502,14 +491,8 @@ static int pick_nt(int N) {
 
 int gemm_parts(int M) { return cdiv(M, G_BM); }
 
-// the streaming kernel takes every shape it supports (FSCNN_GEMM_STREAM=0: tiled kernel only)
-static bool use_stream(const GemmArgs& a, int dtype) {
-  static const bool stream_on = [] {
-    const char* e = getenv("FSCNN_GEMM_STREAM");
-    return !(e && e[0] == '0');
-  }();
-  return stream_on && gemm_stream_ok(a, dtype);
-}
+// the streaming kernel takes every shape it supports
+static bool use_stream(const GemmArgs& a, int dtype) { return gemm_stream_ok(a, dtype); }
 
 // BN partial records one gemm_nt call writes (part / bpart): one per 128-row tile, or one per
 // streaming workgroup of a column group; always <= gemm_parts(M)
@@ -517,7 +500,7 @@ int gemm_nt_parts(const GemmArgs& a, int dtype) {
   return use_stream(a, dtype) ? gemm_stream_parts(a, dtype) : gemm_parts(a.M);
 }
 
-template <typename T, bool BT, bool BS, bool AT = false, bool AX = false, bool X3 = false>
+template <typename T, bool BT, bool BS, bool AT = false, bool X3 = false>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
   constexpr int V = VecW<T>::V;
@@ -528,29 +511,28 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   const size_t red = (size_t)2 * 256 * V * 4;  // bwd-BN column reduction (2 x RG x BN floats)
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
-  if constexpr (!BT && !AX && !X3) {
+  if constexpr (!BT && !X3) {
     if (a.tail_ink) {
       switch (nt) {
-        case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
-        case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
-        case 4: gemm_nt_kernel<T, 4, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
-        case 6: gemm_nt_kernel<T, 6, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
-        default: gemm_nt_kernel<T, 8, BT, BS, AT, AX, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
+        case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
+        default: gemm_nt_kernel<T, 8, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
       }
       return;
     }
   }
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS, AT, AX, X3><<<grid, 256, shm, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
   }
 }
 
-static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool ax, bool bs,
-                         hipStream_t st);
+static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool bs, hipStream_t st);
 
 int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
@@ -570,19 +552,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   int nt = pick_nt(a.N);
   // small-M problems (the 16 K-row bottleneck3 / bottleneck2 projects): split the columns
   // further so the grid covers the 256 CUs (the A tile is then read twice, from L2)
-  static const int min_tiles = [] {  // FSCNN_GEMM_MIN_TILES: grid size below which NT halves
-    const char* e = getenv("FSCNN_GEMM_MIN_TILES");
-    return e ? atoi(e) : 256;
-  }();
+  constexpr int min_tiles = 256;  // grid size below which NT halves
   while ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < min_tiles && (nt == 8 || nt == 6 || nt == 4))
     nt /= 2;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
-  const bool ax = a.atab != nullptr;
-  if (ax && (!a.az || a.a_scale || a.b_trans || a.K % V)) {
-    set_error("gemm_nt: BN-backward A transform needs z, a plain B and K %% %d == 0", V);
-    return E_UNSUPPORTED;
-  }
   const bool at = a.a_scale != nullptr;
   if (at && (!a.a_shift || a.b_trans || a.bpart || a.K > G_ATMAX || a.K % V)) {
     set_error("gemm_nt: lazy BN on A needs a plain GEMM with K <= %d, K %% %d == 0", G_ATMAX, V);
@@ -608,15 +582,15 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   // tiled path: the BN finish runs in the kernel's last workgroups (bn_finish.hpp tail_finish)
   // when the records fit its counters; otherwise as its own fold + finalize launch below
   GemmArgs b = a;
-  b.tail_ink = !stream && a.tail.counters && tail_ink_on(1) && !a.b_trans && !ax &&
+  b.tail_ink = !stream && a.tail.counters && !a.b_trans &&
                a.tail.tsum && a.N <= TAIL_CMAX && tail_fits(gemm_parts(a.M), cdiv(a.N, 16 * nt));
   int rc;
   {
     ProfScope ps(PK_GEMM_NT, st,
-                 E * (M * K * (ax ? 2 : 1) + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
+                 E * (M * K + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
                  2.0 * M * N * K);
     rc = stream ? gemm_stream(a, dtype, st)  // finishes the BN in-kernel (last workgroup)
-                : gemm_nt_tiled(b, dtype, nt, at, ax, bs, st);
+                : gemm_nt_tiled(b, dtype, nt, at, bs, st);
   }
   if (rc || stream || !a.tail.counters || b.tail_ink) return rc;
   // tiled path: the BN finish as its own (fold + finalize) launch over the per-tile records
@@ -631,32 +605,24 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   return OK;
 }
 
-static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool ax, bool bs,
-                         hipStream_t st) {
-  if (dtype == DT_F16) {  // inference plans only: plain forward GEMMs
-    if (a.b_trans || bs || at || ax || a.part) {
-      set_error("gemm_nt: fp16 arithmetic is inference-only");
-      return E_UNSUPPORTED;
-    }
-    launch_nt<f16, false, false>(a, nt, st);
-    return check_launch("gemm_nt");
-  }
+static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool bs, hipStream_t st) {
   if (dtype == DT_F32) {
     static const bool x3 = [] {  // FSCNN_F32_SPLIT=0: exact fp32 MFMA (gemm_stream.hip)
       const char* e = getenv("FSCNN_F32_SPLIT");
       return !(e && e[0] == '0');
     }();
-    if (x3 && !a.b_trans && !ax && !bs && !at && !a.part) launch_nt<float, false, false, false, false, true>(a, nt, st);
+    if (x3 && !a.b_trans && !bs && !at && !a.part) launch_nt<float, false, false, false, true>(a, nt, st);
     else if (a.b_trans) launch_nt<float, true, false>(a, nt, st);
-    else if (ax) { if (bs) launch_nt<float, false, true, false, true>(a, nt, st);
-                   else launch_nt<float, false, false, false, true>(a, nt, st); }
     else if (bs) launch_nt<float, false, true>(a, nt, st);
     else if (at) launch_nt<float, false, false, true>(a, nt, st);
     else launch_nt<float, false, false>(a, nt, st);
+  } else if (dtype == DT_F16) {
+    if (a.b_trans) launch_nt<f16, true, false>(a, nt, st);
+    else if (bs) launch_nt<f16, false, true>(a, nt, st);
+    else if (at) launch_nt<f16, false, false, true>(a, nt, st);
+    else launch_nt<f16, false, false>(a, nt, st);
   } else {
     if (a.b_trans) launch_nt<bf16, true, false>(a, nt, st);
-    else if (ax) { if (bs) launch_nt<bf16, false, true, false, true>(a, nt, st);
-                   else launch_nt<bf16, false, false, false, true>(a, nt, st); }
     else if (bs) launch_nt<bf16, false, true>(a, nt, st);
     else if (at) launch_nt<bf16, false, false, true>(a, nt, st);
     else launch_nt<bf16, false, false>(a, nt, st);
@@ -700,12 +666,22 @@ struct TnOps<bf16> {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
   }
 };
+template <>
+struct TnOps<f16> {  // fp16 train plans (train.py:269's autocast arithmetic)
+  static constexpr int LD = TN_MC + 8;
+  static __device__ __forceinline__ void mma(const f16* a, const f16* b, f32x4& acc) {
+    h16x8 av, bv;
+    __builtin_memcpy(&av, a, 16);
+    __builtin_memcpy(&bv, b, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+  }
+};
 
 // dW[n][k] = sum_m D[m][n] X[m][k] over the block's row split.  Chunks of 64 rows are loaded as
 // 16-B vectors along n / k (coalesced), written TRANSPOSED into LDS (sDt[n][m], sXt[k][m]) so each
 // MFMA operand is one or two 16-B ds_reads; the next chunk's global loads are issued before the
 // current chunk's MFMAs.
-template <typename T, bool XT, bool DX = false>
+template <typename T, bool XT>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int LD = TnOps<T>::LD;
@@ -736,7 +712,6 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
   constexpr int VPR = TN_T / V;                 // vectors per staged row
   constexpr int PAIRS = TN_MC / 2 * VPR / 256;  // row pairs per thread (1 bf16 / 2 f32)
   uint4 rd[PAIRS][2], rx[PAIRS][2];
-  uint4 rdz[DX ? PAIRS : 1][2];  // DX: the pre-BN z beside dy (D = bwdx_apply(dy, z))
   auto load = [&](int mc) {
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
@@ -748,8 +723,6 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
         const int m = mc + 2 * rp + h;
         const bool okd = m < me && n < a.N, okx = m < me && k < a.K;
         rd[i][h] = *reinterpret_cast<const uint4*>(D + (okd ? (size_t)m * a.ldd + n : 0));
-        if constexpr (DX)
-          rdz[i][h] = *reinterpret_cast<const uint4*>((const T*)a.dzz + (okd ? (size_t)m * a.N + n : 0));
         rx[i][h] = *reinterpret_cast<const uint4*>(X + (okx ? (size_t)m * a.ldx + k : 0));
       }
     }
@@ -767,12 +740,6 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
       xsh[j] = a.x_shift[k];
     }
   }
-  // DX: likewise a thread's D vectors all cover n = n0 + (tid % VPR) * V
-  BwdXCoef<T> dxc;
-  if constexpr (DX) {
-    const int nb = n0 + (tid % VPR) * V;
-    dxc.load(a.dtab, nb < a.N ? nb : 0);
-  }
   // tail masks (and XT) right before the LDS stores, not right after issuing the loads (which
   // would make the wave wait for them before the current chunk's MFMAs)
   auto mask = [&](int mc) {
@@ -785,7 +752,6 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
       for (int h = 0; h < 2; ++h) {
         const bool okm = mc + 2 * rp + h < me;
         uint4 dv = rd[i][h];
-        if constexpr (DX) dv = bwdx_apply<T>(dv, rdz[i][h], dxc.al, dxc.be, dxc.gz, dxc.sc, dxc.sh);
         rd[i][h] = zero_tail<T>(dv, okm ? a.N - n : 0);
         uint4 xv = rx[i][h];
         if constexpr (XT) xv = bnrelu_vec<T>(xv, xsc, xsh);
@@ -868,28 +834,19 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
   dim3 grid(cdiv(a.N, TN_T) * cdiv(a.K, TN_T) * splits);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
-  const bool dx = a.dtab != nullptr;
-  ProfScope ps(PK_GEMM_TN, st, E * (M * N * (dx ? 2 : 1) + M * K) + 4.0 * N * K, 2.0 * M * N * K);
+  ProfScope ps(PK_GEMM_TN, st, E * (M * N + M * K) + 4.0 * N * K, 2.0 * M * N * K);
   const bool xt = a.x_scale != nullptr;
   if (xt && (!a.x_shift || a.K % V)) {
     set_error("gemm_tn: lazy BN on X needs x_shift and K %% %d == 0", V);
     return E_UNSUPPORTED;
   }
-  if (dx && (!a.dzz || a.N % V)) {
-    set_error("gemm_tn: BN-backward D transform needs z and N %% %d == 0", V);
-    return E_UNSUPPORTED;
-  }
-#define TN_LAUNCH(T)                                                                  \
-  do {                                                                                \
-    if (dx) {                                                                         \
-      if (xt) gemm_tn_kernel<T, true, true><<<grid, 256, 0, st>>>(a);                 \
-      else gemm_tn_kernel<T, false, true><<<grid, 256, 0, st>>>(a);                   \
-    } else {                                                                          \
-      if (xt) gemm_tn_kernel<T, true><<<grid, 256, 0, st>>>(a);                       \
-      else gemm_tn_kernel<T, false><<<grid, 256, 0, st>>>(a);                         \
-    }                                                                                 \
+#define TN_LAUNCH(T)                                        \
+  do {                                                      \
+    if (xt) gemm_tn_kernel<T, true><<<grid, 256, 0, st>>>(a); \
+    else gemm_tn_kernel<T, false><<<grid, 256, 0, st>>>(a);   \
   } while (0)
   if (dtype == DT_F32) TN_LAUNCH(float);
+  else if (dtype == DT_F16) TN_LAUNCH(f16);
   else TN_LAUNCH(bf16);
 #undef TN_LAUNCH
   return check_launch("gemm_tn");
@@ -1060,6 +1017,7 @@ int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStrea
   int rpb = cdiv(M, P);
   dim3 grid(cdiv(N, 64), P);
   if (dtype == DT_F32) colsum_kernel<float><<<grid, 256, 0, st>>>((const float*)D, M, N, ld, rpb, part);
+  else if (dtype == DT_F16) colsum_kernel<f16><<<grid, 256, 0, st>>>((const f16*)D, M, N, ld, rpb, part);
   else colsum_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)D, M, N, ld, rpb, part);
   return check_launch("colsum");
 }

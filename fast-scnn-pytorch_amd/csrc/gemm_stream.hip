@@ -672,12 +672,8 @@ static int gs_pick_nt(const GemmArgs& a, int ks) {
   if (ks > 8) return N % 64 == 0 ? 4 : (N % 48 == 0 ? 3 : 4);  // deep K: weights [<=64][K] in LDS
   if (N <= 48) return 3;
   if (N <= 64 || a.bpart) return 4;
-  static const bool st4 = [] {  // FSCNN_GS_ST4=0: statistics forms with K > 64 keep NT = 6 (A/B)
-    const char* e = getenv("FSCNN_GS_ST4");
-    return !(e && e[0] == '0');
-  }();
   // statistics forms with ks > 2 cannot hold 6 column tiles in 256 VGPRs: 4 when N allows
-  if (st4 && a.part && ks > 2 && N % 64 == 0) return 4;
+  if (a.part && ks > 2 && N % 64 == 0) return 4;
   if (N % 96 == 0) return 6;
   return a.part ? 4 : 8;
 }
@@ -698,26 +694,17 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   const int KC = dtype == DT_F32 ? 16 : 32;  // k per step
   const int ks = cdiv(a.K, KC);
   const bool sums = a.part || a.bpart;
-  if (a.b_trans || a.atab || (a.part && a.bpart)) return false;
+  if (a.b_trans || (a.part && a.bpart)) return false;
   if (a.part && a.R) return false;
   // lazy BN on A: train-forward producers only (always with statistics)
   if (a.a_scale && (!a.a_shift || !a.part || a.K > GS_KMAX)) return false;
-  if (dtype == DT_F16 && (sums || a.a_scale)) return false;
   // deep K (K = 384 / 512 / 576 16-bit: the projects and the expand dgrads) streams the chunk
   // in 2-6 register parts against a <= 64-column weight slice of up to 75 KB
-  static const bool deep_on = [] {  // FSCNN_GS_DEEP=0: deep-K shapes take the tiled kernel (A/B)
-    const char* e = getenv("FSCNN_GS_DEEP");
-    return !(e && e[0] == '0');
-  }();
   const bool deep = ks == 12 || ks == 16 || ks == 18;
-  if (deep && (dtype == DT_F32 || !deep_on)) return false;
+  if (deep && dtype == DT_F32) return false;
   // (measured: at M <= 65536 each wave streams one or two chunks and the part-by-part load chain
   //  is slower than the tiled kernel; at M = 262,144, e.g. bottleneck1.0's expand dgrad, 10% faster)
-  static const int deep_min = [] {  // FSCNN_GS_DEEP_MIN: smallest M of a deep-K stream (A/B)
-    const char* e = getenv("FSCNN_GS_DEEP_MIN");
-    return e ? atoi(e) : 131072;
-  }();
-  if (deep && a.M < deep_min) return false;
+  if (deep && a.M < 131072) return false;
   if (!(ks == 1 || ks == 2 || ks == 3 || ks == 4 || ks == 6 || ks == 8 || deep)) return false;
   const int nt = gs_pick_nt(a, ks);
   // keep the statistics forms within 256 VGPRs (measured: these would spill)
@@ -735,18 +722,8 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
 }
 
 // workgroups per column group for `slots` resident workgroups shared by `groups` column groups:
-// a multiple of 8 (XCD-aligned), and (FSCNN_GS_ROUND=1, tuning) rounded down so the grid fits
-// one residency round
-static int gs_fill_bpg(int slots, int groups) {
-  static const int mode = [] {
-    const char* e = getenv("FSCNN_GS_ROUND");
-    return e ? atoi(e) : 0;
-  }();
-  int bpg = cdiv(slots, groups);
-  if (mode == 1 && slots / groups >= 8) bpg = slots / groups / 8 * 8;
-  else bpg = (bpg + 7) / 8 * 8;
-  return bpg;
-}
+// a multiple of 8 (XCD-aligned)
+static int gs_fill_bpg(int slots, int groups) { return (cdiv(slots, groups) + 7) / 8 * 8; }
 
 // workgroups per column group = the record count of the statistics forms
 static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
@@ -757,10 +734,7 @@ static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   lds = gs_lds(a, nt, ks, KC);
   const int nchunks = cdiv(a.M, GS_MW);
   // resident workgroups: LDS-limited (160 KB / CU), at most 2 per CU (measured: 3-4 slower)
-  static const int cap = [] {  // FSCNN_GS_PER_CU: tuning override of the residency cap
-    const char* e = getenv("FSCNN_GS_PER_CU");
-    return e ? atoi(e) : 2;
-  }();
+  constexpr int cap = 2;
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
   int bpg = gs_fill_bpg(256 * per_cu, groups);
@@ -836,10 +810,6 @@ static void gs_launch(const GemmArgs& a, int dtype, hipStream_t st) {
   const int groups = cdiv(a.N, 16 * nt);
   dim3 grid((unsigned)(groups * bpg));
   const bool at = a.a_scale != nullptr;
-  if constexpr (std::is_same<T, f16>::value) {  // inference only (checked by the caller)
-    gs_launch_nt<T, false, false, false>(a, nt, ks, grid, lds, bpg, st);
-    return;
-  }
   if (a.bpart) gs_launch_nt<T, false, false, true>(a, nt, ks, grid, lds, bpg, st);
   else if (a.part && at) gs_launch_nt<T, true, true, false>(a, nt, ks, grid, lds, bpg, st);
   else if (a.part) gs_launch_nt<T, false, true, false>(a, nt, ks, grid, lds, bpg, st);
@@ -890,10 +860,6 @@ int gemm_stream(const GemmArgs& a, int dtype, hipStream_t st) {
   if (dtype == DT_F32) {
     if (!gs_x3_launch(a, st)) gs_launch<float>(a, dtype, st);
   } else if (dtype == DT_F16) {
-    if (a.part || a.bpart || a.a_scale) {
-      set_error("gemm_stream: fp16 arithmetic is inference-only");
-      return E_UNSUPPORTED;
-    }
     gs_launch<f16>(a, dtype, st);
   } else {
     gs_launch<bf16>(a, dtype, st);

@@ -287,15 +287,19 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
     const bool f32 = dtype == DT_F32;
     if (a.C == 19) {
       if (f32) ce_head_kernel<float, 19, true><<<grid, HD_T, 0, st>>>(a);
+      else if (dtype == DT_F16) ce_head_kernel<f16, 19, true><<<grid, HD_T, 0, st>>>(a);
       else ce_head_kernel<bf16, 19, true><<<grid, HD_T, 0, st>>>(a);
     } else if (a.C == 2) {
       if (f32) ce_head_kernel<float, 2, true><<<grid, HD_T, 0, st>>>(a);
+      else if (dtype == DT_F16) ce_head_kernel<f16, 2, true><<<grid, HD_T, 0, st>>>(a);
       else ce_head_kernel<bf16, 2, true><<<grid, HD_T, 0, st>>>(a);
     } else if (a.C <= 8) {
       if (f32) ce_head_kernel<float, 8, false><<<grid, HD_T, 0, st>>>(a);
+      else if (dtype == DT_F16) ce_head_kernel<f16, 8, false><<<grid, HD_T, 0, st>>>(a);
       else ce_head_kernel<bf16, 8, false><<<grid, HD_T, 0, st>>>(a);
     } else {
       if (f32) ce_head_kernel<float, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
+      else if (dtype == DT_F16) ce_head_kernel<f16, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
       else ce_head_kernel<bf16, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
     }
     int rc = check_launch("ce_head");
@@ -322,6 +326,8 @@ int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const
   const int total = (int)(M * ld);
   if (dtype == DT_F32)
     ce_head_scale_kernel<float><<<cdiv(total, 256), 256, 0, st>>>(g_raw, (float*)g, (int)M, C, ld, gout, out2);
+  else if (dtype == DT_F16)
+    ce_head_scale_kernel<f16><<<cdiv(total, 256), 256, 0, st>>>(g_raw, (f16*)g, (int)M, C, ld, gout, out2);
   else
     ce_head_scale_kernel<bf16><<<cdiv(total, 256), 256, 0, st>>>(g_raw, (bf16*)g, (int)M, C, ld, gout, out2);
   return check_launch("ce_head_scale");

@@ -417,6 +417,9 @@ int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st) {
   if (g_dtype == DT_F32 && d_dtype == DT_F32) AXB(float, float);
   else if (g_dtype == DT_BF16 && d_dtype == DT_BF16) AXB(bf16, bf16);
   else if (g_dtype == DT_BF16 && d_dtype == DT_F32) AXB(bf16, float);
+  else if (g_dtype == DT_F16 && d_dtype == DT_F32) AXB(f16, float);
+  else if (g_dtype == DT_F32 && d_dtype == DT_F16) AXB(float, f16);
+  else if (g_dtype == DT_F16 && d_dtype == DT_F16) AXB(f16, f16);
   else AXB(float, bf16);
 #undef AXB
   return check_launch("axis_bwd");
@@ -546,6 +549,7 @@ int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st) {
   long long total = (long long)a.N * a.H * a.W * a.C;
   unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) pyramid_pool_bwd_kernel<float><<<grid, 256, 0, st>>>(a);
+  else if (dtype == DT_F16) pyramid_pool_bwd_kernel<f16><<<grid, 256, 0, st>>>(a);
   else pyramid_pool_bwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
   return check_launch("pyramid_pool_bwd");
 }
@@ -644,6 +648,7 @@ int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
   }
   dim3 grid(4, a.N);
   if (dtype == DT_F32) ppm_up_bwd_kernel<float><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
+  else if (dtype == DT_F16) ppm_up_bwd_kernel<f16><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
   else ppm_up_bwd_kernel<bf16><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
   return check_launch("ppm_up_bwd");
 }

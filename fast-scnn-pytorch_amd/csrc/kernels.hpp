@@ -104,10 +104,6 @@ struct DwArgs {
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
   BnBwdPart bs{};  // stride-1 dgrad (the flipped forward): BN-backward partials of y
-  // stride-1 dgrad: x is a BN's dy whose dz is never stored; the staged value is
-  // bwdx_apply(x, xz, xtab) (common.hpp), xz that BN's pre-BN tensor (ld C), or null
-  const void* xz = nullptr;
-  const float* xtab = nullptr;
   // BN finish of the records this launch writes (part: forward statistics; bs.part: stride-1
   // dgrad partials): tail.counters set -> dw_fwd finishes the BN, in the kernel's last
   // workgroups when the records fit (tail_ink, set by the launcher) or as its own launch
@@ -125,9 +121,6 @@ struct DwBwdArgs {
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of x (wgrad) or null
   const float* x_shift = nullptr;
   BnBwdPart bs{};  // dgrad: BN-backward partials of dx (dw_dgrad_parts records)
-  // dy is a BN's dy whose dz is never stored: wgrad and dgrad read bwdx_apply(dy, dyz, dytab)
-  const void* dyz = nullptr;
-  const float* dytab = nullptr;
   BnTail tail{};     // dgrad: finish of the bs.part BN (see DwArgs::tail)
   int tail_ink = 0;
 };
@@ -159,10 +152,6 @@ struct GemmArgs {
   // z, the GEMM consumes relu(fmaf(z, a_scale[k], a_shift[k]))) or null
   const float* a_scale = nullptr;
   const float* a_shift = nullptr;
-  // BN backward applied to the A operand (dgrad of a conv whose output BN's dz is never
-  // stored): A is dy, az the saved pre-BN tensor [M][K] (ld K), atab [K][BWDX_STRIDE]
-  const void* az = nullptr;
-  const float* atab = nullptr;
   BnTail tail{};        // in-kernel finish of the BN whose records this GEMM writes
   int tail_ink = 0;     // (set by the launcher) the tiled kernel runs the finish itself (tail_finish)
 };
@@ -178,8 +167,6 @@ struct GemmTnArgs {
   int splits;
   const float* x_scale = nullptr;  // lazily applied BN+ReLU of X (see GemmArgs::a_scale) or null
   const float* x_shift = nullptr;
-  const void* dzz = nullptr;       // BN backward applied to D (see GemmArgs::az): z [M][N], or null
-  const float* dtab = nullptr;
 };
 
 struct FoldEntry {
@@ -421,7 +408,6 @@ int bn_fold(const FoldTable& t, hipStream_t st);
 int bn_finalize(const BnFinalizeArgs& a, hipStream_t st);
 // FSCNN_TAIL_INK bitmask of the producers that finish their BN in-kernel (A/B, bisection):
 // 1 tiled gemm_nt, 2 depthwise forward, 4 depthwise stride-1 dgrad, 8 stride-2 dgrad
-bool tail_ink_on(int bit);
 int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st);
 int bn_bwd_parts(long long M, int C, int dtype, int* rows_per_block);
 int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st);
@@ -456,8 +442,6 @@ int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hi
 // k-th smallest of n non-negative floats (host-synchronising radix select; hist: 2048 uint32)
 int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* counts, int dtype,
               hipStream_t st);
-int kth_smallest(const float* key, long long n, long long k, unsigned* hist, float* out,
-                 hipStream_t st);
 // the whole OHEM threshold on the device from ohem_prob's counters (no host synchronisation):
 // *thr = inf (keep all labelled) / thresh / the k-th smallest label probability; work: 2056 uint32
 int ohem_threshold_dev(const float* key, long long n, const unsigned long long* counts,

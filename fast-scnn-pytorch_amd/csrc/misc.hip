@@ -183,45 +183,7 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* key, long 
     if (s_h[j]) atomicAdd(&hist[j], s_h[j]);
 }
 
-int kth_smallest(const float* key, long long n, long long k, unsigned* hist, float* out,
-                 hipStream_t st) {
-  if (n <= 0 || k < 1 || k > n) {
-    set_error("kth_smallest: n=%lld k=%lld", n, k);
-    return E_INVALID;
-  }
-  static const int shifts[3] = {21, 10, 0}, widths[3] = {11, 11, 10};
-  unsigned prefix = 0;
-  int pshift = 32;
-  unsigned h[2048];
-  const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 2048);
-  for (int d = 0; d < 3; ++d) {
-    const unsigned bins = 1u << widths[d];
-    if (hipMemsetAsync(hist, 0, bins * sizeof(unsigned), st) != hipSuccess) return E_HIP;
-    radix_hist_kernel<<<grid, 256, 0, st>>>(key, n, shifts[d], bins, pshift, prefix, hist);
-    if (int rc = check_launch("radix_hist")) return rc;
-    if (hipMemcpyAsync(h, hist, bins * sizeof(unsigned), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-      set_error("kth_smallest: copy failed");
-      return E_HIP;
-    }
-    unsigned b = 0;
-    for (; b < bins; ++b) {
-      if ((long long)h[b] >= k) break;
-      k -= h[b];
-    }
-    if (b == bins) {
-      set_error("kth_smallest: selection ran past the histogram");
-      return E_HIP;
-    }
-    prefix = (prefix << widths[d]) | b;
-    pshift = shifts[d];
-  }
-  uint32_t bits = prefix;
-  memcpy(out, &bits, 4);
-  return OK;
-}
-
-// Device-resident form of the same selection (no host round trip, so a train step with the OHEM
+// The OHEM threshold's k-th smallest label probability as a device-side radix selection (no host round trip, so a train step with the OHEM
 // criterion never synchronises): state = {active, k, prefix, pshift}, hist 2048 bins, thr_out.
 //   init  : thr = inf if min_kept >= #labelled (reference: keep every labelled pixel), else
 //           thresh; the radix select runs only when #(prob <= thresh) < k = min(#labelled, min_kept)
@@ -524,6 +486,7 @@ int dropout(const DropArgs& a, int dtype, hipStream_t st) {
   unsigned grid = (unsigned)((total + 255) / 256);
   uint32_t thr = dropout_threshold(a.p);
   if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr);
+  else if (dtype == DT_F16) dropout_kernel<f16><<<grid, 256, 0, st>>>(a, thr);
   else dropout_kernel<bf16><<<grid, 256, 0, st>>>(a, thr);
   return check_launch("dropout");
 }

@@ -161,49 +161,6 @@ struct Alloc {
 
 int dwout(int h, int s) { return (h - 1) / s + 1; }
 
-// FSCNN_DW_BNBWD=1: the depthwise wgrad / dgrad form a dw BN's dz from (dy, z) on load instead
-// of reading a materialised dz.  Off by default: measured on MI355X (cfg3 step, 30 steps) 7.48
-// vs 7.28 ms — the two consumers' extra z reads and their higher register use cost more than
-// the apply pass they replace.  (FSCNN_DW_BNRED, the reduce folded into the dgrad, is the
-// opposite: 7.52 off vs 7.48 on with BNBWD; 7.41 vs 7.28 without.)
-static bool dw_bx_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_DW_BNBWD");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// FSCNN_DW_BNRED=0: depthwise dgrads do not fold the next BN's backward reduce (own pass)
-static bool dw_bnred_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_DW_BNRED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// Where a BN-backward dz is formed: by bn_bwd_apply (materialised), or by its consumers while
-// they stage their operand (common.hpp bwdx_apply).  Measured on MI355X (cfg3): the streaming
-// conv0 wgrad absorbs the extra z read at ~5.4 TB/s (c0's 800 MB apply, 189 us, becomes +49 us),
-// while the latency-bound pointwise wgrad / dgrad GEMMs slow down by more than the apply they
-// replace (+0.89 ms vs -0.58 ms over 15 BNs).  FSCNN_FUSE_BNBWD: 0 never, 1 (default) conv0
-// only, 2 every pointwise consumer too.
-int fuse_bnbwd_mode() {
-  static const int m = [] {
-    const char* e = getenv("FSCNN_FUSE_BNBWD");
-    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
-  }();
-  return m;
-}
-
-bool lazy_bn_enabled() {  // FSCNN_LAZY_BN=0 materialises every BN output (A/B measurements)
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_LAZY_BN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 }  // namespace
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl) {
@@ -211,8 +168,8 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     set_error("plan_build: bad input shape N=%d H=%d W=%d", N, H, W);
     return E_INVALID;
   }
-  if (dtype != DT_F32 && dtype != DT_BF16 && !(dtype == DT_F16 && !train)) {
-    set_error("plan_build: unsupported dtype %d (fp16 arithmetic is inference-only)", dtype);
+  if (dtype != DT_F32 && dtype != DT_BF16 && dtype != DT_F16) {
+    set_error("plan_build: unsupported dtype %d", dtype);
     return E_UNSUPPORTED;
   }
   pl = Plan();
@@ -320,7 +277,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.fcnt = A.get(2 * BN_COUNTERS * 4);
     pl.bcnt = pl.fcnt + BN_COUNTERS * 4;
   }
-  if (train && lazy_bn_enabled()) {
+  if (train) {
     // BN+ReLU outputs whose only consumers are GEMM / depthwise operands (and the wgrads reading
     // them again in the backward) are never stored: bn_apply is skipped and the consumers apply
     // relu(fmaf(z, scale, shift)) while staging.  Saves a read + write of each tensor per step.
@@ -483,7 +440,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.bnpart = B.get(bnp * 4);
     pl.bnpart_floats = bnp;
     pl.coef = B.get(2 * 1024 * 4);
-    pl.xtab = B.get((size_t)NTAB_SLOTS * 1024 * BWDX_STRIDE * 4);  // Exec::tab_slot
+    pl.xtab = B.get((size_t)pl.c0.C * BWDX_STRIDE * 4);  // Exec::tab_slot (conv0's BN)
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
     pl.bws_bytes = B.top;
     auto gu = [&](const std::string& n, const Unit& u) {
@@ -518,13 +475,23 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
 // reduction: every BN-backward output dz and operand table a wgrad reads has its own slot in
 // the step's arenas (no reuse, so no release events; 7.08 -> 7.00 ms/step).
 // FSCNN_SIDE_STREAM=0 keeps one stream.
+// Thread safety (DataParallel replicas, train.py:170-171, call the backward from one worker
+// thread per device; two replicas may share a device and so this plan): the stream lives on the
+// device current at its creation and is only used from calls on that device; every
+// (record, wait) pair on the shared fork / join events is one critical section, so a fork always
+// orders the side stream after the CALLER's main-stream work (a concurrent record in between
+// would hand it another thread's point in time).
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  int dev = -1;
   bool ready = false, failed = false;
+  std::mutex mu;
   bool init() {
-    if (ready || failed) return ready;
+    std::lock_guard<std::mutex> lock(mu);
+    if (ready || failed) return ready && current_device_ok();
     failed = true;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
     hipEvent_t* ev[2] = {&fork, &join};
     for (auto* e : ev)
@@ -532,6 +499,20 @@ struct SideStream {
     ready = true;
     failed = false;
     return true;
+  }
+  bool current_device_ok() const {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess && d == dev;
+  }
+  // the side stream waits for everything enqueued on `main` so far
+  bool fork_from(hipStream_t main) {
+    std::lock_guard<std::mutex> lock(mu);
+    return hipEventRecord(fork, main) == hipSuccess && hipStreamWaitEvent(s, fork, 0) == hipSuccess;
+  }
+  // `main` waits for everything enqueued on the side stream so far
+  bool join_into(hipStream_t main) {
+    std::lock_guard<std::mutex> lock(mu);
+    return hipEventRecord(join, s) == hipSuccess && hipStreamWaitEvent(main, join, 0) == hipSuccess;
   }
   ~SideStream() {
     hipEvent_t ev[2] = {fork, join};
@@ -542,23 +523,6 @@ struct SideStream {
 };
 std::shared_ptr<SideStream> make_side_stream() { return std::make_shared<SideStream>(); }
 
-// FSCNN_FFM_PAIR=0: the FFM's two BN backwards as separate reduce / apply passes (A/B)
-static bool ffm_pair_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_FFM_PAIR");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-static bool side_stream_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_SIDE_STREAM");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 namespace {
 
 #define TRY(x)                 \
@@ -568,6 +532,16 @@ namespace {
   } while (0)
 
 bool graphs_enabled();
+
+// FSCNN_SIDE_STREAM=0: every weight gradient on the caller's stream (one stream; debugging and
+// A/B; tests/test_gpu_switches.py keeps it parity-green)
+bool side_stream_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_SIDE_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // fused BN-backward partials: the dgrad GEMM producing the dy of unit `u` emits its records
 struct BTarget {
@@ -595,14 +569,9 @@ struct Exec {
   void use_side() {
     if (train && side_stream_enabled() && pl.side && pl.side->init()) side = pl.side.get();
   }
-  // the PPM branches as one fused launch each way (ppm.hip; FSCNN_PPM_FUSED=0: general kernels)
-  bool ppm_fused() const {
-    static const bool on = [] {
-      const char* e = getenv("FSCNN_PPM_FUSED");
-      return !(e && e[0] == '0');
-    }();
-    return on && train && ppm_branches_ok((int)pl.ppk[3].M, 128, dt);
-  }
+  // the PPM branches as one fused launch each way (ppm.hip) wherever the branch shapes fit it;
+  // the general per-branch GEMM / BN kernels otherwise
+  bool ppm_fused() const { return train && ppm_branches_ok((int)pl.ppk[3].M, 128, dt); }
   // a weight-gradient launch: queued for the side stream (issued by flush_side), or run now on
   // the main stream without one
   int side_launch(std::function<int(hipStream_t)> f) {
@@ -617,23 +586,13 @@ struct Exec {
     });
     return OK;
   }
-  // the wgrads of one conv (gemm_tn + bias colsum, or the depthwise wgrad) behind one fork.
-  // FSCNN_SIDE_BATCH=1: issue the queue only at the flush points (one fork per block) —
-  // measured slower (7.24 vs 7.00 ms/step): a wgrad started as soon as its dz exists fills the
-  // idle issue slots of the latency-bound dgrad chain, a delayed batch contends with the next
-  // block instead
-  int flush_conv() {
-    static const bool batch = [] {
-      const char* e = getenv("FSCNN_SIDE_BATCH");
-      return e && e[0] == '1';
-    }();
-    return batch ? OK : flush_side();
-  }
+  // the wgrads of one conv (gemm_tn + bias colsum, or the depthwise wgrad) behind one fork:
+  // issued as soon as their dz exists, they fill the idle issue slots of the latency-bound
+  // dgrad chain (queueing a whole block's behind one fork measured slower: 7.24 vs 7.00 ms/step)
   // one fork: everything enqueued on the main stream so far happens before the queued wgrads
   int flush_side() {
     if (!side || sideq.empty()) return OK;
-    if (hipEventRecord(side->fork, r.st) != hipSuccess ||
-        hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess) {
+    if (!side->fork_from(r.st)) {
       set_error("side stream: fork failed");
       return E_HIP;
     }
@@ -644,8 +603,7 @@ struct Exec {
   int join() {
     if (!side) return OK;
     TRY(flush_side());
-    if (hipEventRecord(side->join, side->s) != hipSuccess ||
-        hipStreamWaitEvent(r.st, side->join, 0) != hipSuccess) {
+    if (!side->join_into(r.st)) {
       set_error("side stream: join failed");
       return E_HIP;
     }
@@ -661,17 +619,11 @@ struct Exec {
     dz_top += bytes;
     return p;
   }
-  // BN-backward operand table of unit u (written by its dy producer's BN finish, read by the
-  // consumers of the fused dz): one slot per unit
-  const Unit* tab_units[NTAB_SLOTS] = {};
-  int ntab = 0;
-  float* tab_slot(const Unit& u) {
-    for (int i = 0; i < ntab; ++i)
-      if (tab_units[i] == &u) return (float*)Bw(pl.xtab) + (size_t)i * 1024 * BWDX_STRIDE;
-    if (ntab == NTAB_SLOTS) return nullptr;
-    tab_units[ntab] = &u;
-    return (float*)Bw(pl.xtab) + (size_t)(ntab++) * 1024 * BWDX_STRIDE;
-  }
+  // BN-backward operand table of unit u, written by its dy producer's BN finish and read by the
+  // consumer of the fused dz (bn_bwd_x): only conv0's BN has such a consumer (its streaming
+  // weight gradient), so only that unit owns a table — a fixed slot of the plan, valid across
+  // the separate per-stage backward calls; every other producer writes none
+  float* tab_slot(const Unit& u) const { return &u == &pl.c0 ? (float*)Bw(pl.xtab) : nullptr; }
 
   // the dropout seed: a device slot only when the launches may be captured into a hipGraph
   // (replays must see a new seed); otherwise a kernel argument (no set_u64 launch per step)
@@ -1131,7 +1083,7 @@ struct Exec {
   // reduce + finalize of u's BN backward unless its dy producer did both
   int bn_bwd_stats(const Unit& u, const BnL& bn, const void* dy, int lddy, const void* mask,
                    int ldmask, bool relu_z, const BnBwdTab& tb) {
-    if (u.bdone) return OK;
+    if (u.bdone.get()) return OK;
     BnBwdArgs b{};
     b.M = u.M; b.C = u.C;
     b.dy = dy; b.lddy = lddy; b.mask = mask; b.ldmask = ldmask;
@@ -1145,13 +1097,17 @@ struct Exec {
     return bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b),
                            (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb);
   }
-  // fused form (fuse_bnbwd_mode): reduce + finalize only; the consumers apply it on load
-  // streaming: the consumer is a bandwidth-efficient streaming kernel (conv0's wgrad)
+  // Where a BN-backward dz is formed: by bn_bwd_apply (materialised), or — `streaming`, only
+  // conv0's weight gradient, a bandwidth-efficient streaming consumer — by the consumer while it
+  // stages its operand (common.hpp bwdx_apply): measured on MI355X (cfg3), conv0's wgrad absorbs
+  // the extra z read at ~5.4 TB/s (c0's 800 MB apply, 189 us, becomes +49 us), while the
+  // latency-bound pointwise / depthwise consumers slowed down by more than the apply they replaced
+  // (+0.89 ms vs -0.58 ms over 15 BNs), so they read a materialised dz.
+  // fused form: reduce + finalize only; the consumer applies it on load
   int bn_bwd_x(const Unit& u, const BnL& bn, const void* dy, int lddy, bool relu_z, void* dz,
                Dz& out, bool streaming = false) {
     g_prof_tag = u.name.c_str();
-    const int mode = fuse_bnbwd_mode();
-    if (!train || mode == 0 || (mode == 1 && !streaming)) {
+    if (!train || !streaming) {
       TRY(bn_bwd(u, bn, dy, lddy, nullptr, 0, dz, relu_z));
       out = plain(dz, u.C);
       return OK;
@@ -1247,7 +1203,10 @@ struct Exec {
     GemmTnArgs t{};
     t.M = (int)M; t.N = c.cout; t.K = K; t.D = dz.p; t.ldd = dz.ld; t.X = X.p; t.ldx = X.ld;
     t.x_scale = X.sc; t.x_shift = X.sh;
-    t.dzz = dz.z; t.dtab = dz.tab;
+    if (dz.tab) {  // (bn_bwd_x forms a fused dz for conv0's wgrad only)
+      set_error("pw_bwd: a fused BN-backward operand is not supported here");
+      return E_UNSUPPORTED;
+    }
     int S = gemm_tn_splits((int)M, c.cout, K);
     t.slab = slab_alloc((size_t)S * c.cout * K);
     if (!t.slab) return slab_oom();
@@ -1257,10 +1216,6 @@ struct Exec {
     if (c.b >= 0) {
       float* part = slab_alloc((size_t)colsum_parts((int)M) * c.cout);
       if (!part) return slab_oom();
-      if (dz.tab) {
-        set_error("pw_bwd: bias gradient of a fused BN-backward operand");
-        return E_UNSUPPORTED;
-      }
       const void* dp = dz.p;
       const int Mi = (int)M, co = c.cout, ld = dz.ld;
       TRY(side_launch([dp, Mi, co, ld, part, dtc](hipStream_t s) {
@@ -1268,17 +1223,16 @@ struct Exec {
       }));
       TRY(defer_reduce(part, colsum_parts((int)M), c.cout, G(c.b), 0));
     }
-    TRY(flush_conv());
+    TRY(flush_side());
     if (!dX) return OK;
     GemmArgs g{};
     g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
-    g.az = dz.z; g.atab = dz.tab;
     g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
     g.R = R; g.ldr = ldr;
     g.C = dX; g.ldc = lddx;
     if (bt.u && train) set_btarget(g, bt);
     TRY(gemm_nt(g, dt, r.st));
-    if (bt.u && train) bt.u->bdone = true;
+    if (bt.u && train) bt.u->bdone.set();
     return OK;
   }
   static BTarget relu_target(const Unit& u, const BnL& bn) {
@@ -1300,7 +1254,10 @@ struct Exec {
     DwBwdArgs d{};
     d.N = pl.N; d.H = H; d.W = Wd; d.C = C; d.Ho = Ho; d.Wo = Wo; d.stride = stride;
     d.x = X.p; d.x_scale = X.sc; d.x_shift = X.sh; d.dy = dz.p; d.w = P(c.w); d.dx = dX;
-    d.dyz = dz.z; d.dytab = dz.tab;
+    if (dz.tab) {
+      set_error("dw_bwd: a fused BN-backward operand is not supported here");
+      return E_UNSUPPORTED;
+    }
     const int S = dw_wgrad_parts(pl.N, Ho, Wo, C, dt, stride);
     d.slab = slab_alloc((size_t)S * 9 * C);
     if (!d.slab) return slab_oom();
@@ -1308,10 +1265,10 @@ struct Exec {
       const DwBwdArgs dw = d;
       const int dtc = dt;
       TRY(side_launch([dw, dtc](hipStream_t s) { return dw_wgrad(dw, dtc, s); }));
-      TRY(flush_conv());
+      TRY(flush_side());
     }
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
-    const bool br = bt.u && train && dw_bnred_enabled();
+    const bool br = bt.u && train;
     if (br) {
       const Unit& u = *bt.u;
       d.bs.part = (float*)Bw(pl.bnpart);
@@ -1330,7 +1287,7 @@ struct Exec {
       d.tail.tab = bwd_tab(u, bt.mode == 2, tab_slot(u));
     }
     TRY(dw_dgrad(d, dt, r.st));
-    if (br) bt.u->bdone = true;
+    if (br) bt.u->bdone.set();
     return OK;
   }
 
@@ -1373,14 +1330,14 @@ struct Exec {
     TRY(bn_bwd_x(pl.c2pw, net.cls2.bpw, Bw(pl.c2pw.ga), 128, true, dz_buf(pl.c2pw), d));
     TRY(pw_bwd(net.cls2.pw, pl.c2pw.M, d, act(pl.c2dw), Bw(pl.c2dw.ga), 128, nullptr, 0,
                relu_target(pl.c2dw, net.cls2.bdw)));
-    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz_buf(pl.c2dw), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.c2dw, net.cls2.bdw, Bw(pl.c2dw.ga), 128, true, dz_buf(pl.c2dw), d));
     TRY(dw_bwd(net.cls2.dw, 128, d, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.c1pw.ga),
                relu_target(pl.c1pw, net.cls1.bpw)));
     TRY(flush_side());
     TRY(bn_bwd_x(pl.c1pw, net.cls1.bpw, Bw(pl.c1pw.ga), 128, true, dz_buf(pl.c1pw), d));
     TRY(pw_bwd(net.cls1.pw, pl.c1pw.M, d, act(pl.c1dw), Bw(pl.c1dw.ga), 128, nullptr, 0,
                relu_target(pl.c1dw, net.cls1.bdw)));
-    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz_buf(pl.c1dw), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.c1dw, net.cls1.bdw, Bw(pl.c1dw.ga), 128, true, dz_buf(pl.c1dw), d));
     TRY(dw_bwd(net.cls1.dw, 128, d, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1, Bw(pl.g_f)));
     TRY(flush_side());
     // FFM: f = relu(BN_l(z_l) + BN_h(z_h))
@@ -1388,19 +1345,15 @@ struct Exec {
     //  the FFM dwconv BN; the high branch only needs g_f and writes l2pw.ga)
     void* zl = dz_buf(pl.flow);
     void* zh = dz_buf(pl.fhigh);
-    const bool pair = ffm_pair_enabled();
-    if (pair)  // both branch BNs in one reduce and one apply (same dy g_f and mask f)
-      TRY(bn_bwd_pair(pl.flow, net.ffm_blow, pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f),
-                      128, zl, zh));
-    else
-      TRY(bn_bwd(pl.flow, net.ffm_blow, Bw(pl.g_f), 128, W(pl.f), 128, zl));
+    // both branch BNs in one reduce and one apply (same dy g_f and mask f)
+    TRY(bn_bwd_pair(pl.flow, net.ffm_blow, pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128,
+                    zl, zh));
     TRY(pw_bwd(net.ffm_low, pl.flow.M, plain(zl, 128), act(pl.fdw), Bw(pl.fdw.ga), 128, nullptr, 0,
                relu_target(pl.fdw, net.ffm_bdw)));
-    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz_buf(pl.fdw), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.fdw, net.ffm_bdw, Bw(pl.fdw.ga), 128, true, dz_buf(pl.fdw), d));
     TRY(dw_bwd(net.ffm_dw, 128, d, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1,
                Bw(pl.g_up)));
     TRY(flush_side());
-    if (!pair) TRY(bn_bwd(pl.fhigh, net.ffm_bhigh, Bw(pl.g_f), 128, W(pl.f), 128, zh));
     TRY(pw_bwd(net.ffm_high, pl.fhigh.M, plain(zh, 128), act(pl.l2pw), Bw(pl.l2pw.ga), 64));
     TRY(flush_side());
     if (net.aux) TRY(backward_aux());
@@ -1487,7 +1440,7 @@ struct Exec {
     Dz d;
     TRY(bn_bwd_x(up, l.bp, Bw(up.ga), up.ga_ld, false, dz_buf(up), d));
     TRY(pw_bwd(l.p, up.M, d, act(ud), Bw(ud.ga), e, nullptr, 0, relu_target(ud, l.bd)));
-    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz_buf(ud), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(ud, l.bd, Bw(ud.ga), e, true, dz_buf(ud), d));
     TRY(dw_bwd(l.d, e, d, act(ue), Hin, Win, Ho, Wo, l.stride, Bw(ue.ga), relu_target(ue, l.be)));
     TRY(bn_bwd_x(ue, l.be, Bw(ue.ga), e, true, dz_buf(ue), d));
     // grad wrt x: dgrad (+ identity path of the shortcut, or + FFM's contribution for hr)
@@ -1505,14 +1458,14 @@ struct Exec {
     TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz_buf(pl.l2pw), d));
     TRY(pw_bwd(net.ltd2.pw, pl.l2pw.M, d, act(pl.l2dw), Bw(pl.l2dw.ga), 48, nullptr, 0,
                relu_target(pl.l2dw, net.ltd2.bdw)));
-    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz_buf(pl.l2dw), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.l2dw, net.ltd2.bdw, Bw(pl.l2dw.ga), 48, true, dz_buf(pl.l2dw), d));
     TRY(dw_bwd(net.ltd2.dw, 48, d, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2, Bw(pl.l1pw.ga),
                relu_target(pl.l1pw, net.ltd1.bpw)));
     TRY(flush_side());
     TRY(bn_bwd_x(pl.l1pw, net.ltd1.bpw, Bw(pl.l1pw.ga), 48, true, dz_buf(pl.l1pw), d));
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
-    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(pl.l1dw), d, dw_bx_enabled()));
+    TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(pl.l1dw), d));
     TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
                relu_target(pl.c0, net.b0)));
     TRY(flush_side());

@@ -3,6 +3,7 @@
 // It never allocates device memory: the caller passes the parameter / buffer / gradient arenas
 // and workspaces (see include/fastscnn.h).
 #pragma once
+#include <atomic>
 #include <string>
 #include <memory>
 #include <vector>
@@ -67,7 +68,19 @@ struct Unit {
   int nparts = 0;           // record slots (gemm_parts(M) for GEMM producers: an upper bound)
   // the dgrad producing this unit's dy (GEMM or depthwise) also reduces and finishes its BN
   // backward (set when that dgrad is issued; fixed per plan): the BN backward then only applies
-  mutable bool bdone = false;
+  // (an atomic: concurrent backward calls of DataParallel replicas set it; always to true)
+  struct Flag {
+    std::atomic<bool> v{false};
+    Flag() = default;
+    Flag(const Flag& o) : v(o.v.load(std::memory_order_relaxed)) {}
+    Flag& operator=(const Flag& o) {
+      v.store(o.v.load(std::memory_order_relaxed), std::memory_order_relaxed);
+      return *this;
+    }
+    bool get() const { return v.load(std::memory_order_relaxed); }
+    void set() const { const_cast<std::atomic<bool>&>(v).store(true, std::memory_order_relaxed); }
+  };
+  Flag bdone;
   size_t mean = 0, invstd = 0, scale = 0, shift = 0;  // fp32 [C]
   size_t ga = 0;            // backward: grad wrt a (bwd workspace)
   int ga_ld = 0;
@@ -79,7 +92,6 @@ struct Unit {
 
 struct GraphCache;
 struct SideStream;
-constexpr int NTAB_SLOTS = 64;  // BN-backward operand tables per backward call (Exec::tab_slot)
 
 struct Plan {
   const Net* net = nullptr;

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
 
 static bool ppm_check(int nb, int K, int C, int maxM, int dtype) {
   if (nb < 1 || nb > 4 || C != PPM_C || K < 8 || K % 8 || K > 1024 || maxM < 1 || maxM > 512 ||
-      ppm_branch_lds(maxM, K) > 150 * 1024 || (dtype != DT_F32 && dtype != DT_BF16)) {
+      ppm_branch_lds(maxM, K) > 150 * 1024 || dtype < DT_F32 || dtype > DT_F16) {
     set_error("ppm_branches: nb=%d K=%d C=%d M=%d dtype=%d not supported", nb, K, C, maxM, dtype);
     return false;
   }
@@ -218,7 +218,7 @@ static bool ppm_check(int nb, int K, int C, int maxM, int dtype) {
 bool ppm_branches_ok(int maxM, int K, int dtype) {
   // maxM <= 16 slices x 32 rows: the backward keeps a slice's rows in registers
   return maxM <= 512 && ppm_branch_lds(maxM, K) <= 150 * 1024 && K >= 8 && K % 8 == 0 && K <= 1024 &&
-         (dtype == DT_F32 || dtype == DT_BF16);
+         dtype >= DT_F32 && dtype <= DT_F16;
 }
 
 int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st) {
@@ -231,6 +231,7 @@ int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st) {
   ProfScope ps(PK_PPM, st, rows * (a.K + 2.0 * PPM_C) * (dtype == DT_F32 ? 4 : 2),
                2.0 * a.K * PPM_C * rows);
   if (dtype == DT_F32) ppm_fwd_kernel<float><<<a.nb, PPM_T, lds, st>>>(a);
+  else if (dtype == DT_F16) ppm_fwd_kernel<f16><<<a.nb, PPM_T, lds, st>>>(a);
   else ppm_fwd_kernel<bf16><<<a.nb, PPM_T, lds, st>>>(a);
   return check_launch("ppm_branches_fwd");
 }
@@ -249,6 +250,7 @@ int ppm_branches_bwd(const PpmBwdArgs& a, int dtype, hipStream_t st) {
   for (int i = 0; i < a.nb; ++i) b.wg0[i + 1] = b.wg0[i] + std::max(1, std::min(16, a.b[i].M / 32));
   const int nwg = b.wg0[a.nb];
   if (dtype == DT_F32) ppm_bwd_kernel<float><<<nwg, PPM_T, lds, st>>>(b);
+  else if (dtype == DT_F16) ppm_bwd_kernel<f16><<<nwg, PPM_T, lds, st>>>(b);
   else ppm_bwd_kernel<bf16><<<nwg, PPM_T, lds, st>>>(b);
   return check_launch("ppm_branches_bwd");
 }

@@ -17,6 +17,7 @@ single buffer.  The submodules are parameter containers only: the whole network 
 native forward and one staged native backward.  CPU tensors raise — there is no fallback.
 """
 import os
+import threading
 
 import torch
 import torch.nn as nn
@@ -169,6 +170,7 @@ class _Native:
             _lib.check(lib.fscnn_net_stage_range(h, s, _lib.ctypes.byref(b), _lib.ctypes.byref(e)))
             self.stage_ranges.append((b.value, e.value))
         self.plans = {}
+        self._lock = threading.Lock()
 
     def _info(self, fn, i):
         name, off, numel = _lib.c_char_p(), _lib.c_ll(), _lib.c_ll()
@@ -176,10 +178,18 @@ class _Native:
                                          _lib.ctypes.byref(numel)), fn)
         return name.value.decode(), off.value, numel.value
 
-    def plan(self, N, H, W, dtype_code, train):
-        key = (N, H, W, dtype_code, int(train))
+    def plan(self, N, H, W, dtype_code, train, device=None):
+        """Plan of one (N, H, W, dtype, mode) on one device.  Plans are per device (each owns its
+        side stream and graph cache) and created under a lock: DataParallel's worker threads
+        (train.py:170-171 -> parallel_apply) reach here concurrently."""
+        key = (None if device is None else device.index, N, H, W, dtype_code, int(train))
         p = self.plans.get(key)
-        if p is None:
+        if p is not None:
+            return p
+        with self._lock:
+            p = self.plans.get(key)
+            if p is not None:
+                return p
             h = _lib.c_vp()
             _lib.check(self.lib.fscnn_plan_create(self.h, N, H, W, dtype_code, int(train),
                                                   _lib.ctypes.byref(h)), "fscnn_plan_create")
@@ -199,13 +209,33 @@ class _Native:
             pass
 
 
+class _Shared:
+    """State a FastSCNN shares with its DataParallel replicas: ``replicate()``
+    (torch/nn/parallel/replicate.py, driven by train.py:170-171) shallow-copies the module's
+    ``__dict__``, so every replica sees this same object — one native net handle and one plan
+    cache for the whole wrapper.  A deep copy / pickle of the model starts a fresh one."""
+
+    def __init__(self):
+        self.native = None
+        self.lock = threading.Lock()
+
+    def __deepcopy__(self, memo):
+        return _Shared()
+
+    def __getstate__(self):
+        return {}
+
+    def __setstate__(self, state):
+        self.__init__()
+
+
 class _FastSCNNFunction(torch.autograd.Function):
     """Whole-network forward / staged backward; grads are views of one flat arena."""
 
     @staticmethod
-    def forward(ctx, x, model, *params):
-        outs, ws, seed, dt, xc = model._run_forward(x, train=True)
-        ctx.model = model
+    def forward(ctx, x, model, ar, *params):
+        outs, ws, seed, dt, xc = model._run_forward(x, train=True, ar=ar)
+        ctx.model, ctx.ar = model, ar
         ctx.ws, ctx.seed, ctx.dt = ws, seed, dt
         # the converted dense NCHW fp32/bf16 copy the forward read, not the caller's tensor: the
         # conv0 weight gradient re-reads it as dense NCHW (channels_last / fp16 / expanded inputs)
@@ -216,18 +246,18 @@ class _FastSCNNFunction(torch.autograd.Function):
     def backward(ctx, *gouts):
         (x,) = ctx.saved_tensors
         gaux = gouts[1] if len(gouts) > 1 else None
-        grads = ctx.model._run_backward(gouts[0], x, ctx.ws, ctx.seed, ctx.dt, gaux=gaux)
-        ctx.ws = None
-        return (None, None) + tuple(grads)
+        grads = ctx.model._run_backward(gouts[0], x, ctx.ws, ctx.seed, ctx.dt, ctx.ar, gaux=gaux)
+        ctx.ws = ctx.ar = None
+        return (None, None, None) + tuple(grads)
 
 
 class _FastSCNNLossFunction(torch.autograd.Function):
     """Fused train step head: loss = CE(upsample(logits_lowres), target) at low resolution."""
 
     @staticmethod
-    def forward(ctx, x, target, ignore_index, model, *params):
-        loss2, ws, seed, dt, xc = model._run_forward_loss(x, target, ignore_index)
-        ctx.model = model
+    def forward(ctx, x, target, ignore_index, model, ar, *params):
+        loss2, ws, seed, dt, xc = model._run_forward_loss(x, target, ignore_index, ar)
+        ctx.model, ctx.ar = model, ar
         ctx.ws, ctx.seed, ctx.dt, ctx.loss2 = ws, seed, dt, loss2
         ctx.save_for_backward(xc)
         return loss2[0].clone()
@@ -236,10 +266,10 @@ class _FastSCNNLossFunction(torch.autograd.Function):
     def backward(ctx, gloss):
         (x,) = ctx.saved_tensors
         g = gloss.to(torch.float32).reshape(1).contiguous()
-        grads = ctx.model._run_backward(None, x, ctx.ws, ctx.seed, ctx.dt, gloss=g,
+        grads = ctx.model._run_backward(None, x, ctx.ws, ctx.seed, ctx.dt, ctx.ar, gloss=g,
                                         loss2=ctx.loss2)
-        ctx.ws = None
-        return (None, None, None, None) + tuple(grads)
+        ctx.ws = ctx.ar = None
+        return (None, None, None, None, None) + tuple(grads)
 
 
 class FastSCNN(nn.Module):
@@ -257,19 +287,39 @@ class FastSCNN(nn.Module):
                                           nn.BatchNorm2d(32), nn.ReLU(True), nn.Dropout(0.1),
                                           nn.Conv2d(32, num_classes, 1))
         self.num_classes = num_classes
-        object.__setattr__(self, "_native", None)
+        object.__setattr__(self, "_shared", _Shared())
         object.__setattr__(self, "_arena", None)
         object.__setattr__(self, "grad_stage_hook", None)
 
     # ---- arenas ----------------------------------------------------------------------------
     def native(self):
-        if self._native is None:
-            object.__setattr__(self, "_native", _Native(self.num_classes, self.aux))
-            nat = self._native
-            names = [n for n, _ in self.named_parameters()]
-            if names != [p[0] for p in nat.params]:
-                raise RuntimeError("FastSCNN: parameter table mismatch with the native executor")
-        return self._native
+        sh = self._shared
+        if sh.native is None:
+            with sh.lock:
+                if sh.native is None:
+                    nat = _Native(self.num_classes, self.aux)
+                    names = [n for n, _ in self._named_params()]
+                    if names != [p[0] for p in nat.params]:
+                        raise RuntimeError("FastSCNN: parameter table mismatch with the native "
+                                           "executor")
+                    sh.native = nat
+        return sh.native
+
+    def _is_dp_replica(self):
+        return bool(getattr(self, "_is_replica", False))
+
+    def _named_params(self):
+        """named_parameters() of the module, or of a DataParallel replica: ``replicate()`` keeps
+        a replica's (non-leaf, broadcast) parameter tensors as plain attributes and lists them in
+        each submodule's ``_former_parameters`` in ``_parameters`` order."""
+        if not self._is_dp_replica():
+            return list(self.named_parameters())
+        out = []
+        for mname, m in self.named_modules():
+            for k, t in getattr(m, "_former_parameters", {}).items():
+                if t is not None:
+                    out.append((mname + "." + k if mname else k, t))
+        return out
 
     def _apply(self, fn, recurse=True):
         r = super()._apply(fn, recurse)
@@ -318,6 +368,59 @@ class FastSCNN(nn.Module):
             a = self._pack_arena()
         return a
 
+    def _replica_arena(self, dev):
+        """Arenas of a DataParallel replica (train.py:170-171) on ``dev``.
+
+        Replica 0 aliases the module's own tensors (``comm.broadcast_coalesced`` returns the
+        source device's inputs), so its parameters and buffers already are views of the packed
+        arenas.  Any other replica holds broadcast copies: they are packed into fresh arenas on
+        its device for this call (one multi-tensor copy each), and the running statistics the
+        train forward updates are written back into the replica's own buffers, as aten's
+        batch_norm would have updated them.  ``params`` are always the replica's tensors, so the
+        autograd Function's gradients flow back through ``Broadcast`` (reduce-add to cuda:0)."""
+        nat = self.native()
+        params = [t for _, t in self._named_params()]
+        if len(params) != len(nat.params):
+            raise RuntimeError("FastSCNN replica: %d parameters, executor expects %d"
+                               % (len(params), len(nat.params)))
+        mods = dict(self.named_modules())
+        bufs = []
+        for name, off, numel in nat.buffers:
+            mname, bname = name.rsplit(".", 1)
+            bufs.append((mods[mname]._buffers[bname], off, numel, bname == "num_batches_tracked"))
+        m = self._arena  # the module's arenas, as they were when replicate() copied __dict__
+        if m is not None and m["P"].device == dev:
+            P, R, NBT = m["P"], m["R"], m["NBT"]
+            pb, rb, nb = P.data_ptr(), R.data_ptr(), NBT.data_ptr()
+            alias = all(t.data_ptr() == pb + 4 * off
+                        for t, (_, off, _n) in zip((params[0], params[-1]),
+                                                   (nat.params[0], nat.params[-1])))
+            alias = alias and all(t.data_ptr() == (nb + 8 * off if isn else rb + 4 * off)
+                                  for t, off, _n, isn in (bufs[0], bufs[-1], bufs[1]))
+            if alias:
+                return {"P": P, "R": R, "NBT": NBT, "params": params, "writeback": None}
+        with torch.no_grad():
+            P = torch.zeros(nat.p_total, dtype=torch.float32, device=dev)
+            R = torch.zeros(nat.r_total, dtype=torch.float32, device=dev)
+            NBT = torch.zeros(nat.n_bn, dtype=torch.int64, device=dev)
+            pv = [P[off:off + numel] for _, off, numel in nat.params]
+            torch._foreach_copy_(pv, [p.detach().reshape(-1) for p in params])
+            rv = [NBT[off] if isn else R[off:off + numel] for _, off, numel, isn in bufs]
+            bt = [b if isn else b.reshape(-1) for b, _o, _n, isn in bufs]
+            torch._foreach_copy_(rv, bt)
+        return {"P": P, "R": R, "NBT": NBT, "params": params, "writeback": (bt, rv)}
+
+    def _exec_arena(self, dev):
+        return self._replica_arena(dev) if self._is_dp_replica() else self.arena()
+
+    @staticmethod
+    def _writeback(ar):
+        """Running statistics of a replica's packed copy -> the replica's own buffers."""
+        wb = ar.get("writeback")
+        if wb is not None:
+            with torch.no_grad():
+                torch._foreach_copy_(wb[0], wb[1])
+
     def load_state_dict(self, state_dict, strict=True, assign=False):
         r = super().load_state_dict(state_dict, strict=strict, assign=assign)
         if assign:
@@ -326,19 +429,22 @@ class FastSCNN(nn.Module):
 
     # ---- execution ----------------------------------------------------------------------------
     def _compute_dtype(self, x, train):
-        """Arithmetic of the call: fp32 for fp32 input; fp16 for fp16 input at inference (the
-        cfg5 TuSimple fp16 inference: fp16 images in, fp16 MFMA arithmetic with fp32
-        accumulation, fp16 logits out); bf16 (16-bit activations, fp32 master weights /
-        statistics / accumulation) for bf16 input, for fp16 input in training, and under
-        autocast (train.py:269's AMP)."""
-        if x.dtype == torch.float16 and not train:
-            return torch.float16
-        if x.dtype in (torch.bfloat16, torch.float16):
-            return torch.bfloat16
+        """Arithmetic of the call, as the reference's convolutions would run it.
+
+        * Under ``torch.autocast("cuda")`` (train.py:269's ``torch.cuda.amp.autocast()``, fp16 by
+          default; test_specific_images.py:121's inference): autocast's dtype — fp16 unless the
+          caller asked for bf16.  16-bit activations and logits, fp32 master weights, BN
+          statistics, accumulation and weight gradients.
+        * Otherwise the input's dtype: fp32 (cfg1 / cfg2), bf16 (cfg3's arithmetic), fp16
+          (cfg5's fp16 images).
+        ``train`` does not change the choice: every dtype has forward and backward kernels."""
         if torch.is_autocast_enabled("cuda"):
-            return torch.bfloat16
-        if x.dtype == torch.float32:
-            return torch.float32
+            dt = torch.get_autocast_dtype("cuda")
+            if dt in (torch.float16, torch.bfloat16):
+                return dt
+            raise RuntimeError("FastSCNN: unsupported autocast dtype %s" % (dt,))
+        if x.dtype in (torch.float32, torch.bfloat16, torch.float16):
+            return x.dtype
         raise RuntimeError("FastSCNN: unsupported input dtype %s" % (x.dtype,))
 
     @staticmethod
@@ -357,14 +463,15 @@ class FastSCNN(nn.Module):
     def _dropout_p(self):
         return float(self.classifier.conv[0].p)
 
-    def _run_forward(self, x, train):
+    def _run_forward(self, x, train, ar=None):
         if x.dim() != 4 or x.shape[1] != 3:
             raise RuntimeError("FastSCNN: expected input [N, 3, H, W], got %s" % (tuple(x.shape),))
         if not x.is_cuda:
             raise RuntimeError("FastSCNN: the HIP path needs a ROCm device tensor (got %s); "
                                "move the model and input to 'cuda'" % (x.device,))
         nat = self.native()
-        ar = self.arena()
+        if ar is None:
+            ar = self._exec_arena(x.device)
         if ar["P"].device != x.device:
             raise RuntimeError("FastSCNN: input on %s but parameters on %s"
                                % (x.device, ar["P"].device))
@@ -377,9 +484,9 @@ class FastSCNN(nn.Module):
             # the reference raises from the PPM 1x1 BatchNorm in train mode (SURVEY §0 trap 5)
             raise ValueError("Expected more than 1 value per channel when training, got input "
                              "size torch.Size([1, 32, 1, 1])")
-        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), train)
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), train, x.device)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
-        out_dt = torch.float16 if x.dtype == torch.float16 else dt
+        out_dt = dt  # (autocast: the reference's final F.interpolate returns fp16 logits)
         out = torch.empty((N, self.num_classes, H, W), dtype=out_dt, device=x.device)
         aux_out = torch.empty_like(out) if self.aux else None
         p = self._dropout_p() if train else 0.0
@@ -396,6 +503,8 @@ class FastSCNN(nn.Module):
         else:
             _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(out),
                       _lib.dtype_code(out_dt), *rest[1:])
+        if train:
+            self._writeback(ar)
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return ((out, aux_out) if self.aux else (out,)), ws, seed, dt, x
@@ -413,13 +522,13 @@ class FastSCNN(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("FastSCNN.predict: the HIP path needs a ROCm device tensor")
         nat = self.native()
-        ar = self.arena()
+        ar = self._exec_arena(x.device)
         N, _, H, W = x.shape
         if H < 32 or W < 32:
             raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
         dt = self._compute_dtype(x, False)
         x = self._input(x)
-        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), False)
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), False, x.device)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         labels = torch.empty((N, H, W), dtype=dtype, device=x.device)
         _lib.call("fscnn_predict", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(labels),
@@ -445,7 +554,7 @@ class FastSCNN(nn.Module):
         flat = base[off.value:off.value + n * esz].view(dt)
         return flat.as_strided((rows.value, cols.value), (ld.value, 1))
 
-    def _run_forward_loss(self, x, target, ignore_index):
+    def _run_forward_loss(self, x, target, ignore_index, ar):
         if self.aux:
             raise RuntimeError("forward_loss: the fused loss head covers the main output only; "
                                "with aux=True use MixSoftmaxCrossEntropyLoss(aux=True)"
@@ -453,7 +562,6 @@ class FastSCNN(nn.Module):
         if not x.is_cuda or not target.is_cuda:
             raise RuntimeError("FastSCNN.forward_loss: the HIP path needs ROCm device tensors")
         nat = self.native()
-        ar = self.arena()
         N, _, H, W = x.shape
         if tuple(target.shape) != (N, H, W):
             raise RuntimeError("forward_loss: target %s does not match input %s"
@@ -467,7 +575,7 @@ class FastSCNN(nn.Module):
         from . import loss as _loss
         if _loss.CHECK_TARGETS:
             _loss.check_targets(target, self.num_classes, ignore_index)
-        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), True)
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), True, x.device)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         loss2 = torch.empty(2, dtype=torch.float32, device=x.device)
         p = self._dropout_p()
@@ -479,6 +587,7 @@ class FastSCNN(nn.Module):
                   int(ignore_index), _lib.ptr(loss2), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]),
                   _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p),
                   _lib.c_float(self._momentum()), _lib.stream_ptr(x.device))
+        self._writeback(ar)
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return loss2, ws, seed, dt, x
@@ -490,14 +599,15 @@ class FastSCNN(nn.Module):
         as the unfused path (tests/test_gpu_model.py); requires train mode."""
         if not self.training:
             raise RuntimeError("forward_loss is the training step; call model.train() first")
-        ar = self.arena()
-        return _FastSCNNLossFunction.apply(x, target, ignore_index, self, *ar["params"])
+        if not x.is_cuda:
+            raise RuntimeError("FastSCNN.forward_loss: the HIP path needs ROCm device tensors")
+        ar = self._exec_arena(x.device)
+        return _FastSCNNLossFunction.apply(x, target, ignore_index, self, ar, *ar["params"])
 
-    def _run_backward(self, gout, x, ws, seed, dt, gloss=None, loss2=None, gaux=None):
+    def _run_backward(self, gout, x, ws, seed, dt, ar, gloss=None, loss2=None, gaux=None):
         nat = self.native()
-        ar = self.arena()
         N, _, H, W = x.shape
-        plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), True)
+        plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), True, x.device)
         if gout is not None:
             gout = gout.to(dt).contiguous()
         if self.aux and gloss is None:
@@ -534,10 +644,10 @@ class FastSCNN(nn.Module):
         train = self.training
         needs_grad = train and torch.is_grad_enabled()
         if needs_grad:
-            ar = self.arena() if x.is_cuda else None
-            if ar is None:
+            if not x.is_cuda:
                 self._run_forward(x, train)  # raises the device error
-            out = _FastSCNNFunction.apply(x, self, *ar["params"])
+            ar = self._exec_arena(x.device)
+            out = _FastSCNNFunction.apply(x, self, ar, *ar["params"])
             return tuple(out) if self.aux else (out,)
         return self._run_forward(x, train)[0]
 

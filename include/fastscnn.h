@@ -6,7 +6,13 @@
  * memory: the caller passes arenas and workspaces.  Launches go to the caller's hipStream_t
  * (passed as void*), so calls are graph-capturable and overlap with RCCL on other streams.
  *
- * dtype codes: 0 = fp32, 1 = bf16.  Activations are NHWC; images and logits are NCHW.
+ * dtype codes: 0 = fp32, 1 = bf16, 2 = fp16 (a plan's arithmetic, and image / logit dtypes).
+ * Activations are NHWC; images and logits are NCHW.
+ *
+ * Thread safety: every entry point may be called concurrently from several host threads (the
+ * reference's torch.nn.DataParallel, train.py:170-171, runs one replica per device from its own
+ * worker thread); a plan may be shared by calls on the device it was first used on.  The launch
+ * profiler (fscnn_prof_*) is process-global and meant for single-threaded measurement.
  *
  * Reference interfaces replaced (Shinokawa/Fast-SCNN-pytorch):
  *   fscnn_net_* / fscnn_plan_* / fscnn_forward   FastSCNN.__init__ / forward
@@ -105,8 +111,6 @@ int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, 
  * train.py:190-191):
  * fscnn_ohem_prob: prob[i] = softmax probability of the label of pixel i (2.0 for ignored
  *   pixels); counts[0] += #labelled, counts[1] += #(prob <= thresh)  (device uint64 x 2).
- * fscnn_kth_smallest: k-th smallest of n non-negative floats (the OHEM threshold); writes the
- *   HOST float *out; hist is device scratch of 2048 uint32; synchronises the stream.
  * fscnn_ohem_threshold: the whole threshold rule of utils/loss.py:159-170 on the device, from
  *   fscnn_ohem_prob's counters: *thr (device float) = inf when min_kept >= #labelled, else thresh,
  *   raised to the k-th smallest label probability (k = min(#labelled, min_kept)) when fewer than
@@ -118,8 +122,6 @@ int fscnn_seg_metric(const void* pred, int pred_dtype, const long long* target, 
 int fscnn_ohem_prob(const void* logits, int dtype, const long long* target, int N, int C,
                     long long HW, long long ignore_index, float thresh, float* prob,
                     unsigned long long* counts, void* stream);
-int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* hist, float* out,
-                       void* stream);
 int fscnn_ohem_threshold(const float* prob, long long n, const unsigned long long* counts,
                          long long min_kept, float thresh, unsigned* work, float* thr, void* stream);
 int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
@@ -175,7 +177,8 @@ int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const fl
 /* ---- launch profiler (bench.py roofline, tools/layer_report.py) ----------------------------
  * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 7 bn_apply,
  * 8 bn_bwd (apply), 9 upsample, 10 upsample_bwd, 11 cross_entropy / fused loss head,
- * 12 conv0_wgrad, 13 bn_bwd_reduce, 14 bn_finalize; 100 = every kind.
+ * 12 conv0_wgrad, 13 bn_bwd_reduce, 14 bn_finalize, 15 ppm_branches (the four pyramid-pooling
+ * branch convs + BN + ReLU, one launch each way); 100 = every kind.
  * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
  * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes
  * and flops of those launches (SURVEY.md §8(d) formulas); fscnn_prof_launch then returns launch

@@ -1,0 +1,49 @@
+"""Worker for tests/test_gpu_switches.py (run in a fresh process: the executor reads its FSCNN_*
+switches once per process).  Three fp32 train steps with Dropout(0.1) active and dropout seeds
+5, 9, 5 — alternating the unfused ``model(x)`` + CE path and the fused ``forward_loss`` head —
+then saves every step's loss and flat gradient arena, and the step-3 running statistics.
+
+    python tests/_switch_worker.py OUT.npz
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(out):
+    import numpy as np
+    import torch
+    import _fscnn_boot
+    _fscnn_boot.load()
+    from fast_scnn_pytorch_amd import arch, portable_init
+    from fast_scnn_pytorch_amd.loss import cross_entropy
+    from models.fast_scnn import FastSCNN
+
+    dev = torch.device("cuda", 0)
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+          arch.portable_state_dict(19, seed=0, variant="bnrand").items()}
+    m = FastSCNN(19)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    shape = (2, 3, 96, 160)
+    x = torch.from_numpy(portable_init.input_tensor(3, shape)).to(dev)
+    t = torch.from_numpy(portable_init.target_tensor(4, (2, 96, 160), 19, 0.05)).to(dev)
+    res = {}
+    for i, seed in enumerate((5, 9, 5, 9)):
+        m.zero_grad(set_to_none=True)
+        m._dropout_seed = seed
+        loss = cross_entropy(m(x)[0], t) if i % 2 == 0 else m.forward_loss(x, t)
+        loss.backward()
+        torch.cuda.synchronize()
+        res["loss%d" % i] = np.float32(loss.item())
+        res["grad%d" % i] = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu().numpy()
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            res["bn." + k] = v.cpu().numpy()
+    np.savez(out, **res)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

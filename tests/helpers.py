@@ -80,11 +80,12 @@ def oracle_half_emulated(sd, x, nc, dtype=torch.float16):
         F.conv2d, F.batch_norm, F.interpolate = oc, ob, oi
 
 
-def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True):
+def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True, dtype=torch.bfloat16):
     """One train step (forward, CE(ignore -1), backward) of the oracle: fp64 when ``emulate`` is
-    False, else fp32 with every conv input / weight / output rounded to bf16 — and, because
-    autograd casts gradients back through those roundings, every conv input / output gradient
-    rounded to bf16 as well (cfg3's storage precision).  Returns (loss, {name: fp64 grad})."""
+    False, else fp32 with every conv input / weight / output rounded to ``dtype`` (bf16: cfg3's
+    storage precision; fp16: train.py:269's autocast) — and, because autograd casts gradients
+    back through those roundings, every conv input / output gradient rounded to ``dtype`` as
+    well.  Returns (loss, {name: fp64 grad})."""
     import torch.nn.functional as F
     from oracle import fast_scnn_ref as ref
     dt = torch.float32 if emulate else torch.float64
@@ -93,7 +94,7 @@ def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True):
              (v.to(dt) if v.is_floating_point() else v)) for k, v in sd.items()}
     oc = F.conv2d
     if emulate:
-        q = lambda v: v.to(torch.bfloat16).float()  # noqa: E731
+        q = lambda v: v.to(dtype).float()  # noqa: E731
         F.conv2d = lambda a, w, b=None, *r, **k: q(oc(q(a), q(w), b, *r, **k))
     try:
         outs, _, _ = ref.forward(s, x.to(dt), nc, training=True, dropout_seed=drop_seed)

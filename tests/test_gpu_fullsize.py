@@ -156,8 +156,11 @@ def test_cfg3_full_size_bf16_train_step_properties():
     assert int(m1.state_dict()["classifier.dsconv2.conv.4.num_batches_tracked"]) == 4
 
 
-def test_bf16_train_step_within_emulated_bf16_budget():
-    """cfg3's arithmetic (bf16 activations, fp32 master weights / statistics) at golden size
+@pytest.mark.parametrize("half", ["bf16", "fp16"])
+def test_bf16_train_step_within_emulated_bf16_budget(half):
+    """cfg3's arithmetic (bf16 activations, fp32 master weights / statistics) at golden size,
+    and (half="fp16") the reference's own AMP arithmetic, train.py:269's fp16 autocast over fp32
+    images, against the same oracle emulating fp16 storage,
     against the fp64 oracle, with the budget bf16 itself implies: the oracle run with every conv
     input, weight and output (and, through autograd, every conv gradient) rounded to bf16
     (``oracle_bf16_train_emulated``).  At random init train-mode BN backward cancels most of dy,
@@ -178,10 +181,18 @@ def test_bf16_train_step_within_emulated_bf16_budget():
     m.load_state_dict(sd)
     m = m.to(DEV).train()
     m._dropout_seed = int(g["drop_seed"])
-    loss = cross_entropy(m(x.to(DEV).to(torch.bfloat16))[0], t.to(DEV))
+    if half == "bf16":
+        loss = cross_entropy(m(x.to(DEV).to(torch.bfloat16))[0], t.to(DEV))
+    else:
+        with torch.autocast("cuda"):
+            out = m(x.to(DEV))[0]
+            assert out.dtype == torch.float16
+            loss = cross_entropy(out, t.to(DEV))
     loss.backward()
+    hdt = torch.bfloat16 if half == "bf16" else torch.float16
     l64, g64 = oracle_bf16_train_emulated(sd, x, t, nc, int(g["drop_seed"]), emulate=False)
-    lem, gem = oracle_bf16_train_emulated(sd, x, t, nc, int(g["drop_seed"]), emulate=True)
+    lem, gem = oracle_bf16_train_emulated(sd, x, t, nc, int(g["drop_seed"]), emulate=True,
+                                          dtype=hdt)
     assert abs(loss.item() - l64) <= 1.5 * abs(lem - l64) + 2e-3 * abs(l64)
     named = dict(m.named_parameters())
     mine, truth, emu, ratios = [], [], [], {}
@@ -202,6 +213,9 @@ def test_bf16_train_step_within_emulated_bf16_budget():
     # to 5.7x); the gate is per tensor <= 4x (<= 8x for those), median <= 1.5x, and the
     # whole-vector error / cosine within 2x / 2.5x of the emulation's
     few = lambda k: ".ppm.conv1." in k or ".ppm.conv2." in k or ".bottleneck3." in k  # noqa: E731
+    print("%s train step: per-tensor error / emulated error: median %.2f, max %.2f (%s)"
+          % (half, np.median(list(ratios.values())), max(ratios.values()),
+             max(ratios, key=ratios.get)))
     bad = {k: r for k, r in ratios.items() if r > (8.0 if few(k) else 4.0)}
     assert not bad, (bad, sorted(ratios.items(), key=lambda kv: -kv[1])[:8])
     assert np.median(list(ratios.values())) <= 1.5, sorted(ratios.items(), key=lambda kv: -kv[1])[:8]

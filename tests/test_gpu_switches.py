@@ -1,0 +1,74 @@
+"""Every executor switch left in the library (`getenv` in fast-scnn-pytorch_amd/csrc) keeps its
+non-default path parity-green.  The switches are read once per process, so each case runs in a
+fresh child process:
+
+* ``FSCNN_SIDE_STREAM=0`` — every weight gradient on the caller's stream (one stream);
+* ``FSCNN_F32_SPLIT=0``   — exact fp32 MFMA in the eval pointwise GEMMs instead of the
+  three-way bf16 split of each fp32 operand;
+* ``FSCNN_GRAPHS=1``      — whole forward / backward-stage calls captured into hipGraphs and
+  replayed (the dropout seed then travels through a device slot the forward writes).
+
+Each child re-runs the oracle / golden parity tests that cover the path (fp32 train golden +
+bf16 emulated budget; eval goldens for the fp32 GEMM switch).  The graph switch also replays
+train steps with Dropout active and changing seeds; the losses, gradients and running statistics
+must be bit-identical to direct launches (tests/_switch_worker.py).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRAIN = ["tests/test_gpu_model.py::test_train_fp32_vs_oracle_and_golden",
+         "tests/test_gpu_model.py::test_fused_loss_head_vs_oracle",
+         "tests/test_gpu_model.py::test_train_aux_vs_oracle_and_golden",
+         "tests/test_gpu_fullsize.py::test_bf16_train_step_within_emulated_bf16_budget"]
+EVAL = ["tests/test_gpu_model.py::test_eval_fp32_vs_golden",
+        "tests/test_gpu_model.py::test_eval_fp32_literal_configs",
+        "tests/test_gpu_model.py::test_eval_odd_sizes_vs_oracle",
+        "tests/test_gpu_fullsize.py::test_eval_goldens_argmax_bit_exact"]
+CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL, "FSCNN_GRAPHS=1": TRAIN + EVAL}
+
+
+def _env(switch):
+    env = dict(os.environ)
+    if switch:
+        k, v = switch.split("=")
+        env[k] = v
+    return env
+
+
+@pytest.mark.parametrize("switch", sorted(CASES))
+def test_switch_keeps_oracle_parity(switch):
+    cmd = [sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+           "--timeout", "200", "--timeout-method", "thread"] + CASES[switch]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(switch), capture_output=True, text=True,
+                       timeout=600)
+    tail = (r.stdout + r.stderr)[-3000:]
+    print(switch, tail[-400:])
+    assert r.returncode == 0, "%s: parity tests failed\n%s" % (switch, tail)
+
+
+def _worker(tmp_path, switch):
+    out = str(tmp_path / ("%s.npz" % (switch or "default").replace("=", "_")))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_switch_worker.py"), out],
+                       cwd=ROOT, env=_env(switch), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    return dict(np.load(out))
+
+
+@pytest.mark.parametrize("switch", ["FSCNN_GRAPHS=1", "FSCNN_SIDE_STREAM=0"])
+def test_switch_train_steps_bit_identical_with_dropout(tmp_path, switch):
+    ref = _worker(tmp_path, None)
+    got = _worker(tmp_path, switch)
+    assert sorted(ref) == sorted(got)
+    # the seeds differ between steps 0/1 (and repeat at 2/3): the dropout mask really changes
+    assert not np.array_equal(ref["grad0"], ref["grad1"])
+    # and the same seed gives the same step (train-mode BN does not read the running statistics)
+    assert np.array_equal(ref["grad0"], ref["grad2"])
+    for k in ref:
+        assert np.array_equal(ref[k], got[k]), "%s: %s differs" % (switch, k)

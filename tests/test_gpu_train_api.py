@@ -32,13 +32,16 @@ def _grads(m):
     return torch.cat([p.grad.detach().flatten() for p in m.parameters()]).double()
 
 
+@pytest.mark.parametrize("amp", ["fp16", "bf16"])
 @pytest.mark.parametrize("opt_name", ["torch_sgd", "fused_sgd"])
-def test_autocast_gradscaler_step_as_train_py(opt_name):
-    """AMP step of train.py:269-275: autocast selects the bf16 arithmetic (fp32 master weights);
+def test_autocast_gradscaler_step_as_train_py(opt_name, amp):
+    """AMP step of train.py:269-275: ``torch.cuda.amp.autocast()`` selects fp16 arithmetic (the
+    reference's), ``autocast(dtype=torch.bfloat16)`` bf16; fp32 master weights either way.
     GradScaler scales the loss, unscales the arena-view gradients in place, skips nothing (finite)
-    and steps.  Every backward kernel is linear in dy and the scale is a power of two, so the
-    unscaled gradients and the stepped parameters are bit-identical to the same autocast step run
-    without the scaler."""
+    and steps.  bf16: every backward kernel is linear in dy and the scale is a power of two, so
+    the unscaled gradients and the stepped parameters are bit-identical to the same autocast step
+    run without the scaler.  fp16: the scaled backward keeps small gradients out of fp16's
+    subnormal range (GradScaler's purpose), so the two agree to fp16 rounding only."""
     from fast_scnn_pytorch_amd.loss import MixSoftmaxCrossEntropyLoss
     from fast_scnn_pytorch_amd.optim import FusedSGD
     g = load_golden("train_c19")
@@ -50,14 +53,17 @@ def test_autocast_gradscaler_step_as_train_py(opt_name):
             return torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
         return FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
 
+    dt = torch.float16 if amp == "fp16" else torch.bfloat16
+    ac = (lambda: torch.autocast("cuda")) if amp == "fp16" else \
+        (lambda: torch.autocast("cuda", dtype=torch.bfloat16))  # noqa: E731
     m_amp = _model(g)
     opt = make_opt(m_amp)
     scaler = torch.amp.GradScaler("cuda")
     for it in range(2):
         opt.zero_grad()
-        with torch.autocast("cuda"):
+        with ac():
             outputs = m_amp(x)
-            assert outputs[0].dtype == torch.bfloat16  # the arithmetic autocast selects here
+            assert outputs[0].dtype == dt  # the reference's logits dtype under this autocast
             loss = crit(outputs, t)
         scaler.scale(loss).backward()
         if it == 0:
@@ -72,16 +78,57 @@ def test_autocast_gradscaler_step_as_train_py(opt_name):
     m_ref = _model(g)
     opt2 = make_opt(m_ref)
     opt2.zero_grad()
-    with torch.autocast("cuda"):
+    with ac():
         loss2 = crit(m_ref(x), t)
     loss2.backward()
     g_ref = _grads(m_ref)
     opt2.step()
     scale = (g_scaled.norm() / g_unscaled.norm()).item()
-    assert scale > 1.0 and abs(np.log2(scale) - round(np.log2(scale))) < 1e-6
-    assert torch.equal(g_unscaled, g_ref)
-    for a, b in zip(p_after, m_ref.parameters()):
-        assert torch.equal(a, b.detach())
+    assert scale > 1.0 and abs(np.log2(scale) - round(np.log2(scale))) < 1e-4
+    if amp == "bf16":
+        assert torch.equal(g_unscaled, g_ref)
+        for a, b in zip(p_after, m_ref.parameters()):
+            assert torch.equal(a, b.detach())
+    else:
+        rel = ((g_unscaled - g_ref).norm() / g_ref.norm()).item()
+        cos = (g_unscaled @ g_ref / (g_unscaled.norm() * g_ref.norm())).item()
+        print("fp16 AMP: scaled vs unscaled backward, relative difference %.3g, cosine %.6f"
+              % (rel, cos))
+        assert rel < 5e-2 and cos > 0.998
+
+
+def test_gradscaler_skips_a_step_on_fp16_overflow():
+    """fp16 AMP with a loss scale so large that the scaled logits gradient overflows fp16: the
+    HIP backward produces non-finite gradients (as the reference's fp16 autograd would),
+    GradScaler finds them, skips optimizer.step() (parameters unchanged) and halves its scale;
+    the next step at a sane scale is finite and updates the parameters."""
+    from fast_scnn_pytorch_amd.loss import MixSoftmaxCrossEntropyLoss
+    g = load_golden("train_c19")
+    x, t = golden_input(g).to(DEV), golden_target(g).to(DEV)
+    crit = MixSoftmaxCrossEntropyLoss(aux=False, ignore_label=-1)
+    m = _model(g)
+    opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 40)
+    before = [p.detach().clone() for p in m.parameters()]
+    opt.zero_grad()
+    with torch.autocast("cuda"):
+        loss = crit(m(x), t)
+    scaler.scale(loss).backward()
+    assert not torch.isfinite(_grads(m)).all()  # the overflow really happened
+    scaler.step(opt)
+    scaler.update()
+    assert scaler.get_scale() == 2.0 ** 39
+    for a, b in zip(before, m.parameters()):
+        assert torch.equal(a, b.detach())  # step skipped
+    scaler.update(2.0 ** 10)
+    opt.zero_grad()
+    with torch.autocast("cuda"):
+        loss = crit(m(x), t)
+    scaler.scale(loss).backward()
+    assert torch.isfinite(_grads(m)).all()
+    scaler.step(opt)
+    scaler.update()
+    assert any(not torch.equal(a, b.detach()) for a, b in zip(before, m.parameters()))
 
 
 @pytest.mark.parametrize("layout", ["channels_last", "permuted", "fp16", "expanded"])
@@ -98,7 +145,7 @@ def test_train_input_layouts_give_dense_fp32_gradients(layout):
         xi = x.to(memory_format=torch.channels_last)
     elif layout == "permuted":
         xi = x.permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
-    elif layout == "fp16":  # fp16 images (bf16 arithmetic), channels_last: same as dense fp16
+    elif layout == "fp16":  # fp16 images (fp16 arithmetic), channels_last: same as dense fp16
         xi = x.half().to(memory_format=torch.channels_last)
         m0 = _model(g)
         cross_entropy(m0(x.half().contiguous())[0], t).backward()
