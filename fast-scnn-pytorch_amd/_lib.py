@@ -98,6 +98,9 @@ SIGNATURES = {
                                       c_vp, c_vp, c_vp]),
     "fscnn_pyramid_pool_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
                                        c_vp]),
+    "fscnn_block_ir_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                   c_vp, c_int, c_vp]),
     "fscnn_pyramid_pool_bwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
                                        c_int, c_vp]),
 }

@@ -135,7 +135,8 @@ extern "C" const char* fscnn_prof_kind_name(int kind) {
   static const char* names[PK_COUNT] = {"none", "conv0_fwd", "dw_fwd", "dw_dgrad", "dw_wgrad",
                                         "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
                                         "upsample_bwd", "cross_entropy", "conv0_wgrad",
-                                        "bn_bwd_reduce", "bn_finalize", "ppm_branches"};
+                                        "bn_bwd_reduce", "bn_finalize", "ppm_branches",
+                                        "ir_block"};
   return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
 }
 
@@ -608,6 +609,29 @@ int fscnn_pyramid_pool_bwd(const void* dpooled, int dtype, int N, int H, int W, 
   a.N = N; a.H = H; a.W = W; a.C = C; a.dpooled = dpooled; a.dx = dx; a.lddx = lddx;
   a.accumulate = accumulate;
   return pyramid_pool_bwd(a, dtype, S(stream));
+}
+
+int fscnn_block_ir_fwd(const void* x, int ldx, int dtype, int N, int H, int W, int cin, int expand,
+                       int cout, const void* w_expand, const float* w_dw, const void* w_project,
+                       const float* scale_e, const float* shift_e, const float* scale_d,
+                       const float* shift_d, const float* scale_p, const float* shift_p,
+                       int residual, void* y, int ldy, void* stream) {
+  if (!x || !y || !w_expand || !w_dw || !w_project || !scale_e || !shift_e || !scale_d ||
+      !shift_d || !scale_p || !shift_p) {
+    set_error("fscnn_block_ir_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16) {
+    set_error("fscnn_block_ir_fwd: dtype %d", dtype);
+    return E_INVALID;
+  }
+  IrArgs a{};
+  a.N = N; a.H = H; a.W = W; a.Cin = cin; a.E = expand; a.Cout = cout;
+  a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy;
+  a.we = w_expand; a.wd = w_dw; a.wp = w_project;
+  a.sc_e = scale_e; a.sh_e = shift_e; a.sc_d = scale_d; a.sh_d = shift_d;
+  a.sc_p = scale_p; a.sh_p = shift_p; a.residual = residual;
+  return ir_block_fwd(a, dtype, S(stream));
 }
 
 }  // extern "C"

@@ -392,7 +392,7 @@ enum Status : int { OK = 0, E_INVALID = -1, E_UNSUPPORTED = -2, E_HIP = -3 };
 enum ProfKind : int {
   PK_NONE = 0, PK_CONV0_FWD, PK_DW_FWD, PK_DW_DGRAD, PK_DW_WGRAD, PK_GEMM_NT, PK_GEMM_TN,
   PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_CONV0_WGRAD, PK_BN_BWD_RED, PK_BN_FIN,
-  PK_PPM, PK_COUNT
+  PK_PPM, PK_IR, PK_COUNT
 };
 constexpr int PK_ALL = 100;  // record every kind (per-launch layer report)
 extern int g_prof_kind;  // kind being recorded (PK_NONE = off)

@@ -359,6 +359,25 @@ struct SgdArgs {
 };
 
 // ---- launchers ----------------------------------------------------------------------------
+// fused stride-1 inverted-residual block, inference (ir.hip; models/fast_scnn.py:95-115)
+struct IrArgs {
+  int N, H, W;                 // map (stride 1: output = input size)
+  int Cin, E, Cout;            // block input, expanded (6 Cin), output channels
+  const void* x; int ldx;      // NHWC block input (storage dtype)
+  void* y; int ldy;            // NHWC block output
+  const void* we;              // expand weights [E][Cin] (storage dtype)
+  const float* wd;             // depthwise weights [E][9] (fp32)
+  const void* wp;              // project weights [Cout][E] (storage dtype)
+  const float *sc_e, *sh_e, *sc_d, *sh_d, *sc_p, *sh_p;  // folded eval BatchNorms
+  int residual;                // + x (stride 1, Cin == Cout)
+  // fp32 plans: the expand / project weights already split into three bf16 planes
+  // ([3][E][Cin], [3][Cout][E]; weights_prep mode 3), or null (the kernel splits them)
+  const uint16_t* we3 = nullptr;
+  const uint16_t* wp3 = nullptr;
+};
+bool ir_block_ok(const IrArgs& a, int dtype);
+int ir_block_fwd(const IrArgs& a, int dtype, hipStream_t st);
+
 int conv0_parts(int N, int Ho, int Wo);
 int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st);
 int conv0_wgrad_parts(int N, int Ho, int Wo, int rows_per_block);
@@ -478,7 +497,9 @@ struct PrepJob {
   long long dst;   // element offset in the destination
   int R, Cc;       // source [R][Cc] (row-major)
   int ld;          // trans: destination [Cc][ld] with ld >= R (columns >= R zero)
-  int trans;       // 0 cast, 1 transpose, 2 zero fill of R*Cc elements
+  int trans;       // 0 cast, 1 transpose, 2 zero fill of R*Cc elements, 3 split (below)
+  // 3: the three-term bf16 truncation split of an fp32 [R][Cc] (common.hpp gs_split3) as planes
+  //    [3][R][Cc] of uint16, dst counted in uint16 elements of the destination buffer
 };
 struct PrepTable {
   int n = 0;

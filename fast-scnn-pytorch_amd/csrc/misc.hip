@@ -678,6 +678,18 @@ __global__ __launch_bounds__(256) void weights_prep_kernel(PrepTable t, const fl
     const PrepJob& J = t.j[lo];
     const long long idx = i - t.start[lo];
     float v;
+    if (J.trans == 3) {  // one term of the bf16 truncation split, planes [3][R][Cc]
+      const long long plane = (long long)J.R * J.Cc;
+      const int p = (int)(idx / plane);
+      const float f = P[J.src + (idx - p * plane)];
+      const uint32_t h0 = __float_as_uint(f) & 0xFFFF0000u;
+      const float r1 = f - __uint_as_float(h0);
+      const uint32_t h1 = __float_as_uint(r1) & 0xFFFF0000u;
+      const float r2 = r1 - __uint_as_float(h1);
+      const uint32_t term = p == 0 ? h0 : (p == 1 ? h1 : __float_as_uint(r2) & 0xFFFF0000u);
+      reinterpret_cast<uint16_t*>(dst)[J.dst + idx] = (uint16_t)(term >> 16);
+      continue;
+    }
     if (J.trans == 2) {
       v = 0.f;  // zero fill (counters)
     } else if (J.trans) {
@@ -700,7 +712,7 @@ int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t
   for (int k = 0; k < t.n; ++k) {
     t.start[k] = t.total;
     t.total += t.j[k].trans == 1 ? (long long)t.j[k].Cc * t.j[k].ld
-                                 : t.j[k].R * (long long)t.j[k].Cc;
+                                 : (t.j[k].trans == 3 ? 3LL : 1LL) * t.j[k].R * t.j[k].Cc;
   }
   t.start[t.n] = t.total;
   const unsigned grid = (unsigned)std::min<long long>((t.total + 255) / 256, 4096);

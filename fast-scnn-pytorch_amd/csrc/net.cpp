@@ -163,6 +163,28 @@ int dwout(int h, int s) { return (h - 1) / s + 1; }
 
 }  // namespace
 
+// shape of bottleneck i as one fused inference launch (ir.hip); false when the block runs as
+// its three unfused units (training plans, stride 2, unsupported shapes)
+bool ir_block_shape(const Net& net, const Plan& pl, int i, IrArgs& b) {
+  const LbL& l = net.lb[i];
+  if (pl.train || l.stride != 1 || i == 0) return false;
+  b = IrArgs{};
+  b.N = pl.N;
+  b.H = i < 3 ? pl.H4 : pl.H5;
+  b.W = i < 3 ? pl.W4 : pl.W5;
+  b.Cin = l.cin; b.E = l.cin * 6; b.Cout = l.cout;
+  b.ldx = pl.lbp[i - 1].ld; b.ldy = pl.lbp[i].ld;
+  b.residual = l.cin == l.cout;
+  // one 8 x 8 tile per workgroup: below ~128 tiles (cfg1's 24 x 24 bottleneck3 map is 9 tiles)
+  // the fused launch leaves most CUs idle and the three unfused launches are faster
+  const long long tiles = (long long)b.N * ((b.H + 7) / 8) * ((b.W + 7) / 8);
+  return tiles >= 128 && ir_block_ok(b, pl.dtype);
+}
+
+namespace {
+
+}  // namespace
+
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl) {
   if (N < 1 || H < 3 || W < 3) {
     set_error("plan_build: bad input shape N=%d H=%d W=%d", N, H, W);
@@ -258,6 +280,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     const std::string b = "global_feature_extractor.bottleneck" + std::to_string(i / 3 + 1) + "." +
                           std::to_string(i % 3);
     pl.lbe[i].name = b + ".expand"; pl.lbd[i].name = b + ".dw"; pl.lbp[i].name = b + ".project";
+    pl.lbp[i].block_name = b + " (fused block)";
   }
   for (int i = 0; i < 4; ++i) pl.ppk[i].name = "global_feature_extractor.ppm.conv" + std::to_string(i + 1);
   pl.po.name = "global_feature_extractor.ppm.out";
@@ -287,6 +310,16 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     // LearningToDownsample's output: read by bottleneck1.0's expand and the FFM's high-res
     // branch (both GEMM operands) — unless the aux head's im2col reads it as well
     if (!net.aux) pl.l2pw.lazy = true;
+  }
+  // fp32 inference: the fused bottlenecks' expand / project weights as three bf16 split planes
+  // (weights_prep mode 3, once per forward), so the fused kernel does no split arithmetic
+  if (!train && dtype == DT_F32) {
+    for (int i = 0; i < 9; ++i) {
+      IrArgs b;
+      if (!ir_block_shape(net, pl, i, b)) continue;
+      pl.lb_we3[i] = A.get((size_t)3 * b.E * b.Cin * 2);
+      pl.lb_wp3[i] = A.get((size_t)3 * b.Cout * b.E * 2);
+    }
   }
   // fp64 team sums of the in-kernel BN finishes (last, so the activation offsets above do not move)
   if (train) pl.tsum = A.get((size_t)TAIL_TMAX * 3 * TAIL_CMAX * 8);
@@ -651,6 +684,17 @@ struct Exec {
       j.src = 0; j.dst = (long long)(pl.pbf / 2); j.R = 1; j.Cc = (int)net.p_total; j.ld = 0;
       j.trans = 0;
     }
+    for (int i = 0; i < 9; ++i) {  // fp32 inference: split planes of the fused bottlenecks
+      if (!pl.lb_we3[i]) continue;
+      const LbL& l = net.lb[i];
+      const ConvL* cs[2] = {&l.e, &l.p};
+      const size_t offs[2] = {pl.lb_we3[i], pl.lb_wp3[i]};
+      for (int k = 0; k < 2; ++k) {
+        PrepJob& j = t.j[t.n++];
+        j.src = cs[k]->w; j.dst = (long long)(offs[k] / 2); j.R = cs[k]->cout; j.Cc = cs[k]->cin;
+        j.ld = 0; j.trans = 3;
+      }
+    }
     if (train) {
       auto add = [&](const ConvL& c) {
         PrepJob& j = t.j[t.n++];
@@ -869,6 +913,25 @@ struct Exec {
     for (int i = 0; i < 9; ++i) {
       const LbL& l = net.lb[i];
       int Ho = dwout(Hc, l.stride), Wo = dwout(Wc, l.stride);
+      IrArgs b;
+      if (ir_block_shape(net, pl, i, b)) {
+        // inference: the whole stride-1 block in one launch (ir.hip), the 6x-expanded tensor
+        // never leaves LDS
+        b.x = x; b.y = W(pl.lbp[i].a);
+        b.we = Wg(l.e); b.wd = P(l.d.w); b.wp = Wg(l.p);
+        b.sc_e = Wf(pl.lbe[i].scale); b.sh_e = Wf(pl.lbe[i].shift);
+        b.sc_d = Wf(pl.lbd[i].scale); b.sh_d = Wf(pl.lbd[i].shift);
+        b.sc_p = Wf(pl.lbp[i].scale); b.sh_p = Wf(pl.lbp[i].shift);
+        if (pl.lb_we3[i]) {
+          b.we3 = (const uint16_t*)W(pl.lb_we3[i]);
+          b.wp3 = (const uint16_t*)W(pl.lb_wp3[i]);
+        }
+        g_prof_tag = pl.lbp[i].block_name.c_str();
+        TRY(ir_block_fwd(b, dt, r.st));
+        x = W(pl.lbp[i].a);
+        xld = pl.lbp[i].ld;
+        continue;
+      }
       TRY(pw(pl.lbe[i], l.e, &l.be, i == 0 ? act(pl.l2pw) : raw(x, xld), true));
       TRY(dw(pl.lbd[i], l.d, l.bd, act(pl.lbe[i]), Hc, Wc, Ho, Wo, l.stride));
       bool shortcut = l.stride == 1 && l.cin == l.cout;

@@ -88,6 +88,7 @@ struct Unit {
   // backward wgrads) applies relu(fmaf(z, scale, shift)) to z while staging its operand
   bool lazy = false;
   std::string name;         // reference module path (per-launch profile label)
+  std::string block_name;   // label of a fused whole-block launch (inference bottlenecks)
 };
 
 struct GraphCache;
@@ -110,6 +111,7 @@ struct Plan {
   size_t concat = 0, pooled = 0, feats_a = 0, feats_z = 0, up_low = 0, f = 0, drop = 0,
          logits = 0, aux_drop = 0, aux_logits = 0, aux_col = 0, pbf = 0, fold_tmp = 0;
   size_t wt = 0;                    // transposed weights (train plans), net.wt_total elements
+  size_t lb_we3[9] = {}, lb_wp3[9] = {};  // fp32 inference: split planes of fused bottlenecks
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   size_t fcnt = 0, bcnt = 0;        // BN arrival counters (ws), BN_COUNTERS each
@@ -130,6 +132,7 @@ struct Plan {
 };
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl);
+bool ir_block_shape(const Net& net, const Plan& pl, int i, IrArgs& b);
 std::shared_ptr<GraphCache> make_graph_cache();
 std::shared_ptr<SideStream> make_side_stream();
 

@@ -174,11 +174,28 @@ int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const fl
                         void* bws, unsigned long long dropout_seed, float dropout_p,
                         int stage_from, int stage_to, void* stream);
 
+/* ---- fused blocks (inference) ---------------------------------------------------------------
+ * fscnn_block_ir_fwd: one stride-1 LinearBottleneck (models/fast_scnn.py:95-115) with its three
+ * BatchNorms folded (eval): y = BN_p(W_p * relu(BN_d(dw3x3(relu(BN_e(W_e * x)))))) (+ x when
+ * residual, which needs cin == cout).  x, y NHWC [N][H][W] with row strides ldx / ldy elements
+ * (ldy may exceed cout: the PPM concat buffer); w_expand [expand][cin] and w_project
+ * [cout][expand] in dtype (the nn.Conv2d weight layouts); w_dw [expand][9] fp32; scale_* / shift_*
+ * fp32 per channel (BN folded as gamma/sqrt(var+eps), beta - mean*scale).  cin in {64, 96, 128},
+ * expand a multiple of 64, cout a multiple of 16 <= 128.  The 6x-expanded tensor stays in LDS.
+ * Replaces the three conv+BN(+ReLU) modules of LinearBottleneck.block (:103-108) and the
+ * shortcut add (:113-114). */
+int fscnn_block_ir_fwd(const void* x, int ldx, int dtype, int N, int H, int W, int cin, int expand,
+                       int cout, const void* w_expand, const float* w_dw, const void* w_project,
+                       const float* scale_e, const float* shift_e, const float* scale_d,
+                       const float* shift_d, const float* scale_p, const float* shift_p,
+                       int residual, void* y, int ldy, void* stream);
+
 /* ---- launch profiler (bench.py roofline, tools/layer_report.py) ----------------------------
  * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 7 bn_apply,
  * 8 bn_bwd (apply), 9 upsample, 10 upsample_bwd, 11 cross_entropy / fused loss head,
  * 12 conv0_wgrad, 13 bn_bwd_reduce, 14 bn_finalize, 15 ppm_branches (the four pyramid-pooling
- * branch convs + BN + ReLU, one launch each way); 100 = every kind.
+ * branch convs + BN + ReLU, one launch each way), 16 ir_block (fused inference bottleneck);
+ * 100 = every kind.
  * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
  * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes
  * and flops of those launches (SURVEY.md §8(d) formulas); fscnn_prof_launch then returns launch
