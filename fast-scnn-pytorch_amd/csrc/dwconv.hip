@@ -422,19 +422,30 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
 
 static void dw_block_shape(int C, int V, int& bx, int& by) {
   int cv = C / V;
-  bx = cv < 64 ? cv : 64;
+  bx = cv;  // channel vectors per workgroup row: all of them, or the largest divisor <= 64
+  if (bx > 64) {
+    bx = 64;
+    while (cv % bx) --bx;
+  }
   by = 256 / bx;
   if (by < 1) by = 1;
 }
 
 // ---- input gradient ---------------------------------------------------------------------------
 // dX[n,h,w,c] = sum_{kh,kw} dY[n,ho,wo,c] * w[c,kh,kw] with h = ho*s-1+kh, w = wo*s-1+kw.
-// stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even):
+// stride 2: a thread owns dx rows h0,h0+1 (h0 even) x cols w0..w0+3 (w0 even) of 4 channels:
 //   row h0   <- dy row h0/2 (kh=1);  row h0+1 <- dy rows h0/2+1 (kh=0) and h0/2 (kh=2)
 //   col w0+q <- dy cols w0/2 + (q+1-kw)/2 for the kw of matching parity
+// Four channels per thread (one 8-B vector of 16-bit data, 16 B of fp32) keep the live set near
+// 100 VGPRs, so 4+ waves per SIMD hide the HBM latency; with BR (this dx is the dy of a
+// BatchNorm whose backward partials the launch also emits) that BN's z loads are issued together
+// with the dy loads, before any arithmetic, so the two latencies overlap.  (Measured at cfg3,
+// bf16: bottleneck1.0 147 us, bottleneck2.0 56 us, against 183 / 86 us for 8 channels per thread
+// and 200 / 79 us for a one-column walker over 8 rows with the taps staged in LDS.)
+constexpr int DWD2_V = 4;  // channels per thread
 template <typename T, bool BR, bool TL = false>
-__global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs a) {
-  constexpr int V = VecW<T>::V;
+__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
+  constexpr int V = DWD2_V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
   int bx, by, bz;
   dw_tile(bx, by, bz);
@@ -447,12 +458,44 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
   const bool active = cv < CV && w0 < a.W;
   if (!BR && !active) return;  // (BR: every thread joins the workgroup reduction)
   const int cvc = active ? cv : 0;
+  const int cb = cvc * V;
+  // ---- every global load of the thread first: dy (2 x 3 vectors), BR: z (2 x 4), weights -----
+  const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + cb;
+  const int hb = h0 / 2, wb = w0 / 2;
+  float g[2][3][V];
+#pragma unroll
+  for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+    for (int dc = 0; dc < 3; ++dc) {
+      const int ho = hb + dr, wo = wb + dc;
+      const bool ok = active && ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
+      ld4v(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * a.C, g[dr][dc]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[dr][dc][j] = ok ? g[dr][dc][j] : 0.f;
+    }
+  float z[BR ? 2 : 1][BR ? 4 : 1][V];
+  if constexpr (BR) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = active && h0 + r < a.H && w0 + q < a.W;
+        const size_t pix = ok ? ((size_t)n * a.H + h0 + r) * a.W + w0 + q : 0;
+        ld4v((const T*)a.bs.z + pix * a.C + cb, z[r][q]);
+      }
+  }
   float wt[9][V];
-  const float* wp = a.w + (size_t)cvc * V * 9;
+  const float4* wp = reinterpret_cast<const float4*>(a.w + (size_t)cb * 9);  // 36 floats, 16-B aligned
 #pragma unroll
-  for (int j = 0; j < V; ++j)
+  for (int i = 0; i < 9; ++i) {
+    const float4 t4 = wp[i];
+    const float tt[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wt[t][j] = wp[j * 9 + t];
+    for (int e = 0; e < 4; ++e) {
+      const int f = 4 * i + e;  // = j * 9 + tap
+      wt[f % 9][f / 9] = tt[e];
+    }
+  }
   float acc[2][4][V];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
@@ -460,23 +503,13 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int j = 0; j < V; ++j) acc[r][q][j] = 0.f;
-  const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + (size_t)cvc * V;
-  const int hb = h0 / 2, wb = w0 / 2;
 #pragma unroll
-  for (int dr = 0; dr < 2; ++dr) {       // dy rows hb, hb+1
-    const int ho = hb + dr;
+  for (int dr = 0; dr < 2; ++dr)
 #pragma unroll
-    for (int dc = 0; dc < 3; ++dc) {     // dy cols wb, wb+1, wb+2
-      const int wo = wb + dc;
-      const bool ok = active && ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
-      float g[V];
-      const size_t goff = (ok ? (size_t)ho * a.Wo + wo : 0) * a.C;
-      ldv(gb + goff, g);
-#pragma unroll
-      for (int j = 0; j < V; ++j) g[j] = ok ? g[j] : 0.f;
+    for (int dc = 0; dc < 3; ++dc)
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        // dx row h0+r reads dy row ho with kh = (h0 + r) + 1 - 2*ho
+        // dx row h0+r reads dy row hb+dr with kh = (h0 + r) + 1 - 2*(hb+dr)
         const int kh = r + 1 - 2 * dr;
         if (kh < 0 || kh > 2) continue;
 #pragma unroll
@@ -484,27 +517,24 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
           const int kw = q + 1 - 2 * dc;
           if (kw < 0 || kw > 2) continue;
 #pragma unroll
-          for (int j = 0; j < V; ++j) acc[r][q][j] = fmaf(g[j], wt[kh * 3 + kw][j], acc[r][q][j]);
+          for (int j = 0; j < V; ++j) acc[r][q][j] = fmaf(g[dr][dc][j], wt[kh * 3 + kw][j], acc[r][q][j]);
         }
       }
-    }
-  }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     if (!active || h0 + r >= a.H) continue;
-    T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + (size_t)cv * V;
+    T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + cb;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (w0 + q < a.W) stv(db + (size_t)q * a.C, acc[r][q]);
+      if (w0 + q < a.W) st4v(db + (size_t)q * a.C, acc[r][q]);
   }
   if constexpr (BR) {
     // ---- BN-backward partial sums of the stored dx (the dy of that BN), one record per
-    // workgroup: the BY column groups of a channel vector summed in fixed order
+    // workgroup: the BY column groups of a channel quad summed in fixed order
     __shared__ float s_br[256 * 2 * V];
     __shared__ float s_bc[4][64 * V];  // mean, invstd, mask scale, mask shift of the channels
     const BnBwdPart& b = a.bs;
     const bool m2 = b.mode == 2;
-    const int cb = cvc * V;
     {
       const int c0b = bx * BX * V;
       for (int i = ty * BX + tx; i < BX * V; i += BX * BY) {
@@ -519,16 +549,8 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
     float s1[V], s2[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
-    // one dx row (4 pixels) per batch of z loads: keeps the live set within the register budget
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      float z[4][V];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = active && h0 + r < a.H && w0 + q < a.W;
-        const size_t pix = ok ? ((size_t)n * a.H + h0 + r) * a.W + w0 + q : 0;
-        ldv((const T*)b.z + pix * a.C + cb, z[q]);
-      }
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool ok = active && h0 + r < a.H && w0 + q < a.W;
@@ -536,13 +558,11 @@ __global__ __launch_bounds__(256, BR ? 2 : 3) void dw_dgrad_s2_kernel(DwBwdArgs 
         for (int j = 0; j < V; ++j) {
           const int cl = tx * V + j;
           float gv = round_as<T>(acc[r][q][j]);
-          gv = (ok && fmaf(z[q][j], s_bc[2][cl], s_bc[3][cl]) > 0.f) ? gv : 0.f;
+          gv = (ok && fmaf(z[r][q][j], s_bc[2][cl], s_bc[3][cl]) > 0.f) ? gv : 0.f;
           s1[j] += gv;
-          s2[j] += gv * (z[q][j] - s_bc[0][cl]) * s_bc[1][cl];
+          s2[j] += gv * (z[r][q][j] - s_bc[0][cl]) * s_bc[1][cl];
         }
       }
-      asm volatile("" ::: "memory");  // keep the second row's z loads after the first's use
-    }
     const int t = ty * BX + tx;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -574,6 +594,14 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const bool br = a.bs.part != nullptr;  // + a read of the next BN's z (dx-sized)
   std::optional<ProfScope> ps;  // (closed before a separate finalize launch)
   ps.emplace(PK_DW_DGRAD, st, E * (in_el * (br ? 2 : 1) + out_el) + 36.0 * a.C, 18.0 * out_el);
+  if (a.C % V || (a.stride != 1 && a.stride != 2)) {
+    set_error("dw_dgrad: bad args C=%d stride=%d", a.C, a.stride);
+    return E_INVALID;
+  }
+  if (a.stride == 2 && (uintptr_t)a.w % 16) {
+    set_error("dw_dgrad: weights must be 16-B aligned");
+    return E_INVALID;
+  }
   if (br && (!a.bs.z || !a.bs.mean || !a.bs.invstd || (a.bs.mode == 2 && (!a.bs.scale || !a.bs.shift)))) {
     set_error("dw_dgrad: inconsistent BN-backward partial arguments");
     return E_INVALID;
@@ -598,8 +626,8 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     rc = br ? dw_launch_fwd<true, false, true>(f, dtype, st) : dw_launch_fwd<true, false>(f, dtype, st);
   } else {
     int bx, by;
-    dw_block_shape(a.C, V, bx, by);
-    dim3 grid(cdiv(a.C / V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
+    dw_block_shape(a.C, DWD2_V, bx, by);
+    dim3 grid(cdiv(a.C / DWD2_V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
     DwBwdArgs b = a;
     if (fin) {
       P = (int)(grid.y * grid.z);
@@ -633,7 +661,7 @@ int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
     return (int)(g.y * g.z);
   }
   int bx, by;
-  dw_block_shape(C, V, bx, by);
+  dw_block_shape(C, DWD2_V, bx, by);
   return cdiv(W, by * 4) * N * ((H + 1) / 2);
 }
 

@@ -85,6 +85,24 @@ def main():
         step()
         torch.cuda.synchronize()
         iso.append(time.perf_counter() - s0)
+    # (4) host cost of one step with an empty launch queue (no back-pressure), and a profile
+    import cProfile
+    import pstats
+    enq = []
+    prof = cProfile.Profile()
+    for i in range(10):
+        torch.cuda.synchronize()
+        s0 = time.perf_counter()
+        if i >= 5:
+            prof.enable()
+        step()
+        if i >= 5:
+            prof.disable()
+        enq.append(time.perf_counter() - s0)
+    torch.cuda.synchronize()
+    print("host enqueue of one step, empty queue: median %.3f ms" % (1e3 * sorted(enq)[5]))
+    st = pstats.Stats(prof)
+    st.sort_stats("tottime").print_stats(18)
     print("host enqueue  %.3f ms/step   wall %.3f ms/step" % (1e3 * t_enq / K, 1e3 * t_all / K))
     print("event-to-event GPU step  median %.3f ms  min %.3f  max %.3f"
           % (sorted(gpu)[K // 2], min(gpu), max(gpu)))
