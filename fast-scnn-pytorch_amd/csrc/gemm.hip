@@ -974,9 +974,18 @@ __global__ void reduce_final_multi_kernel(RedTable t) {
 
 int reduce_slabs_multi(const RedTable& t, hipStream_t st) {
   if (t.n <= 0) return OK;
-  bool fold = false;
-  for (int k = 0; k < t.n; ++k) fold = fold || t.j[k].S > RED_Q;
-  if (fold) reduce_fold_multi_kernel<<<dim3(t.blocks, RED_Q), 256, 0, st>>>(t);
+  // the fold pass covers only the jobs with more than RED_Q partials (its grid over the whole
+  // table launched ~64 x more workgroups than work: 135 K for bottleneck3's stage, 50 us)
+  RedTable f;
+  for (int k = 0; k < t.n; ++k) {
+    if (t.j[k].S <= RED_Q) continue;
+    f.j[f.n] = t.j[k];
+    f.blk0[f.n] = f.blocks;
+    f.blocks += cdiv(t.j[k].count, 256);
+    f.n++;
+    f.blk0[f.n] = f.blocks;
+  }
+  if (f.n) reduce_fold_multi_kernel<<<dim3(f.blocks, RED_Q), 256, 0, st>>>(f);
   reduce_final_multi_kernel<<<t.blocks, 256, 0, st>>>(t);
   return check_launch("reduce_slabs_multi");
 }

@@ -76,8 +76,8 @@ __global__ __launch_bounds__(256) void up_nchw_kernel(UpArgs a) {
   const size_t plane = (size_t)a.Ho * a.Wo;
 #pragma unroll 4
   for (int c = 0; c < a.C; ++c) {
-    float o = lh.l0 * (lw.l0 * ld1(q00 + c) + lw.l1 * ld1(q01 + c)) +
-              lh.l1 * (lw.l0 * ld1(q10 + c) + lw.l1 * ld1(q11 + c));
+    float o = lerp2(lh.l0, lerp2(lw.l0, ld1(q00 + c), lw.l1, ld1(q01 + c)),
+                    lh.l1, lerp2(lw.l0, ld1(q10 + c), lw.l1, ld1(q11 + c)));
     st1(yb + c * plane, o);
   }
 }
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
     for (int r = 0; r < UPR_MAXROWS; ++r) {
       const float* row = s_rows + min(r, nrows - 1) * CWP + c * WP;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wr[r][j] = lw[j].l0 * row[lw[j].i0] + lw[j].l1 * row[lw[j].i1];
+      for (int j = 0; j < 4; ++j) wr[r][j] = lerp2(lw[j].l0, row[lw[j].i0], lw[j].l1, row[lw[j].i1]);
     }
     for (int ho = ho0; ho <= ho1; ++ho) {
       const Lerp lh = ac_lerp(ho, a.Hi, a.Ho, sh);
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
           x0 = d0 == r ? wr[r][j] : x0;
           x1 = d1 == r ? wr[r][j] : x1;
         }
-        o[j] = lh.l0 * x0 + lh.l1 * x1;
+        o[j] = lerp2(lh.l0, x0, lh.l1, x1);
       }
       TO* yp = yb + c * plane + (size_t)ho * a.Wo;
       if (VEC && wo0 + 4 <= a.Wo) {
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_argmax_kernel(UpArgs a, TL* la
     for (int r = 0; r < UPR_MAXROWS; ++r) {
       const float* row = s_rows + min(r, nrows - 1) * CWP + c * WP;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wr[r][j] = lw[j].l0 * row[lw[j].i0] + lw[j].l1 * row[lw[j].i1];
+      for (int j = 0; j < 4; ++j) wr[r][j] = lerp2(lw[j].l0, row[lw[j].i0], lw[j].l1, row[lw[j].i1]);
     }
 #pragma unroll
     for (int rr = 0; rr < UPR_R; ++rr) {
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_argmax_kernel(UpArgs a, TL* la
           x0 = d0 == r ? wr[r][j] : x0;
           x1 = d1 == r ? wr[r][j] : x1;
         }
-        float o = lh.l0 * x0 + lh.l1 * x1;
+        float o = lerp2(lh.l0, x0, lh.l1, x1);
         o = round_as<TI>(o);  // the logits up_nchw would store
         const bool gt = o > best[rr][j];
         best[rr][j] = gt ? o : best[rr][j];

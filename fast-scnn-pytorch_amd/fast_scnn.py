@@ -534,6 +534,8 @@ class FastSCNN(nn.Module):
         _lib.call("fscnn_predict", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(labels),
                   1 if dtype == torch.uint8 else 0, _lib.ptr(ar["P"]), _lib.ptr(ar["R"]),
                   _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.stream_ptr(x.device))
+        if getattr(self, "_keep_ws", False):
+            self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return labels
 
     def debug_buffer(self, name):

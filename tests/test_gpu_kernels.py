@@ -125,7 +125,9 @@ def test_dw3x3_fwd_bwd(dt, N, H, W, C, s):
 @pytest.mark.parametrize("M,N,K", [(1000, 48, 32), (4096, 384, 64), (777, 64, 384), (300, 96, 576),
                                    (513, 128, 768), (129, 19, 128), (40, 32, 128), (2048, 128, 256),
                                    (999, 2, 128), (3000, 128, 48), (5000, 576, 96), (2500, 768, 128),
-                                   (70001, 128, 128)])
+                                   (70001, 128, 128),
+                                   # the bottleneck2/3 projects / expand dgrads at cfg3 (M = 16 K)
+                                   (16384, 128, 768), (16383, 96, 576), (65536, 64, 384)])
 def test_pw_gemm(dt, M, N, K):
     A = rnd(M, K, seed=10)
     B = rnd(N, K, seed=11, scale=1 / math.sqrt(K))
@@ -189,7 +191,8 @@ def test_pw_gemm_residual_in_place(dt, M, N, K):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,K", [(3001, 96, 64), (20001, 48, 32), (70000, 64, 64)])
+@pytest.mark.parametrize("M,N,K", [(3001, 96, 64), (20001, 48, 32), (70000, 64, 64),
+                                   (16384, 128, 768), (16385, 96, 384)])
 def test_gemm_bn_statistics(dt, M, N, K):
     """Tiled (M < 4096: one record per 128-row tile) and streaming (one shifted-sum record per
     workgroup) statistics forms; the call reports how many records it writes."""

@@ -17,8 +17,9 @@ _fscnn_boot.load()
 from fast_scnn_pytorch_amd import _lib
 
 # (label, K, N): the bottleneck2/3 expand / project forwards and their dgrads
-SHAPES = [("b2 expand", 64, 384), ("b2 project", 384, 96), ("b3 expand", 96, 576),
-          ("b3 project", 576, 128), ("b3 expand dgrad", 576, 96), ("b3 project dgrad", 128, 576)]
+SHAPES = [("b2 expand", 64, 384), ("b2.0 project", 384, 96), ("b3 expand", 96, 576),
+          ("b3.0 project", 576, 128), ("b2.x project", 576, 96), ("b3.x project", 768, 128),
+          ("b3 project dgrad", 128, 576)]
 
 
 def main():
