@@ -360,11 +360,12 @@ struct Lerp {
   int i0, i1;
   float l0, l1;
 };
-// l0 * a + l1 * b with both products rounded (no fma contraction): every kernel that evaluates
-// the same bilinear tap pair (up_nchw, up_nchw_rows, up_argmax) gets the same bits, so the fused
-// argmax labels equal torch.argmax of the stored logits even at 1-ulp near-ties
+// l0 * a + l1 * b as ONE explicit form, fma(l0, a, round(l1 * b)): left to the compiler, the
+// expression is contracted differently per kernel (hipcc's default -ffp-contract=fast applies to
+// __fmul_rn / __fadd_rn too), and a 1-ulp difference between up_nchw and up_argmax flipped a
+// cfg2 near-tie label; every kernel that evaluates the same bilinear tap pair now gets the same bits
 __device__ __forceinline__ float lerp2(float l0, float a, float l1, float b) {
-  return __fadd_rn(__fmul_rn(l0, a), __fmul_rn(l1, b));
+  return fmaf(l0, a, l1 * b);
 }
 __host__ __device__ __forceinline__ float ac_scale(int in, int out) {
   return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.0f;

@@ -813,9 +813,14 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTnArgs a) {
 }
 
 int gemm_tn_splits(int M, int N, int K) {
-  // ~1024 workgroups; a multiple of 8 splits so xcd_tile keeps a split's tiles on one XCD
+  // ~512 workgroups; a multiple of 8 splits so xcd_tile keeps a split's tiles on one XCD.
+  // The split count sets the partial-slab volume the stage's deferred reduction reads back on
+  // the main stream (366 MB per cfg3 step at ~1024 workgroups, 174 MB at ~512) while the wgrads
+  // themselves run on the side stream; measured per cfg3 step: 1024 -> 6.46-6.51 ms, 512 ->
+  // 6.41 ms, 256 -> 6.45-6.47 ms (the side stream then falls behind)
+  constexpr int target = 512;
   int tiles = cdiv(N, TN_T) * cdiv(K, TN_T);
-  int s = 1024 / tiles;
+  int s = target / tiles;
   int smax = cdiv(M, 4 * TN_MC);
   if (s > smax) s = smax;
   if (s >= 8) s &= ~7;
