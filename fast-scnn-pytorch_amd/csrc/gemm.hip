@@ -934,19 +934,23 @@ __device__ __forceinline__ int red_job(const RedTable& t, int b) {
   return lo;
 }
 
+// fold: job j's blocks are (q, column block) pairs, q < J.Q, thread (i, q) sums slabs q, q + Q,
+// ... into slab q.  Q = cdiv(S, 16) (<= RED_Q): ~16 partials per thread (one global Q = 64 left
+// ~1-2 loads per thread and 41 K workgroups for bottleneck1's stage: 56 us)
 __global__ void reduce_fold_multi_kernel(RedTable t) {
   const int jb = red_job(t, blockIdx.x);
   const RedJob& J = t.j[jb];
-  if (J.S <= RED_Q) return;
-  const int i = (blockIdx.x - t.blk0[jb]) * blockDim.x + threadIdx.x;
-  const int q = blockIdx.y;
+  const int nb = cdiv(J.count, 256);
+  const int local = blockIdx.x - t.blk0[jb];
+  const int q = local / nb;
+  const int i = (local - q * nb) * blockDim.x + threadIdx.x;
   if (i >= J.count) return;
   float s = 0.f;
-  for (int k0 = q; k0 < J.S; k0 += 8 * RED_Q) {
+  for (int k0 = q; k0 < J.S; k0 += 8 * J.Q) {
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int k = k0 + u * RED_Q;
+      const int k = k0 + u * J.Q;
       const float x = J.slab[(size_t)(k < J.S ? k : q) * J.stride + i];
       v[u] = k < J.S ? x : 0.f;
     }
@@ -961,7 +965,7 @@ __global__ void reduce_final_multi_kernel(RedTable t) {
   const RedJob& J = t.j[jb];
   const int i = (blockIdx.x - t.blk0[jb]) * blockDim.x + threadIdx.x;
   if (i >= J.count) return;
-  const int S = J.S > RED_Q ? RED_Q : J.S;
+  const int S = J.S > RED_Q ? J.Q : J.S;
   float s = 0.f;
   for (int k0 = 0; k0 < S; k0 += 8) {
     float v[8];
@@ -977,20 +981,22 @@ __global__ void reduce_final_multi_kernel(RedTable t) {
   J.out[o] = J.accumulate ? J.out[o] + s : s;
 }
 
-int reduce_slabs_multi(const RedTable& t, hipStream_t st) {
-  if (t.n <= 0) return OK;
-  // the fold pass covers only the jobs with more than RED_Q partials (its grid over the whole
-  // table launched ~64 x more workgroups than work: 135 K for bottleneck3's stage, 50 us)
+int reduce_slabs_multi(const RedTable& tin, hipStream_t st) {
+  if (tin.n <= 0) return OK;
+  RedTable t = tin;
+  // the fold pass covers only the jobs with more than RED_Q partials
   RedTable f;
   for (int k = 0; k < t.n; ++k) {
-    if (t.j[k].S <= RED_Q) continue;
-    f.j[f.n] = t.j[k];
+    RedJob& J = t.j[k];
+    if (J.S <= RED_Q) continue;
+    J.Q = cdiv(J.S, 16) < RED_Q ? cdiv(J.S, 16) : RED_Q;
+    f.j[f.n] = J;
     f.blk0[f.n] = f.blocks;
-    f.blocks += cdiv(t.j[k].count, 256);
+    f.blocks += cdiv(J.count, 256) * J.Q;
     f.n++;
     f.blk0[f.n] = f.blocks;
   }
-  if (f.n) reduce_fold_multi_kernel<<<dim3(f.blocks, RED_Q), 256, 0, st>>>(f);
+  if (f.n) reduce_fold_multi_kernel<<<f.blocks, 256, 0, st>>>(f);
   reduce_final_multi_kernel<<<t.blocks, 256, 0, st>>>(t);
   return check_launch("reduce_slabs_multi");
 }

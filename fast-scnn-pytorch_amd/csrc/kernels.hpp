@@ -412,6 +412,7 @@ struct RedJob {
   float* out;
   long long stride;
   int S, count, accumulate, C9;
+  int Q = 0;     // fold fan-out (set by reduce_slabs_multi): S > RED_Q partials fold into Q
 };
 struct RedTable {
   int n = 0;
