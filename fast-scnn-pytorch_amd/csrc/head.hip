@@ -107,10 +107,11 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
       }
       if (active) {
         const Lerp lh = ac_lerp(h, Hl, H, sh);
-        // class pairs (v_pk_* f32): v0 / v1 = the row-interpolated low-res logits of columns
-        // t / t+1 (log2 units), padded to an even class count with zeros
+        // class pairs (v_pk_* f32): v0 = the row-interpolated low-res logits of column t and
+        // dv = (column t+1) - v0 (log2 units), padded to an even class count with zeros; a
+        // pixel's logit is then ONE packed fma, v0 + lw.l1 * dv
         constexpr int CP = (CT + 1) / 2;
-        f32x2 v0[CP], v1[CP];
+        f32x2 v0[CP], dv[CP];
         const f32x2 h0 = {lh.l0, lh.l0}, h1 = {lh.l1, lh.l1};
 #pragma unroll
         for (int p = 0; p < CP; ++p) {
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
           const f32x2 l01 = {L0[SL + c], c + 1 < CT ? L0[SL + c1] : 0.f};
           const f32x2 l11 = {L1[SL + c], c + 1 < CT ? L1[SL + c1] : 0.f};
           v0[p] = __builtin_elementwise_fma(h1, l10, h0 * l00);
-          v1[p] = __builtin_elementwise_fma(h1, l11, h0 * l01);
+          dv[p] = __builtin_elementwise_fma(h1, l11, h0 * l01) - v0[p];
         }
         const long long* trow = tgt + (size_t)h * W;
         for (int w = w_lo; w < w_hi; ++w) {
@@ -133,25 +134,36 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
             ti = (tg != a.ignore_index && tg >= 0 && tg < Cm) ? (int)tg : -1;
           }
           const bool valid = ti >= 0;
-          const f32x2 w0 = {lw.l0, lw.l0}, w1 = {lw.l1, lw.l1};
+          const f32x2 w1 = {lw.l1, lw.l1};
           f32x2 e[CP];
-          float mx = -INFINITY, lt = 0.f;
+          float mx = -INFINITY;
 #pragma unroll
           for (int p = 0; p < CP; ++p) {
-            e[p] = __builtin_elementwise_fma(w1, v1[p], w0 * v0[p]);
+            e[p] = __builtin_elementwise_fma(w1, dv[p], v0[p]);
             if (2 * p < Cm) mx = fmaxf(mx, e[p].x);
             if (2 * p + 1 < Cm) mx = fmaxf(mx, e[p].y);
-            lt = (2 * p == ti) ? e[p].x : lt;
-            lt = (2 * p + 1 == ti) ? e[p].y : lt;
           }
-          float se = 0.f;
+          // the target's logit, re-interpolated from the staged rows with the same operations
+          // (an LDS gather instead of a select over every class)
+          float lt;
+          {
+            const int tc = valid ? ti : 0;
+            const float v0t = fmaf(lh.l1, L1[tc], lh.l0 * L0[tc]);
+            const float v1t = fmaf(lh.l1, L1[SL + tc], lh.l0 * L0[SL + tc]);
+            lt = fmaf(lw.l1, v1t - v0t, v0t);
+          }
+          // v_exp_f32 (2^x) of packed differences, packed partial sums (the loss keeps an
+          // accurate logf)
+          const f32x2 mm = {mx, mx};
+          f32x2 sp = {0.f, 0.f};
 #pragma unroll
-          for (int p = 0; p < CP; ++p) {  // v_exp_f32 (2^x); the loss keeps an accurate logf
-            e[p].x = 2 * p < Cm ? __builtin_amdgcn_exp2f(e[p].x - mx) : 0.f;
-            e[p].y = 2 * p + 1 < Cm ? __builtin_amdgcn_exp2f(e[p].y - mx) : 0.f;
-            se += e[p].x;
-            se += e[p].y;
+          for (int p = 0; p < CP; ++p) {
+            const f32x2 d = e[p] - mm;
+            e[p].x = 2 * p < Cm ? __builtin_amdgcn_exp2f(d.x) : 0.f;
+            e[p].y = 2 * p + 1 < Cm ? __builtin_amdgcn_exp2f(d.y) : 0.f;
+            sp += e[p];
           }
+          const float se = sp.x + sp.y;
           const float inv = valid ? __builtin_amdgcn_rcpf(se) : 0.f;  // v_rcp_f32 (1 ulp)
           if (valid) {
             loss += (mx - lt) * HD_LN2 + logf(se);
