@@ -96,6 +96,85 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_kernel(PpmFwdArgs a) {
     st1(Y + (size_t)m * b.ldy + n, fmaxf(fmaf(round_as<T>(s_z[m * PPM_C + n]), sc, sh), 0.f));
 }
 
+// 16-bit plans, K = 128 (the PPM input): the branch's whole pooled input X [M][128] is staged in
+// LDS with one batch of 16-B loads per thread and each thread keeps its channel's 128 weights in
+// registers, so the row walk reads only LDS (the kernel above walks its rows as a chain of
+// dependent L2 round trips: 34 us for the four branches at cfg3).  Same per-row fmaf order (k
+// ascending), so the values are identical.
+constexpr int PPM_K = 128;
+template <typename T>
+__global__ __launch_bounds__(PPM_T) void ppm_fwd_lds_kernel(PpmFwdArgs a) {
+  constexpr int V = VecW<T>::V;
+  const PpmBranchFwd& b = a.b[blockIdx.x];
+  const int M = b.M, tid = threadIdx.x;
+  const int n = tid & 31, sl = tid >> 5;
+  extern __shared__ float sm[];
+  float* s_z = sm;                                              // [M][C], unrounded conv output
+  T* s_x = reinterpret_cast<T*>(s_z + (size_t)M * PPM_C);       // [M][K]
+  __shared__ double s_r[2][PPM_T];
+  __shared__ float s_ss[2][PPM_C];
+  const T* X = (const T*)b.x;
+  {
+    const int nv = M * PPM_K / V;
+    constexpr int LPT = 288 * PPM_K / 8 / PPM_T;  // 9: the largest branch (M <= 288 checked)
+    uint4 raw[LPT];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int i = tid + u * PPM_T;
+      raw[u] = *reinterpret_cast<const uint4*>(X + (size_t)(i < nv ? i : 0) * V);
+    }
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int i = tid + u * PPM_T;
+      if (i < nv) *reinterpret_cast<uint4*>(s_x + (size_t)i * V) = raw[u];
+    }
+  }
+  float wr[PPM_K];
+  const T* Wt = (const T*)b.w + (size_t)n * PPM_K;
+#pragma unroll
+  for (int k = 0; k < PPM_K; k += V) ldv(Wt + k, *reinterpret_cast<float(*)[V]>(&wr[k]));
+  __syncthreads();
+  T* Z = (T*)b.z;
+  for (int m = sl; m < M; m += 16) {
+    const T* xr = s_x + (size_t)m * PPM_K;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < PPM_K; k += V) {
+      float xv[V];
+      ldv(xr + k, xv);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc = fmaf(xv[j], wr[k + j], acc);
+    }
+    s_z[m * PPM_C + n] = acc;
+    st1(Z + (size_t)m * PPM_C + n, acc);
+  }
+  __syncthreads();
+  double t1 = 0.0, t2 = 0.0;
+  for (int m = sl; m < M; m += 16) {
+    const double v = s_z[m * PPM_C + n];
+    t1 += v;
+    t2 += v * v;
+  }
+  s_r[0][tid] = t1;
+  s_r[1][tid] = t2;
+  __syncthreads();
+  if (tid < PPM_C) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int j = 0; j < 16; ++j) {
+      s1 += s_r[0][j * PPM_C + tid];
+      s2 += s_r[1][j * PPM_C + tid];
+    }
+    bn_fwd_finish(b.f, tid, (double)M, s1, s2);
+    s_ss[0][tid] = b.f.scale[tid];
+    s_ss[1][tid] = b.f.shift[tid];
+  }
+  __syncthreads();
+  T* Y = (T*)b.y;
+  const float sc = s_ss[0][n], sh = s_ss[1][n];
+  for (int m = sl; m < M; m += 16)
+    st1(Y + (size_t)m * b.ldy + n, fmaxf(fmaf(round_as<T>(s_z[m * PPM_C + n]), sc, sh), 0.f));
+}
+
 // G workgroups per branch (a.wg0): each recomputes the branch's BN-backward sums and dz (tiny,
 // block-local, identical arithmetic in every workgroup) and then owns a 1/G slice of the weight
 // gradient's k and of the input gradient's rows — one workgroup per branch was LDS-bound on the
@@ -230,6 +309,12 @@ int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st) {
   for (int i = 0; i < a.nb; ++i) rows += a.b[i].M;
   ProfScope ps(PK_PPM, st, rows * (a.K + 2.0 * PPM_C) * (dtype == DT_F32 ? 4 : 2),
                2.0 * a.K * PPM_C * rows);
+  if (dtype != DT_F32 && a.K == PPM_K && maxM <= 288) {
+    const size_t l2 = (size_t)maxM * PPM_C * 4 + (size_t)maxM * PPM_K * 2;
+    if (dtype == DT_F16) ppm_fwd_lds_kernel<f16><<<a.nb, PPM_T, l2, st>>>(a);
+    else ppm_fwd_lds_kernel<bf16><<<a.nb, PPM_T, l2, st>>>(a);
+    return check_launch("ppm_branches_fwd");
+  }
   if (dtype == DT_F32) ppm_fwd_kernel<float><<<a.nb, PPM_T, lds, st>>>(a);
   else if (dtype == DT_F16) ppm_fwd_kernel<f16><<<a.nb, PPM_T, lds, st>>>(a);
   else ppm_fwd_kernel<bf16><<<a.nb, PPM_T, lds, st>>>(a);
