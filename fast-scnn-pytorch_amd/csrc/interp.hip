@@ -577,32 +577,45 @@ int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st) {
 // feats: bin-major [50][N][CF] (CF = 32); y: concat NHWC [N,H,W] with row stride ldy, level i
 // written to channels [coff + i*CF, coff + (i+1)*CF).   (models/fast_scnn.py:139-143)
 
+// one thread per (pixel, 16-B channel vector of one level): the two lerps once per 4 / 8 channels
 template <typename T>
 __global__ __launch_bounds__(256) void ppm_up_fwd_kernel(PpmUpArgs a) {
+  constexpr int V = VecW<T>::V;
   long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int CT = 4 * a.CF;
-  long long total = (long long)a.N * a.H * a.W * CT;
+  const int CTV = 4 * a.CF / V;
+  long long total = (long long)a.N * a.H * a.W * CTV;
   if (t >= total) return;
-  int cc = (int)(t % CT);
-  long long pix = t / CT;
+  const int cc = (int)(t % CTV) * V;
+  long long pix = t / CTV;
   int w = (int)(pix % a.W);
   long long r = pix / a.W;
   int h = (int)(r % a.H);
   int n = (int)(r / a.H);
-  int lv = cc / a.CF, c = cc - lv * a.CF;
+  const int lv = cc / a.CF, c = cc - lv * a.CF;
   const int k = PP_LEVELS[lv];
   const int base = lv == 0 ? 0 : (lv == 1 ? 1 : (lv == 2 ? 5 : 14));
   Lerp lh = ac_lerp(h, k, a.H, ac_scale(k, a.H));
   Lerp lw = ac_lerp(w, k, a.W, ac_scale(k, a.W));
   const T* f = (const T*)a.feats;
-  auto F = [&](int i, int j) { return ld1(f + ((size_t)(base + i * k + j) * a.N + n) * a.CF + c); };
-  float o = lh.l0 * (lw.l0 * F(lh.i0, lw.i0) + lw.l1 * F(lh.i0, lw.i1)) +
-            lh.l1 * (lw.l0 * F(lh.i1, lw.i0) + lw.l1 * F(lh.i1, lw.i1));
-  st1((T*)a.y + pix * a.ldy + a.coff + cc, o);
+  float q[4][V];
+  ldv(f + ((size_t)(base + lh.i0 * k + lw.i0) * a.N + n) * a.CF + c, q[0]);
+  ldv(f + ((size_t)(base + lh.i0 * k + lw.i1) * a.N + n) * a.CF + c, q[1]);
+  ldv(f + ((size_t)(base + lh.i1 * k + lw.i0) * a.N + n) * a.CF + c, q[2]);
+  ldv(f + ((size_t)(base + lh.i1 * k + lw.i1) * a.N + n) * a.CF + c, q[3]);
+  float o[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j)
+    o[j] = lh.l0 * (lw.l0 * q[0][j] + lw.l1 * q[1][j]) + lh.l1 * (lw.l0 * q[2][j] + lw.l1 * q[3][j]);
+  stv((T*)a.y + pix * a.ldy + a.coff + cc, o);
 }
 
 int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
-  long long total = (long long)a.N * a.H * a.W * 4 * a.CF;
+  const int V = dtype == DT_F32 ? 4 : 8;
+  if (a.CF % V || a.ldy % V || a.coff % V) {
+    set_error("ppm_up_fwd: CF=%d ldy=%d coff=%d", a.CF, a.ldy, a.coff);
+    return E_UNSUPPORTED;
+  }
+  long long total = (long long)a.N * a.H * a.W * (4 * a.CF / V);
   unsigned grid = (unsigned)((total + 255) / 256);
   if (dtype == DT_F32) ppm_up_fwd_kernel<float><<<grid, 256, 0, st>>>(a);
   else if (dtype == DT_F16) ppm_up_fwd_kernel<f16><<<grid, 256, 0, st>>>(a);
