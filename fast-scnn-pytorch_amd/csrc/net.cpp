@@ -323,6 +323,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   }
   // fp64 team sums of the in-kernel BN finishes (last, so the activation offsets above do not move)
   if (train) pl.tsum = A.get((size_t)TAIL_TMAX * 3 * TAIL_CMAX * 8);
+  if (train) pl.tsum2 = A.get((size_t)TAIL_TMAX * 3 * TAIL_CMAX * 8);
   pl.ws_bytes = A.top;
   auto nm = [&](const char* n, size_t off, long long rows, int cols, int ld, int bws) {
     pl.named.push_back({n, off, rows, cols, ld, bws});
@@ -906,6 +907,15 @@ struct Exec {
     TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, act(pl.l1dw), true));
     TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2));
     TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, act(pl.l2dw), true));
+    // train: the FeatureFusionModule's high-res branch (conv_higher_res + its BN statistics, on
+    // the LTD output only) runs on the side stream beside the latency-bound global feature
+    // extractor; its BN finish uses the backward's counters and its own team-sum scratch, so it
+    // never shares arrival state with the main stream's producers; joined before the FFM apply
+    const bool fhigh_side = train && side != nullptr;
+    if (fhigh_side) {
+      TRY(fhigh_fwd(true));
+      TRY(flush_side());
+    }
     // ---- bottlenecks ----
     const void* x = W(pl.l2pw.a);
     int xld = 64;
@@ -998,13 +1008,8 @@ struct Exec {
         g.C = W(pl.flow.z); g.ldc = 128;
         gemm_fin(g, pl.flow, net.ffm_blow);
         TRY(gemm_nt(g, dt, r.st));
-        g_prof_tag = pl.fhigh.name.c_str();
-        const In hin = act(pl.l2pw);
-        g.K = 64; g.A = hin.p; g.lda = hin.ld; g.B = Wg(net.ffm_high); g.ldb = 64;
-        g.a_scale = hin.sc; g.a_shift = hin.sh;
-        g.shift = P(net.ffm_high.b); g.C = W(pl.fhigh.z);
-        gemm_fin(g, pl.fhigh, net.ffm_bhigh);
-        TRY(gemm_nt(g, dt, r.st));
+        if (fhigh_side) TRY(join());
+        else TRY(fhigh_fwd(false));
         BnApplyArgs a{};
         a.M = pl.flow.M; a.C = 128;
         a.z = W(pl.flow.z); a.ldz = 128; a.scale = Wf(pl.flow.scale); a.shift = Wf(pl.flow.shift);
@@ -1064,6 +1069,24 @@ struct Exec {
     u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
     u.x = W(pl.logits); u.ldx = pl.Cp; u.y = r.out; u.ldy = 0;
     return up_nchw(u, dt, r.out_dtype, r.st);
+  }
+
+  // FFM conv_higher_res (models/fast_scnn.py:202) + its BN statistics (train): on the side
+  // stream (queued for the next fork) or the caller's
+  int fhigh_fwd(bool on_side) {
+    g_prof_tag = pl.fhigh.name.c_str();
+    GemmArgs g{};
+    const In hin = act(pl.l2pw);
+    g.M = (int)pl.fhigh.M; g.N = 128; g.K = 64; g.A = hin.p; g.lda = hin.ld;
+    g.a_scale = hin.sc; g.a_shift = hin.sh;
+    g.B = Wg(net.ffm_high); g.ldb = 64; g.shift = P(net.ffm_high.b);
+    g.C = W(pl.fhigh.z); g.ldc = 128;
+    gemm_fin(g, pl.fhigh, net.ffm_bhigh);
+    if (!on_side) return gemm_nt(g, dt, r.st);
+    g.tail.counters = (unsigned*)W(pl.bcnt);
+    g.tail.tsum = (double*)W(pl.tsum2);
+    const int dtc = dt;
+    return side_launch([g, dtc](hipStream_t s) { return gemm_nt(g, dtc, s); });
   }
 
   // aux head (models/fast_scnn.py:24-31,42-45) on the LearningToDownsample output l2pw.a
@@ -1693,6 +1716,7 @@ int net_forward(const Plan& pl, const RunArgs& r) {
     RunArgs rr = r;
     rr.st = st;
     Exec ex(pl, rr);
+    ex.use_side();
     return ex.forward();
   });
 }

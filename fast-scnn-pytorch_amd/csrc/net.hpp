@@ -116,6 +116,7 @@ struct Plan {
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   size_t fcnt = 0, bcnt = 0;        // BN arrival counters (ws), BN_COUNTERS each
   size_t tsum = 0;                  // fp64 team sums of the in-kernel BN finishes (ws)
+  size_t tsum2 = 0;                 // ... of the forward's side-stream producer (FFM high-res)
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
