@@ -7,7 +7,7 @@
 // channels with the 864 weights broadcast from LDS, and the 256x32 tile is written back through
 // LDS as one contiguous, fully coalesced block.  HBM-bound: 12 B (fp32 in) read + 128 B written
 // per output pixel against 1,728 flops.
-#include "kernels.hpp"
+#include "bn_finish.hpp"
 
 namespace fscnn {
 
@@ -665,6 +665,387 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
   else CW_LAUNCH(bf16);
 #undef CW_LAUNCH
   return check_launch("conv0_wgrad");
+}
+
+// ---- fused: LearningToDownsample.dsconv1.dw input gradient + conv0 weight gradient --------------
+// The stride-2 depthwise dgrad (dwconv.hip dw_dgrad_s2, same thread tile and arithmetic: a thread
+// owns dx rows h0, h0+1 x columns w0..w0+3 of 4 channels) produces g, the gradient of conv0's BN
+// output, which only conv0's weight gradient consumes.  Rather than storing g (268 MB at cfg3) and
+// streaming it back with z in a second launch, the workgroup keeps its tile of masked g and of z
+// in LDS as [pixel][channel] images (64-B rows, one 8-B store per thread and pixel), gathers the
+// conv0 patches x^T [tap][pixel] beside them, and accumulates A = sum x g^T and Zx = sum x z^T with
+// v_mfma_f32_32x32x16 (taps x channels, k = 16 pixels): the A operand is one ds_read_b128 of x^T,
+// the B operands are read column-wise with ds_read_b64_tr_b16 (gfx950's transposing LDS read).
+// BN backward is linear in g, z and 1 per channel (bwdx_apply: dz = al*g + gz*z + be), so the
+// conv0 gradient is dW = al*A + gz*Zx + be*B with B = sum x, formed after the BN finish
+// (conv0_wgrad_combine) — the BN's statistics of g are no longer needed before the pass over g.
+// Persistent: LC_MAXP workgroups walk contiguous tile ranges; one BN record and one LC0_SLAB
+// partial row per workgroup (fixed-order reductions: deterministic).
+constexpr int LC_TW = 128;           // tile: 2 dx rows x 128 columns = 256 pixels
+constexpr int LC_LDX = 256 + 8;      // x^T image row stride (elements): conflict-free b128 reads
+constexpr int LC_MAXP = 512;         // 2 workgroups per CU
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T>
+__device__ __forceinline__ void lc_mma(const i16x8& a, const i16x8& b, f32x16& acc) {
+  if constexpr (std::is_same<T, f16>::value) {
+    h16x8 ah, bh;
+    __builtin_memcpy(&ah, &a, 16);
+    __builtin_memcpy(&bh, &b, 16);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+}
+// 4 x 16-bit storage elements (8 B) <-> fp32
+template <typename T>
+__device__ __forceinline__ void lc_unpack4(const uint2& t, float (&v)[4]) {
+  v[0] = s16_to<T>((uint16_t)(t.x & 0xFFFFu)); v[1] = s16_to<T>((uint16_t)(t.x >> 16));
+  v[2] = s16_to<T>((uint16_t)(t.y & 0xFFFFu)); v[3] = s16_to<T>((uint16_t)(t.y >> 16));
+}
+template <typename T>
+__device__ __forceinline__ uint2 lc_pack4(const float (&v)[4]) {
+  uint2 t;
+  t.x = (uint32_t)s16_from<T>(v[0]) | ((uint32_t)s16_from<T>(v[1]) << 16);
+  t.y = (uint32_t)s16_from<T>(v[2]) | ((uint32_t)s16_from<T>(v[3]) << 16);
+  return t;
+}
+__device__ __forceinline__ i16x4 lc_tr(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)p);
+}
+
+template <typename T, int XB, bool TL>
+__global__ __launch_bounds__(256, 2) void ltd_c0_bwd_kernel(LtdC0BwdArgs a) {
+  constexpr int V = 4;
+  constexpr int SG = 256 * 32 * 2;  // bytes of one [pixel][channel] image
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[2 * SG + 32 * LC_LDX * 2];
+  uint16_t* sG = reinterpret_cast<uint16_t*>(s_raw);           // masked g [pixel][channel]
+  uint16_t* sZ = reinterpret_cast<uint16_t*>(s_raw + SG);      // z [pixel][channel]
+  uint16_t* sX = reinterpret_cast<uint16_t*>(s_raw + 2 * SG);  // x^T [tap][pixel]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tx = tid & 7, ty = tid >> 3;  // channel quad, 4-column group
+  const int cb = tx * V;
+  for (int i = tid; i < 5 * LC_LDX; i += 256) sX[27 * LC_LDX + i] = 0;  // taps 27..31: zero
+
+  // depthwise taps [tap][channel] and conv0's BN (mean, invstd, ReLU-mask affine) per channel,
+  // read from LDS where used (in registers they would cost 52 VGPRs of the 2-wave budget)
+  __shared__ __attribute__((aligned(16))) float s_wt[9 * 32];
+  __shared__ __attribute__((aligned(16))) float s_bn[4 * 32];
+  for (int i = tid; i < 9 * 32; i += 256) s_wt[(i % 9) * 32 + i / 9] = a.w[i];
+  if (tid < 32) {
+    const bool m2 = a.bs.mode == 2;
+    s_bn[tid] = a.bs.mean[tid];
+    s_bn[32 + tid] = a.bs.invstd[tid];
+    s_bn[64 + tid] = m2 ? a.bs.scale[tid] : 0.f;  // mode 0: fmaf(z, 0, 1) > 0 always
+    s_bn[96 + tid] = m2 ? a.bs.shift[tid] : 1.f;
+  }
+  __syncthreads();
+  float s1[V], s2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
+  float bx[3][3];  // sums of the x^T values this thread stages ((pair, kw) fixed per thread)
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bx[i][k] = 0.f;
+  f32x16 accA, accZ;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) accA[r] = accZ[r] = 0.f;
+
+  const int CB = cdiv(a.W, LC_TW), RP = (a.H + 1) / 2;
+  const long long tiles = (long long)a.N * RP * CB;
+  const size_t XHW = (size_t)a.XH * a.XW;
+  const long long t_end = tiles * (blockIdx.x + 1) / gridDim.x;
+  for (long long t = tiles * blockIdx.x / gridDim.x; t < t_end; ++t) {
+    const int cbk = (int)(t % CB);
+    const long long nr = t / CB;
+    const int n = (int)(nr / RP), hp = (int)(nr - (long long)n * RP);
+    const int h0 = 2 * hp, wc0 = cbk * LC_TW, w0 = wc0 + 4 * ty;
+    // ---- every global load first: dy 2 x 3, z 2 x 4 (8 B each), the x rows of the patches ---
+    uint2 gr[2][3], zr[2][4];
+    const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * 32 + cb;
+#pragma unroll
+    for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+      for (int dc = 0; dc < 3; ++dc) {
+        const int ho = hp + dr, wo = w0 / 2 + dc;
+        const bool ok = ho < a.Ho && wo < a.Wo && w0 < a.W;
+        const uint2 v = *reinterpret_cast<const uint2*>(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * 32);
+        gr[dr][dc] = ok ? v : make_uint2(0u, 0u);
+      }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = h0 + r < a.H && w0 + q < a.W;
+        const size_t pix = ok ? ((size_t)n * a.H + h0 + r) * a.W + w0 + q : 0;
+        const uint2 v = *reinterpret_cast<const uint2*>((const T*)a.bs.z + pix * 32 + cb);
+        zr[r][q] = ok ? v : make_uint2(0u, 0u);
+      }
+    // x^T staging items i = tid + 256 * it -> (pair = (ci, kh) = i >> 6, row r, column group u):
+    // 9 consecutive image columns 2w .. 2w + 8 of one row give taps kw = 0..2 of 4 pixels
+    uint4 xr[3][XB ? 1 : 2];  // 8 columns (raw), the 9th as fp32
+    float x8[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int i = tid + 256 * it;
+      if (i >= 576) break;  // (wave-uniform: it = 2 is wave 0's alone)
+      const int pair = i >> 6, r = (i >> 5) & 1, u = i & 31;
+      const int ci = pair / 3, kh = pair - 3 * ci;
+      const int h = h0 + r, wq = wc0 + 4 * u;
+      const bool okr = h < a.H && wq < a.W;
+      const int col = okr ? 2 * wq : 0;
+      const size_t o = ((size_t)n * 3 + ci) * XHW + (size_t)(okr ? 2 * h + kh : 0) * a.XW + col;
+      const bool ok8 = okr && col + 8 < a.XW;
+      if constexpr (XB) {
+        xr[it][0] = *reinterpret_cast<const uint4*>((const uint16_t*)a.x + o);
+        const uint16_t e8 = ((const uint16_t*)a.x)[ok8 ? o + 8 : o];
+        x8[it] = ok8 ? in16<XB>(e8) : 0.f;
+      } else {
+        xr[it][0] = *reinterpret_cast<const uint4*>((const float*)a.x + o);
+        xr[it][1] = *reinterpret_cast<const uint4*>((const float*)a.x + o + 4);
+        const float e8 = ((const float*)a.x)[ok8 ? o + 8 : o];
+        x8[it] = ok8 ? e8 : 0.f;
+      }
+    }
+    // ---- dgrad (dw_dgrad_s2's arithmetic), the masked g rounded as stored, BN records ----------
+    uint2 gw[2][4];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      float acc[4][V];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[q][j] = 0.f;
+#pragma unroll
+      for (int dr = 0; dr < 2; ++dr) {
+        const int kh = r + 1 - 2 * dr;
+        if (kh < 0 || kh > 2) continue;
+#pragma unroll
+        for (int dc = 0; dc < 3; ++dc) {
+          float g[V];
+          lc_unpack4<T>(gr[dr][dc], g);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int kw = q + 1 - 2 * dc;
+            if (kw < 0 || kw > 2) continue;
+            const float4 w4 = *reinterpret_cast<const float4*>(s_wt + (kh * 3 + kw) * 32 + cb);
+            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[q][j] = fmaf(g[j], wv[j], acc[q][j]);
+          }
+        }
+      }
+      const float4 bm = *reinterpret_cast<const float4*>(s_bn + cb);
+      const float4 bi = *reinterpret_cast<const float4*>(s_bn + 32 + cb);
+      const float4 ms = *reinterpret_cast<const float4*>(s_bn + 64 + cb);
+      const float4 mh = *reinterpret_cast<const float4*>(s_bn + 96 + cb);
+      const float bmv[4] = {bm.x, bm.y, bm.z, bm.w}, biv[4] = {bi.x, bi.y, bi.z, bi.w};
+      const float msv[4] = {ms.x, ms.y, ms.z, ms.w}, mhv[4] = {mh.x, mh.y, mh.z, mh.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = h0 + r < a.H && w0 + q < a.W;
+        float z[V], gv[V];
+        lc_unpack4<T>(zr[r][q], z);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          float v = round_as<T>(acc[q][j]);
+          v = (ok && fmaf(z[j], msv[j], mhv[j]) > 0.f) ? v : 0.f;
+          s1[j] += v;
+          s2[j] += v * (z[j] - bmv[j]) * biv[j];
+          gv[j] = v;
+        }
+        gw[r][q] = lc_pack4<T>(gv);  // exact: v is a T value
+      }
+    }
+    // x^T values as T (pixels outside the output: 0), and their sums
+    uint2 xw[3][3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int i = tid + 256 * it;
+      if (i >= 576) break;
+      const int r = (i >> 5) & 1, u = i & 31;
+      const int h = h0 + r, wq = wc0 + 4 * u;
+      float xe[9];
+      if constexpr (XB) {
+        const uint32_t wv[4] = {xr[it][0].x, xr[it][0].y, xr[it][0].z, xr[it][0].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xe[2 * k] = in16<XB>((uint16_t)(wv[k] & 0xFFFFu));
+          xe[2 * k + 1] = in16<XB>((uint16_t)(wv[k] >> 16));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          xe[4 * k] = __uint_as_float(xr[it][k].x); xe[4 * k + 1] = __uint_as_float(xr[it][k].y);
+          xe[4 * k + 2] = __uint_as_float(xr[it][k].z); xe[4 * k + 3] = __uint_as_float(xr[it][k].w);
+        }
+      }
+      xe[8] = x8[it];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = h < a.H && wq + q < a.W;
+          v[q] = ok ? round_as<T>(xe[2 * q + kw]) : 0.f;
+        }
+        bx[it][kw] += (v[0] + v[1]) + (v[2] + v[3]);
+        xw[it][kw] = lc_pack4<T>(v);
+      }
+    }
+    __syncthreads();  // the previous tile's MFMA operand reads are done
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = r * 128 + 4 * ty + q;
+        *reinterpret_cast<uint2*>(sG + p * 32 + cb) = gw[r][q];
+        *reinterpret_cast<uint2*>(sZ + p * 32 + cb) = zr[r][q];
+      }
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int i = tid + 256 * it;
+      if (i >= 576) break;
+      const int pair = i >> 6, r = (i >> 5) & 1, u = i & 31;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+        *reinterpret_cast<uint2*>(sX + (pair * 3 + kw) * LC_LDX + r * 128 + 4 * u) = xw[it][kw];
+    }
+    __syncthreads();
+    // ---- MFMA: the wave's 64 pixels in 4 k-steps of 16; D[tap][channel] ---------------------
+    {
+      const int g4 = lane >> 4, li = lane & 15;
+      const int rq = 8 * (g4 >> 1) + (li >> 2), cc = 16 * (g4 & 1) + 4 * (li & 3);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k0 = wave * 64 + ks * 16;
+        i16x8 ax;
+        __builtin_memcpy(&ax, sX + (lane & 31) * LC_LDX + k0 + 8 * (lane >> 5), 16);
+        const uint16_t* pg = sG + (k0 + rq) * 32 + cc;
+        const uint16_t* pz = sZ + (k0 + rq) * 32 + cc;
+        const i16x4 g0 = lc_tr(pg), g1 = lc_tr(pg + 4 * 32);
+        const i16x4 z0 = lc_tr(pz), z1 = lc_tr(pz + 4 * 32);
+        const i16x8 bg = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        const i16x8 bz = {z0[0], z0[1], z0[2], z0[3], z1[0], z1[1], z1[2], z1[3]};
+        lc_mma<T>(ax, bg, accA);
+        lc_mma<T>(ax, bz, accZ);
+      }
+    }
+  }
+
+  // ---- conv0 partials: the 4 waves' accumulators summed in fixed order -----------------------
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(s_raw);  // [wave][A|Zx][32 tap][32 channel] (32 KB)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    red[((wave * 2 + 0) * 32 + m) * 32 + (lane & 31)] = accA[r];
+    red[((wave * 2 + 1) * 32 + m) * 32 + (lane & 31)] = accZ[r];
+  }
+  __syncthreads();
+  float* out = a.slab + (size_t)blockIdx.x * LC0_SLAB;
+  for (int o = tid; o < 1728; o += 256) {
+    const int k = o >= 864 ? 1 : 0, oo = o - 864 * k;
+    const int co = oo / 27, tap = oo - 27 * co;
+    const int e = (k * 32 + tap) * 32 + co;
+    out[o] = (red[e] + red[2048 + e]) + (red[4096 + e] + red[6144 + e]);
+  }
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    if (wave + 4 * it >= 9) break;  // (pair = wave + 4 * it, wave-uniform)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      float v = bx[it][kw];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) out[1728 + (wave + 4 * it) * 3 + kw] = v;
+    }
+  }
+  // ---- conv0 BN-backward record of the workgroup (the 32 column groups in fixed order) -------
+  float* s_br = reinterpret_cast<float*>(s_raw + 2 * SG);  // [256][2 V] (in x^T's space)
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    s_br[tid * 2 * V + j] = s1[j];
+    s_br[tid * 2 * V + V + j] = s2[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int kind = tid >> 5, c = tid & 31;
+    const int qx = c >> 2, j = c & 3;
+    float sum = 0.f;
+    for (int y = 0; y < 32; ++y) sum += s_br[(y * 8 + qx) * 2 * V + kind * V + j];
+    st_wt(a.bs.part + (size_t)blockIdx.x * 64 + kind * 32 + c, sum);
+  }
+  if constexpr (TL)
+    tail_finish<false>(a.bs.part, gridDim.x, 32, blockIdx.x, 0, 32, 0, a.tail,
+                       reinterpret_cast<double*>(s_raw));  // (>= 3 x 256 doubles)
+}
+
+int ltd_c0_bwd_parts(int N, int H, int W) {
+  const long long tiles = (long long)N * ((H + 1) / 2) * cdiv(W, LC_TW);
+  return (int)(tiles < LC_MAXP ? tiles : LC_MAXP);
+}
+
+bool ltd_c0_bwd_ok(int dtype, int x_dtype, int XW, const void* x) {
+  return (dtype == DT_BF16 || dtype == DT_F16) && x_dtype >= 0 && x_dtype <= 2 && XW % 8 == 0 &&
+         (uintptr_t)x % 16 == 0;
+}
+
+int ltd_c0_bwd(const LtdC0BwdArgs& a, int dtype, hipStream_t st) {
+  if (!ltd_c0_bwd_ok(dtype, a.x_dtype, a.XW, a.x) || a.H != (a.XH - 3) / 2 + 1 ||
+      a.W != (a.XW - 3) / 2 + 1 || a.Ho != (a.H - 1) / 2 + 1 || a.Wo != (a.W - 1) / 2 + 1) {
+    set_error("ltd_c0_bwd: unsupported shape / dtype / alignment");
+    return E_INVALID;
+  }
+  if (!a.bs.part || !a.bs.z || !a.bs.mean || !a.bs.invstd ||
+      (a.bs.mode == 2 && (!a.bs.scale || !a.bs.shift)) || !a.slab || (uintptr_t)a.w % 16 ||
+      (uintptr_t)a.dy % 8 || (uintptr_t)a.bs.z % 8) {
+    set_error("ltd_c0_bwd: inconsistent arguments");
+    return E_INVALID;
+  }
+  const int P = ltd_c0_bwd_parts(a.N, a.H, a.W);
+  const bool fin = a.tail.counters != nullptr;
+  const bool ink = fin && a.tail.tsum && tail_fits(P, 1);
+  {
+    const double px = (double)a.N * a.H * a.W;
+    ProfScope ps(PK_CONV0_WGRAD, st,
+                 2.0 * ((double)a.N * a.Ho * a.Wo * 32 + px * 32) +
+                     (a.x_dtype ? 2.0 : 4.0) * a.N * 3.0 * a.XH * a.XW + 36.0 * 32,
+                 18.0 * (double)a.N * a.Ho * a.Wo * 32 + 4.0 * 27 * 32 * px);
+#define LC_LAUNCH(T, XB)                                                              \
+  do {                                                                                \
+    if (ink) ltd_c0_bwd_kernel<T, XB, true><<<P, 256, 0, st>>>(a);                    \
+    else ltd_c0_bwd_kernel<T, XB, false><<<P, 256, 0, st>>>(a);                       \
+  } while (0)
+#define LC_LAUNCH_X(T)                            \
+  do {                                            \
+    if (a.x_dtype == 2) LC_LAUNCH(T, 2);          \
+    else if (a.x_dtype == 1) LC_LAUNCH(T, 1);     \
+    else LC_LAUNCH(T, 0);                         \
+  } while (0)
+    if (dtype == DT_F16) LC_LAUNCH_X(f16);
+    else LC_LAUNCH_X(bf16);
+#undef LC_LAUNCH_X
+#undef LC_LAUNCH
+    const int rc = check_launch("ltd_c0_bwd");
+    if (rc || !fin || ink) return rc;
+  }
+  return bn_bwd_finalize(a.bs.part, P, 32, a.tail.count, a.tail.dgamma, a.tail.dbeta, a.tail.coef,
+                         st, a.tail.counters, a.tail.tab);
+}
+
+__global__ void conv0_wgrad_combine_kernel(const float* s, const float* tab, float* dw) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= 864) return;
+  const int co = o / 27, tap = o - 27 * co;
+  const float* e = tab + (size_t)co * BWDX_STRIDE;  // al, be, gz (bn_finish.hpp bn_bwd_finish)
+  dw[o] = fmaf(e[0], s[o], fmaf(e[2], s[864 + o], e[1] * s[1728 + tap]));
+}
+
+int conv0_wgrad_combine(const float* sums, const float* tab, float* dw, hipStream_t st) {
+  conv0_wgrad_combine_kernel<<<cdiv(864, 256), 256, 0, st>>>(sums, tab, dw);
+  return check_launch("conv0_wgrad_combine");
 }
 
 }  // namespace fscnn

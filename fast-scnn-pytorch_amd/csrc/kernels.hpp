@@ -383,6 +383,30 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st);
 int conv0_wgrad_parts(int N, int Ho, int Wo, int rows_per_block);
 int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
 
+// LearningToDownsample.dsconv1.dw input gradient (stride 2) fused with the conv0 weight gradient
+// (conv0.hip ltd_c0_bwd).  The dgrad's output g is the gradient of conv0's BN output; the launch
+// emits that BN's backward records and finish (bs / tail, as dw_dgrad does) and, instead of
+// storing g, per-workgroup conv0 partials [P][LC0_SLAB] = (A = sum g x^T, Zx = sum z x^T,
+// B = sum x) over the conv0 patches x.  With the finished BN's operand table (common.hpp
+// bwdx_apply: dz = al*g + gz*z + be), conv0_wgrad_combine forms dW = al*A + gz*Zx + be*B.
+constexpr int LC0_SLAB = 2 * 864 + 27;  // [A: co*27+tap][Zx: 864 + co*27+tap][B: 1728 + tap]
+struct LtdC0BwdArgs {
+  int N, H, W;     // conv0 output = the depthwise layer's input (dx) dims
+  int Ho, Wo;      // depthwise output (dy) dims
+  const void* dy;  // NHWC [N,Ho,Wo,32]
+  const float* w;  // depthwise taps [32][9] (16-B aligned)
+  BnBwdPart bs{};  // conv0's BN (z, mean, invstd, scale, shift, mode); part [P][2][32]
+  BnTail tail{};   // its finish
+  const void* x;   // NCHW [N,3,XH,XW] image
+  int x_dtype, XH, XW;
+  float* slab;     // [P][LC0_SLAB]
+};
+int ltd_c0_bwd_parts(int N, int H, int W);
+bool ltd_c0_bwd_ok(int dtype, int x_dtype, int XW, const void* x);
+int ltd_c0_bwd(const LtdC0BwdArgs& a, int dtype, hipStream_t st);
+// dW[co][tap] = al*A + gz*Zx + be*B from the reduced LC0_SLAB sums and the table (BWDX_STRIDE)
+int conv0_wgrad_combine(const float* sums, const float* tab, float* dw, hipStream_t st);
+
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st);

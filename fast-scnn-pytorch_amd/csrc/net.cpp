@@ -438,6 +438,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pw_slab(M2, C, 128, true);                                 // classifier 1x1 (bias)
     if (net.aux) { pw_slab(M2, 32, 576); pw_slab(M2, C, 32, true); }
     add_slab((size_t)conv0_wgrad_parts(N, pl.H1, pl.W1, 8) * 864);
+    add_slab((size_t)ltd_c0_bwd_parts(N, pl.H1, pl.W1) * LC0_SLAB);  // (the fused form's)
     pl.slab_floats = slab;
     pl.slab = B.get(slab * 4);
     // BN backward partials: max P*2*C
@@ -475,6 +476,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     pl.bnpart_floats = bnp;
     pl.coef = B.get(2 * 1024 * 4);
     pl.xtab = B.get((size_t)pl.c0.C * BWDX_STRIDE * 4);  // Exec::tab_slot (conv0's BN)
+    pl.c0sum = B.get((size_t)LC0_SLAB * 4);  // reduced conv0 partials of the fused LTD backward
     pl.cspart = B.get((size_t)colsum_parts((int)M2) * (C > 128 ? C : 128) * 4);
     pl.bws_bytes = B.top;
     auto gu = [&](const std::string& n, const Unit& u) {
@@ -572,6 +574,16 @@ bool graphs_enabled();
 bool side_stream_enabled() {
   static const bool on = [] {
     const char* e = getenv("FSCNN_SIDE_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// FSCNN_LTD_FUSED=0: LTD.dsconv1.dw's input gradient stored and conv0's weight gradient as its
+// own launch (conv0_wgrad) instead of the fused ltd_c0_bwd (A/B; tests/test_gpu_switches.py)
+bool ltd_fused_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_LTD_FUSED");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -748,12 +760,17 @@ struct Exec {
   // slabs are reused only by kernels enqueued after these launches (same stream)
   // (on the side stream instead, behind the stage's wgrads, it measured no faster: 7.11 vs
   // 7.08-7.10 ms/step)
+  bool c0_combine = false;  // the stage's reduce produced the fused conv0 sums (ltd1_c0_bwd)
   int flush_reduce() {
     TRY(join());  // every wgrad slab of the table is written
     const int rc = reduce_slabs_multi(red, r.st);
     red = RedTable();
     slab_top = 0;
-    return rc;
+    if (rc || !c0_combine) return rc;
+    c0_combine = false;
+    g_prof_tag = "learning_to_downsample.conv (weight gradient)";
+    return conv0_wgrad_combine((const float*)Bw(pl.c0sum), (const float*)Bw(pl.xtab), G(net.c0.w),
+                               r.st);
   }
   int slab_oom() {
     set_error("backward: weight-gradient slab arena exhausted");
@@ -1354,6 +1371,7 @@ struct Exec {
       TRY(flush_side());
     }
     TRY(defer_reduce(d.slab, S, 9LL * C, G(c.w), C));
+    if (!dX) return OK;  // input gradient formed elsewhere (ltd1_c0_bwd)
     const bool br = bt.u && train;
     if (br) {
       const Unit& u = *bt.u;
@@ -1539,6 +1557,37 @@ struct Exec {
     return flush_side();  // the block's three wgrads behind one fork
   }
 
+  // LTD.dsconv1.dw input gradient + conv0's BN backward + conv0 weight gradient in one pass
+  // (conv0.hip ltd_c0_bwd); dW is formed from the reduced sums after the stage's reduce
+  int ltd1_c0_bwd(const Dz& d) {
+    g_prof_tag = "learning_to_downsample.dsconv1.dw + conv (backward, fused)";
+    const Unit& u = pl.c0;
+    LtdC0BwdArgs f{};
+    f.N = pl.N; f.H = pl.H1; f.W = pl.W1; f.Ho = pl.H2; f.Wo = pl.W2;
+    f.dy = d.p; f.w = P(net.ltd1.dw.w);
+    f.bs.part = (float*)Bw(pl.bnpart);
+    f.bs.z = W(u.z);
+    f.bs.mean = Wf(u.mean); f.bs.invstd = Wf(u.invstd);
+    f.bs.scale = Wf(u.scale); f.bs.shift = Wf(u.shift);
+    f.bs.mode = 2;
+    f.tail.counters = (unsigned*)W(pl.bcnt);
+    f.tail.tsum = (double*)W(pl.tsum);
+    f.tail.count = (double)u.M;
+    f.tail.dgamma = G(net.b0.g);
+    f.tail.dbeta = G(net.b0.b);
+    f.tail.coef = (float*)Bw(pl.coef);
+    f.tail.tab = bwd_tab(u, true, tab_slot(u));
+    f.x = r.x; f.x_dtype = r.x_dtype; f.XH = pl.H; f.XW = pl.W;
+    const int S = ltd_c0_bwd_parts(pl.N, pl.H1, pl.W1);
+    f.slab = slab_alloc((size_t)S * LC0_SLAB);
+    if (!f.slab) return slab_oom();
+    TRY(ltd_c0_bwd(f, dt, r.st));
+    u.bdone.set();
+    TRY(defer_reduce(f.slab, S, LC0_SLAB, (float*)Bw(pl.c0sum), 0));
+    c0_combine = true;
+    return OK;
+  }
+
   int backward_ltd() {
     Dz d;
     TRY(bn_bwd_x(pl.l2pw, net.ltd2.bpw, Bw(pl.l2pw.ga), 64, true, dz_buf(pl.l2pw), d));
@@ -1552,6 +1601,11 @@ struct Exec {
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
     TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(pl.l1dw), d));
+    if (ltd_fused_enabled() && ltd_c0_bwd_ok(dt, r.x_dtype, pl.W, r.x)) {
+      TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, nullptr));
+      TRY(ltd1_c0_bwd(d));
+      return flush_side();
+    }
     TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
                relu_target(pl.c0, net.b0)));
     TRY(flush_side());

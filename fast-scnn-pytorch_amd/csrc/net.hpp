@@ -120,7 +120,7 @@ struct Plan {
   // backward workspace
   size_t g_logits = 0, t_up = 0, g_drop = 0, g_f = 0, g_up = 0, t_up2 = 0, g_concat = 0,
          g_feats = 0, g_pooled = 0, dz = 0, slab = 0, bnpart = 0, coef = 0, cspart = 0,
-         g_aux = 0, g_auxlog = 0, aux_dcol = 0, xtab = 0;
+         g_aux = 0, g_auxlog = 0, aux_dcol = 0, xtab = 0, c0sum = 0;
   size_t dz_bytes = 0;             // the dz arena (one slot per unit, Exec::dz_buf)
   size_t bnpart_floats = 0;        // capacity of the BN-backward record arena (bnpart)
   // named buffers for debugging / stage-level parity: name -> (offset, rows, cols, ld, in_bws)

@@ -2,8 +2,9 @@
 switches once per process).  Three fp32 train steps with Dropout(0.1) active and dropout seeds
 5, 9, 5 — alternating the unfused ``model(x)`` + CE path and the fused ``forward_loss`` head —
 then saves every step's loss and flat gradient arena, and the step-3 running statistics.
+With ``bf16`` the image is bf16 (the bf16 train plan, cfg3's arithmetic).
 
-    python tests/_switch_worker.py OUT.npz
+    python tests/_switch_worker.py OUT.npz [bf16]
 """
 import os
 import sys
@@ -12,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(out):
+def main(out, half=None):
     import numpy as np
     import torch
     import _fscnn_boot
@@ -29,6 +30,8 @@ def main(out):
     m = m.to(dev).train()
     shape = (2, 3, 96, 160)
     x = torch.from_numpy(portable_init.input_tensor(3, shape)).to(dev)
+    if half == "bf16":
+        x = x.to(torch.bfloat16)
     t = torch.from_numpy(portable_init.target_tensor(4, (2, 96, 160), 19, 0.05)).to(dev)
     res = {}
     for i, seed in enumerate((5, 9, 5, 9)):
@@ -39,6 +42,8 @@ def main(out):
         torch.cuda.synchronize()
         res["loss%d" % i] = np.float32(loss.item())
         res["grad%d" % i] = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu().numpy()
+    res["sizes"] = np.array([p.numel() for p in m.parameters()], dtype=np.int64)
+    res["names"] = np.array([k for k, _ in m.named_parameters()])
     for k, v in m.state_dict().items():
         if "running" in k:
             res["bn." + k] = v.cpu().numpy()
@@ -46,4 +51,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

@@ -6,7 +6,9 @@ fresh child process:
 * ``FSCNN_F32_SPLIT=0``   — exact fp32 MFMA in the eval pointwise GEMMs instead of the
   three-way bf16 split of each fp32 operand;
 * ``FSCNN_GRAPHS=1``      — whole forward / backward-stage calls captured into hipGraphs and
-  replayed (the dropout seed then travels through a device slot the forward writes).
+  replayed (the dropout seed then travels through a device slot the forward writes);
+* ``FSCNN_LTD_FUSED=0``   — (16-bit train plans) LTD.dsconv1.dw's input gradient stored and
+  conv0's weight gradient its own launch, instead of the fused ltd_c0_bwd pass.
 
 Each child re-runs the oracle / golden parity tests that cover the path (fp32 train golden +
 bf16 emulated budget; eval goldens for the fp32 GEMM switch).  The graph switch also replays
@@ -31,7 +33,8 @@ EVAL = ["tests/test_gpu_model.py::test_eval_fp32_vs_golden",
         "tests/test_gpu_model.py::test_eval_fp32_literal_configs",
         "tests/test_gpu_model.py::test_eval_odd_sizes_vs_oracle",
         "tests/test_gpu_fullsize.py::test_eval_goldens_argmax_bit_exact"]
-CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL, "FSCNN_GRAPHS=1": TRAIN + EVAL}
+CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL, "FSCNN_GRAPHS=1": TRAIN + EVAL,
+         "FSCNN_LTD_FUSED=0": TRAIN[-1:]}
 
 
 def _env(switch):
@@ -53,9 +56,10 @@ def test_switch_keeps_oracle_parity(switch):
     assert r.returncode == 0, "%s: parity tests failed\n%s" % (switch, tail)
 
 
-def _worker(tmp_path, switch):
-    out = str(tmp_path / ("%s.npz" % (switch or "default").replace("=", "_")))
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_switch_worker.py"), out],
+def _worker(tmp_path, switch, half=None):
+    out = str(tmp_path / ("%s%s.npz" % ((switch or "default").replace("=", "_"), half or "")))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_switch_worker.py"), out] +
+                       ([half] if half else []),
                        cwd=ROOT, env=_env(switch), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     return dict(np.load(out))
@@ -72,3 +76,28 @@ def test_switch_train_steps_bit_identical_with_dropout(tmp_path, switch):
     assert np.array_equal(ref["grad0"], ref["grad2"])
     for k in ref:
         assert np.array_equal(ref[k], got[k]), "%s: %s differs" % (switch, k)
+
+
+def test_ltd_fused_backward_matches_two_pass(tmp_path):
+    """The fused LTD.dsconv1.dw-dgrad + conv0-wgrad pass (conv0.hip ltd_c0_bwd) against the
+    two-launch form it replaces, bf16 train plan, 4 steps: every gradient other than conv0's
+    weight and its BN's gamma / beta is bit-identical (the fused pass changes no other value); those
+    three differ only by summation order and by dz no longer being rounded to bf16 before the
+    product (dW = al*A + gz*Zx + be*B in fp32): within 1e-2 of the tensor's max |value|."""
+    ref = _worker(tmp_path, "FSCNN_LTD_FUSED=0", "bf16")
+    got = _worker(tmp_path, None, "bf16")
+    names = [str(n) for n in ref["names"]]
+    off = np.concatenate([[0], np.cumsum(ref["sizes"])])
+    loose = {"learning_to_downsample.conv.conv.0.weight", "learning_to_downsample.conv.conv.1.weight",
+             "learning_to_downsample.conv.conv.1.bias"}
+    assert loose <= set(names)
+    for i in range(4):
+        assert ref["loss%d" % i] == got["loss%d" % i]
+        a, b = ref["grad%d" % i], got["grad%d" % i]
+        for j, n in enumerate(names):
+            x, y = a[off[j]:off[j + 1]], b[off[j]:off[j + 1]]
+            if n in loose:
+                scale = float(np.abs(x).max())
+                assert scale > 0 and float(np.abs(x - y).max()) <= 1e-2 * scale, (i, n)
+            else:
+                assert np.array_equal(x, y), (i, n)
