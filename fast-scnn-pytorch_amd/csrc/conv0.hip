@@ -752,14 +752,14 @@ __global__ __launch_bounds__(256, 2) void ltd_c0_bwd_kernel(LtdC0BwdArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) accA[r] = accZ[r] = 0.f;
 
+  // tile t -> (image n, row pair hp, column block cbk); < 2^31 tiles (host check)
   const int CB = cdiv(a.W, LC_TW), RP = (a.H + 1) / 2;
-  const long long tiles = (long long)a.N * RP * CB;
+  const int tiles = a.N * RP * CB;
   const size_t XHW = (size_t)a.XH * a.XW;
-  const long long t_end = tiles * (blockIdx.x + 1) / gridDim.x;
-  for (long long t = tiles * blockIdx.x / gridDim.x; t < t_end; ++t) {
-    const int cbk = (int)(t % CB);
-    const long long nr = t / CB;
-    const int n = (int)(nr / RP), hp = (int)(nr - (long long)n * RP);
+  const int t_end = (int)((long long)tiles * (blockIdx.x + 1) / gridDim.x);
+  for (int t = (int)((long long)tiles * blockIdx.x / gridDim.x); t < t_end; ++t) {
+    const int nr = t / CB, cbk = t - nr * CB;
+    const int n = nr / RP, hp = nr - n * RP;
     const int h0 = 2 * hp, wc0 = cbk * LC_TW, w0 = wc0 + 4 * ty;
     // ---- every global load first: dy 2 x 3, z 2 x 4 (8 B each), the x rows of the patches ---
     uint2 gr[2][3], zr[2][4];
@@ -770,7 +770,7 @@ __global__ __launch_bounds__(256, 2) void ltd_c0_bwd_kernel(LtdC0BwdArgs a) {
       for (int dc = 0; dc < 3; ++dc) {
         const int ho = hp + dr, wo = w0 / 2 + dc;
         const bool ok = ho < a.Ho && wo < a.Wo && w0 < a.W;
-        const uint2 v = *reinterpret_cast<const uint2*>(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * 32);
+        const uint2 v = *reinterpret_cast<const uint2*>(gb + (ok ? ho * a.Wo + wo : 0) * 32);
         gr[dr][dc] = ok ? v : make_uint2(0u, 0u);
       }
 #pragma unroll
@@ -1002,6 +1002,11 @@ int ltd_c0_bwd(const LtdC0BwdArgs& a, int dtype, hipStream_t st) {
       (a.bs.mode == 2 && (!a.bs.scale || !a.bs.shift)) || !a.slab || (uintptr_t)a.w % 16 ||
       (uintptr_t)a.dy % 8 || (uintptr_t)a.bs.z % 8) {
     set_error("ltd_c0_bwd: inconsistent arguments");
+    return E_INVALID;
+  }
+  if ((long long)a.N * ((a.H + 1) / 2) * cdiv(a.W, LC_TW) > 0x7fffffffLL ||
+      (long long)a.Ho * a.Wo > 0x7fffffffLL / 32) {
+    set_error("ltd_c0_bwd: tensor too large");
     return E_INVALID;
   }
   const int P = ltd_c0_bwd_parts(a.N, a.H, a.W);

@@ -136,12 +136,32 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
           const bool valid = ti >= 0;
           const f32x2 w1 = {lw.l1, lw.l1};
           f32x2 e[CP];
-          float mx = -INFINITY;
 #pragma unroll
-          for (int p = 0; p < CP; ++p) {
-            e[p] = __builtin_elementwise_fma(w1, dv[p], v0[p]);
-            if (2 * p < Cm) mx = fmaxf(mx, e[p].x);
-            if (2 * p + 1 < Cm) mx = fmaxf(mx, e[p].y);
+          for (int p = 0; p < CP; ++p) e[p] = __builtin_elementwise_fma(w1, dv[p], v0[p]);
+          // class max as a tree of 3-input maxima (v_max3_f32): a short dependency chain
+          float mx;
+          {
+            float m[2 * CP];
+#pragma unroll
+            for (int p = 0; p < CP; ++p) {
+              m[2 * p] = 2 * p < Cm ? e[p].x : -INFINITY;
+              m[2 * p + 1] = 2 * p + 1 < Cm ? e[p].y : -INFINITY;
+            }
+            int k = 2 * CP;
+#pragma unroll
+            for (int lvl = 0; lvl < 6; ++lvl) {
+              if (k == 1) break;
+              const int k3 = (k + 2) / 3;
+#pragma unroll
+              for (int i = 0; i < k3; ++i) {
+                const float x0 = m[3 * i];
+                const float x1 = 3 * i + 1 < k ? m[3 * i + 1] : x0;
+                const float x2 = 3 * i + 2 < k ? m[3 * i + 2] : x0;
+                m[i] = fmaxf(fmaxf(x0, x1), x2);
+              }
+              k = k3;
+            }
+            mx = m[0];
           }
           // the target's logit, re-interpolated from the staged rows with the same operations
           // (an LDS gather instead of a select over every class)
@@ -152,21 +172,35 @@ __global__ __launch_bounds__(HD_T) void ce_head_kernel(CeHeadArgs a) {
             const float v1t = fmaf(lh.l1, L1[SL + tc], lh.l0 * L0[SL + tc]);
             lt = fmaf(lw.l1, v1t - v0t, v0t);
           }
-          // v_exp_f32 (2^x) of packed differences, packed partial sums (the loss keeps an
-          // accurate logf)
+          // v_exp_f32 (2^x) of packed differences; the loss takes v_log_f32 (log2) of the sum
           const f32x2 mm = {mx, mx};
-          f32x2 sp = {0.f, 0.f};
 #pragma unroll
           for (int p = 0; p < CP; ++p) {
             const f32x2 d = e[p] - mm;
             e[p].x = 2 * p < Cm ? __builtin_amdgcn_exp2f(d.x) : 0.f;
             e[p].y = 2 * p + 1 < Cm ? __builtin_amdgcn_exp2f(d.y) : 0.f;
-            sp += e[p];
           }
-          const float se = sp.x + sp.y;
+          // packed pair sums as a tree (fixed order; short dependency chain)
+          float se;
+          {
+            f32x2 sp[CP];
+#pragma unroll
+            for (int p = 0; p < CP; ++p) sp[p] = e[p];
+            int k = CP;
+#pragma unroll
+            for (int lvl = 0; lvl < 6; ++lvl) {
+              if (k == 1) break;
+              const int k2 = (k + 1) / 2;
+#pragma unroll
+              for (int i = 0; i < k / 2; ++i) sp[i] = sp[2 * i] + sp[2 * i + 1];
+              if (k & 1) sp[k / 2] = sp[k - 1];
+              k = k2;
+            }
+            se = sp[0].x + sp[0].y;
+          }
           const float inv = valid ? __builtin_amdgcn_rcpf(se) : 0.f;  // v_rcp_f32 (1 ulp)
           if (valid) {
-            loss += (mx - lt) * HD_LN2 + logf(se);
+            loss += (mx - lt + __builtin_amdgcn_logf(se)) * HD_LN2;  // v_log_f32: log2
             cnt += 1.f;
           }
           // the four tap products as two packed pairs (v_pk_fma_f32: (00, 01) and (10, 11))
