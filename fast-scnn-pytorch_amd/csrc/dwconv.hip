@@ -764,7 +764,9 @@ static int dw_wgrad_tpb(int N, int Ho, int Wo, int C, int V, int S, dim3& grid, 
   grid = dw_grid(N, Ho, Wo, C, V, S, cbv);
   const long long tiles_w = grid.y;
   const long long blocks = (long long)grid.x * grid.y * grid.z;
-  long long tpb = blocks / 2048;  // ~2048 workgroups; bounded partial count
+  // ~1024 workgroups (bounded partial count): at cfg3 6.05-6.07 ms/step against 6.10-6.11 for
+  // 2048 and 6.12-6.15 for 4096 (A/B pairs on one box); 512 / 768 within noise of 1024
+  long long tpb = blocks / 1024;
   if (tpb < 1) tpb = 1;
   if (tpb > tiles_w) tpb = tiles_w;
   grid.y = (unsigned)cdiv((int)tiles_w, (int)tpb);
