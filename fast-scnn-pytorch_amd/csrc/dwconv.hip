@@ -444,45 +444,32 @@ static void dw_block_shape(int C, int V, int& bx, int& by) {
 // and 200 / 79 us for a one-column walker over 8 rows with the taps staged in LDS.)
 constexpr int DWD2_V = 4;  // channels per thread
 template <typename T, bool BR, bool TL = false>
-__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
+__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a, int rpw) {
   constexpr int V = DWD2_V;
   const int tx = threadIdx.x, ty = threadIdx.y, BX = blockDim.x, BY = blockDim.y;
-  int bx, by, bz;
-  dw_tile(bx, by, bz);
+  int bx, by, bzg;
+  dw_tile(bx, by, bzg);
   const int cv = bx * BX + tx;
   const int CV = a.C / V;
   const int nb = (a.H + 1) / 2;
-  const int n = bz / nb;
-  const int h0 = (bz - n * nb) * 2;
   const int w0 = (by * BY + ty) * 4;
   const bool active = cv < CV && w0 < a.W;
   if (!BR && !active) return;  // (BR: every thread joins the workgroup reduction)
   const int cvc = active ? cv : 0;
   const int cb = cvc * V;
-  // ---- every global load of the thread first: dy (2 x 3 vectors), BR: z (2 x 4), weights -----
-  const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + cb;
-  const int hb = h0 / 2, wb = w0 / 2;
-  float g[2][3][V];
-#pragma unroll
-  for (int dr = 0; dr < 2; ++dr)
-#pragma unroll
-    for (int dc = 0; dc < 3; ++dc) {
-      const int ho = hb + dr, wo = wb + dc;
-      const bool ok = active && ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
-      ld4v(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * a.C, g[dr][dc]);
-#pragma unroll
-      for (int j = 0; j < V; ++j) g[dr][dc][j] = ok ? g[dr][dc][j] : 0.f;
-    }
-  float z[BR ? 2 : 1][BR ? 4 : 1][V];
+  __shared__ float s_bc[4][64 * V];  // BR: mean, invstd, mask scale, mask shift of the channels
   if constexpr (BR) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = active && h0 + r < a.H && w0 + q < a.W;
-        const size_t pix = ok ? ((size_t)n * a.H + h0 + r) * a.W + w0 + q : 0;
-        ld4v((const T*)a.bs.z + pix * a.C + cb, z[r][q]);
-      }
+    const BnBwdPart& b = a.bs;
+    const bool m2 = b.mode == 2;
+    const int c0b = bx * BX * V;
+    for (int i = ty * BX + tx; i < BX * V; i += BX * BY) {
+      const int c = min(c0b + i, a.C - 1);
+      s_bc[0][i] = b.mean[c];
+      s_bc[1][i] = b.invstd[c];
+      s_bc[2][i] = m2 ? b.scale[c] : 0.f;  // mode 0: mask fmaf(z, 0, 1) > 0 always
+      s_bc[3][i] = m2 ? b.shift[c] : 1.f;
+    }
+    __syncthreads();
   }
   float wt[9][V];
   const float4* wp = reinterpret_cast<const float4*>(a.w + (size_t)cb * 9);  // 36 floats, 16-B aligned
@@ -496,73 +483,95 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
       wt[f % 9][f / 9] = tt[e];
     }
   }
-  float acc[2][4][V];
+  float s1[V], s2[V];
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+  for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
+  // rpw consecutive row pairs per workgroup (one BN record for all of them: P stays within the
+  // in-kernel finish's reach)
+  for (int k = 0; k < rpw; ++k) {
+    const int bz = bzg * rpw + k;
+    if (bz >= a.N * nb) break;  // (workgroup-uniform)
+    const int n = bz / nb;
+    const int h0 = (bz - n * nb) * 2;
+    // ---- every global load of the thread first: dy (2 x 3 vectors), BR: z (2 x 4) -----------
+    const T* gb = (const T*)a.dy + (size_t)n * a.Ho * a.Wo * a.C + cb;
+    const int hb = h0 / 2, wb = w0 / 2;
+    float g[2][3][V];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int dr = 0; dr < 2; ++dr)
 #pragma unroll
-      for (int j = 0; j < V; ++j) acc[r][q][j] = 0.f;
+      for (int dc = 0; dc < 3; ++dc) {
+        const int ho = hb + dr, wo = wb + dc;
+        const bool ok = active && ho < a.Ho && wo < a.Wo;  // branch-free clamped load + select
+        ld4v(gb + (ok ? (size_t)ho * a.Wo + wo : 0) * a.C, g[dr][dc]);
 #pragma unroll
-  for (int dr = 0; dr < 2; ++dr)
+        for (int j = 0; j < V; ++j) g[dr][dc][j] = ok ? g[dr][dc][j] : 0.f;
+      }
+    float z[BR ? 2 : 1][BR ? 4 : 1][V];
+    if constexpr (BR) {
 #pragma unroll
-    for (int dc = 0; dc < 3; ++dc)
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        // dx row h0+r reads dy row hb+dr with kh = (h0 + r) + 1 - 2*(hb+dr)
-        const int kh = r + 1 - 2 * dr;
-        if (kh < 0 || kh > 2) continue;
+      for (int r = 0; r < 2; ++r)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int kw = q + 1 - 2 * dc;
-          if (kw < 0 || kw > 2) continue;
-#pragma unroll
-          for (int j = 0; j < V; ++j) acc[r][q][j] = fmaf(g[dr][dc][j], wt[kh * 3 + kw][j], acc[r][q][j]);
+          const bool ok = active && h0 + r < a.H && w0 + q < a.W;
+          const size_t pix = ok ? ((size_t)n * a.H + h0 + r) * a.W + w0 + q : 0;
+          ld4v((const T*)a.bs.z + pix * a.C + cb, z[r][q]);
         }
-      }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    if (!active || h0 + r >= a.H) continue;
-    T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + cb;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (w0 + q < a.W) st4v(db + (size_t)q * a.C, acc[r][q]);
-  }
-  if constexpr (BR) {
-    // ---- BN-backward partial sums of the stored dx (the dy of that BN), one record per
-    // workgroup: the BY column groups of a channel quad summed in fixed order
-    __shared__ float s_br[256 * 2 * V];
-    __shared__ float s_bc[4][64 * V];  // mean, invstd, mask scale, mask shift of the channels
-    const BnBwdPart& b = a.bs;
-    const bool m2 = b.mode == 2;
-    {
-      const int c0b = bx * BX * V;
-      for (int i = ty * BX + tx; i < BX * V; i += BX * BY) {
-        const int c = min(c0b + i, a.C - 1);
-        s_bc[0][i] = b.mean[c];
-        s_bc[1][i] = b.invstd[c];
-        s_bc[2][i] = m2 ? b.scale[c] : 0.f;  // mode 0: mask fmaf(z, 0, 1) > 0 always
-        s_bc[3][i] = m2 ? b.shift[c] : 1.f;
-      }
     }
-    __syncthreads();
-    float s1[V], s2[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
+    float acc[2][4][V];
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = active && h0 + r < a.H && w0 + q < a.W;
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-          const int cl = tx * V + j;
-          float gv = round_as<T>(acc[r][q][j]);
-          gv = (ok && fmaf(z[r][q][j], s_bc[2][cl], s_bc[3][cl]) > 0.f) ? gv : 0.f;
-          s1[j] += gv;
-          s2[j] += gv * (z[r][q][j] - s_bc[0][cl]) * s_bc[1][cl];
+        for (int j = 0; j < V; ++j) acc[r][q][j] = 0.f;
+#pragma unroll
+    for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+      for (int dc = 0; dc < 3; ++dc)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          // dx row h0+r reads dy row hb+dr with kh = (h0 + r) + 1 - 2*(hb+dr)
+          const int kh = r + 1 - 2 * dr;
+          if (kh < 0 || kh > 2) continue;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int kw = q + 1 - 2 * dc;
+            if (kw < 0 || kw > 2) continue;
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[r][q][j] = fmaf(g[dr][dc][j], wt[kh * 3 + kw][j], acc[r][q][j]);
+          }
         }
-      }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (!active || h0 + r >= a.H) continue;
+      T* db = (T*)a.dx + (((size_t)n * a.H + h0 + r) * a.W + w0) * a.C + cb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (w0 + q < a.W) st4v(db + (size_t)q * a.C, acc[r][q]);
+    }
+    if constexpr (BR) {
+      // BN-backward partial sums of the stored dx (the dy of that BN)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = active && h0 + r < a.H && w0 + q < a.W;
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const int cl = tx * V + j;
+            float gv = round_as<T>(acc[r][q][j]);
+            gv = (ok && fmaf(z[r][q][j], s_bc[2][cl], s_bc[3][cl]) > 0.f) ? gv : 0.f;
+            s1[j] += gv;
+            s2[j] += gv * (z[r][q][j] - s_bc[0][cl]) * s_bc[1][cl];
+          }
+        }
+    }
+  }
+  if constexpr (BR) {
+    // ---- one record per workgroup: the BY column groups of a channel quad summed in fixed order
+    __shared__ float s_br[256 * 2 * V];
+    const BnBwdPart& b = a.bs;
     const int t = ty * BX + tx;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -572,7 +581,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
     __syncthreads();
     // every thread sums whole (channel, s1|s2) columns over the BY column groups (fixed order):
     // a single row of reducers would walk BY = 64 rows alone for C = 32
-    float* rec = b.part + ((size_t)bz * gridDim.y + by) * 2 * a.C;
+    float* rec = b.part + ((size_t)bzg * gridDim.y + by) * 2 * a.C;
     for (int col = t; col < BX * 2 * V; col += BX * BY) {
       const int x = col / (2 * V), j2 = col - x * 2 * V;
       if (bx * BX + x >= CV) continue;
@@ -581,10 +590,18 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a) {
       st_wt(rec + (j2 < V ? 0 : a.C) + (size_t)(bx * BX + x) * V + (j2 < V ? j2 : j2 - V), sum);
     }
     if constexpr (TL)
-      tail_finish<false>(b.part, gridDim.y * gridDim.z, a.C, bz * gridDim.y + by, bx * BX * V,
+      tail_finish<false>(b.part, gridDim.y * gridDim.z, a.C, bzg * gridDim.y + by, bx * BX * V,
                          min(BX * V, a.C - bx * BX * V), bx, a.tail,
                          reinterpret_cast<double*>(s_br));  // (>= 3 x 256 doubles)
   }
+}
+
+// row pairs per workgroup of the stride-2 dgrad: the fewest that keep its BN records
+// (grid.y x row-pair groups) within the in-kernel finish's reach (tail_fits: 2048)
+static int dwd2_rpw(int gy, int NB) {
+  int rpw = 1;
+  while ((long long)gy * cdiv(NB, rpw) > 2048 && rpw < NB) ++rpw;
+  return rpw;
 }
 
 int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
@@ -627,7 +644,9 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   } else {
     int bx, by;
     dw_block_shape(a.C, DWD2_V, bx, by);
-    dim3 grid(cdiv(a.C / DWD2_V, bx), cdiv(a.W, by * 4), a.N * ((a.H + 1) / 2)), block(bx, by);
+    const int gy = cdiv(a.W, by * 4), NB = a.N * ((a.H + 1) / 2);
+    const int rpw = dwd2_rpw(gy, NB);
+    dim3 grid(cdiv(a.C / DWD2_V, bx), gy, cdiv(NB, rpw)), block(bx, by);
     DwBwdArgs b = a;
     if (fin) {
       P = (int)(grid.y * grid.z);
@@ -636,9 +655,9 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     }
 #define DWD2(T)                                                                 \
   do {                                                                          \
-    if (br && ink) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(b); \
-    else if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b);        \
-    else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b);               \
+    if (br && ink) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(b, rpw); \
+    else if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b, rpw);        \
+    else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b, rpw);               \
   } while (0)
     if (dtype == DT_F32) DWD2(float);
     else if (dtype == DT_F16) DWD2(f16);
@@ -662,7 +681,8 @@ int dw_dgrad_parts(int N, int H, int W, int C, int dtype, int stride) {
   }
   int bx, by;
   dw_block_shape(C, DWD2_V, bx, by);
-  return cdiv(W, by * 4) * N * ((H + 1) / 2);
+  const int gy = cdiv(W, by * 4), NB = N * ((H + 1) / 2);
+  return gy * cdiv(NB, dwd2_rpw(gy, NB));
 }
 
 // ---- weight gradient: per-workgroup partial [part][9][C] --------------------------------------
