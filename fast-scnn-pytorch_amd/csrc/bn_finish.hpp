@@ -99,7 +99,9 @@ __device__ inline void tail_fold(const float* part, const double* tsum, int N, i
   const int col = tid % nc, sl = tid / nc;
   const int n = c0 + col;
   constexpr int R = TEAM ? 3 : (FWD ? 3 : 2);
-  constexpr int U = R == 3 ? 8 : 4;  // rows per thread per batch (all loads before the sums)
+  // rows per thread per batch (all loads before the sums): the last arriver's fold is a chain of
+  // dependent write-through load batches at the END of its producer, so it wants few, wide ones
+  constexpr int U = R == 3 ? 8 : 16;
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
   if (sl < S && n < N) {
     for (int i0 = sl; i0 < count; i0 += U * S) {

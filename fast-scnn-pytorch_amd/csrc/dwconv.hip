@@ -597,7 +597,8 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(DwBwdArgs a, int rpw) 
 }
 
 // row pairs per workgroup of the stride-2 dgrad: the fewest that keep its BN records
-// (grid.y x row-pair groups) within the in-kernel finish's reach (tail_fits: 2048)
+// (grid.y x row-pair groups) at <= 2048 (bottleneck1.0: 13,312 -> 1,664 records, so the
+// fold+finalize launch reads 5 MB instead of 41 MB)
 static int dwd2_rpw(int gy, int NB) {
   int rpw = 1;
   while ((long long)gy * cdiv(NB, rpw) > 2048 && rpw < NB) ++rpw;
@@ -648,15 +649,12 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     const int rpw = dwd2_rpw(gy, NB);
     dim3 grid(cdiv(a.C / DWD2_V, bx), gy, cdiv(NB, rpw)), block(bx, by);
     DwBwdArgs b = a;
-    if (fin) {
-      P = (int)(grid.y * grid.z);
-      ink = a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)grid.x);
-      b.tail_ink = ink;
-    }
+    // its BN finish as the separate fold+finalize launch: measured 10-15 us per step faster than
+    // the in-kernel finish at these record counts (the last arriver's fold sits on the tail)
+    if (fin) P = (int)(grid.y * grid.z);
 #define DWD2(T)                                                                 \
   do {                                                                          \
-    if (br && ink) dw_dgrad_s2_kernel<T, true, true><<<grid, block, 0, st>>>(b, rpw); \
-    else if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b, rpw);        \
+    if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b, rpw);              \
     else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b, rpw);               \
   } while (0)
     if (dtype == DT_F32) DWD2(float);
