@@ -8,6 +8,7 @@ namespace fscnn {
 
 constexpr int MAX_FOLD = 64;
 
+
 struct Conv0Args {
   const void* x;       // NCHW [N,3,H,W]
   int x_bf16;          // input dtype code: 0 fp32, 1 bf16, 2 fp16

@@ -10,4 +10,4 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/smoke_final.log
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err || { tail -20 gpurun_out/bench_final.err; exit 1; }
 cat gpurun_out/bench_final.json
-bash tools/gpu_prof.sh r03f pmc
+bash tools/gpu_prof.sh r03i pmc

@@ -14,6 +14,6 @@ tail -3 gpurun_out/${TAG}_train_step_trace.txt
 FSCNN_SIDE_STREAM=0 timeout -k 10 300 python -u tools/layer_report.py gpurun_out/${TAG}_layers.md > gpurun_out/layers_${TAG}.log 2>&1 || { tail -20 gpurun_out/layers_${TAG}.log; exit 1; }
 grep -A20 "kernel family" gpurun_out/${TAG}_layers.md | head -50
 if [[ "${2:-}" == pmc ]]; then
-  bash tools/pmc_step.sh ${TAG} > gpurun_out/pmc_${TAG}.txt 2>&1 || { tail -20 gpurun_out/pmc_${TAG}.txt; exit 1; }
+  FSCNN_SIDE_STREAM=0 bash tools/pmc_step.sh ${TAG} > gpurun_out/pmc_${TAG}.txt 2>&1 || { tail -20 gpurun_out/pmc_${TAG}.txt; exit 1; }
   head -40 gpurun_out/pmc_${TAG}.txt
 fi
