@@ -374,6 +374,12 @@ int fscnn_ohem_threshold(const float* prob, long long n, const unsigned long lon
   return ohem_threshold_dev(prob, n, counts, min_kept, thresh, work, thr, S(stream));
 }
 
+int fscnn_kth_smallest(const float*, long long, long long, unsigned*, float*, void*) {
+  set_error("fscnn_kth_smallest was removed in round 3: use fscnn_ohem_threshold (the whole OHEM "
+            "threshold rule on the device, no host sync)");
+  return E_UNSUPPORTED;
+}
+
 int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
                           long long HW, long long ignore_index, const float* weight,
                           const float* prob, const float* thr, float* part, float* out2,
@@ -550,6 +556,32 @@ int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, in
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.b_trans = b_trans;
   a.scale = scale; a.shift = shift; a.R = R; a.ldr = ldr; a.relu = relu; a.C = C; a.ldc = ldc;
   a.part = stats_part;
+  return gemm_nt(a, dtype, S(stream));
+}
+int fscnn_pw_dgrad_bnbwd(int M, int N, int K, const void* D, int ldd, const void* B, int ldb,
+                         const void* R, int ldr, void* dX, int lddx, const void* z, int ldz,
+                         const float* mean, const float* invstd, const float* scale,
+                         const float* shift, int relu_mode, float* part, unsigned* counters,
+                         double* tsum, float* dgamma, float* dbeta, float* coef, int dtype,
+                         int* path, void* stream) {
+  if (!D || !B || !dX || !z || !mean || !invstd || !scale || !shift || !part || !counters ||
+      !tsum || !dgamma || !dbeta || !coef) {
+    set_error("fscnn_pw_dgrad_bnbwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || (relu_mode != 0 && relu_mode != 2)) {
+    set_error("fscnn_pw_dgrad_bnbwd: dtype %d / relu_mode %d", dtype, relu_mode);
+    return E_INVALID;
+  }
+  // the executor's form (net.cpp Exec::pw_bwd + set_btarget)
+  GemmArgs a{};
+  a.M = M; a.N = N; a.K = K; a.A = D; a.lda = ldd; a.B = B; a.ldb = ldb; a.b_trans = 0;
+  a.R = R; a.ldr = ldr; a.C = dX; a.ldc = lddx;
+  a.bpart = part; a.bz = z; a.ldbz = ldz;
+  a.bmean = mean; a.binvstd = invstd; a.bscale = scale; a.bshift = shift; a.bmode = relu_mode;
+  a.tail.counters = counters; a.tail.tsum = tsum; a.tail.count = (double)M;
+  a.tail.dgamma = dgamma; a.tail.dbeta = dbeta; a.tail.coef = coef;
+  if (path) *path = gemm_stream_ok(a, dtype) ? 1 : 0;
   return gemm_nt(a, dtype, S(stream));
 }
 long long fscnn_pw_wgrad_slab_floats(int M, int N, int K) {

@@ -513,21 +513,35 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
 // FSCNN_SIDE_STREAM=0 keeps one stream.
 // Thread safety (DataParallel replicas, train.py:170-171, call the backward from one worker
 // thread per device; two replicas may share a device and so this plan): the stream lives on the
-// device current at its creation and is only used from calls on that device; every
-// (record, wait) pair on the shared fork / join events is one critical section, so a fork always
-// orders the side stream after the CALLER's main-stream work (a concurrent record in between
-// would hand it another thread's point in time).
+// device of the caller's stream at its creation and is only used from calls whose stream AND
+// current device are that device (a call on another device's stream while a different device is
+// current runs on one stream: a side stream of the current device would run the weight gradients
+// against the other device's memory); every (record, wait) pair on the shared fork / join events
+// is one critical section, so a fork always orders the side stream after the CALLER's
+// main-stream work (a concurrent record in between would hand it another thread's point in time).
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   int dev = -1;
   bool ready = false, failed = false;
   std::mutex mu;
-  bool init() {
+  // device of the caller's stream, when it is also the current device; -1 otherwise
+  static int caller_device(hipStream_t main) {
+    int cur = -1, sd = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return -1;
+    if (hipStreamGetDevice(main, &sd) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1;
+    }
+    return sd == cur ? cur : -1;
+  }
+  bool init(hipStream_t main) {
+    const int cd = caller_device(main);
+    if (cd < 0) return false;
     std::lock_guard<std::mutex> lock(mu);
-    if (ready || failed) return ready && current_device_ok();
+    if (ready || failed) return ready && cd == dev;
     failed = true;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
+    dev = cd;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
     hipEvent_t* ev[2] = {&fork, &join};
     for (auto* e : ev)
@@ -535,10 +549,6 @@ struct SideStream {
     ready = true;
     failed = false;
     return true;
-  }
-  bool current_device_ok() const {
-    int d = -1;
-    return hipGetDevice(&d) == hipSuccess && d == dev;
   }
   // the side stream waits for everything enqueued on `main` so far
   bool fork_from(hipStream_t main) {
@@ -608,12 +618,19 @@ struct Exec {
   Exec(const Plan& p, const RunArgs& ra)
       : pl(p), net(*p.net), r(ra), ws((char*)ra.ws), bws((char*)ra.bws), dt(p.dtype),
         E(p.dtype == DT_F32 ? 4 : 2), train(p.train != 0) {}
+  // every return path (a TRY() failure between a fork and its join included) leaves the caller's
+  // stream ordered after the side-stream work already issued: the workspaces it writes are
+  // freed by the caller once the call returns, and a graph capture needs the fork joined
+  ~Exec() {
+    if (side && forked) (void)side->join_into(r.st);
+  }
 
   // ---- side stream for the weight gradients (backward only; see SideStream) ----------------
   SideStream* side = nullptr;
+  bool forked = false;  // side-stream work issued since the last join
   std::vector<std::function<int(hipStream_t)>> sideq;  // wgrads waiting for the next fork
   void use_side() {
-    if (train && side_stream_enabled() && pl.side && pl.side->init()) side = pl.side.get();
+    if (train && side_stream_enabled() && pl.side && pl.side->init(r.st)) side = pl.side.get();
   }
   // the PPM branches as one fused launch each way (ppm.hip) wherever the branch shapes fit it;
   // the general per-branch GEMM / BN kernels otherwise
@@ -642,6 +659,7 @@ struct Exec {
       set_error("side stream: fork failed");
       return E_HIP;
     }
+    forked = true;
     for (auto& f : sideq) TRY(f(side->s));
     sideq.clear();
     return OK;
@@ -649,10 +667,12 @@ struct Exec {
   int join() {
     if (!side) return OK;
     TRY(flush_side());
+    if (!forked) return OK;
     if (!side->join_into(r.st)) {
       set_error("side stream: join failed");
       return E_HIP;
     }
+    forked = false;
     return OK;
   }
   // BN-backward output dz of unit u: its own slot of the step's dz arena (a queued wgrad may

@@ -497,12 +497,13 @@ class FastSCNN(nn.Module):
         rest = (_lib.dtype_code(dt), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]),
                 _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p), _lib.c_float(self._momentum()),
                 _lib.stream_ptr(x.device))
-        if self.aux:  # models/fast_scnn.py:42-45
-            _lib.call("fscnn_forward_aux", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
-                      _lib.ptr(out), _lib.ptr(aux_out), _lib.dtype_code(out_dt), *rest[1:])
-        else:
-            _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(out),
-                      _lib.dtype_code(out_dt), *rest[1:])
+        with torch.cuda.device(x.device):
+            if self.aux:  # models/fast_scnn.py:42-45
+                _lib.call("fscnn_forward_aux", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
+                          _lib.ptr(out), _lib.ptr(aux_out), _lib.dtype_code(out_dt), *rest[1:])
+            else:
+                _lib.call("fscnn_forward", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
+                          _lib.ptr(out), _lib.dtype_code(out_dt), *rest[1:])
         if train:
             self._writeback(ar)
         if getattr(self, "_keep_ws", False):
@@ -531,9 +532,11 @@ class FastSCNN(nn.Module):
         plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), False, x.device)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         labels = torch.empty((N, H, W), dtype=dtype, device=x.device)
-        _lib.call("fscnn_predict", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(labels),
-                  1 if dtype == torch.uint8 else 0, _lib.ptr(ar["P"]), _lib.ptr(ar["R"]),
-                  _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.stream_ptr(x.device))
+        with torch.cuda.device(x.device):
+            _lib.call("fscnn_predict", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
+                      _lib.ptr(labels), 1 if dtype == torch.uint8 else 0, _lib.ptr(ar["P"]),
+                      _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]), _lib.ptr(ws),
+                      _lib.stream_ptr(x.device))
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return labels
@@ -585,10 +588,11 @@ class FastSCNN(nn.Module):
         if p > 0:
             fixed = getattr(self, "_dropout_seed", None)
             seed = int(fixed) if fixed is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
-        _lib.call("fscnn_forward_loss", plan, _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(target),
-                  int(ignore_index), _lib.ptr(loss2), _lib.ptr(ar["P"]), _lib.ptr(ar["R"]),
-                  _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.c_ull(seed), _lib.c_float(p),
-                  _lib.c_float(self._momentum()), _lib.stream_ptr(x.device))
+        with torch.cuda.device(x.device):
+            _lib.call("fscnn_forward_loss", plan, _lib.ptr(x), _lib.dtype_code(x.dtype),
+                      _lib.ptr(target), int(ignore_index), _lib.ptr(loss2), _lib.ptr(ar["P"]),
+                      _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.c_ull(seed),
+                      _lib.c_float(p), _lib.c_float(self._momentum()), _lib.stream_ptr(x.device))
         self._writeback(ar)
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
@@ -621,26 +625,30 @@ class FastSCNN(nn.Module):
             self._debug["bws"] = bws
         hook = self.grad_stage_hook
         for s in range(4):
-            if gloss is None and self.aux:
-                _lib.call("fscnn_backward_aux", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(x),
-                          _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                          _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
-                          _lib.stream_ptr(x.device))
-            elif gloss is None:
-                _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x),
-                          _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                          _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
-                          _lib.stream_ptr(x.device))
-            else:
-                _lib.call("fscnn_backward_loss", plan, _lib.ptr(gloss), _lib.ptr(loss2), _lib.ptr(x),
-                          _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                          _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
-                          _lib.stream_ptr(x.device))
+            with torch.cuda.device(x.device):
+                self._backward_stage(plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p)
             if hook is not None:
                 b, e = nat.stage_ranges[s]
                 hook(s, G, b, e)
         return [G[off:off + numel].view(prm.shape)
                 for prm, (_, off, numel) in zip(ar["params"], nat.params)]
+
+    def _backward_stage(self, plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p):
+        if gloss is None and self.aux:
+            _lib.call("fscnn_backward_aux", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(x),
+                      _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.stream_ptr(x.device))
+        elif gloss is None:
+            _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x),
+                      _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.stream_ptr(x.device))
+        else:
+            _lib.call("fscnn_backward_loss", plan, _lib.ptr(gloss), _lib.ptr(loss2), _lib.ptr(x),
+                      _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.stream_ptr(x.device))
 
     def forward(self, x):
         train = self.training

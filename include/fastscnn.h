@@ -124,6 +124,11 @@ int fscnn_ohem_prob(const void* logits, int dtype, const long long* target, int 
                     unsigned long long* counts, void* stream);
 int fscnn_ohem_threshold(const float* prob, long long n, const unsigned long long* counts,
                          long long min_kept, float thresh, unsigned* work, float* thr, void* stream);
+/* Deprecated (round 3): the host-driven k-th smallest of the OHEM rule was replaced by
+ * fscnn_ohem_threshold, which keeps the threshold on the device.  Kept so old callers still link;
+ * always returns -2 (unsupported) with a message naming the replacement. */
+int fscnn_kth_smallest(const float* values, long long n, long long k, unsigned* hist, float* out,
+                       void* stream);
 int fscnn_ce_weighted_fwd(const void* logits, int dtype, const long long* target, int N, int C,
                           long long HW, long long ignore_index, const float* weight,
                           const float* prob, const float* thr, float* part, float* out2,
@@ -243,6 +248,22 @@ int fscnn_pw_gemm_stats_parts(int M, int N, int K, int lda, int ldc, int dtype);
 int fscnn_pw_gemm(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                   int b_trans, const float* scale, const float* shift, const void* R, int ldr,
                   int relu, void* C, int ldc, float* stats_part, int dtype, void* stream);
+/* Training dgrad of a 1x1 conv whose output is the dy of a BatchNorm (the form the executor runs
+ * for every LinearBottleneck expand dgrad, models/fast_scnn.py:103-104 autograd):
+ *   dX[M][N] = D[M][K] . B^T (+ R), B [N][K] (the transposed conv weight, row stride ldb),
+ * plus that BN's backward reduction over the STORED (rounded) dX, finished in the same call:
+ *   dbeta[n] = sum_m dX*mask, dgamma[n] = sum_m dX*mask*(z - mean[n])*invstd[n],
+ *   coef[n] = dbeta[n] / M, coef[N + n] = dgamma[n] / M,
+ * mask = 1 (relu_mode 0) or (z*scale[n] + shift[n] > 0) (relu_mode 2: the BN feeds a ReLU).
+ * z [M][N] (ld ldz) is the BN's forward input.  Scratch: part >= ceil(M/128)*2*N floats,
+ * counters 512 zeroed uint32 (left zero), tsum 32*3*1024 doubles.  *path (nullable): 1 when the
+ * streaming kernel ran (deep-K form for 16-bit K = 384 / 512 / 576 at M >= 131072), 0 tiled. */
+int fscnn_pw_dgrad_bnbwd(int M, int N, int K, const void* D, int ldd, const void* B, int ldb,
+                         const void* R, int ldr, void* dX, int lddx, const void* z, int ldz,
+                         const float* mean, const float* invstd, const float* scale,
+                         const float* shift, int relu_mode, float* part, unsigned* counters,
+                         double* tsum, float* dgamma, float* dbeta, float* coef, int dtype,
+                         int* path, void* stream);
 long long fscnn_pw_wgrad_slab_floats(int M, int N, int K);
 /* dW[N][K] = sum_m D[m][n] X[m][k] */
 int fscnn_pw_wgrad(int M, int N, int K, const void* D, int ldd, const void* X, int ldx,

@@ -131,3 +131,26 @@ def test_replica_on_copied_arena_writes_back_running_stats():
     # the module itself is untouched by replica 1 (DataParallel keeps replica 0's statistics)
     assert torch.equal(model.state_dict()["learning_to_downsample.conv.conv.1.running_mean"],
                        before)
+
+
+def test_model_on_non_current_device():
+    """A model on cuda:k called while another device is current (``--device cuda:1`` with
+    cuda:0 current): every native call runs under a guard of the input's device, and the
+    executor's weight-gradient side stream is bound to the caller's stream device (skipped, one
+    stream, if they ever differ).  Gradients equal the same step run with its device current.
+    Needs >= 2 GPUs (skipped on the one-GPU box)."""
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs two GPUs")
+    dev = torch.device("cuda", n - 1)
+    xs, ts = _shards(dev)
+    with torch.cuda.device(dev):
+        m = _fresh(dev)
+        cross_entropy(m(xs[0])[0], ts[0]).backward()
+        ref = _grads(m)
+    torch.cuda.set_device(0)
+    m = _fresh(dev)
+    cross_entropy(m(xs[0])[0], ts[0]).backward()
+    torch.cuda.synchronize(dev)
+    for k, v in _grads(m).items():
+        assert torch.equal(v, ref[k]), k
