@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: this process's CPU share)")
     ap.add_argument("--no-cfg5", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the fp16 train-step line and the published-configuration line")
     return ap.parse_args()
 
 
@@ -184,6 +186,87 @@ def cpu_baseline(args):
     return res
 
 
+def _timed_steps(step, n, warm):
+    import torch
+    for _ in range(warm):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n
+
+
+def train_fp16_rate(args, model, x, t, dev):
+    """cfg3's step (fused CE head, FusedSGD, 8 x 3 x 1024 x 2048, 19 classes) in the reference's
+    own AMP arithmetic: train.py:269's autocast() (fp16 activations and weight copies, fp32
+    master weights / statistics / accumulation) over fp32 images."""
+    import torch
+    from fast_scnn_pytorch_amd.optim import FusedSGD
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    xf = x.float()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda"):
+            loss = model.forward_loss(xf, t)
+        loss.backward()
+        opt.step()
+    n = max(5, args.steps // 2)
+    sec = _timed_steps(step, n, 3)
+    return {"value": round(args.batch / sec, 2), "unit": "images/s", "ms_per_step": round(1e3 * sec, 3),
+            "dtype": "fp16", "steps": n,
+            "config": "cfg3 train step under torch.autocast('cuda') (fp16, train.py:269), fp32 images"}
+
+
+def published_config_rate(args, dev):
+    """The reference's only published training number (PERFORMANCE_MONITORING.md:24-25,57-66:
+    232.9 samples/s) is for its train.py loop at: TuSimple (2 classes), batch 8, 768 x 768 crops
+    (train.py:48 --crop-size default), fp16 AMP with GradScaler (train.py:200-201,268-275), aux
+    head (aux_weight 0.4, train.py:55), MixDiceLoss (train.py:70,183-184), SGD momentum 0.9 /
+    wd 1e-4.  The same loop here, including its per-iteration loss.item() (train.py:283) and
+    GradScaler's inf check; synthetic images already on the device (the reference's timer also
+    covers the batch's host-to-device copy and the data wait is excluded)."""
+    import numpy as np
+    import torch
+    from fast_scnn_pytorch_amd import arch, portable_init
+    from fast_scnn_pytorch_amd.loss import MixDiceLoss
+    from fast_scnn_pytorch_amd.optim import FusedSGD
+    from models.fast_scnn import FastSCNN
+    m = FastSCNN(2, aux=True)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                       arch.portable_state_dict(2, aux=True, seed=0).items()})
+    m = m.to(dev).train()
+    B, S = 8, 768
+    xi = torch.from_numpy(portable_init.input_tensor(7, (B, 3, S, S))).to(dev)
+    ti = torch.from_numpy(portable_init.target_tensor(8, (B, S, S), 2, 0.0)).to(dev)
+    crit = MixDiceLoss(aux=True, aux_weight=0.4)
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    scaler = torch.amp.GradScaler("cuda")
+    losses = []
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cuda"):
+            outputs = m(xi)
+            loss = crit(outputs, ti)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+        losses.append(loss.item())
+    n = max(10, args.steps)
+    sec = _timed_steps(step, n, 5)
+    val = B / sec
+    return {"value": round(val, 2), "unit": "samples/s", "ms_per_step": round(1e3 * sec, 3),
+            "steps": n, "published": 232.9, "vs_published": round(val / 232.9, 2),
+            "published_source": "PERFORMANCE_MONITORING.md:24-25,57-66 (GPU not stated)",
+            "dtype": "fp16", "loss_first_last": [round(losses[0], 4), round(losses[-1], 4)],
+            "config": "train.py loop: TuSimple 2 classes, bs 8, 768x768, autocast fp16 + "
+                      "GradScaler, aux=True (0.4), MixDiceLoss, SGD m 0.9 wd 1e-4, "
+                      "loss.item() per step"}
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -276,6 +359,8 @@ def main():
     for i in range(args.steps):
         if i == args.steps - nprof:
             lib.fscnn_prof_begin(kind, 512 * nprof)
+            if world > 1:
+                net.timing = True  # per-bucket all-reduce / exposed comm events (ddp.py)
         loss = step()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -307,10 +392,32 @@ def main():
     roof.update({"kernel": kname, "launches": n.value, "avg_launch_us": round(avg_ms * 1e3, 2),
                  "algo_bytes_per_launch": round(bytes_per_launch),
                  "algo_flops_per_launch": round(flops_per_launch), "traffic": None})
+    roof["timing"] = ("HIP events around each launch on its own stream over the last tenth of "
+                      "the timed steps (each event pair adds its stream's ~7 us event latency)")
+    # HBM traffic per launch from the PMC counters of a committed profiling run (rocprofv3 --pmc
+    # cannot run inside this process); labelled with its file and round
     pmc = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (kname, args.dtype))
     if os.path.exists(pmc):
         try:
-            roof["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pj = json.load(open(pmc))
+            roof["traffic"] = pj.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = "profiles/%s (PMC FETCH_SIZE+WRITE_SIZE, round %s)" % (
+                os.path.basename(pmc), pj.get("round", pj.get("tag", "?")))
+        except Exception:
+            pass
+    # the same family's kernel time from the committed rocprofv3 --kernel-trace --stats summary
+    # of this workload (tools/rocprof_family.py): kernel-only durations, no event latency
+    rpf = os.path.join(ROOT, "profiles", "rocprof_family_%s.json" % args.dtype)
+    if os.path.exists(rpf):
+        try:
+            fam = json.load(open(rpf))
+            fk = fam["families"].get(kname)
+            if fk and fk.get("avg_us"):
+                a_r = bytes_per_launch / (fk["avg_us"] * 1e-6) / 1e9
+                roof["rocprof"] = {"avg_launch_us": fk["avg_us"], "achieved": round(a_r, 1),
+                                   "frac": round(a_r / HBM_PEAK_GBS, 4),
+                                   "source": "profiles/%s (round %s)" % (os.path.basename(rpf),
+                                                                        fam.get("round", "?"))}
         except Exception:
             pass
 
@@ -330,6 +437,16 @@ def main():
                  "world_size": dist.get_world_size() if world > 1 else 1,
                  "buckets": 4 if world > 1 else 0},
     }
+    if world > 1:
+        net.timing = False
+        cs = net.comm_stats()
+        if cs:
+            # HIP events on the comm stream around each bucket's all-reduce (bucket order: head,
+            # bottleneck3, bottleneck2, bottleneck1+LTD) and the comm time left after the
+            # backward's last kernel, over the last tenth of the timed steps (rank 0's view)
+            result["comm"].update(cs)
+            result["comm"]["bucket_mb"] = [round(4 * (e - b) / 1e6, 3)
+                                           for b, e in model.native().stage_ranges]
     if census:
         result["kernel_ms_per_step_census"] = census
         result["census_note"] = ("HIP-event kernel time per family over one profiled step each; "
@@ -382,6 +499,10 @@ def main():
                                       "config": "cfg5 eval 32x3x480x640, 2 classes"}
             del m5, x5
         model.train()
+
+    if rank == 0 and world == 1 and not args.no_extra:
+        result["train_fp16"] = train_fp16_rate(args, model, x, t, dev)
+        result["train_published_cfg"] = published_config_rate(args, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)

@@ -52,6 +52,8 @@ def _worker(rank, port, q):
             m.grad_stage_hook(s, G, b, e)
         res["G"] = G
         res["ranges"] = calls
+        res["log"] = list(ddp.bucket_log)
+        res["pending"] = len(ddp._works)
         res["world"] = ddp.world
 
         # explicit path (allreduce_grads) on ordinary .grad tensors
@@ -108,6 +110,16 @@ def test_stage_buckets_average_gradients(results):
     # every element inside a stage bucket is the rank average; both ranks agree bit-exactly
     assert torch.equal(r0["G"], r1["G"])
     assert torch.allclose(r0["G"][covered], expect[covered])
+
+
+def test_bucket_to_stage_mapping_async(results):
+    """Every stage issues exactly its own bucket as an asynchronous all-reduce (async_op=True,
+    waited at the last stage: nothing is pending after the backward), in backward order."""
+    for r in (0, 1):
+        log = results[r]["log"]
+        assert [(s, b, e) for s, b, e, _ in log] == [tuple(c) for c in results[r]["ranges"]]
+        assert all(a for *_, a in log)
+        assert results[r]["pending"] == 0
 
 
 def test_stage_ranges_partition_all_parameters(results):
