@@ -102,7 +102,12 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
 // 32-k chunk (k = 4lq.., 16+4lq..) form its 8 bf16 k-slots, the same permutation in A and B
 // TL: the launch finishes its BN in its last workgroups (a.tail_ink; a separate instantiation so
 // the other launches keep their register budget)
-template <typename T, int NT, bool BT, bool BS, bool AT, bool X3 = false, bool TL = false>
+// PF: K chunks whose loads are in flight ahead of the one being multiplied (register-staged
+// ring of PF slots).  PF = 1 is the classic one-ahead double buffer; the M <= 64 K-row launches
+// with long K (bottleneck2/3 projects, expand dgrads: 9-12 chunks) are a chain of dependent load
+// latencies at PF = 1 (one 22 KB chunk per CU in flight), so they run PF = 3.
+template <typename T, int NT, bool BT, bool BS, bool AT, bool X3 = false, bool TL = false,
+          int PF = 1>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -139,8 +144,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // ---- staging registers --------------------------------------------------------------------
   constexpr int A_PER = G_BM * G_VROW / 256;            // 4
   constexpr int B_PER = (BN * G_VROW + 255) / 256;      // vectors per thread (non-trans)
-  uint4 ra[A_PER];
-  uint4 rb[BT ? 1 : B_PER];
+  uint4 ra[PF][A_PER];
+  uint4 rb[PF][BT ? 1 : B_PER];
   // transposed-B staging: KC rows (k) x BN cols (n) of scalars, held as raw 16-B vectors along n
   constexpr int BT_VEC = KC * BN / V;                   // vectors per chunk
   constexpr int BT_PER = (BT_VEC + 255) / 256;
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // Branch-free loads: every lane loads from an in-bounds (clamped) address and invalid or tail
   // elements are zeroed with selects afterwards, so all loads of a chunk issue back to back
   // (a branch around a load makes hipcc wait vmcnt(0) at the join).
-  auto load_chunk = [&](int c) {
+  auto load_chunk = [&](int c, int slot) {
     const int k0 = c * KC;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -158,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       int m = m0 + row, k = k0 + vv * V;
       const bool ok = m < a.M && k < a.K;
       const size_t off = ok ? (size_t)m * a.lda + k : 0;
-      ra[i] = *reinterpret_cast<const uint4*>(A + off);
+      ra[slot][i] = *reinterpret_cast<const uint4*>(A + off);
     }
     if (!BT) {
 #pragma unroll
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         int n = n0 + row, k = k0 + vv * V;
         const bool ok = id < BN * G_VROW && n < a.N && k < a.K;
         const size_t off = ok ? (size_t)n * a.ldb + k : 0;
-        rb[i] = *reinterpret_cast<const uint4*>(B + off);
+        rb[slot][i] = *reinterpret_cast<const uint4*>(B + off);
       }
     } else {
 #pragma unroll
@@ -185,14 +190,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // Tail masks (and the lazy BN+ReLU of A) are applied when a chunk is written to LDS, i.e. after
   // the current chunk's MFMAs: applying them right after issuing the loads made every wave wait
   // for the next chunk's loads before computing (no fetch/compute overlap).
-  auto store_chunk = [&](int buf, int c) {
+  auto store_chunk = [&](int buf, int c, int slot) {
     const int k0 = c * KC;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int id = tid + 256 * i;
       int row = id >> 3, vv = id & 7;
       int m = m0 + row, k = k0 + vv * V;
-      uint4 v = ra[i];
+      uint4 v = ra[slot][i];
       if constexpr (AT) {
         const int kc = k < a.K ? k : 0;
         v = bnrelu_vec<T>(v, s_at + kc, s_at + G_ATMAX + kc);
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         int row = id >> 3, vv = id & 7;
         int n = n0 + row, k = k0 + vv * V;
         if (id < BN * G_VROW)
-          sB(buf)[row * G_VPAD + vv] = zero_tail<T>(rb[i], n < a.N ? a.K - k : 0);
+          sB(buf)[row * G_VPAD + vv] = zero_tail<T>(rb[slot][i], n < a.N ? a.K - k : 0);
       }
     } else {
       T* sbs = reinterpret_cast<T*>(sB(buf));
@@ -237,48 +242,60 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       s_at[G_ATMAX + k] = k < a.K ? a.a_shift[k] : 0.f;
     }
   }
-  load_chunk(0);
+  // chunk c's loads go to register slot c % PF; the prologue fills every slot
+  load_chunk(0, 0);
+#pragma unroll
+  for (int p = 1; p < PF; ++p)
+    if (p < nchunks) load_chunk(p, p);
   if constexpr (AT) __syncthreads();
-  store_chunk(0, 0);
+  store_chunk(0, 0, 0);
+  if (PF > 1 && PF < nchunks) load_chunk(PF, 0);
   __syncthreads();
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = nbuf == 2 ? (c & 1) : 0;
-    if (c + 1 < nchunks) load_chunk(c + 1);
-    if constexpr (X3) {
-      uint4 a3[2][3];
+  for (int c0 = 0; c0 < nchunks; c0 += PF) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const uint4* ar = sA(buf) + (wave * 32 + mt * 16 + li) * G_VPAD + lq;
-        gs_split3(ar[0], ar[4], a3[mt]);
+    for (int s = 0; s < PF; ++s) {
+      const int c = c0 + s;
+      if (c >= nchunks) break;
+      const int buf = nbuf == 2 ? (c & 1) : 0;
+      if (PF == 1 && c + 1 < nchunks) load_chunk(c + 1, 0);
+      if constexpr (X3) {
+        uint4 a3[2][3];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const uint4* ar = sA(buf) + (wave * 32 + mt * 16 + li) * G_VPAD + lq;
+          gs_split3(ar[0], ar[4], a3[mt]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const uint4* br = sB(buf) + (nt * 16 + li) * G_VPAD + lq;
+          uint4 b3[3];
+          gs_split3(br[0], br[4], b3);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) gs_mma_x3(a3[mt], b3, acc[mt][nt]);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int vv = lq + 4 * h;
+          uint4 af[2], bfv[NT];
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) af[mt] = sA(buf)[(wave * 32 + mt * 16 + li) * G_VPAD + vv];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB(buf)[(nt * 16 + li) * G_VPAD + vv];
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
+        }
       }
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const uint4* br = sB(buf) + (nt * 16 + li) * G_VPAD + lq;
-        uint4 b3[3];
-        gs_split3(br[0], br[4], b3);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) gs_mma_x3(a3[mt], b3, acc[mt][nt]);
+      if (c + 1 < nchunks) {
+        const int slot = PF == 1 ? 0 : (s + 1) % PF;  // static once the s loop is unrolled
+        if (nbuf == 1) __syncthreads();  // every wave's MFMA reads of this chunk are done
+        store_chunk(nbuf == 2 ? buf ^ 1 : 0, c + 1, slot);
+        if (PF > 1 && c + 1 + PF < nchunks) load_chunk(c + 1 + PF, slot);
       }
-    } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int vv = lq + 4 * h;
-        uint4 af[2], bfv[NT];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) af[mt] = sA(buf)[(wave * 32 + mt * 16 + li) * G_VPAD + vv];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bfv[nt] = sB(buf)[(nt * 16 + li) * G_VPAD + vv];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) MfmaOp<T>::run(af[mt], bfv[nt], acc[mt][nt]);
-      }
+      __syncthreads();
     }
-    if (c + 1 < nchunks) {
-      if (nbuf == 1) __syncthreads();  // every wave's MFMA reads of this chunk are done
-      store_chunk(nbuf == 2 ? buf ^ 1 : 0, c + 1);
-    }
-    __syncthreads();
   }
 
   // ---- epilogue -------------------------------------------------------------------------------
@@ -500,6 +517,32 @@ int gemm_nt_parts(const GemmArgs& a, int dtype) {
   return use_stream(a, dtype) ? gemm_stream_parts(a, dtype) : gemm_parts(a.M);
 }
 
+template <typename T, bool BT, bool BS, bool AT, bool X3, bool TL, int PF>
+static void launch_nt_pf(const GemmArgs& a, int nt, dim3 grid, size_t shm, hipStream_t st) {
+  switch (nt) {
+    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
+  }
+}
+
+// deep prefetch: 16-bit, plain B, >= 4 K chunks, and a grid of at most two workgroups per CU
+// (the long-K launches at M <= 65536, where the chain of chunk load latencies is the time)
+static int nt_prefetch_depth(const GemmArgs& a, int dtype, int nt) {
+  static const int env = [] {
+    const char* e = getenv("FSCNN_GEMM_PF");
+    return e ? atoi(e) : -1;
+  }();
+  const int V = dtype == DT_F32 ? 4 : 8;
+  const int nchunks = cdiv(a.K, G_VROW * V);
+  const long long wgs = (long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt);
+  if (dtype == DT_F32 || a.b_trans || nchunks < 4) return 1;
+  if (env == 1 || env == 3) return env;
+  return wgs <= 512 ? 3 : 1;
+}
+
 template <typename T, bool BT, bool BS, bool AT = false, bool X3 = false>
 static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   dim3 grid(cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt));
@@ -511,25 +554,21 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   const size_t red = (size_t)2 * 256 * V * 4;  // bwd-BN column reduction (2 x RG x BN floats)
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
-  if constexpr (!BT && !X3) {
-    if (a.tail_ink) {
-      switch (nt) {
-        case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
-        case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
-        case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
-        case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
-        default: gemm_nt_kernel<T, 8, BT, BS, AT, X3, true><<<grid, 256, shm, st>>>(a); break;
-      }
+  const int dtype = sizeof(T) == 4 ? DT_F32 : DT_BF16;
+  if constexpr (!BT && !X3 && sizeof(T) == 2) {
+    if (nt_prefetch_depth(a, dtype, nt) == 3) {
+      if (a.tail_ink) launch_nt_pf<T, BT, BS, AT, X3, true, 3>(a, nt, grid, shm, st);
+      else launch_nt_pf<T, BT, BS, AT, X3, false, 3>(a, nt, grid, shm, st);
       return;
     }
   }
-  switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS, AT, X3><<<grid, 256, shm, st>>>(a); break;
+  if constexpr (!BT && !X3) {
+    if (a.tail_ink) {
+      launch_nt_pf<T, BT, BS, AT, X3, true, 1>(a, nt, grid, shm, st);
+      return;
+    }
   }
+  launch_nt_pf<T, BT, BS, AT, X3, false, 1>(a, nt, grid, shm, st);
 }
 
 static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool bs, hipStream_t st);

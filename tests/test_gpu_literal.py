@@ -35,7 +35,8 @@ def _rnd(shape, seed, lo=-1.0, hi=1.0):
     (262144, 64, 384, 0, False, True),   # no-ReLU BN target
     (200003, 64, 384, 2, False, True),   # ragged M (partial last chunk)
     (131072, 96, 576, 2, True, True),    # ks = 18
-    (131075, 64, 512, 0, True, True),    # ks = 16, ragged
+    (131075, 64, 384, 0, True, True),    # ragged, no-ReLU target, residual
+    (131072, 64, 512, 2, True, False),   # ks = 16 at N = 64 would spill: the tiled kernel
     (65536, 64, 384, 2, True, False),    # below the deep-K threshold: the tiled kernel
 ])
 def test_pw_dgrad_bnbwd_executor_form(dt, M, N, K, mode, res, deep):

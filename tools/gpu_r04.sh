@@ -29,7 +29,7 @@ for step in "$@"; do
           || { tail -20 gpurun_out/bench_${TAG}.err; exit 1; }
       cat gpurun_out/bench_${TAG}.json ;;
     quick)
-      timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-forward > gpurun_out/quick_${TAG}.json \
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-forward --no-extra > gpurun_out/quick_${TAG}.json \
           2> gpurun_out/quick_${TAG}.err || { tail -20 gpurun_out/quick_${TAG}.err; exit 1; }
       python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], d['value'], d['roofline'])" \
           gpurun_out/quick_${TAG}.json ;;
@@ -37,6 +37,11 @@ for step in "$@"; do
       bash tools/profile_step.sh ${TAG} --no-forward > gpurun_out/prof_${TAG}.txt 2>&1 \
           || { tail -20 gpurun_out/prof_${TAG}.txt; exit 1; }
       head -45 gpurun_out/prof_${TAG}.txt ;;
+    ab=*)  # ab=A=1+B=2,A=0 : configs separated by ',', env vars of one config by '+'
+      IFS=',' read -ra cfgs <<< "${step#ab=}"
+      args=()
+      for c in "${cfgs[@]}"; do args+=("${c//+/ }"); done
+      bash tools/gpu_ab.sh "${args[@]}" || exit 1 ;;
     file:*)
       f=${step#file:}
       timeout -k 10 400 python -u $f > gpurun_out/$(basename $f .py)_${TAG}.log 2>&1

@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-kind 3 --no-cfg5 "$@" > "$OUT/bench.log" 2>&1
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra --profile-kind 3 --no-cfg5 "$@" > "$OUT/bench.log" 2>&1
 STATS=$(find "$OUT" -name '*kernel_stats.csv' | head -1)
 cp "$STATS" "gpurun_out/prof_${TAG}_kernel_stats.csv"
 python3 - "$STATS" <<'EOF'
