@@ -30,6 +30,7 @@ int check_launch(const char* what) {
 }
 
 // ---- launch profiler --------------------------------------------------------------------
+unsigned long long* g_stamps = nullptr;
 int g_prof_kind = PK_NONE;
 thread_local const char* g_prof_tag = "";
 namespace {
@@ -128,6 +129,13 @@ extern "C" int fscnn_prof_launch(long long i, int* kind, float* ms, double* byte
   if (bytes) *bytes = g_prof.lbytes[i];
   if (flops) *flops = g_prof.lflops[i];
   if (tag) *tag = g_prof.tag[i].c_str();  // valid until the next fscnn_prof_begin
+  return OK;
+}
+
+// Phase stamps of the next launches of the instrumented kernels (the pointwise GEMMs): buf is a
+// device buffer of >= workgroups * 4 * STAMP_SLOTS uint64 (null: off).  Debug / tools only.
+extern "C" int fscnn_debug_stamps(void* buf) {
+  g_stamps = reinterpret_cast<unsigned long long*>(buf);
   return OK;
 }
 

@@ -425,4 +425,16 @@ struct ProfScope {
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// ---- phase stamps (tools/stamp_probe.py; off unless fscnn_debug_stamps set a buffer) ----------
+// Lane 0 of every wave records the 100 MHz wall clock at numbered points of a kernel into
+// stamps[(block * 4 + wave) * STAMP_SLOTS + slot] (vector stores): where a launch's time goes.
+constexpr int STAMP_SLOTS = 8;
+extern unsigned long long* g_stamps;  // device buffer of the next launches, or null
+__device__ __forceinline__ void stamp(unsigned long long* st, int slot) {
+  if (st && (threadIdx.x & 63) == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    st[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + slot] = t;
+  }
+}
+
 }  // namespace fscnn

@@ -242,6 +242,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       s_at[G_ATMAX + k] = k < a.K ? a.a_shift[k] : 0.f;
     }
   }
+  stamp(a.stamps, 0);
   // chunk c's loads go to register slot c % PF; the prologue fills every slot
   load_chunk(0, 0);
 #pragma unroll
@@ -251,6 +252,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   store_chunk(0, 0, 0);
   if (PF > 1 && PF < nchunks) load_chunk(PF, 0);
   __syncthreads();
+  stamp(a.stamps, 1);
   for (int c0 = 0; c0 < nchunks; c0 += PF) {
 #pragma unroll
     for (int s = 0; s < PF; ++s) {
@@ -298,6 +300,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
     }
   }
 
+  stamp(a.stamps, 2);
   // ---- epilogue -------------------------------------------------------------------------------
   // v = acc*scale + shift (registers; also feeds the statistics), staged through LDS as fp32 so
   // the stores (and the residual loads) are whole 16-B vectors: all residual loads are issued
@@ -412,6 +415,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       }
     }
   }
+  stamp(a.stamps, 3);
   if constexpr (bst) {
     // fixed-order column reduction over the RG row groups -> one record per 128-row tile
     __syncthreads();
@@ -434,9 +438,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       st_wt(rec + n0 + tid, t1);
       st_wt(rec + a.N + n0 + tid, t2);
     }
+    stamp(a.stamps, 4);
     if constexpr (TL)
       tail_finish<false>(a.bpart, cdiv(a.M, G_BM), a.N, tm, n0, min(BN, a.N - n0), tn, a.tail,
                          reinterpret_cast<double*>(s_dyn));
+    stamp(a.stamps, 5);
     return;  // a dgrad output never carries forward statistics (acc dies with the epilogue)
   }
   if (a.part == nullptr) return;
@@ -493,9 +499,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       }
     }
   }
+  stamp(a.stamps, 4);
   if constexpr (TL)
     tail_finish<true>(a.part, cdiv(a.M, G_BM), a.N, tm, n0, min(BN, a.N - n0), tn, a.tail,
                       reinterpret_cast<double*>(s_dyn));
+  stamp(a.stamps, 5);
 }
 
 static int pick_nt(int N) {
@@ -618,9 +626,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     return E_INVALID;
   }
   const bool stream = use_stream(a, dtype);
+  GemmArgs as = a;
+  as.stamps = g_stamps;
   // tiled path: the BN finish runs in the kernel's last workgroups (bn_finish.hpp tail_finish)
   // when the records fit its counters; otherwise as its own fold + finalize launch below
-  GemmArgs b = a;
+  GemmArgs b = as;
   b.tail_ink = !stream && a.tail.counters && !a.b_trans &&
                a.tail.tsum && a.N <= TAIL_CMAX && tail_fits(gemm_parts(a.M), cdiv(a.N, 16 * nt));
   int rc;
@@ -628,7 +638,7 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     ProfScope ps(PK_GEMM_NT, st,
                  E * (M * K + M * N * (a.R ? 2 : 1) + N * K + (a.bpart ? M * N : 0)),
                  2.0 * M * N * K);
-    rc = stream ? gemm_stream(a, dtype, st)  // finishes the BN in-kernel (last workgroup)
+    rc = stream ? gemm_stream(as, dtype, st)  // finishes the BN in-kernel (last workgroup)
                 : gemm_nt_tiled(b, dtype, nt, at, bs, st);
   }
   if (rc || stream || !a.tail.counters || b.tail_ink) return rc;

@@ -213,6 +213,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   const int n0 = g * BN;
   const T* A = (const T*)a.A;
   const T* B = (const T*)a.B;
+  stamp(a.stamps, 0);
 
   // ---- weights of the group -> LDS (zero rows n >= N, zero k >= K), per-column tables -------
   for (int i = tid; i < BN * KV; i += 256) {
@@ -244,6 +245,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     }
   }
   __syncthreads();
+  stamp(a.stamps, 1);
 
   const int nchunks = cdiv(a.M, GS_MW);
   const int wstride = bpg * 4;
@@ -449,6 +451,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
     }
   }
 
+  stamp(a.stamps, 2);
   if constexpr (SUMS) {
     // ---- one record per workgroup: lanes (xor butterfly), then the 4 waves (fixed order) ----
     cnt = gs_rowsum(cnt);  // pixels of this wave (every lane row covers the same pixels)
@@ -505,8 +508,10 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
         st_wt(rec + a.N + n, t2);
       }
     }
+    stamp(a.stamps, 3);
     // ---- in-kernel finish by the column group's last workgroup (no finalize launch) ---------
     if (a.tail.counters) gs_finish<ST>(a, g, bi, n0, BN, bpg);
+    stamp(a.stamps, 4);
   }
 }
 

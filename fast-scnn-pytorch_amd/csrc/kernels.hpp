@@ -155,6 +155,7 @@ struct GemmArgs {
   const float* a_shift = nullptr;
   BnTail tail{};        // in-kernel finish of the BN whose records this GEMM writes
   int tail_ink = 0;     // (set by the launcher) the tiled kernel runs the finish itself (tail_finish)
+  unsigned long long* stamps = nullptr;  // (set by the launcher from g_stamps) phase stamps
 };
 
 struct GemmTnArgs {

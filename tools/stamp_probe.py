@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Where a low-resolution pointwise GEMM launch spends its time: per-wave wall-clock stamps
+(common.hpp stamp(), 100 MHz) of the tiled / streaming gemm_nt kernels at the cfg3 bottleneck2/3
+shapes (M = 8 x 32 x 64 = 16384 pixels), one launch each after warm-up.
+
+Stamp slots: 0 kernel entry, 1 after the prologue (first K chunk staged / weights in LDS),
+2 after the K loop (tiled) / chunk loop (streaming), 3 after the stores (tiled) / BN record
+(streaming), 4 before the in-kernel BN finish (tiled) / after it (streaming), 5 after the finish
+(tiled).  Printed per launch: the kernel span (first entry -> last stamp), the spread of wave
+entry times (dispatch ramp) and the median / max of every phase.
+
+    python tools/stamp_probe.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import _fscnn_boot  # noqa: E402
+
+_fscnn_boot.load()
+from fast_scnn_pytorch_amd import _lib  # noqa: E402
+
+SLOTS = 8
+DEV = "cuda"
+
+
+def analyse(label, st):
+    t = st.view(-1, SLOTS).cpu().double()
+    t = t[t[:, 0] > 0]
+    if t.numel() == 0:
+        print("%-40s no stamps" % label)
+        return
+    t0 = t[:, 0].min()
+    rel = (t - t0) / 100.0  # us
+    rel[t == 0] = float("nan")
+    last = torch.nan_to_num(rel, nan=-1.0).max(dim=1).values
+    span = last.max().item()
+    entry = rel[:, 0]
+    parts = []
+    for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5)]:
+        d = rel[:, b] - rel[:, a]
+        d = d[~torch.isnan(d)]
+        if d.numel():
+            parts.append("%d-%d %.1f/%.1f" % (a, b, d.median().item(), d.max().item()))
+    print("%-40s waves %5d span %6.1f us  entry med %.1f max %.1f | %s"
+          % (label, t.shape[0], span, entry.median().item(), entry.max().item(), "  ".join(parts)),
+          flush=True)
+
+
+def main():
+    lib = _lib.load()
+    st = _lib.stream_ptr()
+    buf = torch.zeros(8192 * 4 * SLOTS, dtype=torch.int64, device=DEV)
+    dt = torch.bfloat16
+    M = 16384
+    shapes = [  # (label, K, N, kind): fwd = statistics form, dgrad = BN-backward form + finish
+        ("b2.x expand fwd", 96, 576, "fwd"), ("b3.x expand fwd", 128, 768, "fwd"),
+        ("b2.x project fwd", 576, 96, "fwd"), ("b3.x project fwd", 768, 128, "fwd"),
+        ("b2.x project dgrad", 96, 576, "dgrad"), ("b3.x project dgrad", 128, 768, "dgrad"),
+        ("b2.x expand dgrad", 576, 96, "dgrad"), ("b3.x expand dgrad", 768, 128, "dgrad"),
+    ]
+    for label, K, N, kind in shapes:
+        A = torch.randn(M, K, device=DEV).to(dt)
+        B = (torch.randn(N, K, device=DEV) / K ** 0.5).to(dt)
+        C = torch.empty(M, N, dtype=dt, device=DEV)
+        part = torch.empty((M + 127) // 128 * 3 * N, device=DEV)
+        if kind == "fwd":
+            def run():
+                _lib.call("fscnn_pw_gemm", M, N, K, _lib.ptr(A), K, _lib.ptr(B), K, 0, None, None,
+                          None, 0, 0, _lib.ptr(C), N, _lib.ptr(part), _lib.dtype_code(dt), st)
+        else:
+            z = torch.randn(M, N, device=DEV).to(dt)
+            mean, invstd = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+            sc, sh = torch.ones(N, device=DEV), torch.zeros(N, device=DEV)
+            ctr = torch.zeros(512, dtype=torch.int32, device=DEV)
+            tsum = torch.zeros(32 * 3 * 1024, dtype=torch.float64, device=DEV)
+            dg, db, coef = (torch.empty(N, device=DEV), torch.empty(N, device=DEV),
+                            torch.empty(2 * N, device=DEV))
+
+            def run():
+                _lib.call("fscnn_pw_dgrad_bnbwd", M, N, K, _lib.ptr(A), K, _lib.ptr(B), K, None,
+                          N, _lib.ptr(C), N, _lib.ptr(z), N, _lib.ptr(mean), _lib.ptr(invstd),
+                          _lib.ptr(sc), _lib.ptr(sh), 2, _lib.ptr(part), _lib.ptr(ctr),
+                          _lib.ptr(tsum), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(coef),
+                          _lib.dtype_code(dt), None, st)
+        for _ in range(5):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(20):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1e3
+        buf.zero_()
+        torch.cuda.synchronize()
+        _lib.check(lib.fscnn_debug_stamps(_lib.ptr(buf)))
+        run()
+        torch.cuda.synchronize()
+        _lib.check(lib.fscnn_debug_stamps(None))
+        analyse("%s K%d N%d (%.1f us/launch)" % (label, K, N, us), buf)
+
+
+if __name__ == "__main__":
+    main()
