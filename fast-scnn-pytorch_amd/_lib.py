@@ -90,7 +90,9 @@ SIGNATURES = {
                                      c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, P_int, c_vp]),
     "fscnn_kth_smallest": (c_int, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp]),
-    "fscnn_debug_stamps": (c_int, [c_vp]),
+    "fscnn_debug_stamps": (c_int, [c_vp, c_int]),
+    "fscnn_debug_stamp_count": (c_int, []),
+    "fscnn_debug_stamp_tag": (c_char_p, [c_int]),
     "fscnn_pw_wgrad_slab_floats": (c_ll, [c_int, c_int, c_int]),
     "fscnn_pw_gemm_stats_parts": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "fscnn_pw_wgrad": (c_int, [c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int,

@@ -132,11 +132,28 @@ extern "C" int fscnn_prof_launch(long long i, int* kind, float* ms, double* byte
   return OK;
 }
 
-// Phase stamps of the next launches of the instrumented kernels (the pointwise GEMMs): buf is a
-// device buffer of >= workgroups * 4 * STAMP_SLOTS uint64 (null: off).  Debug / tools only.
-extern "C" int fscnn_debug_stamps(void* buf) {
+// Phase stamps of the next launches of the instrumented kernels (pointwise GEMMs, depthwise
+// forward / stride-1 dgrad): launch i writes buf + i * STAMP_STRIDE (max_launches regions; null:
+// off).  Debug / tools only (process-global, single thread).
+namespace fscnn {
+static int g_stamp_max = 0, g_stamp_used = 0;
+static std::vector<std::string> g_stamp_tags;
+unsigned long long* stamp_region() {
+  if (!g_stamps || g_stamp_used >= g_stamp_max) return nullptr;
+  g_stamp_tags.emplace_back(g_prof_tag ? g_prof_tag : "");
+  return g_stamps + (size_t)(g_stamp_used++) * STAMP_STRIDE;
+}
+}  // namespace fscnn
+extern "C" int fscnn_debug_stamps(void* buf, int max_launches) {
   g_stamps = reinterpret_cast<unsigned long long*>(buf);
+  g_stamp_max = buf ? max_launches : 0;
+  g_stamp_used = 0;
+  g_stamp_tags.clear();
   return OK;
+}
+extern "C" int fscnn_debug_stamp_count(void) { return g_stamp_used; }
+extern "C" const char* fscnn_debug_stamp_tag(int i) {
+  return (i >= 0 && i < (int)g_stamp_tags.size()) ? g_stamp_tags[i].c_str() : "";
 }
 
 extern "C" const char* fscnn_prof_kind_name(int kind) {

@@ -428,12 +428,16 @@ __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a 
 // ---- phase stamps (tools/stamp_probe.py; off unless fscnn_debug_stamps set a buffer) ----------
 // Lane 0 of every wave records the 100 MHz wall clock at numbered points of a kernel into
 // stamps[(block * 4 + wave) * STAMP_SLOTS + slot] (vector stores): where a launch's time goes.
+// Every instrumented launch takes its own STAMP_STRIDE region (stamp_region) and a layer label.
 constexpr int STAMP_SLOTS = 8;
+constexpr long long STAMP_STRIDE = 8192LL * 4 * STAMP_SLOTS;
 extern unsigned long long* g_stamps;  // device buffer of the next launches, or null
+unsigned long long* stamp_region();   // host: the next launch's region (null: off / full)
 __device__ __forceinline__ void stamp(unsigned long long* st, int slot) {
   if (st && (threadIdx.x & 63) == 0) {
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    st[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + slot] = t;
+    const size_t b = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+    if (b < 8192) st[(b * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + slot] = t;
   }
 }
 

@@ -154,6 +154,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   const int n = bz / tiles_h;
   const int th0 = (bz - n * tiles_h) * G::TH, tw0 = by * G::TW;
   const int c0 = bx * cbv * VecW<T>::V + q * 4;  // first channel of the thread's quad
+  stamp(a.stamps, 0);
   dw_stage<T, S, IT>(s_in, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
                      bx * cbv, cbv, tid, nthr, a.in_scale, a.in_shift);
   float wt[9][4];
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = a.w[(size_t)(c0 + j) * 9 + t];
   __syncthreads();
+  stamp(a.stamps, 1);
 
   const T* sl = reinterpret_cast<const T*>(s_in);
   const int pstride = cbv * VecW<T>::V;          // elements per staged pixel
@@ -220,6 +222,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
       }
     }
   }
+  stamp(a.stamps, 2);
   if constexpr (BR) {
     // ---- stride-1 dgrad: BN-backward partial sums of the stored dx (it is that BN's dy) -----
     const BnBwdPart& b = a.bs;
@@ -272,10 +275,12 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
         }
       }
     }
+    stamp(a.stamps, 3);
     if constexpr (TL)
       tail_finish<false>(b.part, gridDim.y * gridDim.z, a.C, bz * gridDim.y + by,
                          bx * cbv * VecW<T>::V, cbv * VecW<T>::V, bx, a.tail,
                          reinterpret_cast<double*>(s_dyn));
+    stamp(a.stamps, 4);
     return;
   }
   if (a.part == nullptr) return;
@@ -324,10 +329,12 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
       st_wt(rec + 2 * a.C + c0 + j, cnt);
     }
   }
+  stamp(a.stamps, 3);
   if constexpr (TL)
     tail_finish<true>(a.part, gridDim.y * gridDim.z, a.C, bz * gridDim.y + by,
                       bx * cbv * VecW<T>::V, cbv * VecW<T>::V, bx, a.tail,
                       reinterpret_cast<double*>(s_dyn));
+  stamp(a.stamps, 4);
 }
 
 // dynamic LDS of the tile kernels: the haloed input tile of cbv vectors + 4 floats per thread
@@ -382,9 +389,11 @@ static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   const int nthr = cbv * 32;  // = quads * groups for both dtypes
-  if (dtype == DT_F32) dw_launch_fwd_t<float, FLIP, IT, BR>(a, grid, nthr, cbv, st);
-  else if (dtype == DT_F16) dw_launch_fwd_t<f16, FLIP, IT, BR>(a, grid, nthr, cbv, st);
-  else dw_launch_fwd_t<bf16, FLIP, IT, BR>(a, grid, nthr, cbv, st);
+  DwArgs as = a;
+  as.stamps = stamp_region();
+  if (dtype == DT_F32) dw_launch_fwd_t<float, FLIP, IT, BR>(as, grid, nthr, cbv, st);
+  else if (dtype == DT_F16) dw_launch_fwd_t<f16, FLIP, IT, BR>(as, grid, nthr, cbv, st);
+  else dw_launch_fwd_t<bf16, FLIP, IT, BR>(as, grid, nthr, cbv, st);
   return check_launch(FLIP ? "dw_dgrad" : "dw_fwd");
 }
 

@@ -627,7 +627,7 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   }
   const bool stream = use_stream(a, dtype);
   GemmArgs as = a;
-  as.stamps = g_stamps;
+  as.stamps = stamp_region();
   // tiled path: the BN finish runs in the kernel's last workgroups (bn_finish.hpp tail_finish)
   // when the records fit its counters; otherwise as its own fold + finalize launch below
   GemmArgs b = as;

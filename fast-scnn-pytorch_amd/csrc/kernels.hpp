@@ -110,6 +110,7 @@ struct DwArgs {
   // workgroups when the records fit (tail_ink, set by the launcher) or as its own launch
   BnTail tail{};
   int tail_ink = 0;
+  unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
 };
 
 struct DwBwdArgs {

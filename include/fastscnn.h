@@ -210,10 +210,14 @@ int fscnn_prof_end(double* total_ms, long long* launches, double* bytes, double*
 int fscnn_prof_launch(long long i, int* kind, float* ms, double* bytes, double* flops,
                       const char** layer);
 const char* fscnn_prof_kind_name(int kind);
-/* Debug: phase stamps of the next pointwise-GEMM launches (per-wave 100 MHz wall clock at fixed
- * points of the kernel, tools/stamp_probe.py) into buf (>= workgroups * 4 * 8 uint64); null: off.
- * Process-global, single-threaded measurement only. */
-int fscnn_debug_stamps(void* buf);
+/* Debug: phase stamps of the next launches of the instrumented kernels (pointwise GEMMs, depthwise
+ * forward / stride-1 dgrad): per-wave 100 MHz wall clock at fixed points of the kernel
+ * (tools/stamp_probe.py).  Launch i writes buf + i * 262144 uint64 (8192 workgroups x 4 waves x
+ * 8 slots), up to max_launches; null: off.  fscnn_debug_stamp_count / _tag: launches recorded and
+ * each one's layer label.  Process-global, single-threaded measurement only. */
+int fscnn_debug_stamps(void* buf, int max_launches);
+int fscnn_debug_stamp_count(void);
+const char* fscnn_debug_stamp_tag(int i);
 
 /* ---- loss / optimizer ------------------------------------------------------------------- */
 /* out2[0] = mean loss over valid pixels, out2[1] = valid count; part: ce_parts*2 floats */

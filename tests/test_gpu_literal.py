@@ -7,10 +7,10 @@
   called here through the C ABI in exactly the executor's form (``fscnn_pw_dgrad_bnbwd`` =
   net.cpp ``Exec::pw_bwd`` + ``set_btarget``) and checked against a torch fp32 restatement: the
   stored dX, and dbeta / dgamma / the apply coefficients recomputed in fp64 from the stored dX.
-* cfg2 at its literal batch (8 x 3 x 1024 x 2048 fp32, eval): every image's logits equal its
+* cfg2 at its literal batch (8 x 3 x 1024 x 2048 fp32, eval): every image's logits against its
   own batch-1 forward (the bs = 8 launches use other grids: the streaming GEMMs' chunking and
-  8x the fused-block tiles), and image 0 (the cfg2 golden input) meets the golden + fp64 argmax
-  contract of tests/test_gpu_fullsize.py.
+  8x the fused-block tiles), image 0 (the cfg2 golden input) against the golden + fp64 argmax
+  contract of tests/test_gpu_fullsize.py, image 7 against the fp64 oracle.
 """
 import numpy as np
 import pytest
@@ -96,12 +96,23 @@ def test_pw_dgrad_bnbwd_executor_form(dt, M, N, K, mode, res, deep):
 
 
 def test_cfg2_literal_batch8_matches_batch1():
-    """cfg2 as BASELINE.json states it: bs = 8, fp32, eval; image 0 is the cfg2 golden input."""
+    """cfg2 as BASELINE.json states it: bs = 8, fp32, eval; image 0 is the cfg2 golden input.
+
+    The batch-8 forward is not bit-identical to batch 1 by design: the fused inference
+    bottleneck (ir.hip) runs only when a block's map gives >= 128 tiles, so bottleneck3 is one
+    launch at bs = 8 (256 tiles) and three at bs = 1 (32 tiles); both evaluate every product as
+    six bf16 MFMAs of exact fp32 splits, but in a different k order (measured: max |d| 1.0e-5 on
+    the logits, no image bit-identical).  Gate: image 0 of the batch meets the golden + fp64
+    contract (1e-4, argmax bit-exact off near-ties); image 7 is within 1e-4 of the fp64 oracle;
+    every image is within 1e-4 of its own batch-1 forward and its argmax differs only where the
+    batch-1 top-2 margin is < 1e-4."""
     from models.fast_scnn import FastSCNN
+    from oracle import fast_scnn_ref as ref
     from test_gpu_fullsize import _check_argmax, _oracle64
     g = load_golden("cfg2_c19_1024x2048")
     m = FastSCNN(19)
-    m.load_state_dict(golden_sd(g))
+    sd = golden_sd(g)
+    m.load_state_dict(sd)
     m = m.to(DEV).eval()
     x0 = golden_input(g)
     assert tuple(x0.shape) == (1, 3, 1024, 2048)
@@ -116,9 +127,20 @@ def test_cfg2_literal_batch8_matches_batch1():
             d = (o8[i:i + 1] - o1).abs().max().item()
             worst = max(worst, d)
             exact += int(torch.equal(o8[i:i + 1], o1))
+            srt = torch.sort(o1, dim=1).values
+            margin = srt[:, -1] - srt[:, -2]
+            flips = (o8[i:i + 1].argmax(1) != o1.argmax(1)) & (margin > 1e-4)
+            assert int(flips.sum()) == 0, "image %d: %d confident argmax flips" % (i, int(flips.sum()))
         o0 = o8[0:1].float().cpu()
+        o7 = o8[7:8].float().cpu()
     print("cfg2 bs=8 vs bs=1: %d of 8 images bit-identical, max |d| %.2e" % (exact, worst))
-    assert worst <= 1e-6
+    assert worst <= 1e-4
     np.testing.assert_allclose(o0.numpy().ravel()[g["out0.sample_idx"]], g["out0.sample_val"],
                                rtol=0, atol=1e-4)
     _check_argmax(o0, g, _oracle64(g, 19))
+    with torch.no_grad():
+        o64 = ref.forward({k: v.double() if v.is_floating_point() else v for k, v in sd.items()},
+                          xs[7].double(), 19)[0][0]
+    d7 = (o7.double() - o64).abs().max().item()
+    print("cfg2 bs=8 image 7 vs fp64 oracle: max |d| %.2e" % d7)
+    assert d7 < 1e-4

@@ -9,7 +9,8 @@ Stamp slots: 0 kernel entry, 1 after the prologue (first K chunk staged / weight
 (tiled).  Printed per launch: the kernel span (first entry -> last stamp), the spread of wave
 entry times (dispatch ramp) and the median / max of every phase.
 
-    python tools/stamp_probe.py
+    python tools/stamp_probe.py           # isolated launches at the low-res shapes
+    python tools/stamp_probe.py step      # every instrumented launch of one cfg3 train step
 """
 import os
 import sys
@@ -23,11 +24,15 @@ _fscnn_boot.load()
 from fast_scnn_pytorch_amd import _lib  # noqa: E402
 
 SLOTS = 8
+STRIDE = 8192 * 4 * SLOTS
 DEV = "cuda"
 
 
-def analyse(label, st):
+def analyse(label, st, base=None):
     t = st.view(-1, SLOTS).cpu().double()
+    if t.numel() == 0:
+        print("%-40s no stamps" % label)
+        return
     t = t[t[:, 0] > 0]
     if t.numel() == 0:
         print("%-40s no stamps" % label)
@@ -44,9 +49,10 @@ def analyse(label, st):
         d = d[~torch.isnan(d)]
         if d.numel():
             parts.append("%d-%d %.1f/%.1f" % (a, b, d.median().item(), d.max().item()))
-    print("%-40s waves %5d span %6.1f us  entry med %.1f max %.1f | %s"
-          % (label, t.shape[0], span, entry.median().item(), entry.max().item(), "  ".join(parts)),
-          flush=True)
+    at = "" if base is None else "@%7.1f " % ((t0.item() - base) / 100.0)
+    print("%-40s %swaves %5d span %6.1f us  entry med %.1f max %.1f | %s"
+          % (label, at, t.shape[0], span, entry.median().item(), entry.max().item(),
+             "  ".join(parts)), flush=True)
 
 
 def main():
@@ -97,12 +103,56 @@ def main():
         us = e0.elapsed_time(e1) / 20 * 1e3
         buf.zero_()
         torch.cuda.synchronize()
-        _lib.check(lib.fscnn_debug_stamps(_lib.ptr(buf)))
+        _lib.check(lib.fscnn_debug_stamps(_lib.ptr(buf), 1))
         run()
         torch.cuda.synchronize()
-        _lib.check(lib.fscnn_debug_stamps(None))
-        analyse("%s K%d N%d (%.1f us/launch)" % (label, K, N, us), buf)
+        _lib.check(lib.fscnn_debug_stamps(None, 0))
+        analyse("%s K%d N%d (%.1f us/launch)" % (label, K, N, us), buf[:STRIDE])
+
+
+def step():
+    """One cfg3 train step (bench.py's workload) with every instrumented launch stamped."""
+    import numpy as np
+    from fast_scnn_pytorch_amd import arch, portable_init
+    from fast_scnn_pytorch_amd.optim import FusedSGD
+    from models.fast_scnn import FastSCNN
+    lib = _lib.load()
+    m = FastSCNN(19)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                       arch.portable_state_dict(19, seed=0).items()})
+    m = m.to(DEV).train()
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    x = torch.from_numpy(portable_init.input_tensor(1, (8, 3, 1024, 2048))).to(DEV).to(torch.bfloat16)
+    t = torch.from_numpy(portable_init.target_tensor(3, (8, 1024, 2048), 19, 0.05)).to(DEV)
+
+    def one():
+        opt.zero_grad(set_to_none=True)
+        m.forward_loss(x, t).backward()
+        opt.step()
+    for _ in range(4):
+        one()
+    nmax = 160
+    buf = torch.zeros(nmax * STRIDE, dtype=torch.int64, device=DEV)
+    torch.cuda.synchronize()
+    _lib.check(lib.fscnn_debug_stamps(_lib.ptr(buf), nmax))
+    one()
+    torch.cuda.synchronize()
+    n = lib.fscnn_debug_stamp_count()
+    tags = [lib.fscnn_debug_stamp_tag(i).decode() for i in range(n)]
+    _lib.check(lib.fscnn_debug_stamps(None, 0))
+    firsts = []
+    for i in range(n):
+        v = buf[i * STRIDE:i * STRIDE + 8192 * 4 * SLOTS].view(-1, SLOTS)[:, 0]
+        v = v[v > 0]
+        if v.numel():
+            firsts.append(int(v.min().item()))
+    base = float(min(firsts)) if firsts else None
+    for i in range(n):
+        analyse("%3d %s" % (i, tags[i][:36]), buf[i * STRIDE:(i + 1) * STRIDE], base)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "step":
+        step()
+    else:
+        main()
