@@ -134,6 +134,77 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
   }
 }
 
+// per-thread staging table of the forward kernel's tile loop, computed once: for load k the
+// element offset of its vector within the tile (relative to the tile origin) and its (row, col)
+// in the haloed tile packed as row << 16 | col (0xFFFF0000: beyond the tile); the tile loop then
+// only adds a uniform base per tile (recomputing the per-load divisions each tile, or keeping
+// them live as 64-bit offsets, held ~40 VGPRs beside the prefetched tile)
+template <typename T, int S, int L>
+struct DwLanes {
+  int off[L];
+  int rc[L];
+  __device__ __forceinline__ void init(int W, int C, int cbv, int tid, int nthr) {
+    using G = DwTile<T, S>;
+    constexpr int V = VecW<T>::V;
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      const int i = tid + k * nthr;
+      const int pix = i / cbv, lv = i - pix * cbv;
+      const int r = pix / G::IC, col = pix - r * G::IC;
+      const bool in = pix < G::IR * G::IC;
+      off[k] = in ? (r * W + col) * C + lv * V : 0;
+      rc[k] = in ? (r << 16) | col : (int)0xFFFF0000;
+    }
+  }
+  // in-image test of load k for a tile whose haloed origin is (hi0, wi0)
+  __device__ __forceinline__ bool ok(int k, int H, int W, int hi0, int wi0) const {
+    const int r = rc[k] >> 16, col = rc[k] & 0xFFFF;
+    return r >= 0 && (unsigned)(hi0 + r) < (unsigned)H && (unsigned)(wi0 + col) < (unsigned)W;
+  }
+};
+
+template <typename T, int S, int L>
+__device__ __forceinline__ void dw_load_t(uint4 (&raw)[L], const DwLanes<T, S, L>& ln, const T* x,
+                                          int H, int W, int C, int n, int hi0, int wi0,
+                                          int cvbase) {
+  constexpr int V = VecW<T>::V;
+  // uniform tile origin (may lie before the image: only in-image loads use it)
+  const long long base = (((long long)n * H + hi0) * W + wi0) * C + (long long)cvbase * V;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    const bool ok = ln.ok(k, H, W, hi0, wi0);
+    raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(x + (ok ? base + ln.off[k] : 0)));
+  }
+}
+template <typename T, int S, bool IT, int L>
+__device__ __forceinline__ void dw_put_t(uint4* s_in, const uint4 (&raw)[L],
+                                         const DwLanes<T, S, L>& ln, int H, int W, int hi0,
+                                         int wi0, int cbv, int tid, int nthr, const float* sc,
+                                         const float* sh) {
+  using G = DwTile<T, S>;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    const int i = tid + k * nthr;
+    if (i < G::IR * G::IC * cbv) {
+      uint4 v = raw[k];
+      if constexpr (IT) v = sel4(ln.ok(k, H, W, hi0, wi0), bnrelu_vec<T>(v, sc, sh));
+      s_in[i] = v;
+    }
+  }
+}
+
+// workgroup -> (channel chunk cx, worker j of gridDim.y): XCD-contiguous (speed only): blocks
+// L = x (mod 8) share an XCD, so residue class x gets a contiguous range of workers, whose tile
+// ranges are neighbours (shared halo rows served by that XCD's L2)
+__device__ __forceinline__ void dw_worker(int& cx, int& j) {
+  const int gx = gridDim.x;
+  const long long T = (long long)gx * gridDim.y;
+  long long L = blockIdx.x + (long long)gx * blockIdx.y;
+  if ((T & 7) == 0) L = (L & 7) * (T >> 3) + (L >> 3);
+  cx = (int)(L % gx);
+  j = (int)(L / gx);
+}
+
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
 // TL: the launch finishes its BN in the last workgroups (a.tail_ink; a separate instantiation so
 // the other launches keep their register budget)
@@ -344,8 +415,318 @@ static size_t dw_shm(int cbv) {
   return (size_t)G::IR * G::IC * cbv * 16 + (size_t)cbv * 32 * 16;
 }
 
-static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv) {
+// ---- forward, 16-bit stride 1: streaming tile loop ------------------------------------------
+// Streaming tile loop: the grid holds every workgroup resident (dw_grid: gridDim.y workers per
+// channel chunk) and worker j walks the contiguous spatial tiles [T*j/wy, T*(j+1)/wy) of its
+// chunk in row-band order; the next tile's loads are in flight (registers) while the current
+// tile computes from LDS.  (Round 3's one-tile-per-workgroup grid ran 2-6 dispatch rounds of
+// load -> compute -> store, with the CU's memory pipe idle during each compute phase.)
+// Train statistics / BN-backward partials are accumulated over the worker's tiles: ONE record
+// per worker (records [wy][3|2][C]); forward statistics as per-thread sums shifted by the
+// worker's first output value of each channel (gemm_stream's convention), merged in fixed order.
+// TL: the launch finishes its BN in the last workgroups (a.tail_ink; a separate instantiation so
+// the other launches keep their register budget)
+template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool TL = false>
+__global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) {
+  using G = DwTile<T, S>;
+  constexpr int V = VecW<T>::V;
+  // LDS sized per launch (dw_shm): the staged tile of cbv channel vectors + the reduction rows
+  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
+  uint4* s_in = s_dyn;
+  float* s_red = reinterpret_cast<float*>(s_dyn + G::IR * G::IC * cbv);
+  // per-channel tables of the chunk (cbv * V channels each): read where used, so the loop
+  // carries only the weights, the prefetched tile and the sums (prefetch + tables in registers
+  // passed 256 VGPRs)
+  float* s_tab = s_red + 3 * cbv * 32 * 4;
+  float* t_isc = s_tab;                 // lazy input BN (IT)
+  float* t_ish = t_isc + cbv * 8;
+  float* t_sc = t_ish + cbv * 8;        // epilogue affine (eval fold) or 1 / 0
+  float* t_sh = t_sc + cbv * 8;
+  float* t_bm = t_sh + cbv * 8;         // BN-backward partials (BR): mean, invstd, mask affine
+  float* t_bi = t_bm + cbv * 8;
+  float* t_bs = t_bi + cbv * 8;
+  float* t_bh = t_bs + cbv * 8;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int QB = cbv * G::QPV;                 // quads per workgroup
+  const int q = tid % QB, grp = tid / QB;
+  const int gx = grp % G::GX, gy = grp / G::GX;
+  int cx, wj;
+  dw_worker(cx, wj);
+  const int wy = gridDim.y;
+  const int tiles_w = cdiv(a.Wo, G::TW), tiles_h = cdiv(a.Ho, G::TH);
+  const int ntiles = a.N * tiles_h * tiles_w;
+  const int t0 = (int)((long long)ntiles * wj / wy), t1 = (int)((long long)ntiles * (wj + 1) / wy);
+  const int cvb = cx * cbv;                       // first channel vector of the chunk
+  const int c0 = cvb * V + q * 4;                 // first channel of the thread's quad
+  auto tile_of = [&](int t, int& n, int& th0, int& tw0) {
+    const int tw = t % tiles_w, r = t / tiles_w;
+    n = r / tiles_h;
+    th0 = (r - n * tiles_h) * G::TH;
+    tw0 = tw * G::TW;
+  };
+  stamp(a.stamps, 0);
+  // next-tile prefetch where the loads fit beside the loop's live set (16-bit stride 1: 6 vectors
+  // per thread); fp32 (12) and stride 2 (10) load each tile at the top of its iteration
+  constexpr bool PF = sizeof(T) == 2 && G::LPT <= 8;
+  DwLanes<T, S, G::LPT> ln;
+  ln.init(a.W, a.C, cbv, tid, nthr);
+  uint4 raw[G::LPT];
+  if (PF && t0 < t1) {
+    int n, th0, tw0;
+    tile_of(t0, n, th0, tw0);
+    dw_load_t<T, S, G::LPT>(raw, ln, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
+                            cvb);
+  }
+  const BnBwdPart& b = a.bs;
+  for (int i = tid; i < cbv * V; i += nthr) {
+    const int c = cvb * V + i;
+    if constexpr (IT) {
+      t_isc[i] = a.in_scale[c];
+      t_ish[i] = a.in_shift[c];
+    }
+    t_sc[i] = a.scale ? a.scale[c] : 1.f;
+    t_sh[i] = a.scale ? a.shift[c] : 0.f;
+    if constexpr (BR) {
+      const bool m2 = b.mode == 2;
+      t_bm[i] = b.mean[c];
+      t_bi[i] = b.invstd[c];
+      t_bs[i] = m2 ? b.scale[c] : 0.f;  // mode 0: mask fmaf(z, 0, 1) > 0 always
+      t_bh[i] = m2 ? b.shift[c] : 1.f;
+    }
+  }
+  float wt[9][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = a.w[(size_t)(c0 + j) * 9 + t];
+  // BN-backward partials (BR) / shifted forward statistics (a.part): per-thread sums
+  float s1[4], s2[4], shf[4];
+  float cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s1[j] = s2[j] = shf[j] = 0.f;
+  const int lq4 = q * 4;  // the thread's quad within the chunk's channel tables
+  __syncthreads();
+  const bool stats = !BR && a.part != nullptr;
+  const T* sl = reinterpret_cast<const T*>(s_in);
+  const int pstride = cbv * V;                   // elements per staged pixel
+  const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
+
+#pragma unroll 1
+  for (int t = t0; t < t1; ++t) {
+    int n, th0, tw0;
+    tile_of(t, n, th0, tw0);
+    if constexpr (!PF)
+      dw_load_t<T, S, G::LPT>(raw, ln, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
+                              cvb);
+    dw_put_t<T, S, IT, G::LPT>(s_in, raw, ln, a.H, a.W, th0 * S - 1, tw0 * S - 1, cbv, tid, nthr,
+                               t_isc + (tid % cbv) * V, t_ish + (tid % cbv) * V);
+    __syncthreads();
+    if (PF && t + 1 < t1) {  // the next tile's loads, in flight during this tile's compute
+      int n2, th2, tw2;
+      tile_of(t + 1, n2, th2, tw2);
+      dw_load_t<T, S, G::LPT>(raw, ln, (const T*)a.x, a.H, a.W, a.C, n2, th2 * S - 1,
+                              tw2 * S - 1, cvb);
+    }
+    if (t == t0) stamp(a.stamps, 1);
+    float acc[G::HS][G::WS][4];
+#pragma unroll
+    for (int r = 0; r < G::HS; ++r)
+#pragma unroll
+      for (int p = 0; p < G::WS; ++p)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][p][j] = 0.f;
+    // one input row of quads at a time (the memory clobber keeps the next row's LDS reads below
+    // it: hoisting all NR x NC quads held ~96 more values live beside the prefetched tile)
+#pragma unroll
+    for (int rr = 0; rr < G::NR; ++rr) {
+#pragma unroll
+      for (int ci = 0; ci < G::NC; ++ci) {
+        float v[4];
+        quad_ld(sl + ((lr0 + rr) * G::IC + lc0 + ci) * pstride + q * 4, v);
+#pragma unroll
+        for (int r = 0; r < G::HS; ++r) {
+          const int kh = rr - r * S;
+          if (kh < 0 || kh > 2) continue;
+#pragma unroll
+          for (int p = 0; p < G::WS; ++p) {
+            const int kw = ci - p * S;
+            if (kw < 0 || kw > 2) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[r][p][j] = fmaf(v[j], wt[kh * 3 + kw][j], acc[r][p][j]);
+          }
+        }
+      }
+      asm volatile("" ::: "memory");
+    }
+    const int ho0 = th0 + gy * G::HS, wo0 = tw0 + gx * G::WS;
+    const int nrow = max(0, min(G::HS, a.Ho - ho0)), ncol = max(0, min(G::WS, a.Wo - wo0));
+    float sc[4], sh[4];
+    {
+      const float4 a4 = *reinterpret_cast<const float4*>(t_sc + lq4);
+      const float4 b4 = *reinterpret_cast<const float4*>(t_sh + lq4);
+      sc[0] = a4.x; sc[1] = a4.y; sc[2] = a4.z; sc[3] = a4.w;
+      sh[0] = b4.x; sh[1] = b4.y; sh[2] = b4.z; sh[3] = b4.w;
+    }
+#pragma unroll
+    for (int r = 0; r < G::HS; ++r) {
+      if (r >= nrow) continue;
+      T* yb = (T*)a.y + (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0) * a.C + c0;
+#pragma unroll
+      for (int p = 0; p < G::WS; ++p) {
+        if (p >= ncol) continue;
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = acc[r][p][j] * sc[j] + sh[j];
+          o[j] = a.relu ? fmaxf(v, 0.f) : v;
+          acc[r][p][j] = o[j];
+        }
+        quad_st(yb + (size_t)p * a.C, o);
+        if (!BR && stats) {  // shifted sums; the shift is the thread's first output value
+          if (cnt == 0.f) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) shf[j] = o[j];
+          }
+          cnt += 1.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = o[j] - shf[j];
+            s1[j] += d;
+            s2[j] += d * d;
+          }
+        }
+      }
+    }
+    if constexpr (BR) {
+      // ---- stride-1 dgrad: BN-backward partial sums of the stored dx (it is that BN's dy) ---
+      float bm[4], bi[4], bsc[4], bsh[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bm[j] = t_bm[lq4 + j];
+        bi[j] = t_bi[lq4 + j];
+        bsc[j] = t_bs[lq4 + j];
+        bsh[j] = t_bh[lq4 + j];
+      }
+#pragma unroll
+      for (int r = 0; r < G::HS; ++r) {
+        float z[G::WS][4];  // one output row of z per batch of loads
+#pragma unroll
+        for (int p = 0; p < G::WS; ++p) {
+          const bool ok = r < nrow && p < ncol;
+          const size_t pix = ok ? ((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0 + p : 0;
+          quad_ld((const T*)b.z + pix * a.C + c0, z[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < G::WS; ++p) {
+          const bool ok = r < nrow && p < ncol;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float gv = round_as<T>(acc[r][p][j]);
+            gv = (ok && fmaf(z[p][j], bsc[j], bsh[j]) > 0.f) ? gv : 0.f;
+            s1[j] += gv;
+            s2[j] += gv * (z[p][j] - bm[j]) * bi[j];
+          }
+        }
+        asm volatile("" ::: "memory");  // next row's z loads after this row's use
+      }
+    }
+    __syncthreads();  // every read of this tile's LDS image (and of s_red) is done
+  }
+  stamp(a.stamps, 2);
+  if (!BR && !stats) return;
+  // ---- one record per worker: the G pixel groups of each channel quad in fixed order ---------
+  constexpr int R = BR ? 2 : 3;
+  float* part = BR ? b.part : a.part;
+  float* rec = part + (size_t)wj * R * a.C;
+  float tot[3][4];
+  if constexpr (!BR) {  // per thread (n, mean, M2) from its shifted sums
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float m = cnt > 0.f ? shf[j] + s1[j] / cnt : 0.f;
+      s2[j] = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
+      s1[j] = m;
+    }
+  }
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    if (pass == 2 && BR) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      s_red[((pass * G::G + grp) * QB + q) * 4 + j] = pass == 0 ? s1[j] : (pass == 1 ? s2[j] : cnt);
+  }
+  __syncthreads();
+  if (grp == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (BR) {
+        float u = 0.f, w = 0.f;
+        for (int g2 = 0; g2 < G::G; ++g2) {
+          u += s_red[((0 * G::G + g2) * QB + q) * 4 + j];
+          w += s_red[((1 * G::G + g2) * QB + q) * 4 + j];
+        }
+        tot[0][j] = u;
+        tot[1][j] = w;
+      } else {  // Chan merge of the groups, fixed order
+        float nn = 0.f, mean = 0.f, m2 = 0.f;
+        for (int g2 = 0; g2 < G::G; ++g2) {
+          const float nb = s_red[((2 * G::G + g2) * QB + q) * 4 + j];
+          if (nb <= 0.f) continue;
+          const float mb = s_red[((0 * G::G + g2) * QB + q) * 4 + j];
+          const float qb = s_red[((1 * G::G + g2) * QB + q) * 4 + j];
+          const float tn = nn + nb, d = mb - mean;
+          mean += d * (nb / tn);
+          m2 += qb + d * d * (nn * nb / tn);
+          nn = tn;
+        }
+        tot[0][j] = mean;
+        tot[1][j] = m2;
+        tot[2][j] = nn;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st_wt(rec + c0 + j, tot[0][j]);
+      st_wt(rec + a.C + c0 + j, tot[1][j]);
+      if constexpr (!BR) st_wt(rec + 2 * a.C + c0 + j, tot[2][j]);
+    }
+  }
+  stamp(a.stamps, 3);
+  if constexpr (TL)
+    tail_finish<!BR>(part, wy, a.C, wj, cvb * V, cbv * V, cx, a.tail,
+                     reinterpret_cast<double*>(s_dyn));
+  stamp(a.stamps, 4);
+}
+
+template <typename T, int S>
+static size_t dw_loop_shm(int cbv) {
+  using G = DwTile<T, S>;
+  return (size_t)G::IR * G::IC * cbv * 16 + (size_t)3 * cbv * 32 * 16 + (size_t)8 * cbv * 8 * 4;
+}
+
+// 16-bit stride-1 forwards run the streaming tile loop (FSCNN_DW_LOOP=0: the one-tile kernel)
+static bool dw_loop_on(int V, int S) {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_DW_LOOP");
+    return !(e && e[0] == '0');
+  }();
+  return on && V == 8 && S == 1;
+}
+
+// fwd: the forward's grid (the loop kernel's gx chunks x wy workers where it applies), else one
+// workgroup per (channel chunk, tile)
+static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv, bool fwd = false) {
   cbv = dw_cbv(C / V);
+  if (fwd && dw_loop_on(V, S)) {
+    // every workgroup resident (2 per CU): gx channel chunks x wy workers, each walking >= 1
+    // of the chunk's T spatial tiles; wy is also the record count of the statistics forms
+    using G = DwTile<bf16, 1>;
+    const int gx = C / V / cbv;
+    const long long T = (long long)N * cdiv(Ho, G::TH) * cdiv(Wo, G::TW);
+    long long wy = cdiv(2 * 256, gx);
+    if (wy > T) wy = T;
+    if (wy < 1) wy = 1;
+    return dim3(gx, (unsigned)wy, 1);
+  }
   int TH, TW;
   if (V == 4) {
     TH = S == 1 ? DwTile<float, 1>::TH : DwTile<float, 2>::TH;
@@ -359,7 +740,7 @@ static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv) {
 
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
   int cbv;
-  dim3 g = dw_grid(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8, stride, cbv);
+  dim3 g = dw_grid(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8, stride, cbv, true);
   return (int)(g.y * g.z);
 }
 
@@ -369,6 +750,14 @@ static void dw_launch_fwd_t(const DwArgs& a, dim3 grid, int nthr, int cbv, hipSt
     if (a.tail_ink) dw_fwd_kernel<T, 1, true, false, true, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
     else dw_fwd_kernel<T, 1, true, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
     return;
+  }
+  if constexpr (!FLIP && sizeof(T) == 2) {
+    if (a.stride == 1 && dw_loop_on(8, 1)) {  // the streaming tile loop (grid: dw_grid fwd)
+      const size_t shm = dw_loop_shm<T, 1>(cbv);
+      if (a.tail_ink) dw_fwd_loop_kernel<T, 1, false, IT, false, true><<<grid, nthr, shm, st>>>(a, cbv);
+      else dw_fwd_loop_kernel<T, 1, false, IT><<<grid, nthr, shm, st>>>(a, cbv);
+      return;
+    }
   }
   if (!FLIP && a.tail_ink) {  // train forward with the in-kernel BN finish
     if (a.stride == 1) dw_fwd_kernel<T, 1, false, IT, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
@@ -383,7 +772,7 @@ template <bool FLIP, bool IT, bool BR = false>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   int cbv;
-  dim3 grid = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
+  dim3 grid = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv, !FLIP);
   if (grid.z > 65535 || grid.y > 65535) {
     set_error("dw: grid too large (%u x %u)", grid.y, grid.z);
     return E_UNSUPPORTED;
@@ -417,7 +806,7 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   int P = 0;
   if (a.part && a.tail.counters) {  // BN finish: in the kernel when the records fit its counters
     int cbv;
-    const dim3 g = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
+    const dim3 g = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv, true);
     P = (int)(g.y * g.z);
     b.tail_ink = a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
   }
