@@ -673,12 +673,14 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
 // output, which only conv0's weight gradient consumes.  Rather than storing g (268 MB at cfg3) and
 // streaming it back with z in a second launch, the workgroup keeps its tile of masked g and of z
 // in LDS as [pixel][channel] images (64-B rows, one 8-B store per thread and pixel), gathers the
-// conv0 patches x^T [tap][pixel] beside them, and accumulates A = sum x g^T and Zx = sum x z^T with
+// conv0 patches x^T [tap][pixel] beside them, and accumulates A = sum x g^T and Zc = sum x (z-mean)^T with
 // v_mfma_f32_32x32x16 (taps x channels, k = 16 pixels): the A operand is one ds_read_b128 of x^T,
 // the B operands are read column-wise with ds_read_b64_tr_b16 (gfx950's transposing LDS read).
 // BN backward is linear in g, z and 1 per channel (bwdx_apply: dz = al*g + gz*z + be), so the
-// conv0 gradient is dW = al*A + gz*Zx + be*B with B = sum x, formed after the BN finish
-// (conv0_wgrad_combine) — the BN's statistics of g are no longer needed before the pass over g.
+// conv0 gradient is dW = al*A + gz*Zc + (be + gz*mean)*B with B = sum x, formed after the BN
+// finish (conv0_wgrad_combine) — the BN's statistics of g are not needed before the pass over g.
+// z is centred before the MFMA (rounded to T as z - mean): summed raw, gz*Zx and be*B would both
+// grow with |mean| / std and cancel.
 // Persistent: LC_MAXP workgroups walk contiguous tile ranges; one BN record and one LC0_SLAB
 // partial row per workgroup (fixed-order reductions: deterministic); the BN finish is the
 // separate fold+finalize launch.
@@ -846,17 +848,19 @@ __global__ __launch_bounds__(256, 2) void ltd_c0_bwd_kernel(LtdC0BwdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool ok = h0 + r < a.H && w0 + q < a.W;
-        float z[V], gv[V];
+        float z[V], gv[V], zc[V];
         lc_unpack4<T>(zr[r][q], z);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           float v = round_as<T>(acc[q][j]);
           v = (ok && fmaf(z[j], msv[j], mhv[j]) > 0.f) ? v : 0.f;
+          zc[j] = z[j] - bmv[j];
           s1[j] += v;
-          s2[j] += v * (z[j] - bmv[j]) * biv[j];
+          s2[j] += v * zc[j] * biv[j];
           gv[j] = v;
         }
         gw[r][q] = lc_pack4<T>(gv);  // exact: v is a T value
+        zr[r][q] = lc_pack4<T>(zc);  // the MFMA's centred z (outside the image: x = 0 there)
       }
     }
     // x^T values as T (pixels outside the output: 0), and their sums
@@ -1035,16 +1039,19 @@ int ltd_c0_bwd(const LtdC0BwdArgs& a, int dtype, hipStream_t st) {
                          st, a.tail.counters, a.tail.tab);
 }
 
-__global__ void conv0_wgrad_combine_kernel(const float* s, const float* tab, float* dw) {
+__global__ void conv0_wgrad_combine_kernel(const float* s, const float* tab, const float* mean,
+                                           float* dw) {
   const int o = blockIdx.x * 256 + threadIdx.x;
   if (o >= 864) return;
   const int co = o / 27, tap = o - 27 * co;
   const float* e = tab + (size_t)co * BWDX_STRIDE;  // al, be, gz (bn_finish.hpp bn_bwd_finish)
-  dw[o] = fmaf(e[0], s[o], fmaf(e[2], s[864 + o], e[1] * s[1728 + tap]));
+  const float be_c = fmaf(e[2], mean[co], e[1]);     // the constant term about the mean
+  dw[o] = fmaf(e[0], s[o], fmaf(e[2], s[864 + o], be_c * s[1728 + tap]));
 }
 
-int conv0_wgrad_combine(const float* sums, const float* tab, float* dw, hipStream_t st) {
-  conv0_wgrad_combine_kernel<<<cdiv(864, 256), 256, 0, st>>>(sums, tab, dw);
+int conv0_wgrad_combine(const float* sums, const float* tab, const float* mean, float* dw,
+                        hipStream_t st) {
+  conv0_wgrad_combine_kernel<<<cdiv(864, 256), 256, 0, st>>>(sums, tab, mean, dw);
   return check_launch("conv0_wgrad_combine");
 }
 

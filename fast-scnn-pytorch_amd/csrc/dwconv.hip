@@ -703,11 +703,14 @@ static size_t dw_loop_shm(int cbv) {
   return (size_t)G::IR * G::IC * cbv * 16 + (size_t)3 * cbv * 32 * 16 + (size_t)8 * cbv * 8 * 4;
 }
 
-// 16-bit stride-1 forwards run the streaming tile loop (FSCNN_DW_LOOP=0: the one-tile kernel)
+// FSCNN_DW_LOOP=1: 16-bit stride-1 forwards run the streaming tile loop.  Off by default:
+// measured r04 (cfg3 bf16 step) 6.20 ms with it vs 6.04 ms with the one-tile kernel -- at <= 2
+// workgroups per CU (its ~240 VGPRs) one tile of prefetch hides less HBM latency than the
+// one-tile kernel's higher occupancy does
 static bool dw_loop_on(int V, int S) {
   static const bool on = [] {
     const char* e = getenv("FSCNN_DW_LOOP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on && V == 8 && S == 1;
 }

@@ -536,8 +536,8 @@ static void launch_nt_pf(const GemmArgs& a, int nt, dim3 grid, size_t shm, hipSt
   }
 }
 
-// deep prefetch: 16-bit, plain B, >= 4 K chunks, and a grid of at most two workgroups per CU
-// (the long-K launches at M <= 65536, where the chain of chunk load latencies is the time)
+// deep prefetch (FSCNN_GEMM_PF=3, off by default): 16-bit, plain B, >= 4 K chunks, and a grid of
+// at most two workgroups per CU (the long-K launches at M <= 65536)
 static int nt_prefetch_depth(const GemmArgs& a, int dtype, int nt) {
   static const int env = [] {
     const char* e = getenv("FSCNN_GEMM_PF");
@@ -547,8 +547,9 @@ static int nt_prefetch_depth(const GemmArgs& a, int dtype, int nt) {
   const int nchunks = cdiv(a.K, G_VROW * V);
   const long long wgs = (long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt);
   if (dtype == DT_F32 || a.b_trans || nchunks < 4) return 1;
-  if (env == 1 || env == 3) return env;
-  return wgs <= 512 ? 3 : 1;
+  // measured r04 (cfg3 bf16 step, A/B): 6.048 ms with the ring at <= 512 workgroups vs 6.023 ms
+  // without -- the ring's extra VGPRs cost more occupancy than the hidden latency buys; opt-in
+  return (env == 3 && wgs <= 512) ? 3 : 1;
 }
 
 template <typename T, bool BT, bool BS, bool AT = false, bool X3 = false>

@@ -322,6 +322,7 @@ struct CeHeadArgs {
   long long ignore_index;
   float* g_raw;              // 2 planes NHWC [N][Hl][Wl][ldl] fp32: own row, spill from row above
   float* part;               // [N * Hl][2]
+  unsigned long long* stamps = nullptr;
 };
 
 struct DropArgs {
@@ -391,7 +392,7 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st);
 // emits that BN's backward records and finish (bs / tail, as dw_dgrad does) and, instead of
 // storing g, per-workgroup conv0 partials [P][LC0_SLAB] = (A = sum g x^T, Zx = sum z x^T,
 // B = sum x) over the conv0 patches x.  With the finished BN's operand table (common.hpp
-// bwdx_apply: dz = al*g + gz*z + be), conv0_wgrad_combine forms dW = al*A + gz*Zx + be*B.
+// bwdx_apply: dz = al*g + gz*z + be), conv0_wgrad_combine forms dW = al*A + gz*Zc + (be+gz*mean)*B.
 constexpr int LC0_SLAB = 2 * 864 + 27;  // [A: co*27+tap][Zx: 864 + co*27+tap][B: 1728 + tap]
 struct LtdC0BwdArgs {
   int N, H, W;     // conv0 output = the depthwise layer's input (dx) dims
@@ -407,8 +408,10 @@ struct LtdC0BwdArgs {
 int ltd_c0_bwd_parts(int N, int H, int W);
 bool ltd_c0_bwd_ok(int dtype, int x_dtype, int XW, const void* x);
 int ltd_c0_bwd(const LtdC0BwdArgs& a, int dtype, hipStream_t st);
-// dW[co][tap] = al*A + gz*Zx + be*B from the reduced LC0_SLAB sums and the table (BWDX_STRIDE)
-int conv0_wgrad_combine(const float* sums, const float* tab, float* dw, hipStream_t st);
+// dW[co][tap] = al*A + gz*Zc + (be + gz*mean)*B from the reduced LC0_SLAB sums (Zc over z - mean)
+// and the table (BWDX_STRIDE)
+int conv0_wgrad_combine(const float* sums, const float* tab, const float* mean, float* dw,
+                        hipStream_t st);
 
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride);
 int dw_fwd(const DwArgs& a, int dtype, hipStream_t st);

@@ -789,8 +789,8 @@ struct Exec {
     if (rc || !c0_combine) return rc;
     c0_combine = false;
     g_prof_tag = "learning_to_downsample.conv (weight gradient)";
-    return conv0_wgrad_combine((const float*)Bw(pl.c0sum), (const float*)Bw(pl.xtab), G(net.c0.w),
-                               r.st);
+    return conv0_wgrad_combine((const float*)Bw(pl.c0sum), (const float*)Bw(pl.xtab),
+                               Wf(pl.c0.mean), G(net.c0.w), r.st);
   }
   int slab_oom() {
     set_error("backward: weight-gradient slab arena exhausted");

@@ -144,3 +144,48 @@ def test_cfg2_literal_batch8_matches_batch1():
     d7 = (o7.double() - o64).abs().max().item()
     print("cfg2 bs=8 image 7 vs fp64 oracle: max |d| %.2e" % d7)
     assert d7 < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nc,N,H,W", [
+    (19, 2, 256, 512),    # one column chunk, targets staged in LDS
+    (19, 2, 64, 2112),    # Wl = 264: two column chunks (carry), W > 2048: targets from HBM
+    (2, 2, 128, 256),     # the TuSimple class count
+])
+def test_fused_ce_head_16bit_vs_fp64(dt, nc, N, H, W):
+    """The 16-bit fused loss head (head.hip ce_head2_kernel: row-factored accumulation, target
+    one-hots in LDS) against autograd in fp64 on the SAME low-res logits the forward stored:
+    bilinear align_corners upsample (models/fast_scnn.py:51) + nn.CrossEntropyLoss(ignore_index=-1)
+    (utils/loss.py:103-124).  Loss to 1e-5; dlogits to one 16-bit rounding of the fp32 sum."""
+    import torch.nn.functional as F
+    from models.fast_scnn import FastSCNN
+    torch.manual_seed(7)
+    m = FastSCNN(nc).to(DEV).train()
+    m._dropout_seed = 3
+    m._keep_ws = True
+    x = _rnd((N, 3, H, W), 11).to(DEV).to(dt)
+    t = (_rnd((N, H, W), 12, 0, nc).floor().long()).clamp_(0, nc - 1)
+    drop = _rnd((N, H, W), 13, 0, 1) < 0.05
+    t[drop] = -1
+    t[:, 5:9, :] = -1          # whole ignored rows
+    t = t.to(DEV)
+    loss = m.forward_loss(x, t)
+    loss.backward()
+    torch.cuda.synchronize()
+    Hl, Wl = H // 8, W // 8
+    L = m.debug_buffer("logits").double().view(N, Hl, Wl, nc).permute(0, 3, 1, 2).clone()
+    G = m.debug_buffer("g_logits").double().view(N, Hl, Wl, nc).permute(0, 3, 1, 2)
+    L.requires_grad_(True)
+    up = F.interpolate(L, (H, W), mode="bilinear", align_corners=True)
+    lref = F.cross_entropy(up, t, ignore_index=-1)
+    lref.backward()
+    gref = L.grad
+    assert abs(loss.item() - lref.item()) <= 1e-5 * abs(lref.item()), (loss.item(), lref.item())
+    ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    err = (G - gref).abs()
+    # f16 stores |g| < 2^-14 as subnormals (spacing 2^-24): unscaled CE gradients at this pixel
+    # count are ~3e-5, so one f16 rounding is up to half that spacing (GradScaler lifts them)
+    sub = 2.0 ** -24 if dt == torch.float16 else 0.0
+    bound = ulp * gref.abs() + 2e-5 * gref.abs().max() + sub
+    assert bool((err <= bound).all()), "dlogits: max err %.3e (max |g| %.3e)" % (
+        err.max().item(), gref.abs().max().item())

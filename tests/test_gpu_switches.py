@@ -101,3 +101,21 @@ def test_ltd_fused_backward_matches_two_pass(tmp_path):
                 assert scale > 0 and float(np.abs(x - y).max()) <= 1e-2 * scale, (i, n)
             else:
                 assert np.array_equal(x, y), (i, n)
+
+
+def test_ltd_fused_backward_with_shifted_bn_mean(tmp_path):
+    """As above with conv0's BN mean far from 0 (image + 4.0, 2 x 3 x 512 x 1024): the fused pass
+    accumulates sum x (z - mean) (conv0.hip ltd_c0_bwd), so dW = al*A + gz*Zc + (be + gz*mean)*B
+    has no cancellation of terms growing with |mean| / std.  Checked after one step (the two
+    paths' weights then diverge by their own rounding)."""
+    ref = _worker(tmp_path, "FSCNN_LTD_FUSED=0", "bf16shift")
+    got = _worker(tmp_path, None, "bf16shift")
+    names = [str(n) for n in ref["names"]]
+    off = np.concatenate([[0], np.cumsum(ref["sizes"])])
+    j = names.index("learning_to_downsample.conv.conv.0.weight")
+    x = ref["grad0"][off[j]:off[j + 1]]
+    y = got["grad0"][off[j]:off[j + 1]]
+    scale = float(np.abs(x).max())
+    err = float(np.abs(x - y).max())
+    print("conv0 dW (shifted mean): max |d| %.3e of max |dW| %.3e" % (err, scale))
+    assert scale > 0 and err <= 1e-2 * scale

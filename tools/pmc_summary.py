@@ -15,10 +15,10 @@ import sys
 # bench.py PROF_KINDS names -> alternatives, each a list of kernel-name substrings that must all
 # match (gemm_nt is the launcher's family: the tiled kernel and the streaming kernel it picks)
 FAMILIES = {
-    "conv0_fwd": [["conv0_fwd_kernel"]], "dw_fwd": [["dw_fwd_kernel<", "false>"]],
+    "conv0_fwd": [["conv0_fwd_kernel"]], "dw_fwd": [["dw_fwd_kernel<", "false>"], ["dw_fwd_loop_kernel<"]],
     "dw_dgrad": [["dw_dgrad_s2_kernel"]], "dw_wgrad": [["dw_wgrad_kernel"]],
     "gemm_nt": [["gemm_nt_kernel"], ["gemm_stream_kernel"]], "gemm_tn": [["gemm_tn_kernel"]],
-    "ce_head": [["ce_head_kernel"]], "conv0_wgrad": [["conv0_wgrad_kernel"]],
+    "ce_head": [["ce_head_kernel"], ["ce_head2_kernel"]], "conv0_wgrad": [["conv0_wgrad_kernel"]],
 }
 
 

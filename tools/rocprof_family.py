@@ -15,12 +15,12 @@ import sys
 FAMILIES = [
     ("gemm_nt", ("gemm_stream_kernel", "gemm_stream_x3_kernel", "gemm_nt_kernel")),
     ("gemm_tn", ("gemm_tn_kernel",)),
-    ("dw_fwd", ("dw_fwd_kernel",)),
+    ("dw_fwd", ("dw_fwd_kernel", "dw_fwd_loop_kernel")),
     ("dw_dgrad", ("dw_dgrad_kernel", "dw_dgrad_s2_kernel")),
     ("dw_wgrad", ("dw_wgrad_kernel",)),
     ("bn_bwd_apply", ("bn_bwd_apply_kernel",)),
     ("bn_apply", ("bn_apply_kernel",)),
-    ("ce_head", ("ce_head_kernel",)),
+    ("ce_head", ("ce_head_kernel", "ce_head2_kernel")),
     ("conv0_fwd", ("conv0_fwd_kernel",)),
     ("conv0_wgrad", ("ltd_c0_bwd_kernel", "conv0_wgrad_kernel")),
     ("lowres_block", ("lowres_",)),
