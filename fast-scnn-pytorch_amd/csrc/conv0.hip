@@ -755,14 +755,17 @@ __global__ __launch_bounds__(256, 2) void ltd_c0_bwd_kernel(LtdC0BwdArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) accA[r] = accZ[r] = 0.f;
 
-  // tile t -> (image n, row pair hp, column block cbk); < 2^31 tiles (host check)
+  // tile t -> (image n, column block cbk, row pair hp), hp fastest: a workgroup walks DOWN one
+  // column block, so the dy row and the image rows a tile shares with the tile above it were
+  // fetched by this workgroup one tile earlier (L2-hot) instead of by another workgroup 8 tiles
+  // apart; < 2^31 tiles (host check)
   const int CB = cdiv(a.W, LC_TW), RP = (a.H + 1) / 2;
   const int tiles = a.N * RP * CB;
   const size_t XHW = (size_t)a.XH * a.XW;
   const int t_end = (int)((long long)tiles * (blockIdx.x + 1) / gridDim.x);
   for (int t = (int)((long long)tiles * blockIdx.x / gridDim.x); t < t_end; ++t) {
-    const int nr = t / CB, cbk = t - nr * CB;
-    const int n = nr / RP, hp = nr - n * RP;
+    const int nc = t / RP, hp = t - nc * RP;
+    const int n = nc / CB, cbk = nc - n * CB;
     const int h0 = 2 * hp, wc0 = cbk * LC_TW, w0 = wc0 + 4 * ty;
     // ---- every global load first: dy 2 x 3, z 2 x 4 (8 B each), the x rows of the patches ---
     uint2 gr[2][3], zr[2][4];

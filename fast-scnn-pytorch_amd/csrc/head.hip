@@ -22,6 +22,7 @@ constexpr int HD_CMAX = 32;
 constexpr int HD_TMAX = 2048;  // max full-res row width whose targets are staged in LDS
 constexpr float HD_LOG2E = 1.4426950408889634f;
 constexpr float HD_LN2 = 0.6931471805599453f;
+constexpr int HD_PD = 4;  // int8 target rows in flight per thread (ce_head2_kernel)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int hd_first_ge(int i, int Lin, int Lout, float sc) {
@@ -380,6 +381,19 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
     const bool lds_t = W <= HD_TMAX;
     constexpr int TPT = HD_TMAX / HD_T;
     int tnext[TPT];
+    // int8 targets (a.tgt8): 8 bytes per thread and row, HD_PD rows in flight (register ring)
+    const bool t8 = a.tgt8 != nullptr && lds_t && W % 8 == 0;
+    const bool t8own = tid * 8 < W;
+    const signed char* trow8 = a.tgt8 + (size_t)n * H * W + tid * 8;
+    uint2 tq[HD_PD];
+    auto load8 = [&](int h, uint2& d) {
+      d = (h < h_hi && t8own) ? *reinterpret_cast<const uint2*>(trow8 + (size_t)h * W)
+                              : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    };
+    if (t8) {
+#pragma unroll
+      for (int j = 0; j < HD_PD; ++j) load8(h_lo + j, tq[j]);
+    }
     auto load_trow = [&](int h) {
       const long long* tr = tgt + (size_t)h * W;
 #pragma unroll
@@ -389,7 +403,7 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
         tnext[k] = (w < W && tg != a.ignore_index && tg >= 0 && tg < CT) ? (int)tg : -1;
       }
     };
-    if (lds_t && h_lo < h_hi) load_trow(h_lo);
+    if (lds_t && !t8 && h_lo < h_hi) load_trow(h_lo);
     const uint32_t* W0 = (const uint32_t*)s_L + tid * SLW;                 // row hl, column t
     const uint32_t* W1 = (const uint32_t*)s_L + ((HD_T + 1) + tid) * SLW;  // row hl + 1
     const uint16_t* L0 = &s_L[tid * SL];
@@ -400,7 +414,13 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
 #pragma unroll 1
     for (int h = h_lo; h < h_hi; ++h) {
       signed char* trow_s = s_t + (h & 1) * HD_TMAX;
-      if (lds_t) {
+      if (t8) {
+        if (t8own) *reinterpret_cast<uint2*>(trow_s + tid * 8) = tq[0];
+#pragma unroll
+        for (int j = 0; j + 1 < HD_PD; ++j) tq[j] = tq[j + 1];
+        load8(h + HD_PD, tq[HD_PD - 1]);
+        __syncthreads();
+      } else if (lds_t) {
 #pragma unroll
         for (int k = 0; k < TPT; ++k)
           if (tid + HD_T * k < W) trow_s[tid + HD_T * k] = (signed char)tnext[k];
@@ -447,6 +467,7 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
           }
         }
         const bool reseed = dvmax * ((w_hi - 1 - w_lo) * sw) > 60.f;
+        if (cb == 0 && h == h_lo) stamp(a.stamps, 5);
         f32x2 S[CP], R[CP];  // per class pair: the segment's sum inv e, sum lw.l1 inv e
 #pragma unroll
         for (int p = 0; p < CP; ++p) S[p] = R[p] = f32x2{0.f, 0.f};
@@ -507,6 +528,7 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
           }
           l1 += sw;
         }
+        if (cb == 0 && h == h_lo) stamp(a.stamps, 6);
         // the segment's end: target -1 terms, then the two row taps
         const f32x2 r0 = {lh.l0, lh.l0}, r1 = {lh.l1, lh.l1};
 #pragma unroll
@@ -520,6 +542,7 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
           a0[c] = __builtin_elementwise_fma(r0, u, a0[c]);
           a1[c] = __builtin_elementwise_fma(r1, u, a1[c]);
         }
+        if (cb == 0 && h == h_lo) stamp(a.stamps, 7);
       }
     }
     if (cb == 0) stamp(a.stamps, 2);
@@ -597,292 +620,43 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
   stamp(a.stamps, 4);
 }
 
-// The 19-class 16-bit head with each low-res column owned by a LANE PAIR (lanes 2k, 2k+1 of a
-// wave): lane 2k + h walks classes [10 h, 10 h + 10) of column k with ce_head2_kernel's
-// arithmetic (walked exponentials, row-factored (S, R) sums, LDS one-hot slots); the pair
-// exchanges the segment bound M and each pixel's exp sum by one DPP swap each.  Half the
-// per-class state per lane (4 x 10 accumulators, 2 x 10 sums, 2 x 10 walk registers) lets three
-// waves share a SIMD where the one-lane-per-column form fits two (measured: its VALU issue was
-// 19 % of a wave's life -- the rest dependency and LDS latency that two waves cannot cover).
-// 128 columns per workgroup chunk.
-__device__ __forceinline__ float hd_pair_swap(float x) {  // value of the partner lane (k ^ 1)
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+// ---- targets -> int8 ----------------------------------------------------------------------
+// The loss head reads every full-resolution target once; as int64 rows that is 16 KB per row and
+// workgroup, and the head's row loop waited ~8 us per row for the next row (stamps).  Packed to
+// int8 (-1 = ignored / out of range, the head's own validity test) by a streaming pass that runs
+// on the side stream during the global feature extractor, a row is 2 KB and the head keeps four
+// rows in flight.
+__global__ __launch_bounds__(256) void ce_pack_targets_kernel(const long long* t, long long n,
+                                                               int C, long long ign,
+                                                               signed char* out) {
+  const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i0 >= n) return;
+  auto cls = [&](long long v) -> uint32_t {
+    return (uint32_t)(uint8_t)(signed char)((v != ign && v >= 0 && v < C) ? (int)v : -1);
+  };
+  if (i0 + 8 <= n && ((uintptr_t)(t + i0) & 15) == 0) {
+    const longlong2* p = reinterpret_cast<const longlong2*>(t + i0);
+    const longlong2 a = p[0], b = p[1], c = p[2], d = p[3];
+    uint2 o;
+    o.x = cls(a.x) | (cls(a.y) << 8) | (cls(b.x) << 16) | (cls(b.y) << 24);
+    o.y = cls(c.x) | (cls(c.y) << 8) | (cls(d.x) << 16) | (cls(d.y) << 24);
+    *reinterpret_cast<uint2*>(out + i0) = o;
+  } else {
+    for (long long i = i0; i < n && i < i0 + 8; ++i) out[i] = (signed char)cls(t[i]);
+  }
 }
 
-template <typename T>
-__global__ __launch_bounds__(HD_T, 3) void ce_head3_kernel(CeHeadArgs a) {
-  constexpr int CT = 19;
-  constexpr int TC = HD_T / 2;                      // columns per chunk
-  constexpr int CH = 10, PH = 5;                    // classes / class pairs per lane
-  constexpr int VPP = 3;                            // 16-byte vectors per pixel (ldl = 24)
-  constexpr int SLW = 11;                           // odd 32-bit word stride per staged pixel
-  constexpr int NSV = (2 * (TC + 1) * VPP + HD_T - 1) / HD_T;
-  __shared__ __attribute__((aligned(16))) uint32_t s_L[2 * (TC + 1) * SLW];
-  __shared__ __attribute__((aligned(16))) f32x2 s_oh[2 * CH * TC];  // [class][column] (1, lw.l1)
-  __shared__ float s_carry[2 * 2 * CH];
-  __shared__ signed char s_t[2 * HD_TMAX];
-  __shared__ float s_r1[HD_T], s_r2[HD_T];
-  const int tid = threadIdx.x, k = tid >> 1, half = tid & 1, c0 = half * CH;
-  const int hl = blockIdx.x, n = blockIdx.y;
-  const int Hl = a.Hl, Wl = a.Wl, H = a.H, W = a.W, ldl = a.ldl;
-  const float sh = ac_scale(Hl, H), sw = ac_scale(Wl, W);
-  const int h_lo = hd_first_ge(hl, Hl, H, sh), h_hi = hd_first_ge(hl + 1, Hl, H, sh);
-  const int hl1 = min(hl + 1, Hl - 1);
-  const uint16_t* lg = (const uint16_t*)a.logits + (size_t)n * Hl * Wl * ldl;
-  float* g0 = a.g_raw;
-  float* g1 = a.g_raw + (size_t)a.N * Hl * Wl * ldl;
-  const long long* tgt = a.target + (size_t)n * H * W;
-  float loss = 0.f, cnt = 0.f;
-  stamp(a.stamps, 0);
-  if (tid < 4 * CH) s_carry[tid] = 0.f;
-  if (hl == 0) {
-    for (int i = tid; i < Wl * ldl; i += HD_T) g1[(size_t)n * Hl * Wl * ldl + i] = 0.f;
+int ce_pack_targets(const long long* t, long long n, int C, long long ignore_index,
+                    signed char* out, hipStream_t st) {
+  if (C < 1 || C > 127 || n < 0 || ((uintptr_t)out & 7)) {
+    set_error("ce_pack_targets: %d classes / misaligned output", C);
+    return E_INVALID;
   }
-  auto unpack = [](uint32_t w) {
-    return f32x2{s16_to<T>((uint16_t)(w & 0xFFFFu)), s16_to<T>((uint16_t)(w >> 16))};
-  };
-  for (int cb = 0; cb < Wl; cb += TC) {
-    __syncthreads();
-    {
-      uint4 v[NSV];
-#pragma unroll
-      for (int j = 0; j < NSV; ++j) {
-        const int i = tid + HD_T * j;
-        const int q = i % VPP, jr = i / VPP;
-        const int col = min(cb + jr % (TC + 1), Wl - 1), row = jr / (TC + 1) ? hl1 : hl;
-        v[j] = i < 2 * (TC + 1) * VPP ? *(const uint4*)(lg + ((size_t)row * Wl + col) * ldl + 8 * q)
-                                      : uint4{0, 0, 0, 0};
-      }
-#pragma unroll
-      for (int j = 0; j < NSV; ++j) {
-        const int i = tid + HD_T * j;
-        if (i < 2 * (TC + 1) * VPP) {
-          const int q = i % VPP, jr = i / VPP;
-          uint32_t* d = s_L + jr * SLW + 4 * q;
-          d[0] = v[j].x;
-          d[1] = v[j].y;
-          if (4 * q + 2 < 10) d[2] = v[j].z;  // words 0..9 hold classes 0..19
-          if (4 * q + 3 < 10) d[3] = v[j].w;
-        }
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < CH; ++c) s_oh[(c0 + c) * TC + k] = f32x2{0.f, 0.f};
-    __syncthreads();
-    if (cb == 0) stamp(a.stamps, 1);
-    const int t = cb + k;
-    const bool active = t < Wl;  // uniform within a lane pair
-    f32x2 a0[CH], a1[CH];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) a0[c] = a1[c] = f32x2{0.f, 0.f};
-    const int w_lo = active ? hd_first_ge(t, Wl, W, sw) : 0;
-    const int w_hi = active ? hd_first_ge(t + 1, Wl, W, sw) : 0;
-    const bool lds_t = W <= HD_TMAX;
-    constexpr int TPT = HD_TMAX / HD_T;
-    int tnext[TPT];
-    auto load_trow = [&](int h) {
-      const long long* tr = tgt + (size_t)h * W;
-#pragma unroll
-      for (int j = 0; j < TPT; ++j) {
-        const int w = tid + HD_T * j;
-        const long long tg = tr[w < W ? w : 0];
-        tnext[j] = (w < W && tg != a.ignore_index && tg >= 0 && tg < CT) ? (int)tg : -1;
-      }
-    };
-    if (lds_t && h_lo < h_hi) load_trow(h_lo);
-    const uint32_t* W0 = s_L + k * SLW + c0 / 2;                 // row hl, column t, own pairs
-    const uint32_t* W1 = s_L + ((TC + 1) + k) * SLW + c0 / 2;    // row hl + 1
-    const uint16_t* L0 = (const uint16_t*)(s_L + k * SLW);
-    const uint16_t* L1 = (const uint16_t*)(s_L + ((TC + 1) + k) * SLW);
-#pragma unroll 1
-    for (int h = h_lo; h < h_hi; ++h) {
-      signed char* trow_s = s_t + (h & 1) * HD_TMAX;
-      if (lds_t) {
-#pragma unroll
-        for (int j = 0; j < TPT; ++j)
-          if (tid + HD_T * j < W) trow_s[tid + HD_T * j] = (signed char)tnext[j];
-        __syncthreads();
-        if (h + 1 < h_hi) load_trow(h + 1);
-      }
-      if (active && w_lo < w_hi) {
-        const Lerp lh = ac_lerp(h, Hl, H, sh);
-        const f32x2 h0 = {lh.l0 * HD_LOG2E, lh.l0 * HD_LOG2E};
-        const f32x2 h1 = {lh.l1 * HD_LOG2E, lh.l1 * HD_LOG2E};
-        const long long* trow = tgt + (size_t)h * W;
-        auto target = [&](int w) -> int {
-          if (lds_t) return trow_s[w];
-          const long long tg = trow[w];
-          return (tg != a.ignore_index && tg >= 0 && tg < CT) ? (int)tg : -1;
-        };
-        auto taps = [&](int p, f32x2& v0, f32x2& dv) {
-          v0 = __builtin_elementwise_fma(h1, unpack(W1[p]), h0 * unpack(W0[p]));
-          dv = __builtin_elementwise_fma(h1, unpack(W1[SLW + p]), h0 * unpack(W0[SLW + p])) - v0;
-          if (c0 + 2 * p + 1 >= CT) v0.y = -INFINITY, dv.y = 0.f;  // class 19: padding
-        };
-        float l1 = ac_lerp(w_lo, Wl, W, sw).l1;
-        f32x2 e[PH], q[PH];
-        float M = -INFINITY, dvmax = 0.f;
-        {
-          const f32x2 L1v = {l1, l1}, SWv = {sw, sw};
-#pragma unroll
-          for (int p = 0; p < PH; ++p) {
-            f32x2 v0, dv;
-            taps(p, v0, dv);
-            e[p] = __builtin_elementwise_fma(L1v, dv, v0);
-            q[p] = dv * SWv;
-            M = fmaxf(M, fmaxf(e[p].x, e[p].y));
-            dvmax = fmaxf(dvmax, fmaxf(fabsf(dv.x), fabsf(dv.y)));
-          }
-          M = fmaxf(M, hd_pair_swap(M));
-          dvmax = fmaxf(dvmax, hd_pair_swap(dvmax));
-#pragma unroll
-          for (int p = 0; p < PH; ++p) {
-            e[p].x = __builtin_amdgcn_exp2f(e[p].x - M);
-            e[p].y = __builtin_amdgcn_exp2f(e[p].y - M);
-            q[p].x = __builtin_amdgcn_exp2f(q[p].x);
-            q[p].y = __builtin_amdgcn_exp2f(q[p].y);
-          }
-        }
-        const bool reseed = dvmax * ((w_hi - 1 - w_lo) * sw) > 60.f;  // same in both lanes
-        f32x2 S[PH], R[PH];
-#pragma unroll
-        for (int p = 0; p < PH; ++p) S[p] = R[p] = f32x2{0.f, 0.f};
-        int ti = target(w_lo);
-#pragma unroll 1
-        for (int w = w_lo; w < w_hi; ++w) {
-          if (reseed && w > w_lo) {  // wide logit spread: evaluate this pixel directly
-            M = -INFINITY;
-            const f32x2 L1v = {l1, l1};
-#pragma unroll
-            for (int p = 0; p < PH; ++p) {
-              f32x2 v0, dv;
-              taps(p, v0, dv);
-              e[p] = __builtin_elementwise_fma(L1v, dv, v0);
-              M = fmaxf(M, fmaxf(e[p].x, e[p].y));
-            }
-            M = fmaxf(M, hd_pair_swap(M));
-#pragma unroll
-            for (int p = 0; p < PH; ++p) {
-              e[p].x = __builtin_amdgcn_exp2f(e[p].x - M);
-              e[p].y = __builtin_amdgcn_exp2f(e[p].y - M);
-            }
-          }
-          const int tcur = ti;
-          if (w + 1 < w_hi) ti = target(w + 1);
-          const bool valid = tcur >= 0;
-          f32x2 sp = (e[0] + e[1]) + (e[2] + e[3]) + e[4];
-          float se = sp.x + sp.y;
-          se += hd_pair_swap(se);  // (half 0's sum) + (half 1's sum) in both lanes
-          const float inv = valid ? __builtin_amdgcn_rcpf(se) : 0.f;
-          if (valid) {
-            if (half == 0) {
-              const float v0t = fmaf(h1.x, s16_to<T>(L1[tcur]), h0.x * s16_to<T>(L0[tcur]));
-              const float v1t = fmaf(h1.x, s16_to<T>(L1[2 * SLW + tcur]),
-                                     h0.x * s16_to<T>(L0[2 * SLW + tcur]));
-              loss += M - fmaf(l1, v1t - v0t, v0t) + __builtin_amdgcn_logf(se);  // log2 units
-              cnt += 1.f;
-            }
-            if (tcur >= c0 && tcur < c0 + CH)
-              s_oh[tcur * TC + k] = s_oh[tcur * TC + k] + f32x2{1.f, l1};
-          }
-          const f32x2 iv = {inv, inv}, lv = {l1 * inv, l1 * inv};
-#pragma unroll
-          for (int p = 0; p < PH; ++p) {
-            S[p] = __builtin_elementwise_fma(iv, e[p], S[p]);
-            R[p] = __builtin_elementwise_fma(lv, e[p], R[p]);
-            e[p] = e[p] * q[p];
-          }
-          l1 += sw;
-        }
-        const f32x2 r0 = {lh.l0, lh.l0}, r1 = {lh.l1, lh.l1};
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const float Sc = (c & 1) ? S[c / 2].y : S[c / 2].x;
-          const float Rc = (c & 1) ? R[c / 2].y : R[c / 2].x;
-          const f32x2 oh = s_oh[(c0 + c) * TC + k];
-          s_oh[(c0 + c) * TC + k] = f32x2{0.f, 0.f};
-          const float d1 = Rc - oh.y;
-          const f32x2 u = {(Sc - oh.x) - d1, d1};
-          a0[c] = __builtin_elementwise_fma(r0, u, a0[c]);
-          a1[c] = __builtin_elementwise_fma(r1, u, a1[c]);
-        }
-      }
-    }
-    if (cb == 0) stamp(a.stamps, 2);
-    float acc00[CH], acc01[CH], acc10[CH], acc11[CH];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      acc00[c] = a0[c].x;
-      acc01[c] = a0[c].y;
-      acc10[c] = a1[c].x;
-      acc11[c] = a1[c].y;
-    }
-    if (active) {
-      if (t == Wl - 1) {
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          acc00[c] += acc01[c];
-          acc10[c] += acc11[c];
-          acc01[c] = acc11[c] = 0.f;
-        }
-      }
-      if (hl1 == hl) {
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          acc00[c] += acc10[c];
-          acc01[c] += acc11[c];
-          acc10[c] = acc11[c] = 0.f;
-        }
-      }
-    }
-    // hand the (*, t+1) shares to column t+1's lane of the same half ([2][TC][2 CH] floats)
-    float* s_h = reinterpret_cast<float*>(s_oh);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      s_h[k * 2 * CH + c0 + c] = acc01[c];
-      s_h[(TC + k) * 2 * CH + c0 + c] = acc11[c];
-    }
-    __syncthreads();
-    if (active) {
-      float* o0 = g0 + (((size_t)n * Hl + hl) * Wl + t) * ldl;
-      float* o1 = g1 + (((size_t)n * Hl + hl + 1) * Wl + t) * ldl;
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        if (c0 + c < CT) {
-          const float left0 = k > 0 ? s_h[(k - 1) * 2 * CH + c0 + c] : s_carry[c0 + c];
-          const float left1 = k > 0 ? s_h[(TC + k - 1) * 2 * CH + c0 + c] : s_carry[2 * CH + c0 + c];
-          o0[c0 + c] = acc00[c] + left0;
-          if (hl1 != hl) o1[c0 + c] = acc10[c] + left1;
-        }
-      }
-    }
-    __syncthreads();
-    if (k == TC - 1) {
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        s_carry[c0 + c] = acc01[c];
-        s_carry[2 * CH + c0 + c] = acc11[c];
-      }
-    }
-  }
-  stamp(a.stamps, 3);
-  s_r1[tid] = loss * HD_LN2;
-  s_r2[tid] = cnt;
-  __syncthreads();
-  for (int off = HD_T / 2; off > 0; off >>= 1) {
-    if (tid < off) {
-      s_r1[tid] += s_r1[tid + off];
-      s_r2[tid] += s_r2[tid + off];
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    const size_t pi = (size_t)n * Hl + hl;
-    a.part[2 * pi] = s_r1[0];
-    a.part[2 * pi + 1] = s_r2[0];
-  }
-  stamp(a.stamps, 4);
+  if (n == 0) return OK;
+  ProfScope ps(PK_CE, st, 9.0 * (double)n, 0.0);
+  const long long blocks = (n + 2047) / 2048;
+  ce_pack_targets_kernel<<<(unsigned)blocks, 256, 0, st>>>(t, n, C, ignore_index, out);
+  return check_launch("ce_pack_targets");
 }
 
 int ce_head_parts(int N, int Hl, int Wl) { return N * Hl; }
@@ -921,16 +695,11 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
                                 8.0 * a.N * a.H * a.W + 2.0 * 4.0 * a.N * a.Hl * a.Wl * a.C,
                  0.0);
     const bool f32 = dtype == DT_F32;
-    static const int form = [] {  // FSCNN_CE_HEAD=1 / 2: the one-hot-select / one-lane form
+    static const int form = [] {  // FSCNN_CE_HEAD=1: the one-hot-select kernel for every dtype
       const char* e = getenv("FSCNN_CE_HEAD");
       return e ? atoi(e) : 2;
     }();
-    if (form >= 3 && !f32 && a.C == 19 && a.ldl == 24) {
-      CeHeadArgs as = a;
-      as.stamps = stamp_region();
-      if (dtype == DT_F16) ce_head3_kernel<f16><<<grid, HD_T, 0, st>>>(as);
-      else ce_head3_kernel<bf16><<<grid, HD_T, 0, st>>>(as);
-    } else if (form >= 2 && !f32 && (a.C == 19 || a.C == 2) && a.ldl == (a.C + 7) / 8 * 8) {
+    if (form >= 2 && !f32 && (a.C == 19 || a.C == 2) && a.ldl == (a.C + 7) / 8 * 8) {
       CeHeadArgs as = a;
       as.stamps = stamp_region();
       if (a.C == 19) {

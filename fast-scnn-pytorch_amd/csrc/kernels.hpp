@@ -323,6 +323,9 @@ struct CeHeadArgs {
   float* g_raw;              // 2 planes NHWC [N][Hl][Wl][ldl] fp32: own row, spill from row above
   float* part;               // [N * Hl][2]
   unsigned long long* stamps = nullptr;
+  // optional: the targets packed to int8 (class or -1; ce_pack_targets), read by the 16-bit
+  // kernels 4 rows ahead instead of the int64 rows
+  const signed char* tgt8 = nullptr;
 };
 
 struct DropArgs {
@@ -505,6 +508,9 @@ int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N,
                   float smooth, float wd, float wf, void* dlogits, hipStream_t st);
 int ce_head_parts(int N, int Hl, int Wl);
 int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
+// targets [n] int64 -> int8: t if 0 <= t < C and t != ignore_index, else -1 (C <= 127)
+int ce_pack_targets(const long long* t, long long n, int C, long long ignore_index,
+                    signed char* out, hipStream_t st);
 // g[m][c] = g_raw[m][c] * gout / count  (c < C; pad columns zeroed)
 int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const float* gout,
                   const float* out2, int dtype, hipStream_t st);

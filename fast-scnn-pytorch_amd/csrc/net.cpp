@@ -292,6 +292,7 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   if (train) {
     pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
+    pl.tgt8 = A.get((size_t)N * pl.H * pl.W);
   }
   if (train) {
     pl.seed_slot = A.get(64);
@@ -664,6 +665,14 @@ struct Exec {
     sideq.clear();
     return OK;
   }
+  // the loss head's targets as int8 (the side stream packs them during the global feature
+  // extractor; the FFM join orders them before the head)
+  static bool ce_head_packs(int C, int dtype) { return dtype != DT_F32 && (C == 19 || C == 2); }
+  int pack_targets(hipStream_t s) {
+    g_prof_tag = "head (targets to int8)";
+    return ce_pack_targets(r.target, (long long)pl.N * pl.H * pl.W, net.num_classes,
+                           r.ignore_index, (signed char*)W(pl.tgt8), s);
+  }
   int join() {
     if (!side) return OK;
     TRY(flush_side());
@@ -949,9 +958,13 @@ struct Exec {
     // extractor; its BN finish uses the backward's counters and its own team-sum scratch, so it
     // never shares arrival state with the main stream's producers; joined before the FFM apply
     const bool fhigh_side = train && side != nullptr;
+    const bool pack = train && r.target && ce_head_packs(net.num_classes, dt);
     if (fhigh_side) {
       TRY(fhigh_fwd(true));
+      if (pack) TRY(side_launch([this](hipStream_t s) { return pack_targets(s); }));
       TRY(flush_side());
+    } else if (pack) {
+      TRY(pack_targets(r.st));
     }
     // ---- bottlenecks ----
     const void* x = W(pl.l2pw.a);
@@ -1093,6 +1106,7 @@ struct Exec {
       h.N = N; h.C = net.num_classes; h.Hl = pl.H3; h.Wl = pl.W3; h.H = pl.H; h.W = pl.W;
       h.logits = W(pl.logits); h.ldl = pl.Cp; h.target = r.target; h.ignore_index = r.ignore_index;
       h.g_raw = Wf(pl.g_raw); h.part = Wf(pl.head_part);
+      if (ce_head_packs(net.num_classes, dt)) h.tgt8 = (const signed char*)W(pl.tgt8);
       return ce_head(h, r.loss2, dt, r.st);
     }
     // ---- final bilinear (align_corners) to NCHW ----

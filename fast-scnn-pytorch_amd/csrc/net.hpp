@@ -113,6 +113,7 @@ struct Plan {
   size_t wt = 0;                    // transposed weights (train plans), net.wt_total elements
   size_t lb_we3[9] = {}, lb_wp3[9] = {};  // fp32 inference: split planes of fused bottlenecks
   size_t g_raw = 0, head_part = 0;  // fused loss head (train plans)
+  size_t tgt8 = 0;                    // the loss head's int8 targets (train plans)
   size_t seed_slot = 0;             // dropout seed (device copy read by the dropout kernels)
   size_t fcnt = 0, bcnt = 0;        // BN arrival counters (ws), BN_COUNTERS each
   size_t tsum = 0;                  // fp64 team sums of the in-kernel BN finishes (ws)

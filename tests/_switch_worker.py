@@ -37,12 +37,16 @@ def main(out, half=None):
         x = x.to(torch.bfloat16)
     t = torch.from_numpy(portable_init.target_tensor(4, (2,) + shape[2:], 19, 0.05)).to(dev)
     res = {}
+    exact = half == "bf16shift" and os.environ.get("FSCNN_LTD_FUSED") == "0"
+    m._keep_ws = exact
     for i, seed in enumerate((5, 9, 5, 9)):
         m.zero_grad(set_to_none=True)
         m._dropout_seed = seed
         loss = cross_entropy(m(x)[0], t) if i % 2 == 0 else m.forward_loss(x, t)
         loss.backward()
         torch.cuda.synchronize()
+        if exact and i == 0:
+            res["c0exact0"] = _conv0_dw_exact(m, x).numpy()
         res["loss%d" % i] = np.float32(loss.item())
         res["grad%d" % i] = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu().numpy()
     res["sizes"] = np.array([p.numel() for p in m.parameters()], dtype=np.int64)
@@ -51,6 +55,29 @@ def main(out, half=None):
         if "running" in k:
             res["bn." + k] = v.cpu().numpy()
     np.savez(out, **res)
+
+
+def _conv0_dw_exact(m, x):
+    """conv0's weight gradient in fp64 from the step's STORED tensors (two-launch path: the
+    gradient g of conv0's BN output is in the workspace): train-mode BN backward through the
+    ReLU mask fmaf(z, scale, shift) > 0, then the stride-2 conv's weight gradient over the bf16
+    image (models/fast_scnn.py:153 autograd)."""
+    import torch
+    from torch.nn.grad import conv2d_weight
+    N, _, H, W = x.shape
+    H1, W1 = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+    g = m.debug_buffer("c0.ga").double().cpu()
+    z = m.debug_buffer("c0.z").double().cpu()
+    mean = m.debug_buffer("c0.mean").double().cpu().reshape(-1)
+    invstd = m.debug_buffer("c0.invstd").double().cpu().reshape(-1)
+    sc32 = m.debug_buffer("c0.scale").float().cpu().reshape(-1)
+    sh32 = m.debug_buffer("c0.shift").float().cpu().reshape(-1)
+    mask = torch.addcmul(sh32, z.float(), sc32) > 0  # the kernels' fmaf(z, scale, shift) > 0
+    gm = torch.where(mask, g, torch.zeros_like(g))
+    xhat = (z - mean) * invstd
+    dz = sc32.double() * (gm - gm.mean(0) - xhat * (gm * xhat).mean(0))
+    dz = dz.view(N, H1, W1, 32).permute(0, 3, 1, 2)
+    return conv2d_weight(x.double().cpu(), (32, 3, 3, 3), dz, stride=2, padding=0).reshape(-1)
 
 
 if __name__ == "__main__":

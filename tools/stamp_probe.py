@@ -44,7 +44,7 @@ def analyse(label, st, base=None):
     span = last.max().item()
     entry = rel[:, 0]
     parts = []
-    for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5)]:
+    for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (1, 5), (5, 6), (6, 7)]:
         d = rel[:, b] - rel[:, a]
         d = d[~torch.isnan(d)]
         if d.numel():
