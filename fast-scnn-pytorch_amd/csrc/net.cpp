@@ -958,10 +958,17 @@ struct Exec {
     // extractor; its BN finish uses the backward's counters and its own team-sum scratch, so it
     // never shares arrival state with the main stream's producers; joined before the FFM apply
     const bool fhigh_side = train && side != nullptr;
-    const bool pack = train && r.target && ce_head_packs(net.num_classes, dt);
+    // the loss head's int8 targets: on the side stream from the start of bottleneck PACK_AT
+    // (FSCNN_CE_PACK: 0 = head reads int64, 1 = beside bottleneck1's HBM-bound launches, 2 =
+    // beside the latency-bound bottleneck2/3), or on the main stream without a side stream
+    static const int pack_mode = [] {
+      const char* e = getenv("FSCNN_CE_PACK");
+      return e ? atoi(e) : 2;
+    }();
+    const bool pack = train && r.target && pack_mode > 0 && ce_head_packs(net.num_classes, dt);
+    const int pack_at = !pack ? -1 : pack_mode == 1 ? 0 : 3;
     if (fhigh_side) {
       TRY(fhigh_fwd(true));
-      if (pack) TRY(side_launch([this](hipStream_t s) { return pack_targets(s); }));
       TRY(flush_side());
     } else if (pack) {
       TRY(pack_targets(r.st));
@@ -971,6 +978,10 @@ struct Exec {
     int xld = 64;
     int Hc = pl.H3, Wc = pl.W3;
     for (int i = 0; i < 9; ++i) {
+      if (fhigh_side && i == pack_at) {
+        TRY(side_launch([this](hipStream_t s) { return pack_targets(s); }));
+        TRY(flush_side());
+      }
       const LbL& l = net.lb[i];
       int Ho = dwout(Hc, l.stride), Wo = dwout(Wc, l.stride);
       IrArgs b;
@@ -1106,7 +1117,7 @@ struct Exec {
       h.N = N; h.C = net.num_classes; h.Hl = pl.H3; h.Wl = pl.W3; h.H = pl.H; h.W = pl.W;
       h.logits = W(pl.logits); h.ldl = pl.Cp; h.target = r.target; h.ignore_index = r.ignore_index;
       h.g_raw = Wf(pl.g_raw); h.part = Wf(pl.head_part);
-      if (ce_head_packs(net.num_classes, dt)) h.tgt8 = (const signed char*)W(pl.tgt8);
+      if (pack) h.tgt8 = (const signed char*)W(pl.tgt8);
       return ce_head(h, r.loss2, dt, r.st);
     }
     // ---- final bilinear (align_corners) to NCHW ----
