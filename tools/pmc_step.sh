@@ -15,7 +15,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i + 1))
   timeout -k 10 400 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-forward --profile-kind 3 "$@" \
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-forward --no-extra --profile-kind 3 "$@" \
       > "$OUT/p$i.log" 2>&1
   echo "pass $i ($grp) done"
 done

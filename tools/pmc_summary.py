@@ -18,7 +18,7 @@ FAMILIES = {
     "conv0_fwd": [["conv0_fwd_kernel"]], "dw_fwd": [["dw_fwd_kernel<", "false>"], ["dw_fwd_loop_kernel<"]],
     "dw_dgrad": [["dw_dgrad_s2_kernel"]], "dw_wgrad": [["dw_wgrad_kernel"]],
     "gemm_nt": [["gemm_nt_kernel"], ["gemm_stream_kernel"]], "gemm_tn": [["gemm_tn_kernel"]],
-    "ce_head": [["ce_head_kernel"], ["ce_head2_kernel"]], "conv0_wgrad": [["conv0_wgrad_kernel"]],
+    "ce_head": [["ce_head_kernel"], ["ce_head2_kernel"]], "conv0_wgrad": [["conv0_wgrad_kernel"], ["ltd_c0_bwd_kernel"]],
 }
 
 
