@@ -247,7 +247,10 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
       for (int j = 0; j < 4; ++j) acc[r][p][j] = 0.f;
   const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
 #pragma unroll
-  for (int rr = 0; rr < G::NR; ++rr)
+  for (int rr = 0; rr < G::NR; ++rr) {
+    // one input row of the thread's window at a time: left to itself the compiler hoists all
+    // NR x NC quad loads (up to 96 live values) and the kernel drops to 3 waves per SIMD
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int ci = 0; ci < G::NC; ++ci) {
       float v[4];
@@ -265,6 +268,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
         }
       }
     }
+  }
 
   const int ho0 = th0 + gy * G::HS, wo0 = tw0 + gx * G::WS;
   const int nrow = max(0, min(G::HS, a.Ho - ho0)), ncol = max(0, min(G::WS, a.Wo - wo0));

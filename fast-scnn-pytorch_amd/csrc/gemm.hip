@@ -598,11 +598,16 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   int nt = pick_nt(a.N);
-  // small-M problems (the 16 K-row bottleneck3 / bottleneck2 projects): split the columns
-  // further so the grid covers the 256 CUs (the A tile is then read twice, from L2)
-  constexpr int min_tiles = 256;  // grid size below which NT halves
-  while ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < min_tiles && (nt == 8 || nt == 6 || nt == 4))
-    nt /= 2;
+  // small-M problems (the 16 K-row bottleneck2/3 projects and expand dgrads: 128 row tiles)
+  // split the columns down to NT = 2 so ~512 workgroups (two per CU, eight waves) are in flight:
+  // measured r04 5.965-5.976 ms/step vs 6.001-6.007 at 256 and 6.016-6.018 at 1024
+  static const int min_tiles = [] {  // grid size below which NT halves (FSCNN_GEMM_MINT)
+    const char* e = getenv("FSCNN_GEMM_MINT");
+    return e ? atoi(e) : 512;
+  }();
+  while ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < min_tiles &&
+         (nt == 8 || nt == 6 || nt == 4 || (nt == 3 && min_tiles > 256)))
+    nt = nt == 3 ? 2 : nt / 2;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;
   const bool at = a.a_scale != nullptr;
