@@ -23,7 +23,8 @@
 
 namespace fscnn {
 
-constexpr int DWL_CB = 8;  // max 16-B channel vectors per workgroup (128 B per pixel)
+constexpr int DWL_CB = 8;  // max 16-B channel vectors per workgroup (128 B per pixel; 4 measured
+                           // r04: 6.12-6.13 vs 6.02-6.06 ms per cfg3 step)
 
 // A thread computes a channel QUAD (4 channels: 16 B fp32 / 8 B bf16 of LDS per read) for an
 // HS x WS block of outputs; G = 32 / (quads per vector) pixel groups of GX x GY cover the tile.
@@ -710,12 +711,15 @@ static size_t dw_loop_shm(int cbv) {
 // FSCNN_DW_LOOP=1: 16-bit stride-1 forwards run the streaming tile loop.  Off by default:
 // measured r04 (cfg3 bf16 step) 6.20 ms with it vs 6.04 ms with the one-tile kernel -- at <= 2
 // workgroups per CU (its ~240 VGPRs) one tile of prefetch hides less HBM latency than the
-// one-tile kernel's higher occupancy does
-static bool dw_loop_on(int V, int S) {
+// one-tile kernel's higher occupancy does; on the low-resolution launches alone (<= 64 K output
+// pixels, where the one-tile grid needs ~1.5 dispatch rounds) it is slower still (6.13-6.16 vs
+// 5.99 ms)
+static bool dw_loop_on(int V, int S, long long px) {
   static const bool on = [] {
     const char* e = getenv("FSCNN_DW_LOOP");
     return e && e[0] == '1';
   }();
+  (void)px;
   return on && V == 8 && S == 1;
 }
 
@@ -723,7 +727,7 @@ static bool dw_loop_on(int V, int S) {
 // workgroup per (channel chunk, tile)
 static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv, bool fwd = false) {
   cbv = dw_cbv(C / V);
-  if (fwd && dw_loop_on(V, S)) {
+  if (fwd && dw_loop_on(V, S, (long long)N * Ho * Wo)) {
     // every workgroup resident (2 per CU): gx channel chunks x wy workers, each walking >= 1
     // of the chunk's T spatial tiles; wy is also the record count of the statistics forms
     using G = DwTile<bf16, 1>;
@@ -759,7 +763,7 @@ static void dw_launch_fwd_t(const DwArgs& a, dim3 grid, int nthr, int cbv, hipSt
     return;
   }
   if constexpr (!FLIP && sizeof(T) == 2) {
-    if (a.stride == 1 && dw_loop_on(8, 1)) {  // the streaming tile loop (grid: dw_grid fwd)
+    if (a.stride == 1 && dw_loop_on(8, 1, (long long)a.N * a.Ho * a.Wo)) {  // (grid: dw_grid fwd)
       const size_t shm = dw_loop_shm<T, 1>(cbv);
       if (a.tail_ink) dw_fwd_loop_kernel<T, 1, false, IT, false, true><<<grid, nthr, shm, st>>>(a, cbv);
       else dw_fwd_loop_kernel<T, 1, false, IT><<<grid, nthr, shm, st>>>(a, cbv);
