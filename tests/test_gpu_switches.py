@@ -14,7 +14,10 @@ fresh child process:
 * ``FSCNN_GEMM_PF=3``     — the tiled pointwise GEMM's three-chunk register prefetch ring for the
   long-K low-M launches (gemm.hip; measured slower, opt-in);
 * ``FSCNN_CE_HEAD=1``     — the 16-bit loss head as the one-hot-select kernel (int64 targets)
-  instead of ce_head2_kernel.
+  instead of ce_head2_kernel;
+* ``FSCNN_CE_PACK=0 / 1`` — ce_head2_kernel reading the int64 targets / the int8 targets packed
+  beside bottleneck1 instead of beside bottleneck2/3;
+* ``FSCNN_GEMM_MINT=256`` — the tiled GEMM's round-3 minimum grid (NT >= 3 on low-M launches).
 
 Each child re-runs the oracle / golden parity tests that cover the path (fp32 train golden +
 bf16 emulated budget; eval goldens for the fp32 GEMM switch).  The graph switch also replays
@@ -43,7 +46,9 @@ HEAD16 = ["tests/test_gpu_literal.py::test_fused_ce_head_16bit_vs_fp64"]
 BF16 = ["tests/test_gpu_model.py::test_bf16_forward_within_bf16_budget"]
 CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL, "FSCNN_GRAPHS=1": TRAIN + EVAL,
          "FSCNN_LTD_FUSED=0": TRAIN[-1:], "FSCNN_DW_LOOP=1": TRAIN[-1:] + BF16,
-         "FSCNN_GEMM_PF=3": TRAIN[-1:], "FSCNN_CE_HEAD=1": HEAD16}
+         "FSCNN_GEMM_PF=3": TRAIN[-1:], "FSCNN_CE_HEAD=1": HEAD16,
+         "FSCNN_CE_PACK=0": HEAD16, "FSCNN_CE_PACK=1": HEAD16,
+         "FSCNN_GEMM_MINT=256": TRAIN[-1:] + ["tests/test_gpu_kernels.py"]}
 
 
 def _env(switch):
