@@ -99,7 +99,7 @@ __device__ __forceinline__ float gs_rowsum(float v) {
 // finalize kernels' arithmetic (bn_finish.hpp).  Folds are fp64 sums in fixed order (thread
 // slice sl takes records sl, sl + S, ... in increasing order; slices summed in order).
 constexpr int GS_TEAM = 16;
-constexpr int GS_CTR_TEAMS = 64;  // counters: [0, 64) groups, then 32 teams per group
+constexpr int GS_CTR_TEAMS = 64;  // counters: [0, 64) groups, then cdiv(bpg, GS_TEAM) teams per group
 
 template <bool FWD>
 __device__ inline void gs_fold(const GemmArgs& a, int n0, int BN, int first, int count, int stride,
@@ -161,7 +161,7 @@ __device__ inline void gs_finish(const GemmArgs& a, int g, int bi, int n0, int B
   const int tsize = min(GS_TEAM, bpg - team * GS_TEAM);
   const int tid = threadIdx.x, col = tid % BN, n = n0 + col;
   const bool owner = tid < BN && n < a.N;  // slice 0 holds the folded sums
-  if (!arrive_last(ctr + GS_CTR_TEAMS + g * 32 + team, (unsigned)tsize)) return;
+  if (!arrive_last(ctr + GS_CTR_TEAMS + g * nteam + team, (unsigned)tsize)) return;
   double s[3];
   gs_fold<FWD>(a, n0, BN, team * GS_TEAM, tsize, 1, s);
   if (owner) {  // the team record replaces slot team * GS_TEAM (every other reader is done)
@@ -178,7 +178,7 @@ __device__ inline void gs_finish(const GemmArgs& a, int g, int bi, int n0, int B
       st_wt(rec + N + n, (float)s[2]);
     }
   }
-  reset_counter(ctr + GS_CTR_TEAMS + g * 32 + team);
+  reset_counter(ctr + GS_CTR_TEAMS + g * nteam + team);
   if (!arrive_last(ctr + g, (unsigned)nteam)) return;
   gs_fold<FWD>(a, n0, BN, 0, nteam, GS_TEAM, s);
   if (owner) {
@@ -695,6 +695,8 @@ static size_t gs_lds(const GemmArgs& a, int nt, int ks, int kc) {
   return b;  // >= the end-of-kernel reduction scratch [4][3][16 nt] (aliases the weights)
 }
 
+static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds);
+
 bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   const int KC = dtype == DT_F32 ? 16 : 32;  // k per step
   const int ks = cdiv(a.K, KC);
@@ -721,8 +723,15 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   if (a.bpart && (!a.bz || a.ldbz % 4 || (a.bmode != 0 && a.bmode != 2))) return false;
   // two resident workgroups per CU (160 KB LDS, 1 KB reserved each)
   if (gs_lds(a, nt, ks, KC) > (deep ? 80 * 1024 - 1024 : 72 * 1024)) return false;
-  // in-kernel BN finish: group counters [0, 64), 32 team counters per group after them
-  if (a.tail.counters && GS_CTR_TEAMS + 32 * cdiv(a.N, 16 * nt) > BN_COUNTERS) return false;
+  // in-kernel BN finish: group counters [0, 64), then each group's team counters
+  if (a.tail.counters) {
+    int nt2, ks2;
+    size_t lds2;
+    const int bpg = gs_bpg(a, dtype, nt2, ks2, lds2);
+    const int groups = cdiv(a.N, 16 * nt);
+    if (groups > GS_CTR_TEAMS || GS_CTR_TEAMS + groups * cdiv(bpg, GS_TEAM) > BN_COUNTERS)
+      return false;
+  }
   return a.M >= 4096;  // tiny GEMMs (PPM bins): loading a weight slice per block does not pay
 }
 
@@ -745,6 +754,7 @@ static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   lds = gs_lds(a, nt, ks, KC);
   const int nchunks = cdiv(a.M, GS_MW);
   // resident workgroups: LDS-limited (160 KB / CU), at most 2 per CU (measured: 3-4 slower)
+  // (r04: the low-M dgrads with BN-backward partials at NT = 2 and 3 per CU measured equal)
   constexpr int cap = 2;
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
