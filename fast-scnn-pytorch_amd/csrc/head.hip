@@ -340,8 +340,21 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
   if (hl == 0) {  // nothing spills into row 0
     for (int i = tid; i < Wl * ldl; i += HD_T) g1[(size_t)n * Hl * Wl * ldl + i] = 0.f;
   }
+  // int8 targets (a.tgt8): 8 bytes per thread and row, HD_PD rows in flight (register ring)
+  const bool t8 = a.tgt8 != nullptr && W <= HD_TMAX && W % 8 == 0;
+  const bool t8own = tid * 8 < W;
+  const signed char* trow8 = a.tgt8 + (size_t)n * H * W + tid * 8;
+  uint2 tq[HD_PD];
+  auto load8 = [&](int h, uint2& d) {
+    d = (h < h_hi && t8own) ? *reinterpret_cast<const uint2*>(trow8 + (size_t)h * W)
+                            : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+  };
   for (int cb = 0; cb < Wl; cb += HD_T) {
     __syncthreads();
+    if (t8) {  // the first target rows' loads go out with the logit staging below
+#pragma unroll
+      for (int j = 0; j < HD_PD; ++j) load8(h_lo + j, tq[j]);
+    }
     {  // both low-res rows, columns cb .. cb + HD_T: 16-byte loads all in flight, then LDS
       uint4 v[NSV];
 #pragma unroll
@@ -381,19 +394,7 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
     const bool lds_t = W <= HD_TMAX;
     constexpr int TPT = HD_TMAX / HD_T;
     int tnext[TPT];
-    // int8 targets (a.tgt8): 8 bytes per thread and row, HD_PD rows in flight (register ring)
-    const bool t8 = a.tgt8 != nullptr && lds_t && W % 8 == 0;
-    const bool t8own = tid * 8 < W;
-    const signed char* trow8 = a.tgt8 + (size_t)n * H * W + tid * 8;
-    uint2 tq[HD_PD];
-    auto load8 = [&](int h, uint2& d) {
-      d = (h < h_hi && t8own) ? *reinterpret_cast<const uint2*>(trow8 + (size_t)h * W)
-                              : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-    };
-    if (t8) {
-#pragma unroll
-      for (int j = 0; j < HD_PD; ++j) load8(h_lo + j, tq[j]);
-    }
+
     auto load_trow = [&](int h) {
       const long long* tr = tgt + (size_t)h * W;
 #pragma unroll
