@@ -17,7 +17,9 @@ fresh child process:
   instead of ce_head2_kernel;
 * ``FSCNN_CE_PACK=0 / 1`` — ce_head2_kernel reading the int64 targets / the int8 targets packed
   beside bottleneck1 instead of beside bottleneck2/3;
-* ``FSCNN_GEMM_MINT=256`` — the tiled GEMM's round-3 minimum grid (NT >= 3 on low-M launches).
+* ``FSCNN_GEMM_MINT=256`` — the tiled GEMM's round-3 minimum grid (NT >= 3 on low-M launches);
+* ``FSCNN_SIDE_PRIO=0``   — the weight-gradient side stream as a plain stream instead of one at
+  the device's lowest priority.
 
 Each child re-runs the oracle / golden parity tests that cover the path (fp32 train golden +
 bf16 emulated budget; eval goldens for the fp32 GEMM switch).  The graph switch also replays
@@ -48,7 +50,8 @@ CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL, "FSCNN_GRAPHS=
          "FSCNN_LTD_FUSED=0": TRAIN[-1:], "FSCNN_DW_LOOP=1": TRAIN[-1:] + BF16,
          "FSCNN_GEMM_PF=3": TRAIN[-1:], "FSCNN_CE_HEAD=1": HEAD16,
          "FSCNN_CE_PACK=0": HEAD16, "FSCNN_CE_PACK=1": HEAD16,
-         "FSCNN_GEMM_MINT=256": TRAIN[-1:] + ["tests/test_gpu_kernels.py"]}
+         "FSCNN_GEMM_MINT=256": TRAIN[-1:] + ["tests/test_gpu_kernels.py"],
+         "FSCNN_SIDE_PRIO=0": TRAIN[:1]}
 
 
 def _env(switch):
