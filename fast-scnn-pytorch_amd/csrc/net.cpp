@@ -550,6 +550,8 @@ struct SideStream {
       const char* e = getenv("FSCNN_SIDE_PRIO");
       return e ? atoi(e) : 1;
     }();
+    // (a CU-masked side stream, hipExtStreamCreateWithCUMask on 1/2 or 1/4 of the CUs, measured
+    // r04 10.6 / 12.3 ms per step: not an option)
     if (prio_mode) {
       int lo = 0, hi = 0;  // numerically: greatest = lowest priority
       if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
