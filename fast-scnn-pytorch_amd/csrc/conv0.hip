@@ -75,49 +75,64 @@ __device__ __forceinline__ void c0_tile(int& seg, int& row) {
   row = (int)(L / gx);
 }
 
+// C0_RB output rows per workgroup: the 2*C0_RB + 1 input rows are staged once (adjacent output
+// rows share an input row), the rows are computed and stored one after the other, and one
+// statistics record covers the workgroup (per-row (mean, M2) merged in fixed order).  Measured r04
+// at C0_RB = 2 (5 instead of 6 input rows per 2 output rows, half the workgroups, 51 KB LDS: 3 per
+// CU): 5.98-5.99 vs 5.955-5.96 ms per cfg3 step, and the fp32 train gradients' merge of two rows'
+// statistics in fp32 sat just outside the oracle gate -- one row stays the default.
+#ifndef C0_RB_DEFAULT
+#define C0_RB_DEFAULT 1
+#endif
+constexpr int C0_RB = C0_RB_DEFAULT;
+
 template <typename TO, int XB>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   // 16-bit output => MFMA operands in that dtype (the plan's compute dtype)
   constexpr int BF = sizeof(TO) == 4 ? 0 : (std::is_same<TO, f16>::value ? 2 : 1);
   using M = C0Mma<BF>;
   using TI = typename std::conditional<XB != 0, uint16_t, float>::type;
+  constexpr int RB = C0_RB;
+  constexpr int NRI = 2 * RB + 1;                   // staged input rows
   constexpr int VI = 16 / sizeof(TI);               // input elements per 16-B vector
   constexpr int NVR = (C0_IN_W + VI - 1) / VI;      // vectors per staged input row
-  constexpr int LPV = (9 * NVR + 255) / 256;        // vector loads per thread
+  constexpr int LPV = (3 * NRI * NVR + 255) / 256;  // vector loads per thread
   constexpr int OST = 32 + 16 / sizeof(TO);         // s_out row stride (elements, 16-B aligned)
-  // the input strip and the output tile are live in disjoint phases: one LDS region (occupancy)
-  // fp32 output (SW): swapped MFMA operands put 4 consecutive channels of one pixel in each lane,
-  // stored straight from registers as 16-B vectors, so no output tile in LDS
-  constexpr bool SW = false;  // measured slower than the LDS-staged tile (256 vs 230 us, cfg2)
-  constexpr int IN_BYTES = (9 * C0_IN_W + VI) * 4;
-  constexpr int OUT_BYTES = SW ? 0 : C0_TILE * OST * (int)sizeof(TO);
-  __shared__ __attribute__((aligned(16))) char s_raw[IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES];
+  constexpr int IN_BYTES = ((3 * NRI * C0_IN_W + VI) * 4 + 15) / 16 * 16;
+  constexpr int OUT_BYTES = C0_TILE * OST * (int)sizeof(TO);
+  // one row: the input strip and the output tile are live in disjoint phases (one region); more
+  // rows: the strip stays live while each row's tile is staged
+  constexpr int RAW = RB == 1 ? (IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES) : IN_BYTES + OUT_BYTES;
+  __shared__ __attribute__((aligned(16))) char s_raw[RAW];
   float* s_in = reinterpret_cast<float*>(s_raw);   // [ci][r][col] (+ slack for the last vector)
-  TO* s_out = reinterpret_cast<TO*>(s_raw);        // [px][OST]
+  TO* s_out = reinterpret_cast<TO*>(s_raw + (RB == 1 ? 0 : IN_BYTES));  // [px][OST]
   __shared__ float s_red[2][4][C0_OUT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  int seg, row;  // row = n * Ho + ho
-  c0_tile(seg, row);
+  int seg, rowb;  // rowb = n * HB + hb
+  c0_tile(seg, rowb);
+  const int HB = cdiv(a.Ho, RB);
   const int wo0 = seg * C0_TILE;
-  const int n = row / a.Ho, ho = row - n * a.Ho;
+  const int n = rowb / HB, ho0 = (rowb - n * HB) * RB;
+  const int nrows = min(RB, a.Ho - ho0);
   const int npx = min(C0_TILE, a.Wo - wo0);
 
-  // ---- stage the 3 x 3 x (2*256+1) input strip with 16-B loads (all issued, then stored) ----
+  // ---- stage the 3 x NRI x (2*256+1) input strip (all loads issued, then stored) ------------
   const int col0 = 2 * wo0;
   const int ncol = min(C0_IN_W, a.W - col0);
   const TI* xin = (const TI*)a.x;
+  auto rowok = [&](int r) { return 2 * ho0 + r < a.H; };
   if (a.W % VI != 0) {  // rows not 16-B aligned: scalar staging (odd widths only)
-    constexpr int NIN = 9 * C0_IN_W, LPT = (NIN + 255) / 256;
+    constexpr int NIN = 3 * NRI * C0_IN_W, LPT = (NIN + 255) / 256;
     float v[LPT];
 #pragma unroll
     for (int k = 0; k < LPT; ++k) {
       const int i = tid + 256 * k;
       const int cr = i / C0_IN_W, c = i - cr * C0_IN_W;
-      const int ci = cr / 3, r = cr - ci * 3;
-      const bool ok = i < NIN && c < ncol;
-      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c : 0;
+      const int ci = cr / NRI, r = cr - ci * NRI;
+      const bool ok = i < NIN && c < ncol && rowok(r);
+      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho0 + r)) * a.W + col0 + c : 0;
       const float t = XB ? in16<XB>((uint16_t)xin[off]) : (float)xin[off];
       v[k] = ok ? t : 0.f;
     }
@@ -129,16 +144,16 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
 #pragma unroll
     for (int k = 0; k < LPV; ++k) {
       const int i = tid + 256 * k;
-      const int cr = i / NVR, v = i - cr * NVR;  // cr = ci*3 + r
-      const int ci = cr / 3, r = cr - ci * 3;
-      const bool ok = i < 9 * NVR && v * VI + VI <= ncol;  // whole vector inside the row
-      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + v * VI : 0;
+      const int cr = i / NVR, v = i - cr * NVR;  // cr = ci*NRI + r
+      const int ci = cr / NRI, r = cr - ci * NRI;
+      const bool ok = i < 3 * NRI * NVR && v * VI + VI <= ncol && rowok(r);  // whole vector inside
+      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho0 + r)) * a.W + col0 + v * VI : 0;
       raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(xin + off));
     }
 #pragma unroll
     for (int k = 0; k < LPV; ++k) {
       const int i = tid + 256 * k;
-      if (i >= 9 * NVR) continue;
+      if (i >= 3 * NRI * NVR) continue;
       const int cr = i / NVR, v = i - cr * NVR;
       const TI* e = reinterpret_cast<const TI*>(&raw[k]);
 #pragma unroll
@@ -149,13 +164,13 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
         else f = (float)e[j];
         if (c < C0_IN_W) s_in[cr * C0_IN_W + c] = f;
       }
-      if (v * VI < ncol && v * VI + VI > ncol) {  // the image's right edge: partial vector
+      const int ci = cr / NRI, r = cr - ci * NRI;
+      if (rowok(r) && v * VI < ncol && v * VI + VI > ncol) {  // the image's right edge
         for (int j = 0; j < VI; ++j) {
           const int c = v * VI + j;
-          const int ci = cr / 3, r = cr - ci * 3;
           float f = 0.f;
           if (c < ncol) {
-            const size_t o = (((size_t)n * 3 + ci) * a.H + (2 * ho + r)) * a.W + col0 + c;
+            const size_t o = (((size_t)n * 3 + ci) * a.H + (2 * ho0 + r)) * a.W + col0 + c;
             f = XB ? in16<XB>((uint16_t)xin[o]) : (float)xin[o];
           }
           if (c < C0_IN_W) s_in[cr * C0_IN_W + c] = f;
@@ -176,119 +191,15 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     }
     bw[jt] = M::pack(wv);
   }
-  // tap k -> offset in s_in relative to the pixel's column 2*px: (ci*3 + kh)*IN_W + kw
+  // tap k -> offset in s_in relative to the pixel's column 2*px of output row 0
   int koff[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int k = 8 * lq + e;
     const int kk = k < 27 ? k : 0;
     const int ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
-    koff[e] = (ci * 3 + kh) * C0_IN_W + kw;
+    koff[e] = (ci * NRI + kh) * C0_IN_W + kw;
   }
-  if constexpr (SW) {
-    __syncthreads();
-    // acc[gi][jt][r] = out[pixel 64w + 16gi + li][channel 16jt + 4lq + r]
-    f32x4 acc[4][2];
-#pragma unroll
-    for (int gi = 0; gi < 4; ++gi) {
-      const int px = wave * 64 + gi * 16 + li;
-      float av[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) av[e] = 8 * lq + e < 27 ? s_in[koff[e] + 2 * px] : 0.f;
-      const typename M::Frag af = M::pack(av);
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        acc[gi][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        M::mma(bw[jt], af, acc[gi][jt]);
-      }
-    }
-    float* y = (float*)a.y + ((size_t)row * a.Wo + wo0) * C0_OUT;
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      float sc[4], sh[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = 16 * jt + 4 * lq + r;
-        sc[r] = a.scale ? a.scale[c] : 1.f;
-        sh[r] = a.scale ? a.shift[c] : 0.f;
-      }
-#pragma unroll
-      for (int gi = 0; gi < 4; ++gi) {
-        const int px = wave * 64 + gi * 16 + li;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[gi][jt][r] * sc[r] + sh[r];
-          if (a.relu) v[r] = fmaxf(v[r], 0.f);
-          acc[gi][jt][r] = v[r];
-        }
-        if (px < npx)
-          *reinterpret_cast<float4*>(y + (size_t)px * C0_OUT + 16 * jt + 4 * lq) =
-              make_float4(v[0], v[1], v[2], v[3]);
-      }
-    }
-    if (a.part == nullptr) return;
-    // per-channel (mean, M2, count) over the block's npx pixels: lanes li hold pixels
-    float sum[2][4];
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = 0.f;
-#pragma unroll
-        for (int gi = 0; gi < 4; ++gi) t += (wave * 64 + gi * 16 + li < npx) ? acc[gi][jt][r] : 0.f;
-        t += __shfl_xor(t, 1);
-        t += __shfl_xor(t, 2);
-        t += __shfl_xor(t, 4);
-        t += __shfl_xor(t, 8);
-        sum[jt][r] = t;
-      }
-    if (li == 0)
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s_red[0][wave][16 * jt + 4 * lq + r] = sum[jt][r];
-    __syncthreads();
-    float mean[2][4];
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = 16 * jt + 4 * lq + r;
-        mean[jt][r] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
-      }
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = 0.f;
-#pragma unroll
-        for (int gi = 0; gi < 4; ++gi) {
-          const float d = acc[gi][jt][r] - mean[jt][r];
-          t += (wave * 64 + gi * 16 + li < npx) ? d * d : 0.f;
-        }
-        t += __shfl_xor(t, 1);
-        t += __shfl_xor(t, 2);
-        t += __shfl_xor(t, 4);
-        t += __shfl_xor(t, 8);
-        sum[jt][r] = t;
-      }
-    if (li == 0)
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s_red[1][wave][16 * jt + 4 * lq + r] = sum[jt][r];
-    __syncthreads();
-    if (tid < C0_OUT) {
-      const size_t pi = (size_t)row * gridDim.x + seg;
-      float* rec = a.part + pi * 3 * C0_OUT;
-      const int c = tid;
-      rec[c] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
-      rec[C0_OUT + c] = (s_red[1][0][c] + s_red[1][1][c]) + (s_red[1][2][c] + s_red[1][3][c]);
-      rec[2 * C0_OUT + c] = (float)npx;
-    }
-    return;
-  } else {
   float fsc[2], fsh[2];  // eval BN fold of the lane's two channels (li, 16 + li)
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
@@ -297,125 +208,147 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   }
   __syncthreads();
 
-  // ---- wave w: pixels [64w, 64w+64) = 4 groups of 16, x 32 channels; acc[gi][jt][r] is
-  //      out[pixel 64w + 16gi + 4lq + r][channel 16jt + li] -------------------------------------
-  f32x4 acc[4][2];
+  float tn = 0.f, tmean[2] = {0.f, 0.f}, tm2[2] = {0.f, 0.f};  // the record (wave 0, lq 0)
+  for (int r = 0; r < nrows; ++r) {  // (workgroup-uniform)
+    const int ho = ho0 + r;
+    // ---- wave w: pixels [64w, 64w+64) = 4 groups of 16, x 32 channels; acc[gi][jt][q] is
+    //      out[pixel 64w + 16gi + 4lq + q][channel 16jt + li] -----------------------------------
+    f32x4 acc[4][2];
 #pragma unroll
-  for (int gi = 0; gi < 4; ++gi) {
-    const int px = wave * 64 + gi * 16 + li;  // A row = pixel
-    float av[8];
+    for (int gi = 0; gi < 4; ++gi) {
+      const int px = wave * 64 + gi * 16 + li;  // A row = pixel
+      float av[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) av[e] = 8 * lq + e < 27 ? s_in[koff[e] + 2 * px] : 0.f;
-    const typename M::Frag af = M::pack(av);
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      acc[gi][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      M::mma(af, bw[jt], acc[gi][jt]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = acc[gi][jt][r] * fsc[jt] + fsh[jt];
-        if (a.relu) v = fmaxf(v, 0.f);
-        acc[gi][jt][r] = v;
-      }
-    }
-  }
-  // ---- stage the tile in the storage type, then coalesced 16-B stores ----------------------
-  __syncthreads();  // every wave is done reading s_in (aliased by s_out)
-#pragma unroll
-  for (int gi = 0; gi < 4; ++gi)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        TO t;
-        if constexpr (BF) t.x = s16_from<TO>(acc[gi][jt][r]);
-        else t = acc[gi][jt][r];
-        s_out[(wave * 64 + gi * 16 + 4 * lq + r) * OST + 16 * jt + li] = t;
-      }
-  __syncthreads();
-  {
-    constexpr int V = VecW<TO>::V;
-    TO* y = (TO*)a.y + ((size_t)row * a.Wo + wo0) * C0_OUT;
-    const int nvec = npx * C0_OUT / V;
-#pragma unroll
-    for (int k = 0; k < C0_TILE * C0_OUT / V / 256; ++k) {
-      const int i = tid + 256 * k;
-      if (i >= nvec) continue;
-      const int p = (i * V) / C0_OUT, c = (i * V) - p * C0_OUT;
-      *reinterpret_cast<uint4*>(y + (size_t)i * V) = *reinterpret_cast<const uint4*>(&s_out[p * OST + c]);
-    }
-  }
-  if (a.part == nullptr) return;
-  // ---- per-channel (mean, M2, count) over the block's npx pixels, from the fp32 registers ----
-  float sum[2] = {0.f, 0.f};
-#pragma unroll
-  for (int gi = 0; gi < 4; ++gi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool ok = wave * 64 + gi * 16 + 4 * lq + r < npx;
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? acc[gi][jt][r] : 0.f;
-    }
-#pragma unroll
-  for (int jt = 0; jt < 2; ++jt) {
-    sum[jt] += __shfl_xor(sum[jt], 16);
-    sum[jt] += __shfl_xor(sum[jt], 32);
-  }
-  if (lq == 0) {
-    s_red[0][wave][li] = sum[0];
-    s_red[0][wave][16 + li] = sum[1];
-  }
-  __syncthreads();
-  float mean[2];
-#pragma unroll
-  for (int jt = 0; jt < 2; ++jt) {
-    const int c = 16 * jt + li;
-    mean[jt] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
-  }
-  float m2[2] = {0.f, 0.f};
-#pragma unroll
-  for (int gi = 0; gi < 4; ++gi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool ok = wave * 64 + gi * 16 + 4 * lq + r < npx;
+      for (int e = 0; e < 8; ++e) av[e] = 8 * lq + e < 27 ? s_in[koff[e] + 2 * r * C0_IN_W + 2 * px] : 0.f;
+      const typename M::Frag af = M::pack(av);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
-        const float d = acc[gi][jt][r] - mean[jt];
-        m2[jt] += ok ? d * d : 0.f;
+        acc[gi][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        M::mma(af, bw[jt], acc[gi][jt]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = acc[gi][jt][q] * fsc[jt] + fsh[jt];
+          if (a.relu) v = fmaxf(v, 0.f);
+          acc[gi][jt][q] = v;
+        }
       }
     }
+    // ---- stage the row's tile in the storage type, then coalesced 16-B stores ----------------
+    __syncthreads();  // RB == 1: every wave is done reading s_in (aliased); else the previous
+                      // row's tile stores are done
 #pragma unroll
-  for (int jt = 0; jt < 2; ++jt) {
-    m2[jt] += __shfl_xor(m2[jt], 16);
-    m2[jt] += __shfl_xor(m2[jt], 32);
+    for (int gi = 0; gi < 4; ++gi)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          TO t;
+          if constexpr (BF) t.x = s16_from<TO>(acc[gi][jt][q]);
+          else t = acc[gi][jt][q];
+          s_out[(wave * 64 + gi * 16 + 4 * lq + q) * OST + 16 * jt + li] = t;
+        }
+    __syncthreads();
+    {
+      constexpr int V = VecW<TO>::V;
+      TO* y = (TO*)a.y + (((size_t)n * a.Ho + ho) * a.Wo + wo0) * C0_OUT;
+      const int nvec = npx * C0_OUT / V;
+#pragma unroll
+      for (int k = 0; k < C0_TILE * C0_OUT / V / 256; ++k) {
+        const int i = tid + 256 * k;
+        if (i >= nvec) continue;
+        const int p = (i * V) / C0_OUT, c = (i * V) - p * C0_OUT;
+        *reinterpret_cast<uint4*>(y + (size_t)i * V) = *reinterpret_cast<const uint4*>(&s_out[p * OST + c]);
+      }
+    }
+    if (a.part == nullptr) continue;
+    // ---- per-channel (mean, M2) of the row's npx pixels, from the fp32 registers -------------
+    float sum[2] = {0.f, 0.f};
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = wave * 64 + gi * 16 + 4 * lq + q < npx;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? acc[gi][jt][q] : 0.f;
+      }
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      sum[jt] += __shfl_xor(sum[jt], 16);
+      sum[jt] += __shfl_xor(sum[jt], 32);
+    }
+    if (lq == 0) {
+      s_red[0][wave][li] = sum[0];
+      s_red[0][wave][16 + li] = sum[1];
+    }
+    __syncthreads();
+    float mean[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const int c = 16 * jt + li;
+      mean[jt] = ((s_red[0][0][c] + s_red[0][1][c]) + (s_red[0][2][c] + s_red[0][3][c])) / (float)npx;
+    }
+    float m2[2] = {0.f, 0.f};
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = wave * 64 + gi * 16 + 4 * lq + q < npx;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          const float d = acc[gi][jt][q] - mean[jt];
+          m2[jt] += ok ? d * d : 0.f;
+        }
+      }
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      m2[jt] += __shfl_xor(m2[jt], 16);
+      m2[jt] += __shfl_xor(m2[jt], 32);
+    }
+    if (lq == 0) {
+      s_red[1][wave][li] = m2[0];
+      s_red[1][wave][16 + li] = m2[1];
+    }
+    __syncthreads();
+    if (wave == 0 && lq == 0) {  // merge the row into the record (Chan, fixed row order)
+      const float nr = (float)npx;
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const int c = 16 * jt + li;
+        const float rm2 = (s_red[1][0][c] + s_red[1][1][c]) + (s_red[1][2][c] + s_red[1][3][c]);
+        if (r == 0) {
+          tmean[jt] = mean[jt];
+          tm2[jt] = rm2;
+        } else {
+          const float nt = tn + nr, d = mean[jt] - tmean[jt];
+          tmean[jt] += d * (nr / nt);
+          tm2[jt] += rm2 + d * d * (tn * nr / nt);
+        }
+      }
+      tn += nr;
+    }
+    __syncthreads();  // s_red is reused by the next row
   }
-  if (lq == 0) {
-    s_red[1][wave][li] = m2[0];
-    s_red[1][wave][16 + li] = m2[1];
-  }
-  __syncthreads();
-  if (wave == 0 && lq == 0) {
-    const size_t pi = (size_t)row * gridDim.x + seg;
+  if (a.part != nullptr && wave == 0 && lq == 0) {
+    const size_t pi = (size_t)rowb * gridDim.x + seg;
     float* rec = a.part + pi * 3 * C0_OUT;
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       const int c = 16 * jt + li;
-      rec[c] = mean[jt];
-      rec[C0_OUT + c] = (s_red[1][0][c] + s_red[1][1][c]) + (s_red[1][2][c] + s_red[1][3][c]);
-      rec[2 * C0_OUT + c] = (float)npx;
+      rec[c] = tmean[jt];
+      rec[C0_OUT + c] = tm2[jt];
+      rec[2 * C0_OUT + c] = tn;
     }
   }
-  }  // SW
 }
 
-int conv0_parts(int N, int Ho, int Wo) { return N * Ho * cdiv(Wo, C0_TILE); }
+int conv0_parts(int N, int Ho, int Wo) { return N * cdiv(Ho, C0_RB) * cdiv(Wo, C0_TILE); }
 
 int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
   if (a.Ho != (a.H - 3) / 2 + 1 || a.Wo != (a.W - 3) / 2 + 1 || a.H < 3 || a.W < 3) {
     set_error("conv0_fwd: bad shape H=%d W=%d Ho=%d Wo=%d", a.H, a.W, a.Ho, a.Wo);
     return E_INVALID;
   }
-  dim3 grid(cdiv(a.Wo, C0_TILE), a.N * a.Ho);
+  dim3 grid(cdiv(a.Wo, C0_TILE), a.N * cdiv(a.Ho, C0_RB));
   const double px = (double)a.N * a.Ho * a.Wo;
   ProfScope ps(PK_CONV0_FWD, st,
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (y_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
