@@ -619,7 +619,7 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
 // separate fold+finalize launch.
 constexpr int LC_TW = 128;           // tile: 2 dx rows x 128 columns = 256 pixels
 constexpr int LC_LDX = 256 + 8;      // x^T image row stride (elements): conflict-free b128 reads
-constexpr int LC_MAXP = 512;         // 2 workgroups per CU
+constexpr int LC_MAXP = 512;         // 2 workgroups per CU (1024: 6.00 vs 5.96 ms per step, r04)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <typename T>
