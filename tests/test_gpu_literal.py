@@ -146,13 +146,22 @@ def test_cfg2_literal_batch8_matches_batch1():
     assert d7 < 1e-4
 
 
+def _low_res(n):
+    """Spatial size of the 1/8-resolution logits (conv0 k3 s2 p0, then two stride-2 3x3 p1)."""
+    n = (n - 3) // 2 + 1
+    n = (n - 1) // 2 + 1
+    return (n - 1) // 2 + 1
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("nc,N,H,W", [
-    (19, 2, 256, 512),    # one column chunk, targets staged in LDS
-    (19, 2, 64, 2112),    # Wl = 264: two column chunks (carry), W > 2048: targets from HBM
-    (2, 2, 128, 256),     # the TuSimple class count
+@pytest.mark.parametrize("nc,N,H,W,ign", [
+    (19, 2, 256, 512, -1),    # one column chunk, int8 targets (4-row ring)
+    (19, 2, 64, 2112, -1),    # Wl = 264: two column chunks (carry), W > 2048: int64 targets
+    (2, 2, 128, 256, -1),     # the TuSimple class count
+    (19, 2, 64, 260, -1),     # W % 8 != 0: int64 targets staged per row; odd low-res width
+    (19, 2, 128, 256, 255),   # another ignore_index (the int8 pack's validity test)
 ])
-def test_fused_ce_head_16bit_vs_fp64(dt, nc, N, H, W):
+def test_fused_ce_head_16bit_vs_fp64(dt, nc, N, H, W, ign):
     """The 16-bit fused loss head (head.hip ce_head2_kernel: row-factored accumulation, target
     one-hots in LDS) against autograd in fp64 on the SAME low-res logits the forward stored:
     bilinear align_corners upsample (models/fast_scnn.py:51) + nn.CrossEntropyLoss(ignore_index=-1)
@@ -166,18 +175,18 @@ def test_fused_ce_head_16bit_vs_fp64(dt, nc, N, H, W):
     x = _rnd((N, 3, H, W), 11).to(DEV).to(dt)
     t = (_rnd((N, H, W), 12, 0, nc).floor().long()).clamp_(0, nc - 1)
     drop = _rnd((N, H, W), 13, 0, 1) < 0.05
-    t[drop] = -1
-    t[:, 5:9, :] = -1          # whole ignored rows
+    t[drop] = ign
+    t[:, 5:9, :] = ign          # whole ignored rows
     t = t.to(DEV)
-    loss = m.forward_loss(x, t)
+    loss = m.forward_loss(x, t, ignore_index=ign)
     loss.backward()
     torch.cuda.synchronize()
-    Hl, Wl = H // 8, W // 8
+    Hl, Wl = _low_res(H), _low_res(W)
     L = m.debug_buffer("logits").double().view(N, Hl, Wl, nc).permute(0, 3, 1, 2).clone()
     G = m.debug_buffer("g_logits").double().view(N, Hl, Wl, nc).permute(0, 3, 1, 2)
     L.requires_grad_(True)
     up = F.interpolate(L, (H, W), mode="bilinear", align_corners=True)
-    lref = F.cross_entropy(up, t, ignore_index=-1)
+    lref = F.cross_entropy(up, t, ignore_index=ign)
     lref.backward()
     gref = L.grad
     assert abs(loss.item() - lref.item()) <= 1e-5 * abs(lref.item()), (loss.item(), lref.item())
