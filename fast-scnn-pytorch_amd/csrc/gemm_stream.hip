@@ -215,57 +215,9 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
   const T* B = (const T*)a.B;
   stamp(a.stamps, 0);
 
-  // ---- weights of the group -> LDS (zero rows n >= N, zero k >= K), per-column tables -------
-  for (int i = tid; i < BN * KV; i += 256) {
-    const int r = i / KV, v = i - r * KV;
-    const int n = n0 + r, k = v * V;
-    const bool ok = n < a.N && k < a.K;
-    const uint4 t = gs_tail<T>(*reinterpret_cast<const uint4*>(B + (ok ? (size_t)n * a.ldb + k : 0)),
-                               ok ? a.K - k : 0);
-    s_w[r * WST + v] = t;
-  }
-  for (int i = tid; i < BN; i += 256) {
-    const int n = n0 + i < a.N ? n0 + i : 0;
-    s_sc[i] = a.scale ? a.scale[n] : 1.f;
-    s_sc[BN + i] = a.shift ? a.shift[n] : 0.f;
-    if constexpr (BS) {
-      // ReLU mask of that BN recomputed as fmaf(z, scale, shift) > 0 (mode 2); mode 0 (no
-      // ReLU) uses scale 0, shift 1 so both are the same select
-      const bool m2 = a.bmode == 2;
-      s_bc[i] = a.bmean[n];
-      s_bc[BN + i] = a.binvstd[n];
-      s_bc[2 * BN + i] = m2 ? a.bscale[n] : 0.f;
-      s_bc[3 * BN + i] = m2 ? a.bshift[n] : 1.f;
-    }
-  }
-  if constexpr (AT) {
-    for (int k = tid; k < KP; k += 256) {
-      s_at[k] = k < a.K ? a.a_scale[k] : 0.f;
-      s_at[KP + k] = k < a.K ? a.a_shift[k] : 0.f;
-    }
-  }
-  __syncthreads();
-  stamp(a.stamps, 1);
-
   const int nchunks = cdiv(a.M, GS_MW);
   const int wstride = bpg * 4;
   int c = bi * 4 + wave;
-
-  // sums of channels n0 + 16nt + 4lq + r over this lane's pixels (ST: shifted by shf)
-  float s1[SUMS ? NT : 1][4], s2[SUMS ? NT : 1][4];
-  float cnt = 0.f;
-  if constexpr (SUMS) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { s1[nt][r] = 0.f; s2[nt][r] = 0.f; }
-  }
-  // ST shift of each channel: its value at the wave's first pixel, kept in LDS (s_shf[wave])
-  float* wshf = s_shf + wave * BN;
-  if constexpr (ST) {
-    for (int i = lane; i < BN; i += 64) wshf[i] = 0.f;
-  }
-  bool first = true;
 
   // Software pipeline over K-parts: a chunk's k-steps are loaded as NH parts of KH steps (a
   // whole chunk double-buffered would pass 256 VGPRs for K > 4 steps), and each part's loads are
@@ -291,6 +243,99 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
       }
     }
   };
+
+  // ---- weights of the group -> LDS (zero rows n >= N, zero k >= K), per-column tables -------
+  // Every global load of the prologue — the first chunk's A part included — is issued before the
+  // first LDS store, in batches of WB vectors per thread: the workgroup waits out one memory
+  // round trip per batch instead of one per loop trip (the stores of a rolled loop each waited
+  // on their own load; the A part then stays in flight across the barrier, which waits on LDS
+  // only).
+  if (c < nchunks) loadx(c, 0, xa);
+  float t_sc = 1.f, t_sh = 0.f, t_bc[4] = {0.f, 0.f, 0.f, 1.f};
+  if (tid < BN) {  // BN <= 128 < 256 threads: one column each
+    const int n = n0 + tid < a.N ? n0 + tid : 0;
+    if (a.scale) t_sc = a.scale[n];
+    if (a.shift) t_sh = a.shift[n];
+    if constexpr (BS) {
+      // ReLU mask of that BN recomputed as fmaf(z, scale, shift) > 0 (mode 2); mode 0 (no
+      // ReLU) uses scale 0, shift 1 so both are the same select
+      t_bc[0] = a.bmean[n];
+      t_bc[1] = a.binvstd[n];
+      if (a.bmode == 2) {
+        t_bc[2] = a.bscale[n];
+        t_bc[3] = a.bshift[n];
+      }
+    }
+  }
+  constexpr int ATI = AT ? (KP + 255) / 256 : 1;
+  float t_at[ATI][2];
+  if constexpr (AT) {
+#pragma unroll
+    for (int u = 0; u < ATI; ++u) {
+      const int k = tid + u * 256;
+      const bool ok = k < a.K;
+      t_at[u][0] = ok ? a.a_scale[k] : 0.f;
+      t_at[u][1] = ok ? a.a_shift[k] : 0.f;
+    }
+  }
+  constexpr int WI = (BN * KV + 255) / 256;  // weight vectors per thread
+  constexpr int WB = WI < 8 ? WI : 8;
+#pragma unroll
+  for (int u0 = 0; u0 < WI; u0 += WB) {
+    uint4 t[WB];
+#pragma unroll
+    for (int u = 0; u < WB; ++u) {
+      const int i = tid + (u0 + u) * 256;
+      const int r = i / KV, v = i - r * KV;
+      const int n = n0 + r, k = v * V;
+      const bool ok = u0 + u < WI && i < BN * KV && n < a.N && k < a.K;
+      t[u] = gs_tail<T>(*reinterpret_cast<const uint4*>(B + (ok ? (size_t)n * a.ldb + k : 0)),
+                        ok ? a.K - k : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < WB; ++u) {
+      const int i = tid + (u0 + u) * 256;
+      const int r = i / KV, v = i - r * KV;
+      if (u0 + u < WI && i < BN * KV) s_w[r * WST + v] = t[u];
+    }
+  }
+  if (tid < BN) {
+    s_sc[tid] = t_sc;
+    s_sc[BN + tid] = t_sh;
+    if constexpr (BS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s_bc[j * BN + tid] = t_bc[j];
+    }
+  }
+  if constexpr (AT) {
+#pragma unroll
+    for (int u = 0; u < ATI; ++u) {
+      const int k = tid + u * 256;
+      if (k < KP) {
+        s_at[k] = t_at[u][0];
+        s_at[KP + k] = t_at[u][1];
+      }
+    }
+  }
+  __syncthreads();
+  stamp(a.stamps, 1);
+
+  // sums of channels n0 + 16nt + 4lq + r over this lane's pixels (ST: shifted by shf)
+  float s1[SUMS ? NT : 1][4], s2[SUMS ? NT : 1][4];
+  float cnt = 0.f;
+  if constexpr (SUMS) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[nt][r] = 0.f; s2[nt][r] = 0.f; }
+  }
+  // ST shift of each channel: its value at the wave's first pixel, kept in LDS (s_shf[wave])
+  float* wshf = s_shf + wave * BN;
+  if constexpr (ST) {
+    for (int i = lane; i < BN; i += 64) wshf[i] = 0.f;
+  }
+  bool first = true;
+
   // at the use site: lazy BN+ReLU (AT), then the row / K-tail zeroing
   auto prep = [&](int chunk, int h, uint4 (&r)[2][KH]) {
 #pragma unroll
@@ -309,7 +354,6 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 
   T* Cp = (T*)a.C;
   const T* Rp = (const T*)a.R;
-  if (c < nchunks) loadx(c, 0, xa);
   for (; c < nchunks; c += wstride) {
     f32x4 acc[2][NT];
 #pragma unroll
