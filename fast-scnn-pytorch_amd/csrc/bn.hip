@@ -484,81 +484,130 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
 }
 
 // dz = scale * (dy_r - coef0 - xhat * coef1)   (train);  dz = scale * dy_r (eval: coef null)
+// Each thread owns ONE channel vector c: its per-channel tables (scale, shift, mean, invstd, the
+// two coefficients; the second BN's for PAIR) are loaded once into registers, and the thread
+// sweeps pixels mu0, mu0 + P, mu0 + 2P, ... (the grid covers P pixels x all CV channel vectors per
+// sweep, so every sweep is one contiguous, coalesced span of the tensor).  U pixels' loads are
+// issued back to back (clamped rows, stores predicated) before their use.  The per-element
+// arithmetic is unchanged, so dz is bit-identical to a one-vector-per-thread pass — that form
+// re-read 6 table vectors (12 16-B loads) for every 2 data loads.
 template <typename T, int MODE, bool TRAIN, bool PAIR = false>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, unsigned P) {
   constexpr int V = VecW<T>::V;
-  const int CV = a.C / V;
-  // 32-bit index math (M*C/V < 2^31 is enforced by the planner)
+  constexpr int U = PAIR ? 2 : 4;
+  const unsigned CV = (unsigned)(a.C / V);
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (unsigned)a.M * (unsigned)CV) return;
-  const unsigned mu = i / (unsigned)CV;
-  const int c = (int)(i - mu * (unsigned)CV) * V;
-  const long long m = mu;
-  float g[V], z[V], mk[V], o[V], z2[PAIR ? V : 1];
-  ldv((const T*)a.dy + m * a.lddy + c, g);
-  if (TRAIN || MODE == 2) ldv((const T*)a.z + m * a.ldz + c, z);
-  if (MODE == 1) ldv((const T*)a.mask + m * a.ldmask + c, mk);
-  if constexpr (PAIR) {  // second BN on the same dy and mask (train, mask mode)
-    ldv((const T*)a.z2 + m * a.ldz + c, z2);
-    float o2[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const float gv = mk[j] > 0.f ? g[j] : 0.f;
-      const float xh = (z2[j] - a.mean2[c + j]) * a.invstd2[c + j];
-      o2[j] = a.scale2[c + j] * (gv - a.coef2[c + j] - xh * a.coef2[a.C + c + j]);
-    }
-    stv((T*)a.dz2 + m * a.lddz + c, o2);
-  }
+  if (i >= P * CV) return;
+  const unsigned mu0 = i / CV;
+  const int c = (int)(i - mu0 * CV) * V;
+  constexpr bool SH = MODE == 2, ST = TRAIN;
+  float t_sc[V], t_sh[SH ? V : 1], t_mn[ST ? V : 1], t_is[ST ? V : 1], t_c0[ST ? V : 1],
+      t_c1[ST ? V : 1];
+  float p_mn[PAIR ? V : 1], p_is[PAIR ? V : 1], p_sc[PAIR ? V : 1], p_c0[PAIR ? V : 1],
+      p_c1[PAIR ? V : 1];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
-    float gv = g[j];
-    if (MODE == 1) gv = mk[j] > 0.f ? gv : 0.f;
-    if (MODE == 2) gv = fmaf(z[j], a.scale[c + j], a.shift[c + j]) > 0.f ? gv : 0.f;
-    if (TRAIN) {
-      const float xh = (z[j] - a.mean[c + j]) * a.invstd[c + j];
-      o[j] = a.scale[c + j] * (gv - a.coef[c + j] - xh * a.coef[a.C + c + j]);
-    } else {
-      o[j] = a.scale[c + j] * gv;
+    t_sc[j] = a.scale[c + j];
+    if constexpr (SH) t_sh[j] = a.shift[c + j];
+    if constexpr (ST) {
+      t_mn[j] = a.mean[c + j];
+      t_is[j] = a.invstd[c + j];
+      t_c0[j] = a.coef[c + j];
+      t_c1[j] = a.coef[a.C + c + j];
+    }
+    if constexpr (PAIR) {
+      p_mn[j] = a.mean2[c + j];
+      p_is[j] = a.invstd2[c + j];
+      p_sc[j] = a.scale2[c + j];
+      p_c0[j] = a.coef2[c + j];
+      p_c1[j] = a.coef2[a.C + c + j];
     }
   }
-  stv((T*)a.dz + m * a.lddz + c, o);
+  const long long M = a.M;
+  for (long long m0 = mu0; m0 < M; m0 += (long long)U * P) {
+    float g[U][V], z[U][V], mk[U][V], z2[PAIR ? U : 1][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long mm = m0 + (long long)u * P;
+      const long long m = mm < M ? mm : m0;
+      ldv((const T*)a.dy + m * a.lddy + c, g[u]);
+      if (TRAIN || MODE == 2) ldv((const T*)a.z + m * a.ldz + c, z[u]);
+      if (MODE == 1) ldv((const T*)a.mask + m * a.ldmask + c, mk[u]);
+      if constexpr (PAIR) ldv((const T*)a.z2 + m * a.ldz + c, z2[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long m = m0 + (long long)u * P;
+      if (m >= M) break;
+      if constexpr (PAIR) {  // second BN on the same dy and mask (train, mask mode)
+        float o2[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float gv = mk[u][j] > 0.f ? g[u][j] : 0.f;
+          const float xh = (z2[u][j] - p_mn[j]) * p_is[j];
+          o2[j] = p_sc[j] * (gv - p_c0[j] - xh * p_c1[j]);
+        }
+        stv((T*)a.dz2 + m * a.lddz + c, o2);
+      }
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float gv = g[u][j];
+        if (MODE == 1) gv = mk[u][j] > 0.f ? gv : 0.f;
+        if constexpr (SH) gv = fmaf(z[u][j], t_sc[j], t_sh[j]) > 0.f ? gv : 0.f;
+        if constexpr (ST) {
+          const float xh = (z[u][j] - t_mn[j]) * t_is[j];
+          o[j] = t_sc[j] * (gv - t_c0[j] - xh * t_c1[j]);
+        } else {
+          o[j] = t_sc[j] * gv;
+        }
+      }
+      stv((T*)a.dz + m * a.lddz + c, o);
+    }
+  }
+}
+
+// pixels per grid sweep: enough sweeps (<= 8 pixels per thread) to amortise the tables, while
+// the grid keeps >= 2048 workgroups (8 per CU) when the tensor has that much work
+static unsigned bn_bwd_apply_sweep(long long M, int CV) {
+  const long long total = M * CV;
+  long long ppt = total / (2048LL * 256);
+  ppt = ppt < 1 ? 1 : (ppt > 8 ? 8 : ppt);
+  return (unsigned)((M + ppt - 1) / ppt);
 }
 
 template <typename T>
-static void bn_bwd_apply_launch(const BnBwdArgs& a, unsigned grid, hipStream_t st) {
+static void bn_bwd_apply_launch(const BnBwdArgs& a, hipStream_t st) {
   const int mode = a.relu_z ? 2 : (a.mask ? 1 : 0);
-  if (a.coef) {
-    if (mode == 0) bn_bwd_apply_kernel<T, 0, true><<<grid, 256, 0, st>>>(a);
-    else if (mode == 1) bn_bwd_apply_kernel<T, 1, true><<<grid, 256, 0, st>>>(a);
-    else bn_bwd_apply_kernel<T, 2, true><<<grid, 256, 0, st>>>(a);
+  const unsigned P = bn_bwd_apply_sweep(a.M, a.C / VecW<T>::V);
+  const unsigned grid = (unsigned)(((long long)P * (a.C / VecW<T>::V) + 255) / 256);
+  if (a.z2) bn_bwd_apply_kernel<T, 1, true, true><<<grid, 256, 0, st>>>(a, P);
+  else if (a.coef) {
+    if (mode == 0) bn_bwd_apply_kernel<T, 0, true><<<grid, 256, 0, st>>>(a, P);
+    else if (mode == 1) bn_bwd_apply_kernel<T, 1, true><<<grid, 256, 0, st>>>(a, P);
+    else bn_bwd_apply_kernel<T, 2, true><<<grid, 256, 0, st>>>(a, P);
   } else {
-    if (mode == 0) bn_bwd_apply_kernel<T, 0, false><<<grid, 256, 0, st>>>(a);
-    else if (mode == 1) bn_bwd_apply_kernel<T, 1, false><<<grid, 256, 0, st>>>(a);
-    else bn_bwd_apply_kernel<T, 2, false><<<grid, 256, 0, st>>>(a);
+    if (mode == 0) bn_bwd_apply_kernel<T, 0, false><<<grid, 256, 0, st>>>(a, P);
+    else if (mode == 1) bn_bwd_apply_kernel<T, 1, false><<<grid, 256, 0, st>>>(a, P);
+    else bn_bwd_apply_kernel<T, 2, false><<<grid, 256, 0, st>>>(a, P);
   }
 }
 
 int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {
-  int V = dtype == DT_F32 ? 4 : 8;
-  long long total = a.M * (a.C / V);
-  unsigned grid = (unsigned)((total + 255) / 256);
   if (a.z2) {  // paired BNs: train, mask mode
     if (!a.mask || !a.coef || !a.coef2 || !a.dz2 || !a.mean2 || !a.invstd2 || !a.scale2) {
       set_error("bn_bwd_apply: a paired BN needs the mask mode, both coefficient sets and dz2");
       return E_INVALID;
     }
-    ProfScope ps(PK_BN_BWD, st, (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * 6, 0.0);
-    if (dtype == DT_F32) bn_bwd_apply_kernel<float, 1, true, true><<<grid, 256, 0, st>>>(a);
-    else if (dtype == DT_F16) bn_bwd_apply_kernel<f16, 1, true, true><<<grid, 256, 0, st>>>(a);
-    else bn_bwd_apply_kernel<bf16, 1, true, true><<<grid, 256, 0, st>>>(a);
-    return check_launch("bn_bwd_apply");
   }
   ProfScope ps(PK_BN_BWD, st,
-               (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * (2 + (a.coef || a.relu_z ? 1 : 0) + (a.mask ? 1 : 0)),
+               a.z2 ? (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C * 6
+                    : (dtype == DT_F32 ? 4.0 : 2.0) * a.M * a.C *
+                          (2 + (a.coef || a.relu_z ? 1 : 0) + (a.mask ? 1 : 0)),
                0.0);
-  if (dtype == DT_F32) bn_bwd_apply_launch<float>(a, grid, st);
-  else if (dtype == DT_F16) bn_bwd_apply_launch<f16>(a, grid, st);
-  else bn_bwd_apply_launch<bf16>(a, grid, st);
+  if (dtype == DT_F32) bn_bwd_apply_launch<float>(a, st);
+  else if (dtype == DT_F16) bn_bwd_apply_launch<f16>(a, st);
+  else bn_bwd_apply_launch<bf16>(a, st);
   return check_launch("bn_bwd_apply");
 }
 
