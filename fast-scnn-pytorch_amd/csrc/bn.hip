@@ -491,10 +491,9 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
 // issued back to back (clamped rows, stores predicated) before their use.  The per-element
 // arithmetic is unchanged, so dz is bit-identical to a one-vector-per-thread pass — that form
 // re-read 6 table vectors (12 16-B loads) for every 2 data loads.
-template <typename T, int MODE, bool TRAIN, bool PAIR = false>
+template <typename T, int MODE, bool TRAIN, bool PAIR, int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, unsigned P) {
   constexpr int V = VecW<T>::V;
-  constexpr int U = PAIR ? 2 : 4;
   const unsigned CV = (unsigned)(a.C / V);
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P * CV) return;
@@ -567,30 +566,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, unsigned
   }
 }
 
-// pixels per grid sweep: enough sweeps (<= 8 pixels per thread) to amortise the tables, while
-// the grid keeps >= 2048 workgroups (8 per CU) when the tensor has that much work
-static unsigned bn_bwd_apply_sweep(long long M, int CV) {
-  const long long total = M * CV;
-  long long ppt = total / (2048LL * 256);
-  ppt = ppt < 1 ? 1 : (ppt > 8 ? 8 : ppt);
-  return (unsigned)((M + ppt - 1) / ppt);
+template <typename T, int U>
+static void bn_bwd_apply_launch_u(const BnBwdArgs& a, unsigned P, hipStream_t st) {
+  const int mode = a.relu_z ? 2 : (a.mask ? 1 : 0);
+  const unsigned grid = (unsigned)(((long long)P * (a.C / VecW<T>::V) + 255) / 256);
+  if (a.z2) bn_bwd_apply_kernel<T, 1, true, true, (U > 2 ? 2 : U)><<<grid, 256, 0, st>>>(a, P);
+  else if (a.coef) {
+    if (mode == 0) bn_bwd_apply_kernel<T, 0, true, false, U><<<grid, 256, 0, st>>>(a, P);
+    else if (mode == 1) bn_bwd_apply_kernel<T, 1, true, false, U><<<grid, 256, 0, st>>>(a, P);
+    else bn_bwd_apply_kernel<T, 2, true, false, U><<<grid, 256, 0, st>>>(a, P);
+  } else {
+    if (mode == 0) bn_bwd_apply_kernel<T, 0, false, false, U><<<grid, 256, 0, st>>>(a, P);
+    else if (mode == 1) bn_bwd_apply_kernel<T, 1, false, false, U><<<grid, 256, 0, st>>>(a, P);
+    else bn_bwd_apply_kernel<T, 2, false, false, U><<<grid, 256, 0, st>>>(a, P);
+  }
 }
 
+// U = pixels in flight per thread: 4 when a thread sweeps >= 4 pixels, else 1 (a one-pixel
+// thread would issue U - 1 clamped duplicate loads)
 template <typename T>
 static void bn_bwd_apply_launch(const BnBwdArgs& a, hipStream_t st) {
-  const int mode = a.relu_z ? 2 : (a.mask ? 1 : 0);
-  const unsigned P = bn_bwd_apply_sweep(a.M, a.C / VecW<T>::V);
-  const unsigned grid = (unsigned)(((long long)P * (a.C / VecW<T>::V) + 255) / 256);
-  if (a.z2) bn_bwd_apply_kernel<T, 1, true, true><<<grid, 256, 0, st>>>(a, P);
-  else if (a.coef) {
-    if (mode == 0) bn_bwd_apply_kernel<T, 0, true><<<grid, 256, 0, st>>>(a, P);
-    else if (mode == 1) bn_bwd_apply_kernel<T, 1, true><<<grid, 256, 0, st>>>(a, P);
-    else bn_bwd_apply_kernel<T, 2, true><<<grid, 256, 0, st>>>(a, P);
-  } else {
-    if (mode == 0) bn_bwd_apply_kernel<T, 0, false><<<grid, 256, 0, st>>>(a, P);
-    else if (mode == 1) bn_bwd_apply_kernel<T, 1, false><<<grid, 256, 0, st>>>(a, P);
-    else bn_bwd_apply_kernel<T, 2, false><<<grid, 256, 0, st>>>(a, P);
-  }
+  const unsigned P = chan_sweep(a.M, a.C / VecW<T>::V);
+  if ((a.M + P - 1) / P >= 4) bn_bwd_apply_launch_u<T, 4>(a, P, st);
+  else bn_bwd_apply_launch_u<T, 1>(a, P, st);
 }
 
 int bn_bwd_apply(const BnBwdArgs& a, int dtype, hipStream_t st) {

@@ -349,6 +349,15 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32
   z = z ^ (z >> 31);
   return (uint32_t)(z >> 40) >= thr;
 }
+// Channel-owning sweeps (bn_bwd_apply, dropout): each thread keeps ONE channel vector's tables
+// in registers and visits pixels p0, p0 + P, ...; P = pixels per grid sweep.  Up to 8 pixels per
+// thread amortise the tables, while the grid keeps >= 2048 workgroups (8 per CU) when the tensor
+// has that much work.
+inline unsigned chan_sweep(long long M, int CV) {
+  long long ppt = M * CV / (2048LL * 256);
+  ppt = ppt < 1 ? 1 : (ppt > 8 ? 8 : ppt);
+  return (unsigned)((M + ppt - 1) / ppt);
+}
 inline uint32_t dropout_threshold(float p) {
   double t = (double)p * 16777216.0;
   uint32_t k = (uint32_t)t;

@@ -118,34 +118,6 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   const int nrows = min(RB, a.Ho - ho0);
   const int npx = min(C0_TILE, a.Wo - wo0);
 
-  // weights and BN-fold tables: loaded by load_w() between the strip's loads and its LDS stores,
-  // so their round trip overlaps the strip's
-  float wv[2][8];  // W[16*jt + li][8*lq + e] (k >= 27 zeroed at the pack)
-  float fsc[2], fsh[2];  // eval BN fold of the lane's two channels (li, 16 + li)
-  auto load_w = [&]() {
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int k = 8 * lq + e;
-        wv[jt][e] = a.w[(16 * jt + li) * 27 + (k < 27 ? k : 0)];
-      }
-      // (branch-free: a null table reads the weights instead and is then replaced)
-      const float t_sc = (a.scale ? a.scale : a.w)[16 * jt + li];
-      const float t_sh = (a.scale ? a.shift : a.w)[16 * jt + li];
-      fsc[jt] = a.scale ? t_sc : 1.f;
-      fsh[jt] = a.scale ? t_sh : 0.f;
-    }
-  };
-  // tap k -> offset in s_in relative to the pixel's column 2*px of output row 0
-  int koff[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = 8 * lq + e;
-    const int kk = k < 27 ? k : 0;
-    const int ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
-    koff[e] = (ci * NRI + kh) * C0_IN_W + kw;
-  }
   // ---- stage the 3 x NRI x (2*256+1) input strip (all loads issued, then stored) ------------
   const int col0 = 2 * wo0;
   const int ncol = min(C0_IN_W, a.W - col0);
@@ -164,7 +136,6 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       const float t = XB ? in16<XB>((uint16_t)xin[off]) : (float)xin[off];
       v[k] = ok ? t : 0.f;
     }
-    load_w();
 #pragma unroll
     for (int k = 0; k < LPT; ++k)
       if (tid + 256 * k < NIN) s_in[tid + 256 * k] = v[k];
@@ -179,7 +150,6 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + (2 * ho0 + r)) * a.W + col0 + v * VI : 0;
       raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(xin + off));
     }
-    load_w();
 #pragma unroll
     for (int k = 0; k < LPV; ++k) {
       const int i = tid + 256 * k;
@@ -208,12 +178,33 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       }
     }
   }
+  // B fragments (weights) for the two 16-channel tiles: W[16*jt + li][8*lq + e], k >= 27 -> 0
   typename M::Frag bw[2];
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
+    float wv[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) wv[jt][e] = 8 * lq + e < 27 ? wv[jt][e] : 0.f;
-    bw[jt] = M::pack(wv[jt]);
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * lq + e;
+      const float t = a.w[(16 * jt + li) * 27 + (k < 27 ? k : 0)];
+      wv[e] = k < 27 ? t : 0.f;
+    }
+    bw[jt] = M::pack(wv);
+  }
+  // tap k -> offset in s_in relative to the pixel's column 2*px of output row 0
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * lq + e;
+    const int kk = k < 27 ? k : 0;
+    const int ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
+    koff[e] = (ci * NRI + kh) * C0_IN_W + kw;
+  }
+  float fsc[2], fsh[2];  // eval BN fold of the lane's two channels (li, 16 + li)
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    fsc[jt] = a.scale ? a.scale[16 * jt + li] : 1.f;
+    fsh[jt] = a.scale ? a.shift[16 * jt + li] : 0.f;
   }
   __syncthreads();
 
@@ -335,7 +326,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       }
       tn += nr;
     }
-    if (r + 1 < nrows) __syncthreads();  // s_red is reused by the next row
+    __syncthreads();  // s_red is reused by the next row
   }
   if (a.part != nullptr && wave == 0 && lq == 0) {
     const size_t pi = (size_t)rowb * gridDim.x + seg;

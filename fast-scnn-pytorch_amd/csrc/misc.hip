@@ -449,31 +449,53 @@ int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N,
 
 // ---- dropout on an NHWC activation, mask indexed in NCHW order (matches the oracle) ----------
 
-// thread = one 16-B channel vector of one pixel; 32-bit index math (pixels * C/V < 2^31)
+// Channel-owning sweep (common.hpp chan_sweep): a thread keeps one 16-B channel vector's lazy-BN
+// tables in registers and visits pixels p0, p0 + P, ..., U pixels' loads issued back to back.
+// The per-element arithmetic and the keep decision (a hash of the NCHW index) are unchanged.
 template <typename T>
-__global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr) {
+__global__ __launch_bounds__(256) void dropout_kernel(DropArgs a, uint32_t thr, unsigned P) {
   constexpr int V = VecW<T>::V;
+  constexpr int U = 4;
   const unsigned CV = (unsigned)(a.C / V), HW = (unsigned)(a.H * a.W);
   const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned total = (unsigned)a.N * HW * CV;
-  if (t >= total) return;
-  const unsigned pix = t / CV, cv = t - pix * CV;
-  const unsigned n = pix / HW, hw = pix - n * HW;
+  if (t >= P * CV) return;
+  const unsigned p0 = t / CV, cv = t - p0 * CV;
+  const long long npix = (long long)a.N * HW;
   const uint64_t seed = (a.seed_ptr ? *a.seed_ptr : a.seed) + a.seed_add;
-  float v[V];
-  ldv((const T*)a.x + (size_t)pix * a.ldx + cv * V, v);
-  if (a.x_scale) {  // lazy BN+ReLU of the producer's z (the activation itself is never stored)
-#pragma unroll
-    for (int j = 0; j < V; ++j)
-      v[j] = round_as<T>(fmaxf(fmaf(v[j], a.x_scale[cv * V + j], a.x_shift[cv * V + j]), 0.f));
-  }
-  const float s = 1.f / (1.f - a.p);
+  const bool lazy = a.x_scale != nullptr;
+  float xs[V], xh[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
-    const uint64_t nchw = ((uint64_t)n * a.C + cv * V + j) * HW + hw;
-    v[j] = dropout_keep(seed, nchw, thr) ? v[j] * s : 0.f;
+    xs[j] = lazy ? a.x_scale[cv * V + j] : 1.f;
+    xh[j] = lazy ? a.x_shift[cv * V + j] : 0.f;
   }
-  stv((T*)a.y + (size_t)pix * a.ldy + cv * V, v);
+  const float s = 1.f / (1.f - a.p);
+  for (long long q0 = p0; q0 < npix; q0 += (long long)U * P) {
+    float v[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long q = q0 + (long long)u * P;
+      const size_t pix = (size_t)(q < npix ? q : q0);
+      ldv((const T*)a.x + pix * a.ldx + cv * V, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long q = q0 + (long long)u * P;
+      if (q >= npix) break;
+      const unsigned pix = (unsigned)q;
+      const unsigned n = pix / HW, hw = pix - n * HW;
+      if (lazy) {  // lazy BN+ReLU of the producer's z (the activation itself is never stored)
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[u][j] = round_as<T>(fmaxf(fmaf(v[u][j], xs[j], xh[j]), 0.f));
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const uint64_t nchw = ((uint64_t)n * a.C + cv * V + j) * HW + hw;
+        v[u][j] = dropout_keep(seed, nchw, thr) ? v[u][j] * s : 0.f;
+      }
+      stv((T*)a.y + (size_t)pix * a.ldy + cv * V, v[u]);
+    }
+  }
 }
 
 int dropout(const DropArgs& a, int dtype, hipStream_t st) {
@@ -483,11 +505,12 @@ int dropout(const DropArgs& a, int dtype, hipStream_t st) {
     set_error("dropout: C=%d ldx=%d ldy=%d", a.C, a.ldx, a.ldy);
     return E_UNSUPPORTED;
   }
-  unsigned grid = (unsigned)((total + 255) / 256);
+  const unsigned P = chan_sweep((long long)a.N * a.H * a.W, a.C / V);
+  const unsigned grid = (unsigned)(((long long)P * (a.C / V) + 255) / 256);
   uint32_t thr = dropout_threshold(a.p);
-  if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr);
-  else if (dtype == DT_F16) dropout_kernel<f16><<<grid, 256, 0, st>>>(a, thr);
-  else dropout_kernel<bf16><<<grid, 256, 0, st>>>(a, thr);
+  if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr, P);
+  else if (dtype == DT_F16) dropout_kernel<f16><<<grid, 256, 0, st>>>(a, thr, P);
+  else dropout_kernel<bf16><<<grid, 256, 0, st>>>(a, thr, P);
   return check_launch("dropout");
 }
 
