@@ -583,6 +583,10 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
 static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool bs, hipStream_t st);
 
 int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
+  if (a.drop_hw && !gemm_stream_ok(a, dtype)) {
+    set_error("gemm_nt: an output dropout needs the streaming kernel (M=%d N=%d K=%d)", a.M, a.N, a.K);
+    return E_UNSUPPORTED;
+  }
   const int V = dtype == DT_F32 ? 4 : 8;
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) {
     set_error("gemm_nt: empty problem M=%d N=%d K=%d", a.M, a.N, a.K);

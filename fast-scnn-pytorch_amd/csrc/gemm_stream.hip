@@ -354,6 +354,12 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 
   T* Cp = (T*)a.C;
   const T* Rp = (const T*)a.R;
+  // output dropout: compiled into the one-k-step dgrad-with-partials forms only (the classifier
+  // conv's dgrad, K = classes <= 32); elsewhere its registers would spill the BS kernels
+  constexpr bool DROP_OK = BS && KS == 1;
+  const bool drop = DROP_OK && a.drop_hw != 0;
+  const uint64_t dseed = drop ? (a.drop_seed_ptr ? *a.drop_seed_ptr : a.drop_seed) + a.drop_seed_add : 0;
+  const float dscale = 1.f / (1.f - a.drop_p);
   for (; c < nchunks; c += wstride) {
     f32x4 acc[2][NT];
 #pragma unroll
@@ -449,6 +455,15 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
             }
             if (Rp) v += rv[nt][r];
             o[r] = a.relu ? fmaxf(v, 0.f) : v;
+          }
+          if (DROP_OK && drop) {  // the dropout kernel's law on the stored value (misc.hip dropout_kernel)
+            const unsigned HW = (unsigned)a.drop_hw;
+            const unsigned pn = (unsigned)mr / HW, hw = (unsigned)mr - pn * HW;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint64_t nchw = ((uint64_t)pn * a.N + (unsigned)(n0 + nl + r)) * HW + hw;
+              o[r] = dropout_keep(dseed, nchw, a.drop_thr) ? round_as<T>(o[r]) * dscale : 0.f;
+            }
           }
           if (mok) st4v(Cp + mr * a.ldc + n0 + nl, o);
           if constexpr (BS) {  // partials of the value as stored, masked by that BN's ReLU
@@ -765,6 +780,7 @@ bool gemm_stream_ok(const GemmArgs& a, int dtype) {
   if (a.bpart && dtype == DT_F32 && nt == 4 && ks > 2) return false;  // would spill
   if (gs_tail_needed(a, nt) && (nt != 2 || sums)) return false;  // scalar tail: N <= 32 only
   if (a.bpart && (!a.bz || a.ldbz % 4 || (a.bmode != 0 && a.bmode != 2))) return false;
+  if (a.drop_hw && (!a.bpart || ks != 1 || gs_tail_needed(a, nt) || a.M % a.drop_hw)) return false;
   // two resident workgroups per CU (160 KB LDS, 1 KB reserved each)
   if (gs_lds(a, nt, ks, KC) > (deep ? 80 * 1024 - 1024 : 72 * 1024)) return false;
   // in-kernel BN finish: group counters [0, 64), then each group's team counters

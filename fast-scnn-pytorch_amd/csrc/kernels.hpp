@@ -156,6 +156,16 @@ struct GemmArgs {
   const float* a_shift = nullptr;
   BnTail tail{};        // in-kernel finish of the BN whose records this GEMM writes
   int tail_ink = 0;     // (set by the launcher) the tiled kernel runs the finish itself (tail_finish)
+  // Dropout of the OUTPUT (train backward of the classifier's Dropout, models/fast_scnn.py:235:
+  // the dgrad stores keep ? round(out) / (1 - drop_p) : 0, the dropout kernel's law, so its BN
+  // partials (bpart) are those of the dropped gradient).  The mask hashes the NCHW index of
+  // output element (m = n * drop_hw + hw, channel c); drop_hw 0: none.  Streaming kernel only.
+  int drop_hw = 0;
+  uint32_t drop_thr = 0;
+  float drop_p = 0.f;
+  uint64_t drop_seed = 0;                    // seed (+ drop_seed_add) or the device slot below
+  const uint64_t* drop_seed_ptr = nullptr;
+  uint64_t drop_seed_add = 0;
   unsigned long long* stamps = nullptr;  // (set by the launcher from g_stamps) phase stamps
 };
 

@@ -616,6 +616,17 @@ bool ltd_fused_enabled() {
   return on;
 }
 
+// FSCNN_DROP_FUSED=0: the classifier's Dropout backward as its own launch and dsconv2 pw's
+// BN-backward reduce as its own pass, instead of both in the classifier conv's dgrad epilogue
+// (A/B; tests/test_gpu_switches.py)
+bool drop_dgrad_on() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_DROP_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // fused BN-backward partials: the dgrad GEMM producing the dy of unit `u` emits its records
 struct BTarget {
   const Unit* u = nullptr;
@@ -1361,8 +1372,25 @@ struct Exec {
     return tb;
   }
   // pw conv backward given dz [M][cout]: wgrad into G, dgrad into dX (ld lddx) (+R)
+  GemmArgs pw_dgrad_args(const ConvL& c, long long M, Dz dz, void* dX, int lddx, const void* R,
+                         int ldr, BTarget bt, const DropArgs* dro) {
+    GemmArgs g{};
+    g.M = (int)M; g.N = c.cin * c.k * c.k; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
+    g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
+    g.R = R; g.ldr = ldr;
+    g.C = dX; g.ldc = lddx;
+    if (bt.u && train) set_btarget(g, bt);
+    if (dro) {
+      g.drop_hw = dro->H * dro->W; g.drop_thr = dropout_threshold(dro->p); g.drop_p = dro->p;
+      g.drop_seed = dro->seed; g.drop_seed_ptr = dro->seed_ptr; g.drop_seed_add = dro->seed_add;
+    }
+    return g;
+  }
+  // dro: a Dropout between this conv's input and the BN that bt names (the classifier): the
+  // dgrad applies its mask to dX (GemmArgs::drop_hw), so the BN partials are the dropped ones
   int pw_bwd(const ConvL& c, long long M, Dz dz, In X, void* dX, int lddx,
-             const void* R = nullptr, int ldr = 0, BTarget bt = BTarget()) {
+             const void* R = nullptr, int ldr = 0, BTarget bt = BTarget(),
+             const DropArgs* dro = nullptr) {
     const int K = c.cin * c.k * c.k;
     GemmTnArgs t{};
     t.M = (int)M; t.N = c.cout; t.K = K; t.D = dz.p; t.ldd = dz.ld; t.X = X.p; t.ldx = X.ld;
@@ -1389,12 +1417,7 @@ struct Exec {
     }
     TRY(flush_side());
     if (!dX) return OK;
-    GemmArgs g{};
-    g.M = (int)M; g.N = K; g.K = c.cout; g.A = dz.p; g.lda = dz.ld;
-    g.B = WT(c); g.ldb = c.ldt; g.b_trans = 0;
-    g.R = R; g.ldr = ldr;
-    g.C = dX; g.ldc = lddx;
-    if (bt.u && train) set_btarget(g, bt);
+    const GemmArgs g = pw_dgrad_args(c, M, dz, dX, lddx, R, ldr, bt, dro);
     TRY(gemm_nt(g, dt, r.st));
     if (bt.u && train) bt.u->bdone.set();
     return OK;
@@ -1480,10 +1503,26 @@ struct Exec {
     }
     // classifier 1x1 (+bias), dropout
     const bool drop = r.dropout_p > 0.f;
-    TRY(pw_bwd(net.cls_out, pl.c2pw.M, plain(Bw(pl.g_logits), pl.Cp),
-               raw(drop ? W(pl.drop) : W(pl.c2pw.a), 128), drop ? Bw(pl.g_drop) : Bw(pl.c2pw.ga),
-               128));
-    if (drop) {
+    // train: the dgrad applies the dropout mask itself and folds dsconv2 pw's BN-backward reduce
+    // (one 128-channel write + read and the dropout and reduce launches fewer)
+    // (the streaming kernel only: not for the small test shapes, M < 4096)
+    DropArgs dd{};
+    dd.N = N; dd.H = pl.H3; dd.W = pl.W3; dd.C = 128; dd.seed = r.seed; dd.p = r.dropout_p;
+    dd.seed_ptr = seed_ptr();
+    const BTarget dbt = relu_target(pl.c2pw, net.cls2.bpw);
+    const bool dfuse = drop && train && drop_dgrad_on() &&
+                       gemm_stream_ok(pw_dgrad_args(net.cls_out, pl.c2pw.M, plain(Bw(pl.g_logits), pl.Cp),
+                                                    Bw(pl.c2pw.ga), 128, nullptr, 0, dbt, &dd),
+                                      dt);
+    if (dfuse) {
+      TRY(pw_bwd(net.cls_out, pl.c2pw.M, plain(Bw(pl.g_logits), pl.Cp), raw(W(pl.drop), 128),
+                 Bw(pl.c2pw.ga), 128, nullptr, 0, dbt, &dd));
+    } else {
+      TRY(pw_bwd(net.cls_out, pl.c2pw.M, plain(Bw(pl.g_logits), pl.Cp),
+                 raw(drop ? W(pl.drop) : W(pl.c2pw.a), 128), drop ? Bw(pl.g_drop) : Bw(pl.c2pw.ga),
+                 128));
+    }
+    if (drop && !dfuse) {
       DropArgs d{};
       d.N = N; d.H = pl.H3; d.W = pl.W3; d.C = 128; d.x = Bw(pl.g_drop); d.ldx = 128;
       d.y = Bw(pl.c2pw.ga); d.ldy = 128; d.seed = r.seed; d.p = r.dropout_p;

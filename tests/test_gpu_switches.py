@@ -19,7 +19,9 @@ fresh child process:
   beside bottleneck1 instead of beside bottleneck2/3;
 * ``FSCNN_GEMM_MINT=256`` — the tiled GEMM's round-3 minimum grid (NT >= 3 on low-M launches);
 * ``FSCNN_SIDE_PRIO=0``   — the weight-gradient side stream as a plain stream instead of one at
-  the device's lowest priority.
+  the device's lowest priority;
+* ``FSCNN_DROP_FUSED=0``  — the classifier's Dropout backward and dsconv2 pw's BN-backward reduce
+  as their own passes instead of in the classifier conv's dgrad epilogue.
 
 Each child re-runs the oracle / golden parity tests that cover the path (fp32 train golden +
 bf16 emulated budget; eval goldens for the fp32 GEMM switch).  The graph switch also replays
@@ -51,7 +53,7 @@ CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL, "FSCNN_GRAPHS=
          "FSCNN_GEMM_PF=3": TRAIN[-1:], "FSCNN_CE_HEAD=1": HEAD16,
          "FSCNN_CE_PACK=0": HEAD16, "FSCNN_CE_PACK=1": HEAD16,
          "FSCNN_GEMM_MINT=256": TRAIN[-1:] + ["tests/test_gpu_kernels.py"],
-         "FSCNN_SIDE_PRIO=0": TRAIN[:1]}
+         "FSCNN_SIDE_PRIO=0": TRAIN[:1], "FSCNN_DROP_FUSED=0": TRAIN}
 
 
 def _env(switch):
