@@ -351,10 +351,11 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32
 }
 // Channel-owning sweeps (bn_bwd_apply, dropout): each thread keeps ONE channel vector's tables
 // in registers and visits pixels p0, p0 + P, ...; P = pixels per grid sweep.  Up to 8 pixels per
-// thread amortise the tables, while the grid keeps >= 2048 workgroups (8 per CU) when the tensor
-// has that much work.
+// thread amortise the tables, while the grid keeps >= 1024 workgroups (4 per CU) when the tensor
+// has that much work (measured r04, cfg3 step: 1024 -> 5.786 ms, 2048 -> 5.804, 4096 -> 5.835;
+// a cap of 16 pixels per thread: no change).
 inline unsigned chan_sweep(long long M, int CV) {
-  long long ppt = M * CV / (2048LL * 256);
+  long long ppt = M * CV / (1024LL * 256);
   ppt = ppt < 1 ? 1 : (ppt > 8 ? 8 : ppt);
   return (unsigned)((M + ppt - 1) / ppt);
 }
