@@ -375,6 +375,29 @@ def main():
         per_rank_ms = [round(1e3 * float(v.item()) / args.steps, 3) for v in allt]
         elapsed = max(float(v.item()) for v in allt)
 
+    # per-step distribution (BASELINE.md §2 asks for a median over >= 20 iterations): K more
+    # steps AFTER the timed region, each bracketed by events on the caller's stream (one event per
+    # step boundary; it idles the stream ~7 us, so these steps are not the ones `value` times)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(max(20, args.steps) + 1)]
+    evs[0].record()
+    for i in range(1, len(evs)):
+        step()
+        evs[i].record()
+    torch.cuda.synchronize()
+    step_ms = sorted(evs[i - 1].elapsed_time(evs[i]) for i in range(1, len(evs)))
+    median_ms = step_ms[len(step_ms) // 2]
+    # pointwise (1x1 conv) MFMA utilisation, one profiled step per family (untimed): the
+    # forward / dgrad GEMMs (gemm_nt) and the weight gradients (gemm_tn), dense bf16 peak
+    mfma_util = {}
+    for pk, pname in ((5, "gemm_nt"), (6, "gemm_tn")):
+        pms, pn, pb, pf = prof(lib, pk, step, 4096)
+        if pms > 0:
+            tfs = pf / (pms * 1e-3) / 1e12
+            mfma_util[pname] = {"launches": pn, "ms": round(pms, 4), "tflops": round(tfs, 2),
+                                "peak_tflops": MFMA_PEAK_TFS[args.dtype],
+                                "frac": round(tfs / MFMA_PEAK_TFS[args.dtype], 4)}
+    barrier()
+
     value = world * B * args.steps / elapsed
     avg_ms = ms.value / max(1, n.value)
     bytes_per_launch = b.value / max(1, n.value)
@@ -425,6 +448,12 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "step_ms_distribution": {"median": round(median_ms, 3), "min": round(step_ms[0], 3),
+                                 "max": round(step_ms[-1], 3), "n": len(step_ms),
+                                 "timing": "HIP events per step boundary on the caller's stream, "
+                                           "%d steps after the timed region (rank 0)" % len(step_ms)},
+        "mfma_utilisation": dict(mfma_util, note="1x1-conv GEMM families, HIP-event time over one "
+                                 "profiled step each; algorithmic flops 2*M*N*K per launch"),
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (portable counter-based generator; random-init weights, default law)",
         "config": {"workload": ("cfg3 train step: fwd + CE(ignore -1) + bwd + fused SGD" + (" (unfused CE)" if args.unfused_loss else " (fused low-res upsample+CE head)")),

@@ -60,6 +60,8 @@ SIGNATURES = {
                                    c_ull, c_float, c_float, c_vp]),
     "fscnn_backward_loss": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_ull,
                                     c_float, c_int, c_int, c_vp]),
+    "fscnn_backward_dx": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
+                                  c_vp, c_vp, c_vp, c_ull, c_float, c_int, c_int, c_vp]),
     "fscnn_prof_begin": (c_int, [c_int, c_int]),
     "fscnn_prof_end": (c_int, [ctypes.POINTER(ctypes.c_double), P_ll, ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_double)]),

@@ -22,6 +22,10 @@ __global__ void bn_fold_kernel(FoldTable t) {
     float b = e.bias ? e.bias[c] : 0.f;
     e.scale[c] = s;
     e.shift[c] = e.beta[c] + (b - e.rmean[c]) * s;
+    if (e.mean) {
+      e.mean[c] = e.rmean[c];
+      e.invstd[c] = 1.f / sqrtf(e.rvar[c] + BN_EPS);
+    }
   }
 }
 

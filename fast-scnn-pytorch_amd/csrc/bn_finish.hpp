@@ -35,12 +35,16 @@ __device__ __forceinline__ void bn_fwd_finish(const BnFinalizeArgs& a, int c, do
 // backward: s1 = sum dy_r, s2 = sum dy_r * xhat of channel c (C channels) -> dbeta, dgamma, the
 // apply coefficients and (t.tab) the BN-backward operand table
 // dz = scale*(dy_r - c0 - (z - mean)*invstd*c1) = al*dy_r + gz*z + be
+// count == BN_FROZEN_COUNT: a BN normalised with its running statistics (eval-mode autograd,
+// models/fast_scnn.py in .eval() with grad enabled): mean and invstd are constants, so the batch
+// terms vanish (c0 = c1 = 0) and dz = scale * dy_r; dgamma / dbeta keep their sums
 __device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2, double count,
                                               float* dgamma, float* dbeta, float* coef,
                                               const BnBwdTab& t) {
   if (dbeta) dbeta[c] = (float)s1;
   if (dgamma) dgamma[c] = (float)s2;
-  const float c0 = (float)(s1 / count), c1 = (float)(s2 / count);
+  const bool frozen = count == BN_FROZEN_COUNT;
+  const float c0 = frozen ? 0.f : (float)(s1 / count), c1 = frozen ? 0.f : (float)(s2 / count);
   coef[c] = c0;
   coef[C + c] = c1;
   if (t.tab) {

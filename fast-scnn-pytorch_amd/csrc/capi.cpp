@@ -486,6 +486,24 @@ int fscnn_backward_loss(const fscnn_plan* plan, const float* grad_loss, const fl
   GUARD(net_backward(plan->plan, r, stage_from, stage_to));
 }
 
+int fscnn_backward_dx(const fscnn_plan* plan, const void* dout, const void* daux,
+                      const float* grad_loss, const float* loss2, const void* x, int x_dtype,
+                      void* dx, int dx_dtype, const float* params, float* grads, void* ws,
+                      void* bws, unsigned long long seed, float dropout_p, int stage_from,
+                      int stage_to, void* stream) {
+  if (!plan || !x || !params || !grads || !ws || !bws || (!dout && !grad_loss) ||
+      (dout && grad_loss) || (grad_loss && !loss2)) {
+    set_error("fscnn_backward_dx: null argument (exactly one of dout / grad_loss + loss2)");
+    return E_INVALID;
+  }
+  RunArgs r{};
+  r.dout = dout; r.daux = daux; r.gloss = grad_loss; r.loss2 = const_cast<float*>(loss2);
+  r.x = x; r.x_dtype = x_dtype; r.dx = dx; r.dx_dtype = dx_dtype;
+  r.P = params; r.G = grads; r.ws = ws; r.bws = bws;
+  r.seed = seed; r.dropout_p = dropout_p; r.st = S(stream);
+  GUARD(net_backward(plan->plan, r, stage_from, stage_to));
+}
+
 long long fscnn_ce_parts(int N, long long HW) { return ce_parts(N, HW); }
 
 int fscnn_ce_fwd(const void* logits, int dtype, const long long* target, int N, int C,

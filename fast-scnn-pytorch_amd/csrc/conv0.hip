@@ -600,6 +600,82 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
   return check_launch("conv0_wgrad");
 }
 
+// ---- conv0 input gradient (x.grad; autograd of the image through models/fast_scnn.py:153) --------
+// dx[n][ci][h][w] = sum over the output pixels (oh, ow) whose 3x3 stride-2 window (padding 0)
+// covers (h, w) -- at most 2 x 2 of them, kh = h - 2oh in {0, 1, 2} -- and the 32 channels of
+// dz[n][oh][ow][co] * w[co][ci][kh][kw].  A gather with one thread per image pixel (no atomics,
+// deterministic); neighbouring threads share their dz vectors through the cache.  HBM-bound:
+// e * 32 * N*Ho*Wo read + dx_e * 3 * N*H*W written.  Runs only when the caller asks for x.grad.
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void conv0_dgrad_kernel(Conv0DgradArgs a) {
+  constexpr int V = VecW<T>::V;
+  __shared__ float sw[9][3][32];  // [kh * 3 + kw][ci][co]
+  for (int i = threadIdx.x; i < 864; i += 256) {
+    const int co = i / 27, r = i - co * 27, ci = r / 9, k = r - ci * 9;
+    sw[k][ci][co] = a.w[i];
+  }
+  __syncthreads();
+  const long long HW = (long long)a.H * a.W;
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long long)a.N * HW) return;
+  const int n = (int)(p / HW);
+  const long long hw = p - (long long)n * HW;
+  const int h = (int)(hw / a.W), w = (int)(hw - (long long)h * a.W);
+  float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) {
+    const int kh = (h & 1) + 2 * dh;
+    const int oh = (h - kh) >> 1;
+    if (kh > 2 || oh < 0 || oh >= a.Ho) continue;
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int kw = (w & 1) + 2 * dw;
+      const int ow = (w - kw) >> 1;
+      if (kw > 2 || ow < 0 || ow >= a.Wo) continue;
+      const T* d = (const T*)a.dz + (((size_t)n * a.Ho + oh) * a.Wo + ow) * 32;
+      const int k = kh * 3 + kw;
+#pragma unroll
+      for (int q = 0; q < 32 / V; ++q) {
+        float v[V];
+        unpack<T>(*reinterpret_cast<const uint4*>(d + q * V), v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int co = q * V + j;
+          acc[0] = fmaf(v[j], sw[k][0][co], acc[0]);
+          acc[1] = fmaf(v[j], sw[k][1][co], acc[1]);
+          acc[2] = fmaf(v[j], sw[k][2][co], acc[2]);
+        }
+      }
+    }
+  }
+  TO* dx = (TO*)a.dx + (size_t)n * 3 * HW + hw;
+#pragma unroll
+  for (int ci = 0; ci < 3; ++ci) st1(dx + ci * HW, acc[ci]);
+}
+
+int conv0_dgrad(const Conv0DgradArgs& a, int dz_dtype, hipStream_t st) {
+  if (!a.dz || !a.w || !a.dx || a.N < 1 || a.Ho != (a.H - 3) / 2 + 1 || a.Wo != (a.W - 3) / 2 + 1) {
+    set_error("conv0_dgrad: bad arguments (N %d, %dx%d -> %dx%d)", a.N, a.H, a.W, a.Ho, a.Wo);
+    return E_INVALID;
+  }
+  if ((uintptr_t)a.dz % 16) {
+    set_error("conv0_dgrad: dz must be 16-B aligned");
+    return E_INVALID;
+  }
+  const int blocks = cdiv((long long)a.N * a.H * a.W, 256);
+#define C0D_LAUNCH(T)                                                                          \
+  do {                                                                                         \
+    if (a.dx_dtype == DT_BF16) conv0_dgrad_kernel<T, bf16><<<blocks, 256, 0, st>>>(a);         \
+    else if (a.dx_dtype == DT_F16) conv0_dgrad_kernel<T, f16><<<blocks, 256, 0, st>>>(a);      \
+    else conv0_dgrad_kernel<T, float><<<blocks, 256, 0, st>>>(a);                              \
+  } while (0)
+  if (dz_dtype == DT_F32) C0D_LAUNCH(float);
+  else if (dz_dtype == DT_F16) C0D_LAUNCH(f16);
+  else C0D_LAUNCH(bf16);
+#undef C0D_LAUNCH
+  return check_launch("conv0_dgrad");
+}
+
 // ---- fused: LearningToDownsample.dsconv1.dw input gradient + conv0 weight gradient --------------
 // The stride-2 depthwise dgrad (dwconv.hip dw_dgrad_s2, same thread tile and arithmetic: a thread
 // owns dx rows h0, h0+1 x columns w0..w0+3 of 4 channels) produces g, the gradient of conv0's BN

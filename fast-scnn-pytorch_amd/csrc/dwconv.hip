@@ -135,77 +135,6 @@ __device__ __forceinline__ void dw_stage(uint4* s_in, const T* x, int H, int W, 
   }
 }
 
-// per-thread staging table of the forward kernel's tile loop, computed once: for load k the
-// element offset of its vector within the tile (relative to the tile origin) and its (row, col)
-// in the haloed tile packed as row << 16 | col (0xFFFF0000: beyond the tile); the tile loop then
-// only adds a uniform base per tile (recomputing the per-load divisions each tile, or keeping
-// them live as 64-bit offsets, held ~40 VGPRs beside the prefetched tile)
-template <typename T, int S, int L>
-struct DwLanes {
-  int off[L];
-  int rc[L];
-  __device__ __forceinline__ void init(int W, int C, int cbv, int tid, int nthr) {
-    using G = DwTile<T, S>;
-    constexpr int V = VecW<T>::V;
-#pragma unroll
-    for (int k = 0; k < L; ++k) {
-      const int i = tid + k * nthr;
-      const int pix = i / cbv, lv = i - pix * cbv;
-      const int r = pix / G::IC, col = pix - r * G::IC;
-      const bool in = pix < G::IR * G::IC;
-      off[k] = in ? (r * W + col) * C + lv * V : 0;
-      rc[k] = in ? (r << 16) | col : (int)0xFFFF0000;
-    }
-  }
-  // in-image test of load k for a tile whose haloed origin is (hi0, wi0)
-  __device__ __forceinline__ bool ok(int k, int H, int W, int hi0, int wi0) const {
-    const int r = rc[k] >> 16, col = rc[k] & 0xFFFF;
-    return r >= 0 && (unsigned)(hi0 + r) < (unsigned)H && (unsigned)(wi0 + col) < (unsigned)W;
-  }
-};
-
-template <typename T, int S, int L>
-__device__ __forceinline__ void dw_load_t(uint4 (&raw)[L], const DwLanes<T, S, L>& ln, const T* x,
-                                          int H, int W, int C, int n, int hi0, int wi0,
-                                          int cvbase) {
-  constexpr int V = VecW<T>::V;
-  // uniform tile origin (may lie before the image: only in-image loads use it)
-  const long long base = (((long long)n * H + hi0) * W + wi0) * C + (long long)cvbase * V;
-#pragma unroll
-  for (int k = 0; k < L; ++k) {
-    const bool ok = ln.ok(k, H, W, hi0, wi0);
-    raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(x + (ok ? base + ln.off[k] : 0)));
-  }
-}
-template <typename T, int S, bool IT, int L>
-__device__ __forceinline__ void dw_put_t(uint4* s_in, const uint4 (&raw)[L],
-                                         const DwLanes<T, S, L>& ln, int H, int W, int hi0,
-                                         int wi0, int cbv, int tid, int nthr, const float* sc,
-                                         const float* sh) {
-  using G = DwTile<T, S>;
-#pragma unroll
-  for (int k = 0; k < L; ++k) {
-    const int i = tid + k * nthr;
-    if (i < G::IR * G::IC * cbv) {
-      uint4 v = raw[k];
-      if constexpr (IT) v = sel4(ln.ok(k, H, W, hi0, wi0), bnrelu_vec<T>(v, sc, sh));
-      s_in[i] = v;
-    }
-  }
-}
-
-// workgroup -> (channel chunk cx, worker j of gridDim.y): XCD-contiguous (speed only): blocks
-// L = x (mod 8) share an XCD, so residue class x gets a contiguous range of workers, whose tile
-// ranges are neighbours (shared halo rows served by that XCD's L2)
-__device__ __forceinline__ void dw_worker(int& cx, int& j) {
-  const int gx = gridDim.x;
-  const long long T = (long long)gx * gridDim.y;
-  long long L = blockIdx.x + (long long)gx * blockIdx.y;
-  if ((T & 7) == 0) L = (L & 7) * (T >> 3) + (L >> 3);
-  cx = (int)(L % gx);
-  j = (int)(L / gx);
-}
-
 // ---- forward (and stride-1 dgrad with FLIP) -------------------------------------------------
 // TL: the launch finishes its BN in the last workgroups (a.tail_ink; a separate instantiation so
 // the other launches keep their register budget)
@@ -413,46 +342,60 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   stamp(a.stamps, 4);
 }
 
-// dynamic LDS of the tile kernels: the haloed input tile of cbv vectors + 4 floats per thread
-template <typename T, int S>
-static size_t dw_shm(int cbv) {
-  using G = DwTile<T, S>;
-  return (size_t)G::IR * G::IC * cbv * 16 + (size_t)cbv * 32 * 16;
+// ---- forward: persistent tile loop, haloed tiles staged by LDS-DMA (double-buffered) ---------
+// A workgroup (worker wj of its channel chunk) walks a contiguous range of spatial tiles in
+// row-band order.  Each tile's haloed input is copied HBM -> LDS by global_load_lds_dwordx4 (no
+// VGPR destination: the staging costs no registers, unlike a register prefetch ring, which at
+// ~240 VGPRs held the round-4 tile loop to 2 workgroups per CU and lost to the one-tile kernel),
+// into the other of two LDS buffers while the current tile computes:
+//     issue DMA(t0) ; for t: [wait own DMA(t)] [IT: BN+ReLU own slots] barrier
+//                            issue DMA(t+1) into the other buffer ; compute + store tile t
+// so a CU keeps its resident workgroups' next tiles in flight for their whole life (one barrier
+// per tile).  The DMA image is lane-linear: slot k*nthr + tid is thread tid's k-th 16-B vector,
+// exactly the one-tile kernel's staging order; out-of-image and tail slots read a 16-B zero.
+// The copies are inline asm (M0 = the wave's LDS base), outside hipcc's waitcnt bookkeeping, so
+// the compiler neither drains them before the compute's LDS reads nor at the barrier; this kernel
+// waits for them itself (vmcnt(0) at the top of the next tile: they and the previous tile's
+// output stores are all that is outstanding).
+// IT (train, the input is a lazy BatchNorm+ReLU): after its own DMAs land, each thread applies
+// relu(fmaf(z, sc, sh)) (bn_apply's arithmetic, rounded to T) to its own slots in place --
+// its channel vector is fixed (slot % cbv == tid % cbv), so the 2V table values stay in registers;
+// padding stays zero.
+// Statistics (a.part) / the in-kernel BN finish (TL): per-thread sums shifted by the thread's
+// first output value, merged in fixed order into ONE record per worker (records [wy][3][C]).
+// workgroup -> (channel chunk cx, worker j of gridDim.y): XCD-contiguous (speed only): blocks
+// L = x (mod 8) share an XCD, so residue class x gets a contiguous range of workers, whose tile
+// ranges are neighbours (shared halo rows served by that XCD's L2)
+__device__ __forceinline__ void dw_worker(int& cx, int& j) {
+  const int gx = gridDim.x;
+  const long long T = (long long)gx * gridDim.y;
+  long long L = blockIdx.x + (long long)gx * blockIdx.y;
+  if ((T & 7) == 0) L = (L & 7) * (T >> 3) + (L >> 3);
+  cx = (int)(L % gx);
+  j = (int)(L / gx);
 }
 
-// ---- forward, 16-bit stride 1: streaming tile loop ------------------------------------------
-// Streaming tile loop: the grid holds every workgroup resident (dw_grid: gridDim.y workers per
-// channel chunk) and worker j walks the contiguous spatial tiles [T*j/wy, T*(j+1)/wy) of its
-// chunk in row-band order; the next tile's loads are in flight (registers) while the current
-// tile computes from LDS.  (Round 3's one-tile-per-workgroup grid ran 2-6 dispatch rounds of
-// load -> compute -> store, with the CU's memory pipe idle during each compute phase.)
-// Train statistics / BN-backward partials are accumulated over the worker's tiles: ONE record
-// per worker (records [wy][3|2][C]); forward statistics as per-thread sums shifted by the
-// worker's first output value of each channel (gemm_stream's convention), merged in fixed order.
-// TL: the launch finishes its BN in the last workgroups (a.tail_ink; a separate instantiation so
-// the other launches keep their register budget)
-template <typename T, int S, bool FLIP, bool IT, bool BR = false, bool TL = false>
-__global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) {
+__device__ const uint4 g_dw_zero = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_dst)
+      : "memory");
+}
+
+template <typename T, int S, bool IT, bool TL = false>
+__global__ __launch_bounds__(256, 3) void dw_fwd_dma_kernel(DwArgs a, int cbv) {
   using G = DwTile<T, S>;
   constexpr int V = VecW<T>::V;
-  // LDS sized per launch (dw_shm): the staged tile of cbv channel vectors + the reduction rows
+  constexpr int LPT = G::LPT;                    // 16-B slots per thread and tile (= IR*IC/32)
   extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
-  uint4* s_in = s_dyn;
-  float* s_red = reinterpret_cast<float*>(s_dyn + G::IR * G::IC * cbv);
-  // per-channel tables of the chunk (cbv * V channels each): read where used, so the loop
-  // carries only the weights, the prefetched tile and the sums (prefetch + tables in registers
-  // passed 256 VGPRs)
-  float* s_tab = s_red + 3 * cbv * 32 * 4;
-  float* t_isc = s_tab;                 // lazy input BN (IT)
-  float* t_ish = t_isc + cbv * 8;
-  float* t_sc = t_ish + cbv * 8;        // epilogue affine (eval fold) or 1 / 0
-  float* t_sh = t_sc + cbv * 8;
-  float* t_bm = t_sh + cbv * 8;         // BN-backward partials (BR): mean, invstd, mask affine
-  float* t_bi = t_bm + cbv * 8;
-  float* t_bs = t_bi + cbv * 8;
-  float* t_bh = t_bs + cbv * 8;
   const int tid = threadIdx.x, nthr = blockDim.x;
-  const int QB = cbv * G::QPV;                 // quads per workgroup
+  const int wave = tid >> 6;
+  const int QB = cbv * G::QPV;                   // quads per workgroup
   const int q = tid % QB, grp = tid / QB;
   const int gx = grp % G::GX, gy = grp / G::GX;
   int cx, wj;
@@ -461,78 +404,87 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) 
   const int tiles_w = cdiv(a.Wo, G::TW), tiles_h = cdiv(a.Ho, G::TH);
   const int ntiles = a.N * tiles_h * tiles_w;
   const int t0 = (int)((long long)ntiles * wj / wy), t1 = (int)((long long)ntiles * (wj + 1) / wy);
-  const int cvb = cx * cbv;                       // first channel vector of the chunk
-  const int c0 = cvb * V + q * 4;                 // first channel of the thread's quad
+  const int cvb = cx * cbv;                      // first channel vector of the chunk
+  const int c0 = cvb * V + q * 4;                // first channel of the thread's quad
+  const int lv = tid % cbv, p0 = tid / cbv;      // the thread's DMA slots: pixel k*32 + p0
+  const T* xin = (const T*)a.x + (size_t)(cvb + lv) * V;
+  const int bufv = LPT * nthr;                   // 16-B slots per buffer
+  const uint32_t lds0 = (uint32_t)(uintptr_t)s_dyn;
   auto tile_of = [&](int t, int& n, int& th0, int& tw0) {
     const int tw = t % tiles_w, r = t / tiles_w;
     n = r / tiles_h;
     th0 = (r - n * tiles_h) * G::TH;
     tw0 = tw * G::TW;
   };
-  stamp(a.stamps, 0);
-  // next-tile prefetch where the loads fit beside the loop's live set (16-bit stride 1: 6 vectors
-  // per thread); fp32 (12) and stride 2 (10) load each tile at the top of its iteration
-  constexpr bool PF = sizeof(T) == 2 && G::LPT <= 8;
-  DwLanes<T, S, G::LPT> ln;
-  ln.init(a.W, a.C, cbv, tid, nthr);
-  uint4 raw[G::LPT];
-  if (PF && t0 < t1) {
+  auto issue = [&](int t, int buf) {
     int n, th0, tw0;
-    tile_of(t0, n, th0, tw0);
-    dw_load_t<T, S, G::LPT>(raw, ln, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
-                            cvb);
-  }
-  const BnBwdPart& b = a.bs;
-  for (int i = tid; i < cbv * V; i += nthr) {
-    const int c = cvb * V + i;
-    if constexpr (IT) {
-      t_isc[i] = a.in_scale[c];
-      t_ish[i] = a.in_shift[c];
-    }
-    t_sc[i] = a.scale ? a.scale[c] : 1.f;
-    t_sh[i] = a.scale ? a.shift[c] : 0.f;
-    if constexpr (BR) {
-      const bool m2 = b.mode == 2;
-      t_bm[i] = b.mean[c];
-      t_bi[i] = b.invstd[c];
-      t_bs[i] = m2 ? b.scale[c] : 0.f;  // mode 0: mask fmaf(z, 0, 1) > 0 always
-      t_bh[i] = m2 ? b.shift[c] : 1.f;
-    }
-  }
-  float wt[9][4];
+    tile_of(t, n, th0, tw0);
+    const int hi0 = th0 * S - 1, wi0 = tw0 * S - 1;
+    const uint32_t base = lds0 + (uint32_t)(buf * bufv + wave * 64) * 16u;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+    for (int k = 0; k < LPT; ++k) {
+      const int pix = k * 32 + p0;
+      const int r = pix / G::IC, col = pix - r * G::IC;
+      const int hi = hi0 + r, wi = wi0 + col;
+      const bool ok = pix < G::IR * G::IC && (unsigned)hi < (unsigned)a.H &&
+                      (unsigned)wi < (unsigned)a.W;
+      const void* src = ok ? (const void*)(xin + (((size_t)n * a.H + hi) * a.W + wi) * a.C)
+                           : (const void*)&g_dw_zero;
+      glds16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(k * nthr) * 16u));
+    }
+  };
+  stamp(a.stamps, 0);
+  if (t0 < t1) issue(t0, 0);
+  // per-worker registers: the thread's 4 channels' taps and epilogue affine, its vector's lazy BN
+  float wt[9][4], sc[4], sh[4];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wt[FLIP ? 8 - t : t][j] = a.w[(size_t)(c0 + j) * 9 + t];
-  // BN-backward partials (BR) / shifted forward statistics (a.part): per-thread sums
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t][j] = a.w[(size_t)(c0 + j) * 9 + t];
+    sc[j] = a.scale ? a.scale[c0 + j] : 1.f;
+    sh[j] = a.scale ? a.shift[c0 + j] : 0.f;
+  }
+  float isc[IT ? V : 1], ish[IT ? V : 1];
+  if constexpr (IT) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      isc[j] = a.in_scale[(cvb + lv) * V + j];
+      ish[j] = a.in_shift[(cvb + lv) * V + j];
+    }
+  }
+  const bool stats = a.part != nullptr;
   float s1[4], s2[4], shf[4];
   float cnt = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) s1[j] = s2[j] = shf[j] = 0.f;
-  const int lq4 = q * 4;  // the thread's quad within the chunk's channel tables
-  __syncthreads();
-  const bool stats = !BR && a.part != nullptr;
-  const T* sl = reinterpret_cast<const T*>(s_in);
   const int pstride = cbv * V;                   // elements per staged pixel
   const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
 
 #pragma unroll 1
   for (int t = t0; t < t1; ++t) {
+    const int buf = (t - t0) & 1;
     int n, th0, tw0;
     tile_of(t, n, th0, tw0);
-    if constexpr (!PF)
-      dw_load_t<T, S, G::LPT>(raw, ln, (const T*)a.x, a.H, a.W, a.C, n, th0 * S - 1, tw0 * S - 1,
-                              cvb);
-    dw_put_t<T, S, IT, G::LPT>(s_in, raw, ln, a.H, a.W, th0 * S - 1, tw0 * S - 1, cbv, tid, nthr,
-                               t_isc + (tid % cbv) * V, t_ish + (tid % cbv) * V);
-    __syncthreads();
-    if (PF && t + 1 < t1) {  // the next tile's loads, in flight during this tile's compute
-      int n2, th2, tw2;
-      tile_of(t + 1, n2, th2, tw2);
-      dw_load_t<T, S, G::LPT>(raw, ln, (const T*)a.x, a.H, a.W, a.C, n2, th2 * S - 1,
-                              tw2 * S - 1, cvb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's DMA of tile t landed
+    uint4* sb = s_dyn + buf * bufv;
+    if constexpr (IT) {
+      const int hi0 = th0 * S - 1, wi0 = tw0 * S - 1;
+#pragma unroll
+      for (int k = 0; k < LPT; ++k) {
+        const int pix = k * 32 + p0;
+        const int r = pix / G::IC, col = pix - r * G::IC;
+        const bool ok = pix < G::IR * G::IC && (unsigned)(hi0 + r) < (unsigned)a.H &&
+                        (unsigned)(wi0 + col) < (unsigned)a.W;
+        uint4& v = sb[k * nthr + tid];
+        v = sel4(ok, bnrelu_vec<T>(v, isc, ish));
+      }
     }
+    // every wave's DMA of tile t is visible (and, IT, transformed); every wave is done reading
+    // the other buffer (tile t - 1)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 1 < t1) issue(t + 1, buf ^ 1);
     if (t == t0) stamp(a.stamps, 1);
+    const T* sl = reinterpret_cast<const T*>(sb);
     float acc[G::HS][G::WS][4];
 #pragma unroll
     for (int r = 0; r < G::HS; ++r)
@@ -540,10 +492,9 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) 
       for (int p = 0; p < G::WS; ++p)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[r][p][j] = 0.f;
-    // one input row of quads at a time (the memory clobber keeps the next row's LDS reads below
-    // it: hoisting all NR x NC quads held ~96 more values live beside the prefetched tile)
 #pragma unroll
     for (int rr = 0; rr < G::NR; ++rr) {
+      asm volatile("" ::: "memory");  // one input row of quads at a time (see dw_fwd_kernel)
 #pragma unroll
       for (int ci = 0; ci < G::NC; ++ci) {
         float v[4];
@@ -561,17 +512,9 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) 
           }
         }
       }
-      asm volatile("" ::: "memory");
     }
     const int ho0 = th0 + gy * G::HS, wo0 = tw0 + gx * G::WS;
     const int nrow = max(0, min(G::HS, a.Ho - ho0)), ncol = max(0, min(G::WS, a.Wo - wo0));
-    float sc[4], sh[4];
-    {
-      const float4 a4 = *reinterpret_cast<const float4*>(t_sc + lq4);
-      const float4 b4 = *reinterpret_cast<const float4*>(t_sh + lq4);
-      sc[0] = a4.x; sc[1] = a4.y; sc[2] = a4.z; sc[3] = a4.w;
-      sh[0] = b4.x; sh[1] = b4.y; sh[2] = b4.z; sh[3] = b4.w;
-    }
 #pragma unroll
     for (int r = 0; r < G::HS; ++r) {
       if (r >= nrow) continue;
@@ -584,10 +527,9 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) 
         for (int j = 0; j < 4; ++j) {
           const float v = acc[r][p][j] * sc[j] + sh[j];
           o[j] = a.relu ? fmaxf(v, 0.f) : v;
-          acc[r][p][j] = o[j];
         }
         quad_st(yb + (size_t)p * a.C, o);
-        if (!BR && stats) {  // shifted sums; the shift is the thread's first output value
+        if (stats) {  // shifted sums; the shift is the thread's first output value
           if (cnt == 0.f) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) shf[j] = o[j];
@@ -602,142 +544,110 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_loop_kernel(DwArgs a, int cbv) 
         }
       }
     }
-    if constexpr (BR) {
-      // ---- stride-1 dgrad: BN-backward partial sums of the stored dx (it is that BN's dy) ---
-      float bm[4], bi[4], bsc[4], bsh[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bm[j] = t_bm[lq4 + j];
-        bi[j] = t_bi[lq4 + j];
-        bsc[j] = t_bs[lq4 + j];
-        bsh[j] = t_bh[lq4 + j];
-      }
-#pragma unroll
-      for (int r = 0; r < G::HS; ++r) {
-        float z[G::WS][4];  // one output row of z per batch of loads
-#pragma unroll
-        for (int p = 0; p < G::WS; ++p) {
-          const bool ok = r < nrow && p < ncol;
-          const size_t pix = ok ? ((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0 + p : 0;
-          quad_ld((const T*)b.z + pix * a.C + c0, z[p]);
-        }
-#pragma unroll
-        for (int p = 0; p < G::WS; ++p) {
-          const bool ok = r < nrow && p < ncol;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float gv = round_as<T>(acc[r][p][j]);
-            gv = (ok && fmaf(z[p][j], bsc[j], bsh[j]) > 0.f) ? gv : 0.f;
-            s1[j] += gv;
-            s2[j] += gv * (z[p][j] - bm[j]) * bi[j];
-          }
-        }
-        asm volatile("" ::: "memory");  // next row's z loads after this row's use
-      }
-    }
-    __syncthreads();  // every read of this tile's LDS image (and of s_red) is done
   }
   stamp(a.stamps, 2);
-  if (!BR && !stats) return;
-  // ---- one record per worker: the G pixel groups of each channel quad in fixed order ---------
-  constexpr int R = BR ? 2 : 3;
-  float* part = BR ? b.part : a.part;
-  float* rec = part + (size_t)wj * R * a.C;
-  float tot[3][4];
-  if constexpr (!BR) {  // per thread (n, mean, M2) from its shifted sums
+  if (!stats) return;
+  // ---- one record per worker: (n, mean, M2) per thread, Chan-merged over the pixel groups in
+  // fixed order (the scratch aliases the first tile buffer: every read of it is done)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* s_red = reinterpret_cast<float*>(s_dyn);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float m = cnt > 0.f ? shf[j] + s1[j] / cnt : 0.f;
-      s2[j] = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
-      s1[j] = m;
-    }
+  for (int j = 0; j < 4; ++j) {
+    const float m = cnt > 0.f ? shf[j] + s1[j] / cnt : 0.f;
+    s2[j] = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
+    s1[j] = m;
   }
 #pragma unroll
-  for (int pass = 0; pass < 3; ++pass) {
-    if (pass == 2 && BR) break;
+  for (int pass = 0; pass < 3; ++pass)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       s_red[((pass * G::G + grp) * QB + q) * 4 + j] = pass == 0 ? s1[j] : (pass == 1 ? s2[j] : cnt);
-  }
   __syncthreads();
+  float* rec = a.part + (size_t)wj * 3 * a.C;
   if (grp == 0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if constexpr (BR) {
-        float u = 0.f, w = 0.f;
-        for (int g2 = 0; g2 < G::G; ++g2) {
-          u += s_red[((0 * G::G + g2) * QB + q) * 4 + j];
-          w += s_red[((1 * G::G + g2) * QB + q) * 4 + j];
-        }
-        tot[0][j] = u;
-        tot[1][j] = w;
-      } else {  // Chan merge of the groups, fixed order
-        float nn = 0.f, mean = 0.f, m2 = 0.f;
-        for (int g2 = 0; g2 < G::G; ++g2) {
-          const float nb = s_red[((2 * G::G + g2) * QB + q) * 4 + j];
-          if (nb <= 0.f) continue;
-          const float mb = s_red[((0 * G::G + g2) * QB + q) * 4 + j];
-          const float qb = s_red[((1 * G::G + g2) * QB + q) * 4 + j];
-          const float tn = nn + nb, d = mb - mean;
-          mean += d * (nb / tn);
-          m2 += qb + d * d * (nn * nb / tn);
-          nn = tn;
-        }
-        tot[0][j] = mean;
-        tot[1][j] = m2;
-        tot[2][j] = nn;
+      float nn = 0.f, mean = 0.f, m2 = 0.f;
+      for (int g2 = 0; g2 < G::G; ++g2) {
+        const float nb = s_red[((2 * G::G + g2) * QB + q) * 4 + j];
+        if (nb <= 0.f) continue;
+        const float mb = s_red[((0 * G::G + g2) * QB + q) * 4 + j];
+        const float qb = s_red[((1 * G::G + g2) * QB + q) * 4 + j];
+        const float tn = nn + nb, d = mb - mean;
+        mean += d * (nb / tn);
+        m2 += qb + d * d * (nn * nb / tn);
+        nn = tn;
       }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      st_wt(rec + c0 + j, tot[0][j]);
-      st_wt(rec + a.C + c0 + j, tot[1][j]);
-      if constexpr (!BR) st_wt(rec + 2 * a.C + c0 + j, tot[2][j]);
+      st_wt(rec + c0 + j, mean);
+      st_wt(rec + a.C + c0 + j, m2);
+      st_wt(rec + 2 * a.C + c0 + j, nn);
     }
   }
   stamp(a.stamps, 3);
   if constexpr (TL)
-    tail_finish<!BR>(part, wy, a.C, wj, cvb * V, cbv * V, cx, a.tail,
-                     reinterpret_cast<double*>(s_dyn));
+    tail_finish<true>(a.part, wy, a.C, wj, cvb * V, cbv * V, cx, a.tail,
+                      reinterpret_cast<double*>(s_dyn));
   stamp(a.stamps, 4);
 }
 
+// channel vectors per DMA-forward workgroup: the largest divisor of C / V whose staged tile
+// (LPT * 32 * cbv 16-B slots) is <= 26 KiB, so two buffers per workgroup and 3 workgroups per CU
+// fit the CU's 160 KiB of LDS
+constexpr int DWD_TILE_MAX = 26 * 1024;
 template <typename T, int S>
-static size_t dw_loop_shm(int cbv) {
-  using G = DwTile<T, S>;
-  return (size_t)G::IR * G::IC * cbv * 16 + (size_t)3 * cbv * 32 * 16 + (size_t)8 * cbv * 8 * 4;
+static int dw_dma_cbv(int CV) {
+  for (int b = DWL_CB; b > 1; --b)
+    if (CV % b == 0 && (size_t)DwTile<T, S>::LPT * 32 * b * 16 <= (size_t)DWD_TILE_MAX) return b;
+  return 1;
 }
-
-// FSCNN_DW_LOOP=1: 16-bit stride-1 forwards run the streaming tile loop.  Off by default:
-// measured r04 (cfg3 bf16 step) 6.20 ms with it vs 6.04 ms with the one-tile kernel -- at <= 2
-// workgroups per CU (its ~240 VGPRs) one tile of prefetch hides less HBM latency than the
-// one-tile kernel's higher occupancy does; on the low-resolution launches alone (<= 64 K output
-// pixels, where the one-tile grid needs ~1.5 dispatch rounds) it is slower still (6.13-6.16 vs
-// 5.99 ms)
-static bool dw_loop_on(int V, int S, long long px) {
+template <typename T, int S>
+static size_t dw_dma_shm(int cbv) {
+  const size_t buf = (size_t)DwTile<T, S>::LPT * 32 * cbv * 16;
+  const size_t red = (size_t)3 * cbv * 32 * 4 * 4;  // the record scratch (aliases buffer 0)
+  return 2 * buf > red ? 2 * buf : red;
+}
+// FSCNN_DW_DMA=1: the DMA forward (A/B while it is measured)
+static bool dw_dma_on() {
   static const bool on = [] {
-    const char* e = getenv("FSCNN_DW_LOOP");
+    const char* e = getenv("FSCNN_DW_DMA");
     return e && e[0] == '1';
   }();
-  (void)px;
-  return on && V == 8 && S == 1;
+  return on;
+}
+// the DMA forward's grid: gx channel chunks x wy workers, every workgroup resident
+template <typename T, int S>
+static dim3 dw_dma_grid(int N, int Ho, int Wo, int C, int& cbv) {
+  using G = DwTile<T, S>;
+  cbv = dw_dma_cbv<T, S>(C / VecW<T>::V);
+  const int gx = C / VecW<T>::V / cbv;
+  const long long ntiles = (long long)N * cdiv(Ho, G::TH) * cdiv(Wo, G::TW);
+  const int waves = cbv * 32 / 64 > 0 ? cbv * 32 / 64 : 1;
+  int per_cu = (int)(160 * 1024 / (dw_dma_shm<T, S>(cbv) + 512));
+  if (per_cu * waves > 12) per_cu = 12 / waves;  // 3 waves per SIMD (launch bounds)
+  if (per_cu < 1) per_cu = 1;
+  long long wy = cdiv((long long)per_cu * 256, gx);
+  if (wy > ntiles) wy = ntiles;
+  if (wy < 1) wy = 1;
+  return dim3(gx, (unsigned)wy, 1);
 }
 
-// fwd: the forward's grid (the loop kernel's gx chunks x wy workers where it applies), else one
-// workgroup per (channel chunk, tile)
+// dynamic LDS of the tile kernels: the haloed input tile of cbv vectors + 4 floats per thread
+template <typename T, int S>
+static size_t dw_shm(int cbv) {
+  using G = DwTile<T, S>;
+  return (size_t)G::IR * G::IC * cbv * 16 + (size_t)cbv * 32 * 16;
+}
+
+// one workgroup per (channel chunk, tile).  (A streaming tile-loop forward -- every workgroup
+// resident, the next tile's loads in flight during the current tile's compute -- measured r04
+// 6.20 vs 6.04 ms per cfg3 step: at <= 2 workgroups per CU one tile of prefetch hid less HBM
+// latency than this kernel's occupancy does; removed in r05.)
 static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv, bool fwd = false) {
-  cbv = dw_cbv(C / V);
-  if (fwd && dw_loop_on(V, S, (long long)N * Ho * Wo)) {
-    // every workgroup resident (2 per CU): gx channel chunks x wy workers, each walking >= 1
-    // of the chunk's T spatial tiles; wy is also the record count of the statistics forms
-    using G = DwTile<bf16, 1>;
-    const int gx = C / V / cbv;
-    const long long T = (long long)N * cdiv(Ho, G::TH) * cdiv(Wo, G::TW);
-    long long wy = cdiv(2 * 256, gx);
-    if (wy > T) wy = T;
-    if (wy < 1) wy = 1;
-    return dim3(gx, (unsigned)wy, 1);
+  if (fwd && dw_dma_on()) {
+    if (V == 4) return S == 1 ? dw_dma_grid<float, 1>(N, Ho, Wo, C, cbv) : dw_dma_grid<float, 2>(N, Ho, Wo, C, cbv);
+    return S == 1 ? dw_dma_grid<bf16, 1>(N, Ho, Wo, C, cbv) : dw_dma_grid<bf16, 2>(N, Ho, Wo, C, cbv);
   }
+  cbv = dw_cbv(C / V);
   int TH, TW;
   if (V == 4) {
     TH = S == 1 ? DwTile<float, 1>::TH : DwTile<float, 2>::TH;
@@ -762,11 +672,15 @@ static void dw_launch_fwd_t(const DwArgs& a, dim3 grid, int nthr, int cbv, hipSt
     else dw_fwd_kernel<T, 1, true, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
     return;
   }
-  if constexpr (!FLIP && sizeof(T) == 2) {
-    if (a.stride == 1 && dw_loop_on(8, 1, (long long)a.N * a.Ho * a.Wo)) {  // (grid: dw_grid fwd)
-      const size_t shm = dw_loop_shm<T, 1>(cbv);
-      if (a.tail_ink) dw_fwd_loop_kernel<T, 1, false, IT, false, true><<<grid, nthr, shm, st>>>(a, cbv);
-      else dw_fwd_loop_kernel<T, 1, false, IT><<<grid, nthr, shm, st>>>(a, cbv);
+  if constexpr (!FLIP) {
+    if (dw_dma_on()) {  // (grid: dw_grid fwd)
+      if (a.stride == 1) {
+        if (a.tail_ink) dw_fwd_dma_kernel<T, 1, IT, true><<<grid, nthr, dw_dma_shm<T, 1>(cbv), st>>>(a, cbv);
+        else dw_fwd_dma_kernel<T, 1, IT><<<grid, nthr, dw_dma_shm<T, 1>(cbv), st>>>(a, cbv);
+      } else {
+        if (a.tail_ink) dw_fwd_dma_kernel<T, 2, IT, true><<<grid, nthr, dw_dma_shm<T, 2>(cbv), st>>>(a, cbv);
+        else dw_fwd_dma_kernel<T, 2, IT><<<grid, nthr, dw_dma_shm<T, 2>(cbv), st>>>(a, cbv);
+      }
       return;
     }
   }

@@ -102,12 +102,11 @@ __device__ __forceinline__ void xcd_tile(int b, int nmajor, int nminor, int& maj
 // 32-k chunk (k = 4lq.., 16+4lq..) form its 8 bf16 k-slots, the same permutation in A and B
 // TL: the launch finishes its BN in its last workgroups (a.tail_ink; a separate instantiation so
 // the other launches keep their register budget)
-// PF: K chunks whose loads are in flight ahead of the one being multiplied (register-staged
-// ring of PF slots).  PF = 1 is the classic one-ahead double buffer; the M <= 64 K-row launches
-// with long K (bottleneck2/3 projects, expand dgrads: 9-12 chunks) are a chain of dependent load
-// latencies at PF = 1 (one 22 KB chunk per CU in flight), so they run PF = 3.
-template <typename T, int NT, bool BT, bool BS, bool AT, bool X3 = false, bool TL = false,
-          int PF = 1>
+// The next K chunk's loads are in flight (registers) while the current chunk multiplies from LDS
+// (one-ahead double buffer).  (A three-chunk register ring for the long-K low-M launches measured
+// r04 6.048 vs 6.023 ms per cfg3 step -- its registers cost more occupancy than the latency it
+// hid -- and was removed in r05.)
+template <typename T, int NT, bool BT, bool BS, bool AT, bool X3 = false, bool TL = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   constexpr int V = VecW<T>::V;
   constexpr int BN = 16 * NT;
@@ -144,8 +143,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // ---- staging registers --------------------------------------------------------------------
   constexpr int A_PER = G_BM * G_VROW / 256;            // 4
   constexpr int B_PER = (BN * G_VROW + 255) / 256;      // vectors per thread (non-trans)
-  uint4 ra[PF][A_PER];
-  uint4 rb[PF][BT ? 1 : B_PER];
+  uint4 ra[A_PER];
+  uint4 rb[BT ? 1 : B_PER];
   // transposed-B staging: KC rows (k) x BN cols (n) of scalars, held as raw 16-B vectors along n
   constexpr int BT_VEC = KC * BN / V;                   // vectors per chunk
   constexpr int BT_PER = (BT_VEC + 255) / 256;
@@ -154,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // Branch-free loads: every lane loads from an in-bounds (clamped) address and invalid or tail
   // elements are zeroed with selects afterwards, so all loads of a chunk issue back to back
   // (a branch around a load makes hipcc wait vmcnt(0) at the join).
-  auto load_chunk = [&](int c, int slot) {
+  auto load_chunk = [&](int c) {
     const int k0 = c * KC;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -163,7 +162,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
       int m = m0 + row, k = k0 + vv * V;
       const bool ok = m < a.M && k < a.K;
       const size_t off = ok ? (size_t)m * a.lda + k : 0;
-      ra[slot][i] = *reinterpret_cast<const uint4*>(A + off);
+      ra[i] = *reinterpret_cast<const uint4*>(A + off);
     }
     if (!BT) {
 #pragma unroll
@@ -173,7 +172,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         int n = n0 + row, k = k0 + vv * V;
         const bool ok = id < BN * G_VROW && n < a.N && k < a.K;
         const size_t off = ok ? (size_t)n * a.ldb + k : 0;
-        rb[slot][i] = *reinterpret_cast<const uint4*>(B + off);
+        rb[i] = *reinterpret_cast<const uint4*>(B + off);
       }
     } else {
 #pragma unroll
@@ -190,14 +189,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   // Tail masks (and the lazy BN+ReLU of A) are applied when a chunk is written to LDS, i.e. after
   // the current chunk's MFMAs: applying them right after issuing the loads made every wave wait
   // for the next chunk's loads before computing (no fetch/compute overlap).
-  auto store_chunk = [&](int buf, int c, int slot) {
+  auto store_chunk = [&](int buf, int c) {
     const int k0 = c * KC;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       int id = tid + 256 * i;
       int row = id >> 3, vv = id & 7;
       int m = m0 + row, k = k0 + vv * V;
-      uint4 v = ra[slot][i];
+      uint4 v = ra[i];
       if constexpr (AT) {
         const int kc = k < a.K ? k : 0;
         v = bnrelu_vec<T>(v, s_at + kc, s_at + G_ATMAX + kc);
@@ -211,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         int row = id >> 3, vv = id & 7;
         int n = n0 + row, k = k0 + vv * V;
         if (id < BN * G_VROW)
-          sB(buf)[row * G_VPAD + vv] = zero_tail<T>(rb[slot][i], n < a.N ? a.K - k : 0);
+          sB(buf)[row * G_VPAD + vv] = zero_tail<T>(rb[i], n < a.N ? a.K - k : 0);
       }
     } else {
       T* sbs = reinterpret_cast<T*>(sB(buf));
@@ -243,23 +242,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
     }
   }
   stamp(a.stamps, 0);
-  // chunk c's loads go to register slot c % PF; the prologue fills every slot
-  load_chunk(0, 0);
-#pragma unroll
-  for (int p = 1; p < PF; ++p)
-    if (p < nchunks) load_chunk(p, p);
+  load_chunk(0);
   if constexpr (AT) __syncthreads();
-  store_chunk(0, 0, 0);
-  if (PF > 1 && PF < nchunks) load_chunk(PF, 0);
+  store_chunk(0, 0);
   __syncthreads();
   stamp(a.stamps, 1);
-  for (int c0 = 0; c0 < nchunks; c0 += PF) {
-#pragma unroll
-    for (int s = 0; s < PF; ++s) {
-      const int c = c0 + s;
-      if (c >= nchunks) break;
+  {
+    for (int c = 0; c < nchunks; ++c) {
       const int buf = nbuf == 2 ? (c & 1) : 0;
-      if (PF == 1 && c + 1 < nchunks) load_chunk(c + 1, 0);
+      if (c + 1 < nchunks) load_chunk(c + 1);
       if constexpr (X3) {
         uint4 a3[2][3];
 #pragma unroll
@@ -291,10 +282,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
         }
       }
       if (c + 1 < nchunks) {
-        const int slot = PF == 1 ? 0 : (s + 1) % PF;  // static once the s loop is unrolled
         if (nbuf == 1) __syncthreads();  // every wave's MFMA reads of this chunk are done
-        store_chunk(nbuf == 2 ? buf ^ 1 : 0, c + 1, slot);
-        if (PF > 1 && c + 1 + PF < nchunks) load_chunk(c + 1 + PF, slot);
+        store_chunk(nbuf == 2 ? buf ^ 1 : 0, c + 1);
       }
       __syncthreads();
     }
@@ -525,31 +514,15 @@ int gemm_nt_parts(const GemmArgs& a, int dtype) {
   return use_stream(a, dtype) ? gemm_stream_parts(a, dtype) : gemm_parts(a.M);
 }
 
-template <typename T, bool BT, bool BS, bool AT, bool X3, bool TL, int PF>
-static void launch_nt_pf(const GemmArgs& a, int nt, dim3 grid, size_t shm, hipStream_t st) {
+template <typename T, bool BT, bool BS, bool AT, bool X3, bool TL>
+static void launch_nt_tl(const GemmArgs& a, int nt, dim3 grid, size_t shm, hipStream_t st) {
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS, AT, X3, TL, PF><<<grid, 256, shm, st>>>(a); break;
+    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
+    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
+    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
+    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
+    default: gemm_nt_kernel<T, 8, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
   }
-}
-
-// deep prefetch (FSCNN_GEMM_PF=3, off by default): 16-bit, plain B, >= 4 K chunks, and a grid of
-// at most two workgroups per CU (the long-K launches at M <= 65536)
-static int nt_prefetch_depth(const GemmArgs& a, int dtype, int nt) {
-  static const int env = [] {
-    const char* e = getenv("FSCNN_GEMM_PF");
-    return e ? atoi(e) : -1;
-  }();
-  const int V = dtype == DT_F32 ? 4 : 8;
-  const int nchunks = cdiv(a.K, G_VROW * V);
-  const long long wgs = (long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt);
-  if (dtype == DT_F32 || a.b_trans || nchunks < 4) return 1;
-  // measured r04 (cfg3 bf16 step, A/B): 6.048 ms with the ring at <= 512 workgroups vs 6.023 ms
-  // without -- the ring's extra VGPRs cost more occupancy than the hidden latency buys; opt-in
-  return (env == 3 && wgs <= 512) ? 3 : 1;
 }
 
 template <typename T, bool BT, bool BS, bool AT = false, bool X3 = false>
@@ -563,21 +536,13 @@ static void launch_nt(const GemmArgs& a, int nt, hipStream_t st) {
   const size_t red = (size_t)2 * 256 * V * 4;  // bwd-BN column reduction (2 x RG x BN floats)
   if (a.bpart && red > ctile) ctile = red;
   const size_t shm = tiles > ctile ? tiles : ctile;
-  const int dtype = sizeof(T) == 4 ? DT_F32 : DT_BF16;
-  if constexpr (!BT && !X3 && sizeof(T) == 2) {
-    if (nt_prefetch_depth(a, dtype, nt) == 3) {
-      if (a.tail_ink) launch_nt_pf<T, BT, BS, AT, X3, true, 3>(a, nt, grid, shm, st);
-      else launch_nt_pf<T, BT, BS, AT, X3, false, 3>(a, nt, grid, shm, st);
-      return;
-    }
-  }
   if constexpr (!BT && !X3) {
     if (a.tail_ink) {
-      launch_nt_pf<T, BT, BS, AT, X3, true, 1>(a, nt, grid, shm, st);
+      launch_nt_tl<T, BT, BS, AT, X3, true>(a, nt, grid, shm, st);
       return;
     }
   }
-  launch_nt_pf<T, BT, BS, AT, X3, false, 1>(a, nt, grid, shm, st);
+  launch_nt_tl<T, BT, BS, AT, X3, false>(a, nt, grid, shm, st);
 }
 
 static int gemm_nt_tiled(const GemmArgs& a, int dtype, int nt, bool at, bool bs, hipStream_t st);
@@ -604,13 +569,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
   int nt = pick_nt(a.N);
   // small-M problems (the 16 K-row bottleneck2/3 projects and expand dgrads: 128 row tiles)
   // split the columns down to NT = 2 so ~512 workgroups (two per CU, eight waves) are in flight:
-  // measured r04 5.965-5.976 ms/step vs 6.001-6.007 at 256 and 6.016-6.018 at 1024
-  static const int min_tiles = [] {  // grid size below which NT halves (FSCNN_GEMM_MINT)
-    const char* e = getenv("FSCNN_GEMM_MINT");
-    return e ? atoi(e) : 512;
-  }();
+  // measured r04 5.965-5.976 ms/step vs 6.001-6.007 at a minimum grid of 256 and 6.016-6.018 at
+  // 1024
+  constexpr int min_tiles = 512;
   while ((long long)cdiv(a.M, G_BM) * cdiv(a.N, 16 * nt) < min_tiles &&
-         (nt == 8 || nt == 6 || nt == 4 || (nt == 3 && min_tiles > 256)))
+         (nt == 8 || nt == 6 || nt == 4 || nt == 3))
     nt = nt == 3 ? 2 : nt / 2;
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   const double M = a.M, N = a.N, K = a.K;

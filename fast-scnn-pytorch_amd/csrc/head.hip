@@ -685,6 +685,13 @@ __global__ __launch_bounds__(256) void ce_head_finalize_kernel(const float* part
   }
 }
 
+bool ce_head2_form(int C, int ldl, int dtype) {
+  return dtype != DT_F32 && (C == 19 || C == 2) && ldl == (C + 7) / 8 * 8;
+}
+bool ce_head_reads_tgt8(int C, int ldl, int W, int dtype) {
+  return ce_head2_form(C, ldl, dtype) && W <= HD_TMAX && W % 8 == 0;
+}
+
 int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
   if (a.C < 1 || a.C > HD_CMAX) {
     set_error("ce_head: %d classes (max %d)", a.C, HD_CMAX);
@@ -696,11 +703,9 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
                                 8.0 * a.N * a.H * a.W + 2.0 * 4.0 * a.N * a.Hl * a.Wl * a.C,
                  0.0);
     const bool f32 = dtype == DT_F32;
-    static const int form = [] {  // FSCNN_CE_HEAD=1: the one-hot-select kernel for every dtype
-      const char* e = getenv("FSCNN_CE_HEAD");
-      return e ? atoi(e) : 2;
-    }();
-    if (form >= 2 && !f32 && (a.C == 19 || a.C == 2) && a.ldl == (a.C + 7) / 8 * 8) {
+    // (16-bit plans: the walked-exponential kernel; round 3's one-hot-select kernel for these
+    // shapes measured 211 vs 158-164 us and was retired as a switch in r05)
+    if (ce_head2_form(a.C, a.ldl, dtype)) {
       CeHeadArgs as = a;
       as.stamps = stamp_region();
       if (a.C == 19) {

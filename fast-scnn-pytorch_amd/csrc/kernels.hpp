@@ -6,7 +6,10 @@
 
 namespace fscnn {
 
-constexpr int MAX_FOLD = 64;
+constexpr int MAX_FOLD = 48;  // (45 BatchNorms with the aux head; the table is a kernel argument)
+// BN-backward element count of a BatchNorm normalised with its running statistics (plans with
+// train == 2, eval-mode autograd): bn_bwd_finish then drops the batch-mean terms
+constexpr double BN_FROZEN_COUNT = -1.0;
 
 
 struct Conv0Args {
@@ -191,6 +194,10 @@ struct FoldEntry {
   float* scale;
   float* shift;
   int C;
+  // running-statistics BN of a differentiable eval forward (train == 2 plans): the constants
+  // the backward's x_hat uses, mean = running_mean, invstd = 1 / sqrt(running_var + eps), or null
+  float* mean = nullptr;
+  float* invstd = nullptr;
 };
 
 struct FoldTable {
@@ -395,6 +402,15 @@ struct IrArgs {
 bool ir_block_ok(const IrArgs& a, int dtype);
 int ir_block_fwd(const IrArgs& a, int dtype, hipStream_t st);
 
+// input gradient of conv0 (autograd of the image through models/fast_scnn.py:153)
+struct Conv0DgradArgs {
+  const void* dz;  // NHWC [N,Ho,Wo,32] in the plan dtype (conv0's BN-backward output)
+  const float* w;  // [32][3][3][3] fp32 master weights
+  int N, H, W, Ho, Wo;
+  void* dx;        // NCHW [N,3,H,W] in dx_dtype (0 fp32, 1 bf16, 2 fp16)
+  int dx_dtype;
+};
+int conv0_dgrad(const Conv0DgradArgs& a, int dz_dtype, hipStream_t st);
 int conv0_parts(int N, int Ho, int Wo);
 int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st);
 int conv0_wgrad_parts(int N, int Ho, int Wo, int rows_per_block);
@@ -518,6 +534,10 @@ int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N,
                   float smooth, float wd, float wf, void* dlogits, hipStream_t st);
 int ce_head_parts(int N, int Hl, int Wl);
 int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st);
+// the 16-bit loss-head kernel (ce_head2_kernel) takes these shapes; it reads CeHeadArgs::tgt8
+// (when given) only where ce_head_reads_tgt8 holds, so only then are the targets packed
+bool ce_head2_form(int C, int ldl, int dtype);
+bool ce_head_reads_tgt8(int C, int ldl, int W, int dtype);
 // targets [n] int64 -> int8: t if 0 <= t < C and t != ignore_index, else -1 (C <= 127)
 int ce_pack_targets(const long long* t, long long n, int C, long long ignore_index,
                     signed char* out, hipStream_t st);

@@ -302,16 +302,21 @@ int ohem_threshold_dev(const float* key, long long n, const unsigned long long* 
 // ---- Dice / Focal+Dice (utils/loss.py:12-100; train.py:183-188 for binary lane segmentation) ----
 // p1 = softmax(logits)[:, 1] (C > 1) or sigmoid(logits[:, 0]) (C == 1), t = float(target):
 //   dice = (2 sum(p1 t) + s) / (sum p1 + sum t + s), DiceLoss = 1 - dice;
-//   focal (C > 1) = mean_i alpha (1 - pt_i)^gamma ce_i, ce_i = lse_i - x_{t_i}, pt_i = exp(-ce_i).
+//   focal = mean_i alpha (1 - pt_i)^gamma ce_i with (FocalDiceLoss.focal_loss, :81-95)
+//     C > 1: ce_i = lse_i - x_{t_i}, pt_i = exp(-ce_i);
+//     C = 1: p = sigmoid(x), ce_i = F.binary_cross_entropy(p, t) = -(t max(log p, -100) +
+//            (1 - t) max(log(1 - p), -100)), pt_i = t == 1 ? p : 1 - p.
 // Forward: per-block partials of (sum p1 t, sum p1, sum t, sum focal), merged in fixed order in
-// fp64.  Backward: dL/dx_c = wd * dDice/dp1 * dp1/dx_c + wf/n * dfocal/dce * (p_c - [c == t]).
+// fp64.  Backward: dL/dx_c = wd * dDice/dp1 * dp1/dx_c + wf/n * dfocal/dce * (p_c - [c == t]);
+// C = 1: autograd's chain through where / pow / BCE (aten's BCE backward divides by
+// max(p (1 - p), 1e-12)) and sigmoid.
 struct DiceArgs {
   const void* logits;
   const long long* target;
   long long N, HW;
   int C;
   float alpha, gamma;
-  int focal;  // compute the focal term (C > 1)
+  int focal;  // compute the focal term
 };
 
 template <typename T>
@@ -325,6 +330,10 @@ __device__ __forceinline__ void dice_pixel(const DiceArgs& a, long long i, float
     p1 = 1.f / (1.f + expf(-ld1(lb)));
     ce = 0.f;
     pt = 0.f;
+    if (a.focal) {
+      ce = -(tf * fmaxf(logf(p1), -100.f) + (1.f - tf) * fmaxf(logf(1.f - p1), -100.f));
+      pt = tf == 1.f ? p1 : 1.f - p1;
+    }
     return;
   }
   float mx = -INFINITY;
@@ -396,7 +405,7 @@ __global__ __launch_bounds__(256) void dice_bwd_kernel(DiceArgs a, const double*
   // d(1 - dice)/dp1 = -(2 t den - (2 I + s)) / den^2
   const float gd = (float)(-(2.0 * tf * den - (2.0 * I + smooth)) / (den * den)) * wd * gout[0];
   float gf = 0.f;
-  if (a.focal) {
+  if (a.focal && a.C > 1) {
     const float om = 1.f - pt;
     const float dfdce = a.alpha * (powf(om, a.gamma) + ce * a.gamma * powf(om, a.gamma - 1.f) * pt);
     gf = dfdce * wf * gout[0] / (float)(a.N * a.HW);
@@ -404,7 +413,16 @@ __global__ __launch_bounds__(256) void dice_bwd_kernel(DiceArgs a, const double*
   const T* lb = (const T*)a.logits + (size_t)n * a.C * a.HW + p;
   T* db = (T*)dlogits + (size_t)n * a.C * a.HW + p;
   if (a.C == 1) {
-    st1(db, gd * p1 * (1.f - p1));
+    const float s = p1 * (1.f - p1);  // sigmoid backward
+    float g = gd * s;
+    if (a.focal) {
+      const float om = 1.f - pt;
+      const float dce = (p1 - tf) / fmaxf(s, 1e-12f) * s;
+      const float dpt = (tf == 1.f ? 1.f : -1.f) * s;
+      const float df = a.alpha * (powf(om, a.gamma) * dce - a.gamma * powf(om, a.gamma - 1.f) * dpt * ce);
+      g += df * wf * gout[0] / (float)(a.N * a.HW);
+    }
+    st1(db, g);
     return;
   }
   float mx = -INFINITY;
@@ -422,8 +440,8 @@ __global__ __launch_bounds__(256) void dice_bwd_kernel(DiceArgs a, const double*
 
 int dice_loss_fwd(const void* logits, int dtype, const long long* target, int N, int C, long long HW,
                   float alpha, float gamma, int focal, float* part, double* stats, hipStream_t st) {
-  if (C < 1 || (focal && C < 2)) {
-    set_error("dice_loss: C=%d (focal term needs C > 1)", C);
+  if (C < 1) {
+    set_error("dice_loss: C=%d", C);
     return E_INVALID;
   }
   DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};

@@ -194,6 +194,11 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     set_error("plan_build: unsupported dtype %d", dtype);
     return E_UNSUPPORTED;
   }
+  if (train < 0 || train > 2) {
+    set_error("plan_build: train must be 0 (inference), 1 (training) or 2 (differentiable "
+              "inference: running-statistics BatchNorm)");
+    return E_INVALID;
+  }
   pl = Plan();
   pl.net = &net;
   pl.N = N; pl.H = H; pl.W = W; pl.dtype = dtype; pl.train = train;
@@ -292,7 +297,8 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
   if (train) {
     pl.g_raw = A.get((size_t)2 * M2 * pl.Cp * 4);  // own-row plane + row-spill plane
     pl.head_part = A.get((size_t)ce_head_parts(N, pl.H3, pl.W3) * 2 * 4);
-    pl.tgt8 = A.get((size_t)N * pl.H * pl.W);
+    if (train == 1 && ce_head_reads_tgt8(net.num_classes, pl.Cp, pl.W, dtype))
+      pl.tgt8 = A.get((size_t)N * pl.H * pl.W);
   }
   if (train) {
     pl.seed_slot = A.get(64);
@@ -643,9 +649,16 @@ struct Exec {
   int dt;
   size_t E;
   bool train;
+  // train == 2 plans (eval-mode autograd): the training dataflow (pre-BN z stored, BN applied by
+  // the consumers, the staged backward) with every BatchNorm normalised by its running statistics
+  // (fold_all before the forward): no batch statistics, no running-stat update, no Dropout, and
+  // the BN backward without its batch-mean terms (BN_FROZEN_COUNT)
+  bool frozen;
   Exec(const Plan& p, const RunArgs& ra)
       : pl(p), net(*p.net), r(ra), ws((char*)ra.ws), bws((char*)ra.bws), dt(p.dtype),
-        E(p.dtype == DT_F32 ? 4 : 2), train(p.train != 0) {}
+        E(p.dtype == DT_F32 ? 4 : 2), train(p.train != 0), frozen(p.train == 2) {}
+  // element count of unit u's BN backward (frozen: the running-statistics form)
+  double bcount(const Unit& u) const { return frozen ? BN_FROZEN_COUNT : (double)u.M; }
   // every return path (a TRY() failure between a fork and its join included) leaves the caller's
   // stream ordered after the side-stream work already issued: the workspaces it writes are
   // freed by the caller once the call returns, and a graph capture needs the fork joined
@@ -662,7 +675,7 @@ struct Exec {
   }
   // the PPM branches as one fused launch each way (ppm.hip) wherever the branch shapes fit it;
   // the general per-branch GEMM / BN kernels otherwise
-  bool ppm_fused() const { return train && ppm_branches_ok((int)pl.ppk[3].M, 128, dt); }
+  bool ppm_fused() const { return train && !frozen && ppm_branches_ok((int)pl.ppk[3].M, 128, dt); }
   // a weight-gradient launch: queued for the side stream (issued by flush_side), or run now on
   // the main stream without one
   int side_launch(std::function<int(hipStream_t)> f) {
@@ -693,8 +706,8 @@ struct Exec {
     return OK;
   }
   // the loss head's targets as int8 (the side stream packs them during the global feature
-  // extractor; the FFM join orders them before the head)
-  static bool ce_head_packs(int C, int dtype) { return dtype != DT_F32 && (C == 19 || C == 2); }
+  // extractor; the FFM join orders them before the head), where the head reads them
+  bool ce_head_packs() const { return pl.tgt8 != 0; }
   int pack_targets(hipStream_t s) {
     g_prof_tag = "head (targets to int8)";
     return ce_pack_targets(r.target, (long long)pl.N * pl.H * pl.W, net.num_classes,
@@ -902,7 +915,7 @@ struct Exec {
     }
     g.scale = nullptr; g.shift = P(c.b);
     g.C = W(u.z); g.ldc = u.C;
-    gemm_fin(g, u, *bn);
+    if (!frozen) gemm_fin(g, u, *bn);
     TRY(gemm_nt(g, dt, r.st));
     return (u.lazy || !store_out) ? OK : apply(u, relu, res, ldres);
   }
@@ -920,10 +933,13 @@ struct Exec {
       d.scale = Wf(u.scale); d.shift = Wf(u.shift); d.relu = 1; d.y = W(u.a);
       return dw_fwd(d, dt, r.st);
     }
-    d.relu = 0; d.y = W(u.z); d.part = Wf(u.part);
-    d.tail.counters = (unsigned*)W(pl.fcnt);  // dw_fwd finishes the BN (in-kernel when it fits)
-    d.tail.fwd = fin_args(u, bn);
-    d.tail.tsum = (double*)W(pl.tsum);
+    d.relu = 0; d.y = W(u.z);
+    if (!frozen) {
+      d.part = Wf(u.part);
+      d.tail.counters = (unsigned*)W(pl.fcnt);  // dw_fwd finishes the BN (in-kernel when it fits)
+      d.tail.fwd = fin_args(u, bn);
+      d.tail.tsum = (double*)W(pl.tsum);
+    }
     TRY(dw_fwd(d, dt, r.st));
     return u.lazy ? OK : apply(u, true);
   }
@@ -933,8 +949,10 @@ struct Exec {
     auto add = [&](const BnL& bn, const Unit& u, const ConvL* conv) {
       FoldEntry& e = t.e[t.n++];
       e.gamma = P(bn.g); e.beta = P(bn.b); e.rmean = r.R + bn.rm; e.rvar = r.R + bn.rv;
-      e.bias = (conv && conv->b >= 0) ? P(conv->b) : nullptr;
+      // (frozen: the stored z already carries the conv bias, as in training plans)
+      e.bias = (!frozen && conv && conv->b >= 0) ? P(conv->b) : nullptr;
       e.scale = Wf(u.scale); e.shift = Wf(u.shift); e.C = bn.C;
+      if (frozen) { e.mean = Wf(u.mean); e.invstd = Wf(u.invstd); }
     };
     add(net.b0, pl.c0, nullptr);
     add(net.ltd1.bdw, pl.l1dw, nullptr); add(net.ltd1.bpw, pl.l1pw, nullptr);
@@ -960,7 +978,7 @@ struct Exec {
     const int N = pl.N;
     g_prof_tag = "weights_prep";
     TRY(prep_weights());
-    if (!train) TRY(fold_all());
+    if (!train || frozen) TRY(fold_all());
     g_prof_tag = pl.c0.name.c_str();
     // ---- LearningToDownsample ----
     {
@@ -969,10 +987,10 @@ struct Exec {
       c.N = N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
       c.w = P(net.c0.w);
       if (!train) { c.scale = Wf(pl.c0.scale); c.shift = Wf(pl.c0.shift); c.relu = 1; c.y = W(pl.c0.a); }
-      else { c.relu = 0; c.y = W(pl.c0.z); c.part = Wf(pl.c0.part); }
+      else { c.relu = 0; c.y = W(pl.c0.z); c.part = frozen ? nullptr : Wf(pl.c0.part); }
       TRY(conv0_fwd(c, dt, r.st));
       if (train) {
-        TRY(finalize(pl.c0, net.b0));
+        if (!frozen) TRY(finalize(pl.c0, net.b0));
         if (!pl.c0.lazy) TRY(apply(pl.c0, true));
       }
     }
@@ -985,15 +1003,12 @@ struct Exec {
     // extractor; its BN finish uses the backward's counters and its own team-sum scratch, so it
     // never shares arrival state with the main stream's producers; joined before the FFM apply
     const bool fhigh_side = train && side != nullptr;
-    // the loss head's int8 targets: on the side stream from the start of bottleneck PACK_AT
-    // (FSCNN_CE_PACK: 0 = head reads int64, 1 = beside bottleneck1's HBM-bound launches, 2 =
-    // beside the latency-bound bottleneck2/3), or on the main stream without a side stream
-    static const int pack_mode = [] {
-      const char* e = getenv("FSCNN_CE_PACK");
-      return e ? atoi(e) : 2;
-    }();
-    const bool pack = train && r.target && pack_mode > 0 && ce_head_packs(net.num_classes, dt);
-    const int pack_at = !pack ? -1 : pack_mode == 1 ? 0 : 3;
+    // the loss head's int8 targets: on the side stream from the start of bottleneck2, beside its
+    // latency-bound launches, or on the main stream without a side stream.  (Measured r04, cfg3
+    // A/B: the head reading int64 targets 6.07 ms per step, packed beside bottleneck1's HBM-bound
+    // launches 6.03, beside bottleneck2/3 6.015; the alternatives were retired as switches in r05.)
+    const bool pack = train && !frozen && r.target && ce_head_packs();
+    const int pack_at = pack ? 3 : -1;
     if (fhigh_side) {
       TRY(fhigh_fwd(true));
       TRY(flush_side());
@@ -1094,7 +1109,7 @@ struct Exec {
         g.a_scale = fin.sc; g.a_shift = fin.sh;
         g.B = Wg(net.ffm_low); g.ldb = 128; g.shift = P(net.ffm_low.b);
         g.C = W(pl.flow.z); g.ldc = 128;
-        gemm_fin(g, pl.flow, net.ffm_blow);
+        if (!frozen) gemm_fin(g, pl.flow, net.ffm_blow);
         TRY(gemm_nt(g, dt, r.st));
         if (fhigh_side) TRY(join());
         else TRY(fhigh_fwd(false));
@@ -1135,8 +1150,8 @@ struct Exec {
     if (net.aux && r.aux_out) TRY(forward_aux());
     if (r.target) {
       // ---- fused training head: upsample + CE + gradient at low resolution ----
-      if (!train) {
-        set_error("forward_loss needs a training plan");
+      if (!train || frozen) {
+        set_error("forward_loss needs a training plan (train=1)");
         return E_INVALID;
       }
       g_prof_tag = "head (upsample + cross entropy)";
@@ -1170,10 +1185,12 @@ struct Exec {
     g.a_scale = hin.sc; g.a_shift = hin.sh;
     g.B = Wg(net.ffm_high); g.ldb = 64; g.shift = P(net.ffm_high.b);
     g.C = W(pl.fhigh.z); g.ldc = 128;
-    gemm_fin(g, pl.fhigh, net.ffm_bhigh);
+    if (!frozen) gemm_fin(g, pl.fhigh, net.ffm_bhigh);
     if (!on_side) return gemm_nt(g, dt, r.st);
-    g.tail.counters = (unsigned*)W(pl.bcnt);
-    g.tail.tsum = (double*)W(pl.tsum2);
+    if (!frozen) {
+      g.tail.counters = (unsigned*)W(pl.bcnt);
+      g.tail.tsum = (double*)W(pl.tsum2);
+    }
     const int dtc = dt;
     return side_launch([g, dtc](hipStream_t s) { return gemm_nt(g, dtc, s); });
   }
@@ -1269,7 +1286,7 @@ struct Exec {
     TRY(bn_bwd_reduce(b, dt, r.st));
     int rpb;
     const int P = bn_bwd_parts(u.M, u.C, dt, &rpb);
-    return bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, (double)u.M, G(bn.g), G(bn.b),
+    return bn_bwd_finalize((float*)Bw(pl.bnpart), P, u.C, bcount(u), G(bn.g), G(bn.b),
                            (float*)Bw(pl.coef), r.st, (unsigned*)W(pl.bcnt), tb);
   }
   // Where a BN-backward dz is formed: by bn_bwd_apply (materialised), or — `streaming`, only
@@ -1334,9 +1351,9 @@ struct Exec {
     TRY(bn_bwd_reduce(b, dt, r.st));
     float* coef = (float*)Bw(pl.coef);
     float* coef2 = coef + 2 * u1.C;
-    TRY(bn_bwd_finalize(b.part, P, u1.C, (double)u1.M, G(bn1.g), G(bn1.b), coef, r.st,
+    TRY(bn_bwd_finalize(b.part, P, u1.C, bcount(u1), G(bn1.g), G(bn1.b), coef, r.st,
                         (unsigned*)W(pl.bcnt), BnBwdTab()));
-    TRY(bn_bwd_finalize(b.part2, P, u2.C, (double)u2.M, G(bn2.g), G(bn2.b), coef2, r.st,
+    TRY(bn_bwd_finalize(b.part2, P, u2.C, bcount(u2), G(bn2.g), G(bn2.b), coef2, r.st,
                         (unsigned*)W(pl.bcnt), BnBwdTab()));
     b.coef = coef; b.coef2 = coef2;
     b.dz = dz1; b.dz2 = dz2; b.lddz = u1.C;
@@ -1356,7 +1373,7 @@ struct Exec {
     g.bmode = t.mode;
     g.tail.counters = (unsigned*)W(pl.bcnt);
     g.tail.tsum = (double*)W(pl.tsum);
-    g.tail.count = (double)u.M;
+    g.tail.count = bcount(u);
     g.tail.dgamma = G(t.bn->g);
     g.tail.dbeta = G(t.bn->b);
     g.tail.coef = (float*)Bw(pl.coef);
@@ -1468,7 +1485,7 @@ struct Exec {
       // kernel's last workgroups when its records fit the counters, else its own launch
       d.tail.counters = (unsigned*)W(pl.bcnt);
       d.tail.tsum = (double*)W(pl.tsum);
-      d.tail.count = (double)u.M;
+      d.tail.count = bcount(u);
       d.tail.dgamma = G(bt.bn->g);
       d.tail.dbeta = G(bt.bn->b);
       d.tail.coef = (float*)Bw(pl.coef);
@@ -1672,7 +1689,7 @@ struct Exec {
     f.bs.mode = 2;
     f.tail.counters = (unsigned*)W(pl.bcnt);
     f.tail.tsum = (double*)W(pl.tsum);
-    f.tail.count = (double)u.M;
+    f.tail.count = bcount(u);
     f.tail.dgamma = G(net.b0.g);
     f.tail.dbeta = G(net.b0.b);
     f.tail.coef = (float*)Bw(pl.coef);
@@ -1701,7 +1718,9 @@ struct Exec {
     TRY(pw_bwd(net.ltd1.pw, pl.l1pw.M, d, act(pl.l1dw), Bw(pl.l1dw.ga), 32, nullptr, 0,
                relu_target(pl.l1dw, net.ltd1.bdw)));
     TRY(bn_bwd_x(pl.l1dw, net.ltd1.bdw, Bw(pl.l1dw.ga), 32, true, dz_buf(pl.l1dw), d));
-    if (ltd_fused_enabled() && ltd_c0_bwd_ok(dt, r.x_dtype, pl.W, r.x)) {
+    // the fused pass never forms conv0's dz, which the input gradient needs
+    const bool want_dx = r.dx != nullptr;
+    if (!want_dx && ltd_fused_enabled() && ltd_c0_bwd_ok(dt, r.x_dtype, pl.W, r.x)) {
       TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, nullptr));
       TRY(ltd1_c0_bwd(d));
       return flush_side();
@@ -1709,7 +1728,15 @@ struct Exec {
     TRY(dw_bwd(net.ltd1.dw, 32, d, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2, Bw(pl.c0.ga),
                relu_target(pl.c0, net.b0)));
     TRY(flush_side());
-    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz_buf(pl.c0), d, true));
+    TRY(bn_bwd_x(pl.c0, net.b0, Bw(pl.c0.ga), 32, true, dz_buf(pl.c0), d, !want_dx));
+    if (want_dx) {  // d is conv0's materialised dz
+      g_prof_tag = "learning_to_downsample.conv (input gradient)";
+      Conv0DgradArgs c{};
+      c.dz = d.p; c.w = P(net.c0.w);
+      c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
+      c.dx = r.dx; c.dx_dtype = r.dx_dtype;
+      TRY(conv0_dgrad(c, dt, r.st));
+    }
     Conv0WgradArgs c{};
     c.x = r.x; c.x_bf16 = r.x_dtype;
     c.N = pl.N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
@@ -1778,7 +1805,7 @@ std::vector<uint64_t> run_key(int kind, int s0, int s1, const RunArgs& r) {
   return {(uint64_t)kind, (uint64_t)s0, (uint64_t)s1, P(r.x), (uint64_t)r.x_dtype, P(r.out),
           (uint64_t)r.out_dtype, P(r.aux_out), P(r.labels), (uint64_t)r.label_u8, P(r.P), P(r.R), P(r.NBT), P(r.G), P(r.ws),
           P(r.bws), P(r.dout), P(r.daux), fbits(r.dropout_p), fbits(r.momentum), P(r.target),
-          (uint64_t)r.ignore_index, P(r.loss2), P(r.gloss)};
+          (uint64_t)r.ignore_index, P(r.loss2), P(r.gloss), P(r.dx), (uint64_t)r.dx_dtype};
 }
 
 template <typename F>
@@ -1864,11 +1891,16 @@ int net_forward(const Plan& pl, const RunArgs& r) {
     set_error("fscnn_forward: this net has the aux head; use fscnn_forward_aux");
     return E_INVALID;
   }
-  if (pl.train && r.dropout_p > 0.f && graphs_enabled())  // read by the dropout kernels
+  if (r.dx_dtype < DT_F32 || r.dx_dtype > DT_F16) {
+    set_error("input gradient dtype code must be 0 (fp32), 1 (bf16) or 2 (fp16)");
+    return E_INVALID;
+  }
+  if (pl.train == 1 && r.dropout_p > 0.f && graphs_enabled())  // read by the dropout kernels
     TRY(set_u64(reinterpret_cast<uint64_t*>((char*)r.ws + pl.seed_slot), r.seed, r.st));
   return run_graphed(pl, run_key(0, 0, 0, r), r.st, [&](hipStream_t st) -> int {
     RunArgs rr = r;
     rr.st = st;
+    if (pl.train == 2) rr.dropout_p = 0.f;  // differentiable inference: Dropout is the identity
     Exec ex(pl, rr);
     ex.use_side();
     return ex.forward();
@@ -1891,9 +1923,14 @@ int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to)
       set_error("net_backward: bad stage %d", s);
       return E_INVALID;
     }
+  if (r.dx_dtype < DT_F32 || r.dx_dtype > DT_F16) {
+    set_error("input gradient dtype code must be 0 (fp32), 1 (bf16) or 2 (fp16)");
+    return E_INVALID;
+  }
   return run_graphed(pl, run_key(1, stage_from, stage_to, r), r.st, [&](hipStream_t st) -> int {
     RunArgs rr = r;
     rr.st = st;
+    if (pl.train == 2) rr.dropout_p = 0.f;
     Exec ex(pl, rr);
     ex.use_side();
     for (int s = stage_from; s <= stage_to; ++s) {

@@ -164,6 +164,10 @@ struct RunArgs {
   // eval prediction: forward with labels != null writes argmax(upsampled logits) instead of out
   void* labels = nullptr;
   int label_u8 = 0;
+  // backward: gradient of the input image, NCHW [N][3][H][W] in dx_dtype (autograd of x through
+  // conv0, models/fast_scnn.py:153), or null
+  void* dx = nullptr;
+  int dx_dtype = 0;
 };
 
 int net_forward(const Plan& pl, const RunArgs& r);

@@ -17,6 +17,8 @@ communication stream around the collective) and the exposed communication time (
 the backward's last kernel on the compute stream to the end of the last all-reduce);
 ``comm_stats()`` averages them over the recorded steps.
 """
+import collections
+
 import torch
 import torch.distributed as dist
 
@@ -35,7 +37,8 @@ class DistributedFastSCNN(torch.nn.Module):
         self.timing = False
         self._step_events = []   # per recorded step: ([(stage, start, end)], main_end)
         self._cur_events = []
-        self.bucket_log = []     # (stage, begin, end, async) of every all-reduce issued
+        # (stage, begin, end, async) of the all-reduces issued, the last 64 (4 per step)
+        self.bucket_log = collections.deque(maxlen=64)
         if broadcast:
             self.broadcast_parameters()
         model.grad_stage_hook = self._stage_hook

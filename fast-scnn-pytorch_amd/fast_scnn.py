@@ -229,26 +229,51 @@ class _Shared:
         self.__init__()
 
 
+MODE_EVAL, MODE_TRAIN, MODE_EVAL_GRAD = 0, 1, 2  # plan modes (include/fastscnn.h fscnn_plan_create)
+
+
 class _FastSCNNFunction(torch.autograd.Function):
-    """Whole-network forward / staged backward; grads are views of one flat arena."""
+    """Whole-network forward / staged backward; grads are views of one flat arena.
+
+    train mode: the training forward keeps its workspace (every pre-BN tensor) for the backward.
+    eval mode (the reference module stays differentiable: models/fast_scnn.py:33-46 has no
+    no_grad, and eval.py:43 calls it with grad enabled): the forward is the fused inference path
+    (same speed and memory as under no_grad), and the backward first recomputes the forward as a
+    differentiable-inference plan (mode 2: every BatchNorm normalised by its running statistics,
+    Dropout off) and then runs the staged backward of that plan.  The parameters are saved for
+    the backward, so autograd refuses one that changed in place in between, as it would for the
+    reference's convolution weights."""
 
     @staticmethod
     def forward(ctx, x, model, ar, *params):
-        outs, ws, seed, dt, xc = model._run_forward(x, train=True, ar=ar)
         ctx.model, ctx.ar = model, ar
-        ctx.ws, ctx.seed, ctx.dt = ws, seed, dt
+        if model.training:
+            outs, ws, seed, dt, xc = model._run_forward(x, MODE_TRAIN, ar=ar)
+            ctx.mode, ctx.ws, ctx.seed, ctx.dt = MODE_TRAIN, ws, seed, dt
+        else:
+            outs, _, _, dt, xc = model._run_forward(x, MODE_EVAL, ar=ar)
+            ctx.mode, ctx.ws, ctx.seed, ctx.dt = MODE_EVAL_GRAD, None, 0, dt
+        ctx.x_dtype = x.dtype
         # the converted dense NCHW fp32/bf16 copy the forward read, not the caller's tensor: the
         # conv0 weight gradient re-reads it as dense NCHW (channels_last / fp16 / expanded inputs)
-        ctx.save_for_backward(xc)
+        ctx.save_for_backward(xc, *params)
         return outs if len(outs) > 1 else outs[0]
 
     @staticmethod
     def backward(ctx, *gouts):
-        (x,) = ctx.saved_tensors
+        x = ctx.saved_tensors[0]  # (autograd checks the saved parameters' versions here)
         gaux = gouts[1] if len(gouts) > 1 else None
-        grads = ctx.model._run_backward(gouts[0], x, ctx.ws, ctx.seed, ctx.dt, ctx.ar, gaux=gaux)
+        model, ws = ctx.model, ctx.ws
+        if ctx.mode == MODE_EVAL_GRAD:
+            # (in the forward's arithmetic: autocast is not active where autograd runs backward)
+            _, ws, _, _, _ = model._run_forward(x, MODE_EVAL_GRAD, ar=ctx.ar, dt=ctx.dt)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        grads = model._run_backward(gouts[0], x, ws, ctx.seed, ctx.dt, ctx.ar, gaux=gaux,
+                                    mode=ctx.mode, dx=dx)
         ctx.ws = ctx.ar = None
-        return (None, None, None) + tuple(grads)
+        if dx is not None and dx.dtype != ctx.x_dtype:
+            dx = dx.to(ctx.x_dtype)
+        return (dx, None, None) + tuple(grads)
 
 
 class _FastSCNNLossFunction(torch.autograd.Function):
@@ -259,17 +284,23 @@ class _FastSCNNLossFunction(torch.autograd.Function):
         loss2, ws, seed, dt, xc = model._run_forward_loss(x, target, ignore_index, ar)
         ctx.model, ctx.ar = model, ar
         ctx.ws, ctx.seed, ctx.dt, ctx.loss2 = ws, seed, dt, loss2
-        ctx.save_for_backward(xc)
-        return loss2[0].clone()
+        ctx.x_dtype = x.dtype
+        ctx.save_for_backward(xc, *params)
+        # a view of the (mean, count) pair the head wrote: the backward reads the count from
+        # loss2 itself, which autograd never writes, so no copy is needed
+        return loss2[0]
 
     @staticmethod
     def backward(ctx, gloss):
-        (x,) = ctx.saved_tensors
+        x = ctx.saved_tensors[0]
         g = gloss.to(torch.float32).reshape(1).contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         grads = ctx.model._run_backward(None, x, ctx.ws, ctx.seed, ctx.dt, ctx.ar, gloss=g,
-                                        loss2=ctx.loss2)
+                                        loss2=ctx.loss2, dx=dx)
         ctx.ws = ctx.ar = None
-        return (None, None, None, None, None) + tuple(grads)
+        if dx is not None and dx.dtype != ctx.x_dtype:
+            dx = dx.to(ctx.x_dtype)
+        return (dx, None, None, None, None) + tuple(grads)
 
 
 class FastSCNN(nn.Module):
@@ -463,7 +494,10 @@ class FastSCNN(nn.Module):
     def _dropout_p(self):
         return float(self.classifier.conv[0].p)
 
-    def _run_forward(self, x, train, ar=None):
+    def _run_forward(self, x, mode, ar=None, dt=None):
+        """One native forward; mode: MODE_EVAL (0), MODE_TRAIN (1), MODE_EVAL_GRAD (2); dt: the
+        arithmetic (default: _compute_dtype)."""
+        train = mode == MODE_TRAIN
         if x.dim() != 4 or x.shape[1] != 3:
             raise RuntimeError("FastSCNN: expected input [N, 3, H, W], got %s" % (tuple(x.shape),))
         if not x.is_cuda:
@@ -478,13 +512,14 @@ class FastSCNN(nn.Module):
         N, _, H, W = x.shape
         if H < 32 or W < 32:
             raise RuntimeError("FastSCNN: input %dx%d too small (needs >= 32x32)" % (H, W))
-        dt = self._compute_dtype(x, train)
+        if dt is None:
+            dt = self._compute_dtype(x, train)
         x = self._input(x)
         if train and N < 2:
             # the reference raises from the PPM 1x1 BatchNorm in train mode (SURVEY §0 trap 5)
             raise ValueError("Expected more than 1 value per channel when training, got input "
                              "size torch.Size([1, 32, 1, 1])")
-        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), train, x.device)
+        plan, fw, _ = nat.plan(N, H, W, _lib.dtype_code(dt), mode, x.device)
         ws = torch.empty(max(fw, 1), dtype=torch.uint8, device=x.device)
         out_dt = dt  # (autocast: the reference's final F.interpolate returns fp16 logits)
         out = torch.empty((N, self.num_classes, H, W), dtype=out_dt, device=x.device)
@@ -610,31 +645,48 @@ class FastSCNN(nn.Module):
         ar = self._exec_arena(x.device)
         return _FastSCNNLossFunction.apply(x, target, ignore_index, self, ar, *ar["params"])
 
-    def _run_backward(self, gout, x, ws, seed, dt, ar, gloss=None, loss2=None, gaux=None):
+    def _run_backward(self, gout, x, ws, seed, dt, ar, gloss=None, loss2=None, gaux=None,
+                      mode=MODE_TRAIN, dx=None):
+        """The staged native backward of a MODE_TRAIN / MODE_EVAL_GRAD forward whose workspace
+        is ``ws``; parameter gradients are views of one flat arena G, and ``dx`` (dense NCHW,
+        the dtype of ``x``) receives the input gradient when given."""
         nat = self.native()
         N, _, H, W = x.shape
-        plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), True, x.device)
+        plan, _, bw = nat.plan(N, H, W, _lib.dtype_code(dt), mode, x.device)
         if gout is not None:
             gout = gout.to(dt).contiguous()
         if self.aux and gloss is None:
             gaux = torch.zeros_like(gout) if gaux is None else gaux.to(dt).contiguous()
-        G = torch.zeros(nat.p_total, dtype=torch.float32, device=x.device)
+        # every element of every parameter's gradient is written by the backward (a reduction,
+        # a BN finish or the PPM kernel; tests/test_gpu_model.py fills G with NaN to check), so
+        # the arena is not zeroed; only the 64-B alignment gaps between tensors are left as is
+        G = torch.empty(nat.p_total, dtype=torch.float32, device=x.device)
+        if getattr(self, "_debug_fill_grads", None) is not None:
+            G.fill_(self._debug_fill_grads)
         bws = torch.empty(max(bw, 1), dtype=torch.uint8, device=x.device)
-        p = self._dropout_p()
+        p = self._dropout_p() if mode == MODE_TRAIN else 0.0
         if getattr(self, "_keep_ws", False):
             self._debug["bws"] = bws
         hook = self.grad_stage_hook
         for s in range(4):
             with torch.cuda.device(x.device):
-                self._backward_stage(plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p)
+                self._backward_stage(plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p,
+                                     dx)
             if hook is not None:
                 b, e = nat.stage_ranges[s]
                 hook(s, G, b, e)
         return [G[off:off + numel].view(prm.shape)
                 for prm, (_, off, numel) in zip(ar["params"], nat.params)]
 
-    def _backward_stage(self, plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p):
-        if gloss is None and self.aux:
+    def _backward_stage(self, plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p,
+                        dx=None):
+        if dx is not None:  # the general entry point: also writes the input gradient (stage 3)
+            _lib.call("fscnn_backward_dx", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(gloss),
+                      _lib.ptr(loss2), _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(dx),
+                      _lib.dtype_code(dx.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.stream_ptr(x.device))
+        elif gloss is None and self.aux:
             _lib.call("fscnn_backward_aux", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(x),
                       _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
                       _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
@@ -650,16 +702,25 @@ class FastSCNN(nn.Module):
                       _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
                       _lib.stream_ptr(x.device))
 
+    def _needs_graph(self, x):
+        """Whether this call is differentiable, as the reference's would be: train mode with
+        grad enabled (the training step), or any mode when autograd would record the call (an
+        input or a parameter requires grad).  eval() under torch.no_grad() is the inference path."""
+        if not torch.is_grad_enabled():
+            return False
+        if self.training or x.requires_grad:
+            return True
+        return any(p.requires_grad for p in self.parameters())
+
     def forward(self, x):
-        train = self.training
-        needs_grad = train and torch.is_grad_enabled()
-        if needs_grad:
+        mode = MODE_TRAIN if self.training else MODE_EVAL
+        if self._needs_graph(x):
             if not x.is_cuda:
-                self._run_forward(x, train)  # raises the device error
+                self._run_forward(x, mode)  # raises the device error
             ar = self._exec_arena(x.device)
             out = _FastSCNNFunction.apply(x, self, ar, *ar["params"])
             return tuple(out) if self.aux else (out,)
-        return self._run_forward(x, train)[0]
+        return self._run_forward(x, mode)[0]
 
 
 def get_fast_scnn(dataset="citys", pretrained=False, root="./weights", map_cpu=False, **kwargs):

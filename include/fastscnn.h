@@ -59,7 +59,10 @@ int fscnn_net_buffer_info(const fscnn_net* net, int i, const char** name, long l
 /* backward stage s (0..3) finalises the gradients of parameters [begin, end) of the arena */
 int fscnn_net_stage_range(const fscnn_net* net, int stage, long long* begin, long long* end);
 
-/* ---- plan: shapes + workspace sizes for one (N, H, W, dtype, mode) ---------------------- */
+/* ---- plan: shapes + workspace sizes for one (N, H, W, dtype, mode) ----------------------
+ * train: 0 inference (BatchNorm folded, fused blocks), 1 training (batch statistics, running-stat
+ * update, Dropout, staged backward), 2 differentiable inference (the training dataflow with
+ * running-statistics BatchNorm: model.eval() under autograd) */
 int fscnn_plan_create(const fscnn_net* net, int N, int H, int W, int dtype, int train,
                       fscnn_plan** out);
 void fscnn_plan_destroy(fscnn_plan* plan);
@@ -79,6 +82,20 @@ int fscnn_backward(const fscnn_plan* plan, const void* dout, const void* x, int 
                    const float* params, float* grads, void* ws, void* bws,
                    unsigned long long dropout_seed, float dropout_p, int stage_from,
                    int stage_to, void* stream);
+
+/* General backward (any of the three heads above) that can also return the gradient of the input
+ * image: autograd of x through the whole network (models/fast_scnn.py:33-46; the reference module
+ * is differentiable in its input like any nn.Module).  Exactly one of dout (d logits, with daux for
+ * an aux net) or grad_loss + loss2 (the fused loss head) is given.  dx: NCHW [N][3][H][W] in
+ * dx_dtype (0 fp32, 1 bf16, 2 fp16), written by the stage-3 call, or null.
+ * Plans: train = 1 (train-mode BatchNorm, batch statistics) or 2 (eval-mode autograd: every
+ * BatchNorm normalised by its running statistics, Dropout off, no running-stat update; the
+ * reference's model.eval() with grad enabled, e.g. eval.py:43). */
+int fscnn_backward_dx(const fscnn_plan* plan, const void* dout, const void* daux,
+                      const float* grad_loss, const float* loss2, const void* x, int x_dtype,
+                      void* dx, int dx_dtype, const float* params, float* grads, void* ws,
+                      void* bws, unsigned long long dropout_seed, float dropout_p, int stage_from,
+                      int stage_to, void* stream);
 
 /* FastSCNN(aux=True) (models/fast_scnn.py:24-31, 42-45): the same forward / backward plus the
  * auxiliary head (3x3 conv 64->32 + BN + ReLU + Dropout + 1x1 on the LearningToDownsample output,

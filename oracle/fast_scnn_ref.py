@@ -278,9 +278,16 @@ def dice_loss(pred, target, smooth=1e-6):
 
 
 def focal_dice_loss(pred, target, alpha=0.5, gamma=2.0, dice_weight=0.5, smooth=1e-6):
-    """FocalDiceLoss (utils/loss.py:71-100), multi-class logits."""
-    ce = F.cross_entropy(pred, target, reduction="none")
-    pt = torch.exp(-ce)
+    """FocalDiceLoss (utils/loss.py:71-100): multi-class logits (:83-86), or one logit channel
+    with the sigmoid + binary cross entropy focal term (:87-92)."""
+    if pred.size(1) > 1:
+        ce = F.cross_entropy(pred, target, reduction="none")
+        pt = torch.exp(-ce)
+    else:
+        prob = torch.sigmoid(pred.squeeze(1))
+        tf = target.to(prob.dtype)
+        ce = F.binary_cross_entropy(prob, tf, reduction="none")
+        pt = torch.where(tf == 1, prob, 1 - prob)
     focal = (alpha * (1 - pt) ** gamma * ce).mean()
     return (1 - dice_weight) * focal + dice_weight * dice_loss(pred, target, smooth)
 

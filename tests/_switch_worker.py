@@ -3,9 +3,11 @@ switches once per process).  Three fp32 train steps with Dropout(0.1) active and
 5, 9, 5 — alternating the unfused ``model(x)`` + CE path and the fused ``forward_loss`` head —
 then saves every step's loss and flat gradient arena, and the step-3 running statistics.
 With ``bf16`` the image is bf16 (the bf16 train plan, cfg3's arithmetic); ``bf16shift`` adds 4.0 to
-a 2 x 3 x 512 x 1024 image, which moves conv0's output (hence its BN mean) well away from 0.
+a 2 x 3 x 512 x 1024 image, which moves conv0's output (hence its BN mean) well away from 0;
+``bf16drop`` runs a bf16 2 x 3 x 256 x 512 image (M = 4096 low-res pixels: the classifier conv's
+dgrad takes the streaming kernel with the Dropout backward in its epilogue).
 
-    python tests/_switch_worker.py OUT.npz [bf16|bf16shift]
+    python tests/_switch_worker.py OUT.npz [bf16|bf16shift|bf16drop]
 """
 import os
 import sys
@@ -29,11 +31,11 @@ def main(out, half=None):
     m = FastSCNN(19)
     m.load_state_dict(sd)
     m = m.to(dev).train()
-    shape = (2, 3, 512, 1024) if half == "bf16shift" else (2, 3, 96, 160)
+    shape = {"bf16shift": (2, 3, 512, 1024), "bf16drop": (2, 3, 256, 512)}.get(half, (2, 3, 96, 160))
     x = torch.from_numpy(portable_init.input_tensor(3, shape)).to(dev)
     if half == "bf16shift":
         x = x + 4.0
-    if half in ("bf16", "bf16shift"):
+    if half in ("bf16", "bf16shift", "bf16drop"):
         x = x.to(torch.bfloat16)
     t = torch.from_numpy(portable_init.target_tensor(4, (2,) + shape[2:], 19, 0.05)).to(dev)
     res = {}

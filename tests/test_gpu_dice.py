@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("case", ["dice_c2", "dice_c1", "focal_c2", "focal_c4", "mix_aux"])
+@pytest.mark.parametrize("case", ["dice_c2", "dice_c1", "focal_c2", "focal_c4", "mix_aux",
+                                  "focal_c1"])
 def test_dice_losses_match_reference(case):
     from fast_scnn_pytorch_amd.loss import DiceLoss, FocalDiceLoss, MixDiceLoss
     g = load_golden("dice")
@@ -21,7 +22,7 @@ def test_dice_losses_match_reference(case):
     x2 = None
     if case.startswith("dice"):
         loss = DiceLoss()(x, t)
-    elif case == "focal_c2":
+    elif case in ("focal_c2", "focal_c1"):
         loss = FocalDiceLoss()(x, t)
     elif case == "focal_c4":
         loss = FocalDiceLoss(alpha=0.25, gamma=1.5)(x, t)

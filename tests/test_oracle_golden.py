@@ -119,7 +119,8 @@ def test_oracle_ohem_matches_reference(case):
         assert thr > 0.7
 
 
-@pytest.mark.parametrize("case", ["dice_c2", "dice_c1", "focal_c2", "focal_c4", "mix_aux"])
+@pytest.mark.parametrize("case", ["dice_c2", "dice_c1", "focal_c2", "focal_c4", "mix_aux",
+                                  "focal_c1"])
 def test_oracle_dice_matches_reference(case):
     """oracle Dice / Focal+Dice against the reference criteria run on CPU
     (tools/gen_dice_golden.py)."""
@@ -128,7 +129,7 @@ def test_oracle_dice_matches_reference(case):
     t = torch.from_numpy(g[case + ".target"])
     if case.startswith("dice"):
         loss = ref.dice_loss(x, t)
-    elif case == "focal_c2":
+    elif case in ("focal_c2", "focal_c1"):
         loss = ref.focal_dice_loss(x, t)
     elif case == "focal_c4":
         loss = ref.focal_dice_loss(x, t, alpha=0.25, gamma=1.5)
