@@ -342,295 +342,6 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
   stamp(a.stamps, 4);
 }
 
-// ---- forward: persistent tile loop, haloed tiles staged by LDS-DMA (double-buffered) ---------
-// A workgroup (worker wj of its channel chunk) walks a contiguous range of spatial tiles in
-// row-band order.  Each tile's haloed input is copied HBM -> LDS by global_load_lds_dwordx4 (no
-// VGPR destination: the staging costs no registers, unlike a register prefetch ring, which at
-// ~240 VGPRs held the round-4 tile loop to 2 workgroups per CU and lost to the one-tile kernel),
-// into the other of two LDS buffers while the current tile computes:
-//     issue DMA(t0) ; for t: [wait own DMA(t)] [IT: BN+ReLU own slots] barrier
-//                            issue DMA(t+1) into the other buffer ; compute + store tile t
-// so a CU keeps its resident workgroups' next tiles in flight for their whole life (one barrier
-// per tile).  The DMA image is lane-linear: slot k*nthr + tid is thread tid's k-th 16-B vector,
-// exactly the one-tile kernel's staging order; out-of-image and tail slots read a 16-B zero.
-// The copies are inline asm (M0 = the wave's LDS base), outside hipcc's waitcnt bookkeeping, so
-// the compiler neither drains them before the compute's LDS reads nor at the barrier; this kernel
-// waits for them itself (vmcnt(0) at the top of the next tile: they and the previous tile's
-// output stores are all that is outstanding).
-// IT (train, the input is a lazy BatchNorm+ReLU): after its own DMAs land, each thread applies
-// relu(fmaf(z, sc, sh)) (bn_apply's arithmetic, rounded to T) to its own slots in place --
-// its channel vector is fixed (slot % cbv == tid % cbv), so the 2V table values stay in registers;
-// padding stays zero.
-// Statistics (a.part) / the in-kernel BN finish (TL): per-thread sums shifted by the thread's
-// first output value, merged in fixed order into ONE record per worker (records [wy][3][C]).
-// workgroup -> (channel chunk cx, worker j of gridDim.y): XCD-contiguous (speed only): blocks
-// L = x (mod 8) share an XCD, so residue class x gets a contiguous range of workers, whose tile
-// ranges are neighbours (shared halo rows served by that XCD's L2)
-__device__ __forceinline__ void dw_worker(int& cx, int& j) {
-  const int gx = gridDim.x;
-  const long long T = (long long)gx * gridDim.y;
-  long long L = blockIdx.x + (long long)gx * blockIdx.y;
-  if ((T & 7) == 0) L = (L & 7) * (T >> 3) + (L >> 3);
-  cx = (int)(L % gx);
-  j = (int)(L / gx);
-}
-
-__device__ const uint4 g_dw_zero = {0u, 0u, 0u, 0u};
-
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds_dst)
-      : "memory");
-}
-
-template <typename T, int S, bool IT, bool TL = false>
-__global__ __launch_bounds__(256, 3) void dw_fwd_dma_kernel(DwArgs a, int cbv) {
-  using G = DwTile<T, S>;
-  constexpr int V = VecW<T>::V;
-  constexpr int LPT = G::LPT;                    // 16-B slots per thread and tile (= IR*IC/32)
-  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
-  const int tid = threadIdx.x, nthr = blockDim.x;
-  const int wave = tid >> 6;
-  const int QB = cbv * G::QPV;                   // quads per workgroup
-  const int q = tid % QB, grp = tid / QB;
-  const int gx = grp % G::GX, gy = grp / G::GX;
-  int cx, wj;
-  dw_worker(cx, wj);
-  const int wy = gridDim.y;
-  const int tiles_w = cdiv(a.Wo, G::TW), tiles_h = cdiv(a.Ho, G::TH);
-  const int ntiles = a.N * tiles_h * tiles_w;
-  const int t0 = (int)((long long)ntiles * wj / wy), t1 = (int)((long long)ntiles * (wj + 1) / wy);
-  const int cvb = cx * cbv;                      // first channel vector of the chunk
-  const int c0 = cvb * V + q * 4;                // first channel of the thread's quad
-  const int lv = tid % cbv, p0 = tid / cbv;      // the thread's DMA slots: pixel k*32 + p0
-  const T* xin = (const T*)a.x + (size_t)(cvb + lv) * V;
-  const int bufv = LPT * nthr;                   // 16-B slots per buffer
-  const uint32_t lds0 = (uint32_t)(uintptr_t)s_dyn;
-  auto tile_of = [&](int t, int& n, int& th0, int& tw0) {
-    const int tw = t % tiles_w, r = t / tiles_w;
-    n = r / tiles_h;
-    th0 = (r - n * tiles_h) * G::TH;
-    tw0 = tw * G::TW;
-  };
-  auto issue = [&](int t, int buf) {
-    int n, th0, tw0;
-    tile_of(t, n, th0, tw0);
-    const int hi0 = th0 * S - 1, wi0 = tw0 * S - 1;
-    const uint32_t base = lds0 + (uint32_t)(buf * bufv + wave * 64) * 16u;
-#pragma unroll
-    for (int k = 0; k < LPT; ++k) {
-      const int pix = k * 32 + p0;
-      const int r = pix / G::IC, col = pix - r * G::IC;
-      const int hi = hi0 + r, wi = wi0 + col;
-      const bool ok = pix < G::IR * G::IC && (unsigned)hi < (unsigned)a.H &&
-                      (unsigned)wi < (unsigned)a.W;
-      const void* src = ok ? (const void*)(xin + (((size_t)n * a.H + hi) * a.W + wi) * a.C)
-                           : (const void*)&g_dw_zero;
-      glds16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(k * nthr) * 16u));
-    }
-  };
-  stamp(a.stamps, 0);
-  if (t0 < t1) issue(t0, 0);
-  // per-worker registers: the thread's 4 channels' taps and epilogue affine, its vector's lazy BN
-  float wt[9][4], sc[4], sh[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) wt[t][j] = a.w[(size_t)(c0 + j) * 9 + t];
-    sc[j] = a.scale ? a.scale[c0 + j] : 1.f;
-    sh[j] = a.scale ? a.shift[c0 + j] : 0.f;
-  }
-  float isc[IT ? V : 1], ish[IT ? V : 1];
-  if constexpr (IT) {
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      isc[j] = a.in_scale[(cvb + lv) * V + j];
-      ish[j] = a.in_shift[(cvb + lv) * V + j];
-    }
-  }
-  const bool stats = a.part != nullptr;
-  float s1[4], s2[4], shf[4];
-  float cnt = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s1[j] = s2[j] = shf[j] = 0.f;
-  const int pstride = cbv * V;                   // elements per staged pixel
-  const int lr0 = gy * G::HS * S, lc0 = gx * G::WS * S;
-
-#pragma unroll 1
-  for (int t = t0; t < t1; ++t) {
-    const int buf = (t - t0) & 1;
-    int n, th0, tw0;
-    tile_of(t, n, th0, tw0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's DMA of tile t landed
-    uint4* sb = s_dyn + buf * bufv;
-    if constexpr (IT) {
-      const int hi0 = th0 * S - 1, wi0 = tw0 * S - 1;
-#pragma unroll
-      for (int k = 0; k < LPT; ++k) {
-        const int pix = k * 32 + p0;
-        const int r = pix / G::IC, col = pix - r * G::IC;
-        const bool ok = pix < G::IR * G::IC && (unsigned)(hi0 + r) < (unsigned)a.H &&
-                        (unsigned)(wi0 + col) < (unsigned)a.W;
-        uint4& v = sb[k * nthr + tid];
-        v = sel4(ok, bnrelu_vec<T>(v, isc, ish));
-      }
-    }
-    // every wave's DMA of tile t is visible (and, IT, transformed); every wave is done reading
-    // the other buffer (tile t - 1)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (t + 1 < t1) issue(t + 1, buf ^ 1);
-    if (t == t0) stamp(a.stamps, 1);
-    const T* sl = reinterpret_cast<const T*>(sb);
-    float acc[G::HS][G::WS][4];
-#pragma unroll
-    for (int r = 0; r < G::HS; ++r)
-#pragma unroll
-      for (int p = 0; p < G::WS; ++p)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[r][p][j] = 0.f;
-#pragma unroll
-    for (int rr = 0; rr < G::NR; ++rr) {
-      asm volatile("" ::: "memory");  // one input row of quads at a time (see dw_fwd_kernel)
-#pragma unroll
-      for (int ci = 0; ci < G::NC; ++ci) {
-        float v[4];
-        quad_ld(sl + ((lr0 + rr) * G::IC + lc0 + ci) * pstride + q * 4, v);
-#pragma unroll
-        for (int r = 0; r < G::HS; ++r) {
-          const int kh = rr - r * S;
-          if (kh < 0 || kh > 2) continue;
-#pragma unroll
-          for (int p = 0; p < G::WS; ++p) {
-            const int kw = ci - p * S;
-            if (kw < 0 || kw > 2) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[r][p][j] = fmaf(v[j], wt[kh * 3 + kw][j], acc[r][p][j]);
-          }
-        }
-      }
-    }
-    const int ho0 = th0 + gy * G::HS, wo0 = tw0 + gx * G::WS;
-    const int nrow = max(0, min(G::HS, a.Ho - ho0)), ncol = max(0, min(G::WS, a.Wo - wo0));
-#pragma unroll
-    for (int r = 0; r < G::HS; ++r) {
-      if (r >= nrow) continue;
-      T* yb = (T*)a.y + (((size_t)n * a.Ho + ho0 + r) * a.Wo + wo0) * a.C + c0;
-#pragma unroll
-      for (int p = 0; p < G::WS; ++p) {
-        if (p >= ncol) continue;
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v = acc[r][p][j] * sc[j] + sh[j];
-          o[j] = a.relu ? fmaxf(v, 0.f) : v;
-        }
-        quad_st(yb + (size_t)p * a.C, o);
-        if (stats) {  // shifted sums; the shift is the thread's first output value
-          if (cnt == 0.f) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) shf[j] = o[j];
-          }
-          cnt += 1.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float d = o[j] - shf[j];
-            s1[j] += d;
-            s2[j] += d * d;
-          }
-        }
-      }
-    }
-  }
-  stamp(a.stamps, 2);
-  if (!stats) return;
-  // ---- one record per worker: (n, mean, M2) per thread, Chan-merged over the pixel groups in
-  // fixed order (the scratch aliases the first tile buffer: every read of it is done)
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  float* s_red = reinterpret_cast<float*>(s_dyn);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float m = cnt > 0.f ? shf[j] + s1[j] / cnt : 0.f;
-    s2[j] = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
-    s1[j] = m;
-  }
-#pragma unroll
-  for (int pass = 0; pass < 3; ++pass)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      s_red[((pass * G::G + grp) * QB + q) * 4 + j] = pass == 0 ? s1[j] : (pass == 1 ? s2[j] : cnt);
-  __syncthreads();
-  float* rec = a.part + (size_t)wj * 3 * a.C;
-  if (grp == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float nn = 0.f, mean = 0.f, m2 = 0.f;
-      for (int g2 = 0; g2 < G::G; ++g2) {
-        const float nb = s_red[((2 * G::G + g2) * QB + q) * 4 + j];
-        if (nb <= 0.f) continue;
-        const float mb = s_red[((0 * G::G + g2) * QB + q) * 4 + j];
-        const float qb = s_red[((1 * G::G + g2) * QB + q) * 4 + j];
-        const float tn = nn + nb, d = mb - mean;
-        mean += d * (nb / tn);
-        m2 += qb + d * d * (nn * nb / tn);
-        nn = tn;
-      }
-      st_wt(rec + c0 + j, mean);
-      st_wt(rec + a.C + c0 + j, m2);
-      st_wt(rec + 2 * a.C + c0 + j, nn);
-    }
-  }
-  stamp(a.stamps, 3);
-  if constexpr (TL)
-    tail_finish<true>(a.part, wy, a.C, wj, cvb * V, cbv * V, cx, a.tail,
-                      reinterpret_cast<double*>(s_dyn));
-  stamp(a.stamps, 4);
-}
-
-// channel vectors per DMA-forward workgroup: the largest divisor of C / V whose staged tile
-// (LPT * 32 * cbv 16-B slots) is <= 26 KiB, so two buffers per workgroup and 3 workgroups per CU
-// fit the CU's 160 KiB of LDS
-constexpr int DWD_TILE_MAX = 26 * 1024;
-template <typename T, int S>
-static int dw_dma_cbv(int CV) {
-  for (int b = DWL_CB; b > 1; --b)
-    if (CV % b == 0 && (size_t)DwTile<T, S>::LPT * 32 * b * 16 <= (size_t)DWD_TILE_MAX) return b;
-  return 1;
-}
-template <typename T, int S>
-static size_t dw_dma_shm(int cbv) {
-  const size_t buf = (size_t)DwTile<T, S>::LPT * 32 * cbv * 16;
-  const size_t red = (size_t)3 * cbv * 32 * 4 * 4;  // the record scratch (aliases buffer 0)
-  return 2 * buf > red ? 2 * buf : red;
-}
-// FSCNN_DW_DMA=1: the DMA forward (A/B while it is measured)
-static bool dw_dma_on() {
-  static const bool on = [] {
-    const char* e = getenv("FSCNN_DW_DMA");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-// the DMA forward's grid: gx channel chunks x wy workers, every workgroup resident
-template <typename T, int S>
-static dim3 dw_dma_grid(int N, int Ho, int Wo, int C, int& cbv) {
-  using G = DwTile<T, S>;
-  cbv = dw_dma_cbv<T, S>(C / VecW<T>::V);
-  const int gx = C / VecW<T>::V / cbv;
-  const long long ntiles = (long long)N * cdiv(Ho, G::TH) * cdiv(Wo, G::TW);
-  const int waves = cbv * 32 / 64 > 0 ? cbv * 32 / 64 : 1;
-  int per_cu = (int)(160 * 1024 / (dw_dma_shm<T, S>(cbv) + 512));
-  if (per_cu * waves > 12) per_cu = 12 / waves;  // 3 waves per SIMD (launch bounds)
-  if (per_cu < 1) per_cu = 1;
-  long long wy = cdiv((long long)per_cu * 256, gx);
-  if (wy > ntiles) wy = ntiles;
-  if (wy < 1) wy = 1;
-  return dim3(gx, (unsigned)wy, 1);
-}
-
 // dynamic LDS of the tile kernels: the haloed input tile of cbv vectors + 4 floats per thread
 template <typename T, int S>
 static size_t dw_shm(int cbv) {
@@ -642,11 +353,7 @@ static size_t dw_shm(int cbv) {
 // resident, the next tile's loads in flight during the current tile's compute -- measured r04
 // 6.20 vs 6.04 ms per cfg3 step: at <= 2 workgroups per CU one tile of prefetch hid less HBM
 // latency than this kernel's occupancy does; removed in r05.)
-static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv, bool fwd = false) {
-  if (fwd && dw_dma_on()) {
-    if (V == 4) return S == 1 ? dw_dma_grid<float, 1>(N, Ho, Wo, C, cbv) : dw_dma_grid<float, 2>(N, Ho, Wo, C, cbv);
-    return S == 1 ? dw_dma_grid<bf16, 1>(N, Ho, Wo, C, cbv) : dw_dma_grid<bf16, 2>(N, Ho, Wo, C, cbv);
-  }
+static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv) {
   cbv = dw_cbv(C / V);
   int TH, TW;
   if (V == 4) {
@@ -661,7 +368,7 @@ static dim3 dw_grid(int N, int Ho, int Wo, int C, int V, int S, int& cbv, bool f
 
 int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
   int cbv;
-  dim3 g = dw_grid(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8, stride, cbv, true);
+  dim3 g = dw_grid(N, Ho, Wo, C, dtype == DT_F32 ? 4 : 8, stride, cbv);
   return (int)(g.y * g.z);
 }
 
@@ -671,18 +378,6 @@ static void dw_launch_fwd_t(const DwArgs& a, dim3 grid, int nthr, int cbv, hipSt
     if (a.tail_ink) dw_fwd_kernel<T, 1, true, false, true, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
     else dw_fwd_kernel<T, 1, true, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
     return;
-  }
-  if constexpr (!FLIP) {
-    if (dw_dma_on()) {  // (grid: dw_grid fwd)
-      if (a.stride == 1) {
-        if (a.tail_ink) dw_fwd_dma_kernel<T, 1, IT, true><<<grid, nthr, dw_dma_shm<T, 1>(cbv), st>>>(a, cbv);
-        else dw_fwd_dma_kernel<T, 1, IT><<<grid, nthr, dw_dma_shm<T, 1>(cbv), st>>>(a, cbv);
-      } else {
-        if (a.tail_ink) dw_fwd_dma_kernel<T, 2, IT, true><<<grid, nthr, dw_dma_shm<T, 2>(cbv), st>>>(a, cbv);
-        else dw_fwd_dma_kernel<T, 2, IT><<<grid, nthr, dw_dma_shm<T, 2>(cbv), st>>>(a, cbv);
-      }
-      return;
-    }
   }
   if (!FLIP && a.tail_ink) {  // train forward with the in-kernel BN finish
     if (a.stride == 1) dw_fwd_kernel<T, 1, false, IT, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
@@ -697,7 +392,7 @@ template <bool FLIP, bool IT, bool BR = false>
 static int dw_launch_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   int cbv;
-  dim3 grid = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv, !FLIP);
+  dim3 grid = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
   if (grid.z > 65535 || grid.y > 65535) {
     set_error("dw: grid too large (%u x %u)", grid.y, grid.z);
     return E_UNSUPPORTED;
@@ -731,7 +426,7 @@ int dw_fwd(const DwArgs& a, int dtype, hipStream_t st) {
   int P = 0;
   if (a.part && a.tail.counters) {  // BN finish: in the kernel when the records fit its counters
     int cbv;
-    const dim3 g = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv, true);
+    const dim3 g = dw_grid(a.N, a.Ho, a.Wo, a.C, V, a.stride, cbv);
     P = (int)(g.y * g.z);
     b.tail_ink = a.tail.tsum && a.C <= TAIL_CMAX && tail_fits(P, (int)g.x);
   }

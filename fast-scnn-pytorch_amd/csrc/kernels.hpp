@@ -296,7 +296,8 @@ struct PpmBranchBwd {
   const void* dy; int lddy;  // gradient of y
   const void* y; int ldy;    // forward output (its ReLU mask)
   const void* z;             // [M][32]
-  const float *mean, *invstd, *scale;
+  const float *mean, *invstd, *scale;  // (the forward's; the backward recomputes them in fp64)
+  const float* gamma;        // BN weight [32]
   const void* x;             // pooled rows [M][K]
   const void* w;             // [32][K], storage type
   float *dgamma, *dbeta;     // [32]

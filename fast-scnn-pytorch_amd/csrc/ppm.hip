@@ -192,18 +192,21 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
   float* s_w = sm;                  // [C][K]
   float* s_dz = s_w + PPM_C * K;    // [M][C + 1], dz as stored (rounded)
   __shared__ double s_r[2][PPM_T];
-  __shared__ float s_cf[2 * PPM_C];
   const T* Wt = (const T*)b.w;
   for (int i = tid; i < PPM_C * K; i += PPM_T) s_w[i] = ld1(Wt + i);
   const T* G = (const T*)b.dy;
   const T* Y = (const T*)b.y;
   const T* Z = (const T*)b.z;
-  const float mean = b.mean[n], istd = b.invstd[n], scale = b.scale[n];
-  // BN backward sums: dy masked by the forward ReLU (y > 0), xhat of the stored z
+  // BN backward in fp64 from the stored z: the branch's batch statistics are recomputed here
+  // (block-local, M <= 512 values per channel) and x_hat, the sums and dz formed in fp64.  The
+  // pool-1 branch normalises N values per channel (2 at batch 2): x_hat = +-a with 1 - a^2 =
+  // eps / (d^2 + eps) small, so dz = scale (dy - c0 - x_hat c1) cancels to ~(1 - a^2) |dy| and
+  // a float x_hat (relative error 1e-7) made it ~1 % rounding noise, which the pool backward
+  // spreads over every upstream gradient.
   // the slice's rows are loaded once, 4 rows per batch of loads, and kept for the dz pass
   constexpr int RMAX = 32;  // rows per slice held in registers (M <= 16 * RMAX)
-  float gr[RMAX], xr[RMAX];
-  double t1 = 0.0, t2 = 0.0;
+  float gr[RMAX], zr[RMAX];
+  double t0 = 0.0;
   const int nr = M > sl ? (M - sl + 15) / 16 : 0;
 #pragma unroll
   for (int i0 = 0; i0 < RMAX; i0 += 4) {
@@ -219,32 +222,45 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool ok = i0 + u < nr;
-      const float gv = (ok && y4[u] > 0.f) ? g4[u] : 0.f;
-      const float xh = (z4[u] - mean) * istd;
-      gr[i0 + u] = gv;
-      xr[i0 + u] = xh;
-      t1 += gv;
-      t2 += (double)gv * xh;
+      gr[i0 + u] = (ok && y4[u] > 0.f) ? g4[u] : 0.f;
+      zr[i0 + u] = ok ? z4[u] : 0.f;
+      t0 += ok ? (double)z4[u] : 0.0;
     }
   }
-  s_r[0][tid] = t1;
-  s_r[1][tid] = t2;
-  __syncthreads();
-  if (tid < PPM_C) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int j = 0; j < 16; ++j) {
-      s1 += s_r[0][j * PPM_C + tid];
-      s2 += s_r[1][j * PPM_C + tid];
-    }
-    bn_bwd_finish(tid, PPM_C, s1, s2, (double)M, gpart == 0 ? b.dgamma : nullptr,
-                  gpart == 0 ? b.dbeta : nullptr, s_cf, BnBwdTab());
-  }
-  __syncthreads();
-  const float c0 = s_cf[n], c1 = s_cf[PPM_C + n];
+  // (fixed-order block sums of the 16 row slices: deterministic)
+  auto colsum = [&](double v, int k) -> double {
+    __syncthreads();
+    s_r[k][tid] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int j = 0; j < 16; ++j) r += s_r[k][j * PPM_C + n];
+    return r;
+  };
+  const double mean = colsum(t0, 0) / (double)M;
+  double tv = 0.0;
+#pragma unroll
+  for (int i = 0; i < RMAX; ++i)
+    if (i < nr) tv += ((double)zr[i] - mean) * ((double)zr[i] - mean);
+  const double istd = 1.0 / sqrt(colsum(tv, 1) / (double)M + (double)BN_EPS);
+  double t1 = 0.0, t2 = 0.0;
 #pragma unroll
   for (int i = 0; i < RMAX; ++i) {
     if (i >= nr) continue;
-    s_dz[(sl + 16 * i) * DZ + n] = round_as<T>(scale * (gr[i] - c0 - xr[i] * c1));
+    t1 += (double)gr[i];
+    t2 += (double)gr[i] * (((double)zr[i] - mean) * istd);
+  }
+  const double s1 = colsum(t1, 0), s2 = colsum(t2, 1);
+  if (tid < PPM_C && gpart == 0) {  // dgamma = sum dy_r x_hat, dbeta = sum dy_r
+    b.dgamma[n] = (float)s2;
+    b.dbeta[n] = (float)s1;
+  }
+  const double c0 = s1 / (double)M, c1 = s2 / (double)M;
+  const double scale = (double)b.gamma[n] * istd;
+#pragma unroll
+  for (int i = 0; i < RMAX; ++i) {
+    if (i >= nr) continue;
+    const double xh = ((double)zr[i] - mean) * istd;
+    s_dz[(sl + 16 * i) * DZ + n] = round_as<T>((float)(scale * ((double)gr[i] - c0 - xh * c1)));
   }
   __syncthreads();
   // weight gradient dW[c][k] = sum_m dz[m][c] x[m][k]: thread (k, 8-channel group), m ascending

@@ -45,9 +45,19 @@ def _reference(m, sd, x, t, nc, training, drop_seed=None):
     flips = relu_flips(masks, acts)
     assert all(w <= 1e-4 for _, _, w in flips), flips
     l64, g64, dx64 = _oracle(sd, x, t, nc, training, drop_seed, relu_masks=masks)
-    _, g32, dx32 = _oracle(sd, x, t, nc, training, drop_seed, dt=torch.float32, relu_masks=masks)
-    spread = {k: (g32[k].double() - g64[k].double()).norm().item() for k in g64}
-    dx_spread = (dx32.double() - dx64.double()).norm().item()
+    # the reference's own fp32 variability (test_gpu_model.reference_fp32_spread): as is,
+    # single-threaded, and on the input moved by one ulp
+    runs = [_oracle(sd, x, t, nc, training, drop_seed, dt=torch.float32, relu_masks=masks)]
+    nth = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        runs.append(_oracle(sd, x, t, nc, training, drop_seed, dt=torch.float32, relu_masks=masks))
+    finally:
+        torch.set_num_threads(nth)
+    xp = torch.nextafter(x.float(), torch.full_like(x.float(), float("inf")))
+    runs.append(_oracle(sd, xp, t, nc, training, drop_seed, dt=torch.float32, relu_masks=masks))
+    spread = {k: max((r[1][k].double() - g64[k].double()).norm().item() for r in runs) for k in g64}
+    dx_spread = max((r[2].double() - dx64.double()).norm().item() for r in runs)
     return l64, g64, spread, dx64, dx_spread
 
 

@@ -13,7 +13,8 @@ Two steps, the first under rocprofv3 on the GPU box:
 issue order) a few warm-up cfg3 bf16 train steps, then ONE profiled train step and ONE profiled
 cfg2 fp32 eval forward with the library's launch profiler in "every launch" mode: it lists the
 launch scopes (layer tag, kernel family, algorithmic bytes and flops) in issue order.  A
-`hipDeviceSynchronize`-separated marker kernel (a 1-element torch fill) brackets each phase.
+synchronised marker kernel (a 1-element torch bitwise_not, which no step launches) brackets each
+phase.
 `table` walks the trace's dispatches between the markers in order and gives each scope the next
 dispatch whose kernel name belongs to the scope's family (unscoped launches -- weight prep, slab
 reductions, SGD -- are skipped), then prints the per-launch and per-family tables.
@@ -46,7 +47,7 @@ FAMILY_RE = {
     "ppm_branches": r"ppm_(fwd|fwd_lds|bwd)_kernel",
     "ir_block": r"ir_block_kernel",
 }
-MARK = re.compile(r"[Ff]ill")  # torch's fill kernel (the phase marker)
+MARK = re.compile(r"bitwise_not")  # torch's bitwise_not kernel (the phase marker: no step uses it)
 
 
 def record(out, eval_only=False):
@@ -79,11 +80,11 @@ def record(out, eval_only=False):
                         "bytes": by.value, "flops": fl.value, "event_us": t.value * 1e3})
         return res
 
-    marker = torch.zeros(1, device=dev)
+    marker = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def mark():
         torch.cuda.synchronize()
-        marker.fill_(1.0)
+        marker.bitwise_not_()
         torch.cuda.synchronize()
 
     m = FastSCNN(19)
@@ -128,9 +129,8 @@ def table(trace, scopes_json, out):
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     marks = [i for i, n in enumerate(names) if MARK.search(n) and "fscnn" not in n]
     phases = json.load(open(scopes_json))["phases"]
-    # the phases are the LAST len(phases) marker-bracketed spans (warm-up runs precede them)
-    spans = [(marks[i] + 1, marks[i + 1]) for i in range(len(marks) - 1)]
-    spans = [sp for sp in spans if sp[1] > sp[0]][-len(phases):]
+    # every phase is bracketed by its own pair of markers (warm-up runs lie between the pairs)
+    spans = [(marks[2 * i] + 1, marks[2 * i + 1]) for i in range(len(marks) // 2)]
     lines = ["# Per-layer kernel time (MI355X, one GPU, rocprofv3 kernel trace)", "",
              "Generated by `tools/rocprof_layers.py`: launch order and algorithmic bytes from the "
              "library's launch profiler, durations from `rocprofv3 --kernel-trace` of the same run "
