@@ -161,7 +161,7 @@ extern "C" const char* fscnn_prof_kind_name(int kind) {
                                         "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
                                         "upsample_bwd", "cross_entropy", "conv0_wgrad",
                                         "bn_bwd_reduce", "bn_finalize", "ppm_branches",
-                                        "ir_block"};
+                                        "ir_block", "ltd_stem"};
   return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
 }
 
@@ -707,6 +707,32 @@ int fscnn_block_ir_fwd(const void* x, int ldx, int dtype, int N, int H, int W, i
   a.sc_e = scale_e; a.sh_e = shift_e; a.sc_d = scale_d; a.sh_d = shift_d;
   a.sc_p = scale_p; a.sh_p = shift_p; a.residual = residual;
   return ir_block_fwd(a, dtype, S(stream));
+}
+
+int fscnn_block_ltd_fwd(const void* x, int x_dtype, int dtype, int N, int H, int W,
+                        const float* w_conv, const float* scale_0, const float* shift_0,
+                        const float* w_dw, const float* scale_d, const float* shift_d,
+                        const void* w_pw, const float* scale_p, const float* shift_p, void* y,
+                        int ldy, void* stream) {
+  if (!x || !y || !w_conv || !scale_0 || !shift_0 || !w_dw || !scale_d || !shift_d || !w_pw ||
+      !scale_p || !shift_p) {
+    set_error("fscnn_block_ltd_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || x_dtype < 0 || x_dtype > 2 || H < 3 || W < 3) {
+    set_error("fscnn_block_ltd_fwd: dtype %d x_dtype %d H %d W %d", dtype, x_dtype, H, W);
+    return E_INVALID;
+  }
+  StemArgs a{};
+  a.x = x; a.x_dtype = x_dtype;
+  a.N = N; a.H = H; a.W = W;
+  a.H1 = (H - 3) / 2 + 1; a.W1 = (W - 3) / 2 + 1;
+  a.H2 = (a.H1 - 1) / 2 + 1; a.W2 = (a.W1 - 1) / 2 + 1;
+  a.w0 = w_conv; a.sc0 = scale_0; a.sh0 = shift_0;
+  a.wd = w_dw; a.scd = scale_d; a.shd = shift_d;
+  a.wp = w_pw; a.scp = scale_p; a.shp = shift_p;
+  a.y = y; a.ldy = ldy;
+  return stem_fwd(a, dtype, S(stream));
 }
 
 }  // extern "C"

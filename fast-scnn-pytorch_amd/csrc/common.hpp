@@ -231,6 +231,51 @@ __device__ __forceinline__ void gs_mma_x3(const uint4 (&w)[3], const uint4 (&x)[
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
 }
 
+// LearningToDownsample.conv (conv0.hip, stem.hip): MFMA helpers for the im2col GEMM out[px][co] = sum_k patch[px][k] * W[co][k], K = 27 -> 32:
+// lane (li, lq) supplies k = 8*lq .. 8*lq+7 for its row (pixel li / channel li).
+template <int BF>
+struct C0Mma;
+template <>
+struct C0Mma<2> {  // fp16 operands (inference plans of dtype fp16): v_mfma_f32_16x16x32_f16
+  using Frag = h16x8;
+  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
+    Frag f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (_Float16)v[e];
+    return f;
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc, 0, 0, 0);
+  }
+};
+template <>
+struct C0Mma<1> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x 16 co
+  using Frag = i16x8;
+  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
+    Frag f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (short)f2bf(v[e]);
+    return f;
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+};
+template <>
+struct C0Mma<0> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
+  struct Frag { float v[8]; };
+  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
+    Frag f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f.v[e] = v[e];
+    return f;
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[e], b.v[e], acc, 0, 0, 0);
+  }
+};
+
 // ---- 4-element vectors (16 B fp32 / 8 B bf16) ------------------------------------------------
 __device__ __forceinline__ void st4v(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
@@ -409,7 +454,7 @@ enum Status : int { OK = 0, E_INVALID = -1, E_UNSUPPORTED = -2, E_HIP = -3 };
 enum ProfKind : int {
   PK_NONE = 0, PK_CONV0_FWD, PK_DW_FWD, PK_DW_DGRAD, PK_DW_WGRAD, PK_GEMM_NT, PK_GEMM_TN,
   PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_CONV0_WGRAD, PK_BN_BWD_RED, PK_BN_FIN,
-  PK_PPM, PK_IR, PK_COUNT
+  PK_PPM, PK_IR, PK_STEM, PK_COUNT
 };
 constexpr int PK_ALL = 100;  // record every kind (per-launch layer report)
 extern int g_prof_kind;  // kind being recorded (PK_NONE = off)
@@ -447,7 +492,14 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int slot) {
   if (st && (threadIdx.x & 63) == 0) {
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     const size_t b = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-    if (b < 8192) st[(b * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + slot] = t;
+    if (b < 8192) {
+      st[(b * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + slot] = t;
+      if (slot == 0) {  // placement of the wave: XCC id << 32 | HW_ID (CU, SIMD, SE) in slot 7
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        st[(b * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + 7] = ((unsigned long long)(xcc & 15) << 32) | hw;
+      }
+    }
   }
 }
 

@@ -17,50 +17,7 @@ constexpr int C0_IN_W = 2 * C0_TILE + 1;  // staged input columns
 constexpr int C0_OSTR = 36;              // LDS floats per staged output pixel (16B aligned)
 
 
-// MFMA helpers for the im2col GEMM out[px][co] = sum_k patch[px][k] * W[co][k], K = 27 -> 32:
-// lane (li, lq) supplies k = 8*lq .. 8*lq+7 for its row (pixel li / channel li).
-template <int BF>
-struct C0Mma;
-template <>
-struct C0Mma<2> {  // fp16 operands (inference plans of dtype fp16): v_mfma_f32_16x16x32_f16
-  using Frag = h16x8;
-  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
-    Frag f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = (_Float16)v[e];
-    return f;
-  }
-  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc, 0, 0, 0);
-  }
-};
-template <>
-struct C0Mma<1> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x 16 co
-  using Frag = i16x8;
-  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
-    Frag f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = (short)f2bf(v[e]);
-    return f;
-  }
-  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-  }
-};
-template <>
-struct C0Mma<0> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
-  struct Frag { float v[8]; };
-  static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
-    Frag f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f.v[e] = v[e];
-    return f;
-  }
-  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[e], b.v[e], acc, 0, 0, 0);
-  }
-};
+// (MFMA helpers of the im2col GEMM: common.hpp C0Mma)
 
 // XCD-contiguous block order: linear blocks L = x (mod 8) share an XCD, so residue class x takes
 // the contiguous logical range [x*T/8, (x+1)*T/8) of (segment, row) in segment-fastest order.

@@ -543,7 +543,6 @@ __global__ __launch_bounds__(HD_T, 2) void ce_head2_kernel(CeHeadArgs a) {
           a0[c] = __builtin_elementwise_fma(r0, u, a0[c]);
           a1[c] = __builtin_elementwise_fma(r1, u, a1[c]);
         }
-        if (cb == 0 && h == h_lo) stamp(a.stamps, 7);
       }
     }
     if (cb == 0) stamp(a.stamps, 2);

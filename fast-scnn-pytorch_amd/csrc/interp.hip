@@ -625,40 +625,76 @@ int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
 
 // backward: dfeats[bin][n][c] = sum_{h,w} wy(h,bi) wx(w,bj) dy[n,h,w,coff+lv*CF+c]  (gather)
 // Separable, one workgroup per (level, image): phase 1 reduces every row of the level's dy slice
-// onto the k column bins (rows[h][bj][c] = sum_w wx(w,bj) dy[h,w,c], one thread per (c, row)),
-// phase 2 folds the rows onto the k row bins (one thread per (c, bin)), fixed order throughout.
-constexpr int PPB_THREADS = 1024;
+// onto the k column bins (rows[h][bj][c] = sum_w wx(w,bj) dy[h,w,c]), phase 2 folds the rows onto
+// the k row bins (one thread per (c, bin)), fixed order throughout.  Phase 1: a thread takes one
+// 16-B channel vector of one row and the columns w = s, s + 8, ... of its segment s (8 segments on
+// 8 adjacent lanes): its <= 8 vector loads per batch are all in flight at once (one memory round
+// trip for W <= 64), and the 8 segments' bin sums meet in a fixed xor butterfly.
+constexpr int PPB_THREADS = 512;
 constexpr int PPB_MAXH = 80;  // LDS rows[H][6][CF<=32] fp32
+constexpr int PPB_SEG = 8;    // column segments (adjacent lanes)
 
 template <typename T>
 __global__ __launch_bounds__(PPB_THREADS) void ppm_up_bwd_kernel(PpmUpArgs a, void* dfeats) {
+  constexpr int V = VecW<T>::V;
   __shared__ float rows[PPB_MAXH * 6 * 32];
   const int lv = blockIdx.x, n = blockIdx.y;
   const int k = PP_LEVELS[lv];
   const int base = lv == 0 ? 0 : (lv == 1 ? 1 : (lv == 2 ? 5 : 14));
   const float sh = ac_scale(k, a.H), sw = ac_scale(k, a.W);
-  const int CF = a.CF, G = PPB_THREADS / CF;
-  const int c = threadIdx.x % CF, g = threadIdx.x / CF;
-  const T* gp = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * CF + c;
-  for (int h = g; h < a.H; h += G) {
-    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const T* gr = gp + (size_t)h * a.W * a.ldy;
-    for (int w0 = 0; w0 < a.W; w0 += 8) {
-      float v[8];
+  const int CF = a.CF, CV = CF / V;
+  const int sg = threadIdx.x % PPB_SEG, rest = threadIdx.x / PPB_SEG;
+  const int cv = rest % CV;
+  const int RP = PPB_THREADS / PPB_SEG / CV;  // rows per pass
+  const T* gp = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * CF + cv * V;
+  // (the pass loop is uniform across the wave's 8-lane segment groups: RP rows per pass)
+  for (int h0 = 0; h0 < a.H; h0 += RP) {
+    const int h = h0 + rest / CV;
+    const bool hok = h < a.H;
+    float acc[6][V];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {  // 8 independent loads per batch (clamped + selected)
-        const int w = w0 + u < a.W ? w0 + u : a.W - 1;
-        v[u] = w0 + u < a.W ? ld1(gr + (size_t)w * a.ldy) : 0.f;
+    for (int bj = 0; bj < 6; ++bj)
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[bj][e] = 0.f;
+    const T* gr = gp + (size_t)(hok ? h : 0) * a.W * a.ldy;
+    for (int w0 = sg; w0 < a.W; w0 += 8 * PPB_SEG) {
+      float v[8][V];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // all loads of the batch issued, then used
+        const int w = w0 + u * PPB_SEG;
+        ldv(gr + (size_t)(w < a.W ? w : 0) * a.ldy, v[u]);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const Lerp lw = ac_lerp(w0 + u < a.W ? w0 + u : a.W - 1, k, a.W, sw);
+        const int w = w0 + u * PPB_SEG;
+        const bool ok = hok && w < a.W;
+        const Lerp lw = ac_lerp(ok ? w : 0, k, a.W, sw);
 #pragma unroll
-        for (int bj = 0; bj < 6; ++bj)
-          acc[bj] += ((lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f)) * v[u];
+        for (int bj = 0; bj < 6; ++bj) {
+          const float wt = ok ? (lw.i0 == bj ? lw.l0 : 0.f) + (lw.i1 == bj ? lw.l1 : 0.f) : 0.f;
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[bj][e] = fmaf(wt, v[u][e], acc[bj][e]);
+        }
       }
     }
-    for (int bj = 0; bj < k; ++bj) rows[(h * 6 + bj) * 32 + c] = acc[bj];
+#pragma unroll
+    for (int bj = 0; bj < 6; ++bj)
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        float t = acc[bj][e];
+        t += __shfl_xor(t, 1);
+        t += __shfl_xor(t, 2);
+        t += __shfl_xor(t, 4);
+        acc[bj][e] = t;
+      }
+    if (sg == 0 && hok) {
+#pragma unroll
+      for (int bj = 0; bj < 6; ++bj)
+        if (bj < k) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) rows[(h * 6 + bj) * 32 + cv * V + e] = acc[bj][e];
+        }
+    }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < k * k * CF; t += PPB_THREADS) {
@@ -674,7 +710,9 @@ __global__ __launch_bounds__(PPB_THREADS) void ppm_up_bwd_kernel(PpmUpArgs a, vo
 }
 
 int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
-  if (a.CF <= 0 || a.CF > 32 || PPB_THREADS % a.CF || a.H > PPB_MAXH || a.N > 65535) {
+  const int V = dtype == DT_F32 ? 4 : 8;
+  if (a.CF <= 0 || a.CF > 32 || a.CF % V || a.ldy % V || a.coff % V || a.H > PPB_MAXH ||
+      a.N > 65535) {
     set_error("ppm_up_bwd: CF=%d H=%d unsupported", a.CF, a.H);
     return E_UNSUPPORTED;
   }

@@ -403,6 +403,23 @@ struct IrArgs {
 bool ir_block_ok(const IrArgs& a, int dtype);
 int ir_block_fwd(const IrArgs& a, int dtype, hipStream_t st);
 
+// inference LearningToDownsample stem (stem.hip): conv0 + BN + ReLU -> dsconv1.dw + BN + ReLU ->
+// dsconv1.pw + BN + ReLU in one launch (models/fast_scnn.py:153-154), BatchNorms folded
+struct StemArgs {
+  const void* x; int x_dtype;  // NCHW [N,3,H,W] image: 0 fp32, 1 bf16, 2 fp16 (16-B aligned, W % 16 B)
+  int N, H, W;
+  int H1, W1, H2, W2;          // conv0 (3x3 s2 p0) and dsconv1 (3x3 s2 p1) output maps
+  const float* w0;             // conv0 weights [32][27] fp32
+  const float *sc0, *sh0;      // folded BN of conv0
+  const float* wd;             // dsconv1.dw weights [32][9] fp32
+  const float *scd, *shd;      // folded BN of dsconv1.dw
+  const void* wp;              // dsconv1.pw weights [48][32] in the storage dtype
+  const float *scp, *shp;      // folded BN of dsconv1.pw
+  void* y; int ldy;            // NHWC [N,H2,W2] x 48 channels (row stride ldy elements)
+};
+bool stem_ok(const StemArgs& a);
+int stem_fwd(const StemArgs& a, int dtype, hipStream_t st);
+
 // input gradient of conv0 (autograd of the image through models/fast_scnn.py:153)
 struct Conv0DgradArgs {
   const void* dz;  // NHWC [N,Ho,Wo,32] in the plan dtype (conv0's BN-backward output)

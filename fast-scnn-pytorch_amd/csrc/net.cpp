@@ -944,6 +944,15 @@ struct Exec {
     return u.lazy ? OK : apply(u, true);
   }
 
+  // inference stem fusion (stem.hip); FSCNN_STEM_FUSED=0 runs the three unfused launches (the
+  // bit-identity test, tests/test_gpu_switches.py)
+  static bool stem_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("FSCNN_STEM_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   int fold_all() {
     FoldTable t{};
     auto add = [&](const BnL& bn, const Unit& u, const ConvL* conv) {
@@ -981,7 +990,19 @@ struct Exec {
     if (!train || frozen) TRY(fold_all());
     g_prof_tag = pl.c0.name.c_str();
     // ---- LearningToDownsample ----
-    {
+    StemArgs sa{};
+    if (!train) {  // inference: conv + dsconv1 (dw, pw) in one launch (stem.hip) when it fits
+      sa.x = r.x; sa.x_dtype = r.x_dtype;
+      sa.N = N; sa.H = pl.H; sa.W = pl.W; sa.H1 = pl.H1; sa.W1 = pl.W1; sa.H2 = pl.H2; sa.W2 = pl.W2;
+      sa.w0 = P(net.c0.w); sa.sc0 = Wf(pl.c0.scale); sa.sh0 = Wf(pl.c0.shift);
+      sa.wd = P(net.ltd1.dw.w); sa.scd = Wf(pl.l1dw.scale); sa.shd = Wf(pl.l1dw.shift);
+      sa.wp = Wg(net.ltd1.pw); sa.scp = Wf(pl.l1pw.scale); sa.shp = Wf(pl.l1pw.shift);
+      sa.y = W(pl.l1pw.a); sa.ldy = pl.l1pw.ld;
+    }
+    if (!train && stem_enabled() && stem_ok(sa)) {
+      g_prof_tag = "learning_to_downsample.conv + dsconv1 (fused stem)";
+      TRY(stem_fwd(sa, dt, r.st));
+    } else {
       Conv0Args c{};
       c.x = r.x; c.x_bf16 = r.x_dtype;
       c.N = N; c.H = pl.H; c.W = pl.W; c.Ho = pl.H1; c.Wo = pl.W1;
@@ -993,9 +1014,9 @@ struct Exec {
         if (!frozen) TRY(finalize(pl.c0, net.b0));
         if (!pl.c0.lazy) TRY(apply(pl.c0, true));
       }
+      TRY(dw(pl.l1dw, net.ltd1.dw, net.ltd1.bdw, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2));
+      TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, act(pl.l1dw), true));
     }
-    TRY(dw(pl.l1dw, net.ltd1.dw, net.ltd1.bdw, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2));
-    TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, act(pl.l1dw), true));
     TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2));
     TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, act(pl.l2dw), true));
     // train: the FeatureFusionModule's high-res branch (conv_higher_res + its BN statistics, on

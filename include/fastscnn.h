@@ -212,6 +212,21 @@ int fscnn_block_ir_fwd(const void* x, int ldx, int dtype, int N, int H, int W, i
                        const float* shift_d, const float* scale_p, const float* shift_p,
                        int residual, void* y, int ldy, void* stream);
 
+/* fscnn_block_ltd_fwd: the inference LearningToDownsample stem up to dsconv1 in one launch
+ * (models/fast_scnn.py:153-154): y = BN_p(W_p * relu(BN_d(dw3x3_s2_p1(relu(BN_0(conv3x3_s2_p0(x)))))))
+ * followed by ReLU, every BN folded (scale, shift fp32 per channel).  x NCHW [N][3][H][W] of
+ * x_dtype (0 fp32, 1 bf16, 2 fp16; 16-B aligned, W a multiple of 16 B / element size); w_conv
+ * [32][3][3][3] fp32, w_dw [32][9] fp32, w_pw [48][32] in dtype (the plan's storage type);
+ * y NHWC [N][H2][W2] x 48 channels with row stride ldy elements (>= 48, multiple of 4), where
+ * H1 = (H-3)/2+1, H2 = (H1-1)/2+1 (same for W).  conv0's and the depthwise output never reach
+ * memory.  Replaces LearningToDownsample.conv (_ConvBNReLU, :52) and .dsconv1 (_DSConv, :64-78);
+ * the executor uses it for every eval plan whose image fits these constraints. */
+int fscnn_block_ltd_fwd(const void* x, int x_dtype, int dtype, int N, int H, int W,
+                        const float* w_conv, const float* scale_0, const float* shift_0,
+                        const float* w_dw, const float* scale_d, const float* shift_d,
+                        const void* w_pw, const float* scale_p, const float* shift_p, void* y,
+                        int ldy, void* stream);
+
 /* ---- launch profiler (bench.py roofline, tools/layer_report.py) ----------------------------
  * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 7 bn_apply,
  * 8 bn_bwd (apply), 9 upsample, 10 upsample_bwd, 11 cross_entropy / fused loss head,

@@ -14,6 +14,8 @@ fresh child process:
 * ``FSCNN_DROP_FUSED=0``  — the classifier's Dropout backward and dsconv2 pw's BN-backward reduce
   as their own passes instead of in the classifier conv's dgrad epilogue (the fused form runs only
   at M >= 4096 low-res pixels in 16-bit plans: test_drop_fused_matches_separate_passes).
+* ``FSCNN_STEM_FUSED=0``  — (inference) conv0, LTD.dsconv1.dw and .pw as three launches instead of
+  the fused stem (csrc/stem.hip): bit-identical outputs (test_stem_fused_bit_identical).
 
 (Round 5 removed the measured-slower variants and their switches: FSCNN_DW_LOOP, FSCNN_GEMM_PF,
 FSCNN_CE_HEAD, FSCNN_CE_PACK, FSCNN_GEMM_MINT.)
@@ -48,7 +50,7 @@ BF16 = ["tests/test_gpu_model.py::test_bf16_forward_within_bf16_budget"]
 CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_GRAPHS=1": TRAIN + EVAL + HEAD16 + ["tests/test_gpu_autograd.py"],
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
-         "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16}
+         "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL}
 
 
 def _env(switch):
@@ -77,6 +79,30 @@ def _worker(tmp_path, switch, half=None):
                        cwd=ROOT, env=_env(switch), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     return dict(np.load(out))
+
+
+def _stem_worker(tmp_path, switch):
+    out = str(tmp_path / ("stem_%s.npz" % (switch or "default").replace("=", "_")))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_stem_worker.py"), out],
+                       cwd=ROOT, env=_env(switch), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    return dict(np.load(out))
+
+
+def test_stem_fused_bit_identical(tmp_path):
+    """The fused inference stem (conv0 + LTD.dsconv1 dw + pw in one launch, csrc/stem.hip) gives
+    bit-identical outputs to the three unfused launches: fp32 / bf16 / fp16 images, autocast fp16
+    over an fp32 image, partial edge tiles (tests/_stem_worker.py).  The default run really took
+    the fused launch; the unaligned-width case falls back to the unfused launches."""
+    ref = _stem_worker(tmp_path, "FSCNN_STEM_FUSED=0")
+    got = _stem_worker(tmp_path, None)
+    assert int(ref["stem_launches"]) == 0 and int(got["stem_launches"]) == 1
+    for k in ref:
+        if k == "stem_launches":
+            continue
+        assert np.isfinite(got[k]).all(), k
+        assert np.array_equal(ref[k], got[k]), "%s: max |diff| %g" % (
+            k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
 
 
 @pytest.mark.parametrize("switch", ["FSCNN_GRAPHS=1", "FSCNN_SIDE_STREAM=0"])

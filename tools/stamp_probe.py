@@ -37,6 +37,8 @@ def analyse(label, st, base=None):
     if t.numel() == 0:
         print("%-40s no stamps" % label)
         return
+    place = t[:, 7].long()
+    t = t[:, :7]
     t0 = t[:, 0].min()
     rel = (t - t0) / 100.0  # us
     rel[t == 0] = float("nan")
@@ -44,7 +46,7 @@ def analyse(label, st, base=None):
     span = last.max().item()
     entry = rel[:, 0]
     parts = []
-    for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (1, 5), (5, 6), (6, 7)]:
+    for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (1, 5), (5, 6)]:
         d = rel[:, b] - rel[:, a]
         d = d[~torch.isnan(d)]
         if d.numel():
@@ -53,6 +55,30 @@ def analyse(label, st, base=None):
     print("%-40s %swaves %5d span %6.1f us  entry med %.1f max %.1f | %s"
           % (label, at, t.shape[0], span, entry.median().item(), entry.max().item(),
              "  ".join(parts)), flush=True)
+    if os.environ.get("STAMP_PLACE") and t.shape[0] <= 8192:
+        # phase 1-2 (the main loop) and the wave's end (last stamp) by placement
+        loop = rel[:, 2] - rel[:, 1]
+        end = torch.nan_to_num(rel, nan=-1.0).max(dim=1).values
+        xcc = (place >> 32) & 15
+        hw = place & 0xFFFFFFFF
+        simd = (hw >> 4) & 3
+        cu = (hw >> 8) & 15
+        se = (hw >> 13) & 7
+        def by(name, key, n):
+            row = []
+            for k in range(n):
+                sel = (key == k) & ~torch.isnan(loop)
+                if sel.any():
+                    row.append("%d:%.1f/%.1f" % (k, loop[sel].median().item(), end[sel].median().item()))
+            print("    %-5s loop/end med: %s" % (name, " ".join(row)))
+        by("xcc", xcc, 8)
+        by("simd", simd, 4)
+        by("se", se, 8)
+        by("wave", torch.arange(t.shape[0]) % 4, 4)
+        slow = torch.argsort(torch.nan_to_num(loop, nan=0.0), descending=True)[:6]
+        print("    slowest waves (block, wave, xcc, se, cu, simd, loop us, entry us):",
+              [(int(i) // 4, int(i) % 4, int(xcc[i]), int(se[i]), int(cu[i]), int(simd[i]),
+                round(loop[i].item(), 1), round(entry[i].item(), 1)) for i in slow])
 
 
 def main():
