@@ -805,16 +805,6 @@ static int gs_fill_bpg(int slots, int groups) {
   return b >= 8 ? b : (cdiv(slots, groups) + 7) / 8 * 8;
 }
 
-// A/B knob: resident-slot rounds of workgroups per launch (FSCNN_GS_ROUNDS)
-static int gs_rounds() {
-  static const int r = [] {
-    const char* e = getenv("FSCNN_GS_ROUNDS");
-    const int v = e ? atoi(e) : 1;
-    return v >= 1 && v <= 16 ? v : 1;
-  }();
-  return r;
-}
-
 // workgroups per column group = the record count of the statistics forms
 static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   const int KC = dtype == DT_F32 ? 16 : 32;
@@ -828,7 +818,9 @@ static int gs_bpg(const GemmArgs& a, int dtype, int& nt, int& ks, size_t& lds) {
   constexpr int cap = 2;
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
-  int bpg = gs_fill_bpg(256 * per_cu, groups) * gs_rounds();
+  // (2 or 4 rounds of resident workgroups instead of one, for dynamic balance: measured r05
+  //  6.16 / 6.50 vs 5.78 ms per cfg3 step -- each extra round pays the prologue and records again)
+  int bpg = gs_fill_bpg(256 * per_cu, groups);
   const int need = cdiv(nchunks, 4);  // <= cdiv(M, 128) = gemm_parts(M): fits the record slots
   if (bpg > need) bpg = need;
   // the finish's team counters: [GS_CTR_TEAMS, BN_COUNTERS) shared by the groups
@@ -924,7 +916,7 @@ static bool gs_x3_launch(const GemmArgs& a, hipStream_t st) {
   const int groups = cdiv(a.N, 16 * nt);
   int per_cu = (int)((160 * 1024) / (lds + 1024));
   per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
-  int bpg = gs_fill_bpg(256 * per_cu, groups) * gs_rounds();
+  int bpg = gs_fill_bpg(256 * per_cu, groups);
   const int need = cdiv(cdiv(a.M, GS_MW), 4);
   if (bpg > need) bpg = need;
   if (bpg < 1) bpg = 1;
