@@ -262,17 +262,20 @@ struct C0Mma<1> {  // bf16 operands, one v_mfma_f32_16x16x32_bf16 per 16 px x 16
   }
 };
 template <>
-struct C0Mma<0> {  // exact fp32: 8 x v_mfma_f32_16x16x4_f32 (k = 8*lq + e)
-  struct Frag { float v[8]; };
+struct C0Mma<0> {  // fp32: the three-term bf16 split of both operands, six bf16 MFMAs (gs_mma_x3)
+  // (r05: replaces 8 x v_mfma_f32_16x16x4_f32 = 256 matrix cycles per 16 px x 16 co by 96; the
+  //  dropped split terms are below fp32's own product rounding)
+  struct Frag { uint4 t[3]; };
   static __device__ __forceinline__ Frag pack(const float (&v)[8]) {
     Frag f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f.v[e] = v[e];
+    gs_split3(make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                         __float_as_uint(v[3])),
+              make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
+                         __float_as_uint(v[7])), f.t);
     return f;
   }
   static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4& acc) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[e], b.v[e], acc, 0, 0, 0);
+    gs_mma_x3(a.t, b.t, acc);
   }
 };
 
@@ -492,7 +495,7 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int slot) {
   if (st && (threadIdx.x & 63) == 0) {
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     const size_t b = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-    if (b < 8192) {
+    if (b < 8192 && (threadIdx.x >> 6) < 4) {  // (waves 0-3 of larger workgroups)
       st[(b * 4 + (threadIdx.x >> 6)) * STAMP_SLOTS + slot] = t;
       if (slot == 0) {  // placement of the wave: XCC id << 32 | HW_ID (CU, SIMD, SE) in slot 7
         const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);

@@ -416,6 +416,7 @@ struct StemArgs {
   const void* wp;              // dsconv1.pw weights [48][32] in the storage dtype
   const float *scp, *shp;      // folded BN of dsconv1.pw
   void* y; int ldy;            // NHWC [N,H2,W2] x 48 channels (row stride ldy elements)
+  unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
 };
 bool stem_ok(const StemArgs& a);
 int stem_fwd(const StemArgs& a, int dtype, hipStream_t st);

@@ -9,6 +9,10 @@
 // depthwise outputs, then their 48 pointwise channels: HBM sees the image once and the stem
 // output once.
 //
+// (r05 alternatives measured at cfg2 fp32, forward ms per batch: 512-thread workgroups 2.174 vs
+// 2.163; a persistent tile loop with the next tile's image in flight 2.381 -- its 80-register
+// budget at 3 workgroups per CU spills)
+//
 // Bit-identical to the three unfused launches (conv0_fwd_kernel, dw_fwd_kernel,
 // gemm_stream(_x3)_kernel) by construction: the same MFMA fragments and instruction sequence per
 // output (conv0: common.hpp C0Mma over k = 8 lq + e; pointwise: weights as the A operand,
@@ -94,6 +98,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
     th = (int)(r % gy);
     n = (int)(r / gy);
   }
+  stamp(a.stamps, 0);
   const int th0 = th * ST_TH, tw0 = tw * ST_TW;       // first dsconv1 output
   const int r1o = 2 * th0 - 1, c1o = 2 * tw0 - 1;     // conv0 tile origin (may be -1: padding)
   const int iro = 2 * r1o, ico = 2 * c1o;             // image tile origin
@@ -154,6 +159,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
     koff[e] = (ci * ST_IR + kh) * SW + kw + coff;
   }
   __syncthreads();
+  stamp(a.stamps, 1);
 
   // ---- conv0 on the 9 x 33 tile: wave w takes pixel groups w, w + 4, ... -------------------
   f32x4 c0v[ST_GPW][2];
@@ -180,6 +186,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
       c0v[gi][jt] = acc;
     }
   }
+  stamp(a.stamps, 2);
   __syncthreads();  // every wave is done reading the image tile (s_c0 aliases it)
 #pragma unroll
   for (int gi = 0; gi < ST_GPW; ++gi) {
@@ -196,6 +203,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
     }
   }
   __syncthreads();
+  stamp(a.stamps, 3);
 
   // ---- dsconv1.dw: thread (quad qd, outputs os, os + 32); taps in row-major order ----------
   {
@@ -233,6 +241,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
     }
   }
   __syncthreads();
+  stamp(a.stamps, 4);
 
   // ---- dsconv1.pw: wave w = outputs 16w .. 16w + 15 x 48 channels (3 column tiles) --------
   {
@@ -280,6 +289,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
       }
     }
   }
+  stamp(a.stamps, 5);
 }
 
 bool stem_ok(const StemArgs& a) {
@@ -298,15 +308,17 @@ int stem_fwd(const StemArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   const dim3 grid(cdiv(a.W2, ST_TW), cdiv(a.H2, ST_TH), a.N);
+  StemArgs as = a;
+  as.stamps = stamp_region();
   const double px0 = (double)a.N * a.H1 * a.W1, px2 = (double)a.N * a.H2 * a.W2;
   const int E = dtype == DT_F32 ? 4 : 2;
   ProfScope ps(PK_STEM, st, (a.x_dtype ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (double)E * px2 * ST_C2,
                2.0 * 27 * ST_C1 * px0 + 2.0 * 9 * ST_C1 * px2 + 2.0 * ST_C1 * ST_C2 * px2);
 #define STEM_L(T)                                                                  \
   do {                                                                             \
-    if (a.x_dtype == 2) stem_fwd_kernel<T, 2><<<grid, 256, 0, st>>>(a);            \
-    else if (a.x_dtype == 1) stem_fwd_kernel<T, 1><<<grid, 256, 0, st>>>(a);       \
-    else stem_fwd_kernel<T, 0><<<grid, 256, 0, st>>>(a);                           \
+    if (a.x_dtype == 2) stem_fwd_kernel<T, 2><<<grid, 256, 0, st>>>(as);            \
+    else if (a.x_dtype == 1) stem_fwd_kernel<T, 1><<<grid, 256, 0, st>>>(as);       \
+    else stem_fwd_kernel<T, 0><<<grid, 256, 0, st>>>(as);                           \
   } while (0)
   if (dtype == DT_F32) STEM_L(float);
   else if (dtype == DT_F16) STEM_L(f16);

@@ -177,8 +177,37 @@ def step():
         analyse("%3d %s" % (i, tags[i][:36]), buf[i * STRIDE:(i + 1) * STRIDE], base)
 
 
+def eval_fwd():
+    """One cfg2 fp32 eval forward (bench.py's forward_fp32) with every instrumented launch stamped."""
+    import numpy as np
+    from fast_scnn_pytorch_amd import arch, portable_init
+    from models.fast_scnn import FastSCNN
+    lib = _lib.load()
+    m = FastSCNN(19)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                       arch.portable_state_dict(19, seed=0).items()})
+    m = m.to(DEV).eval()
+    x = torch.from_numpy(portable_init.input_tensor(1, (8, 3, 1024, 2048))).to(DEV)
+    with torch.no_grad():
+        for _ in range(3):
+            m(x)
+        nmax = 40
+        buf = torch.zeros(nmax * STRIDE, dtype=torch.int64, device=DEV)
+        torch.cuda.synchronize()
+        _lib.check(lib.fscnn_debug_stamps(_lib.ptr(buf), nmax))
+        m(x)
+        torch.cuda.synchronize()
+    n = lib.fscnn_debug_stamp_count()
+    tags = [lib.fscnn_debug_stamp_tag(i).decode() for i in range(n)]
+    _lib.check(lib.fscnn_debug_stamps(None, 0))
+    for i in range(n):
+        analyse("%3d %s" % (i, tags[i][:36]), buf[i * STRIDE:(i + 1) * STRIDE])
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "step":
         step()
+    elif len(sys.argv) > 1 and sys.argv[1] == "eval":
+        eval_fwd()
     else:
         main()
