@@ -38,7 +38,7 @@ FAMILY_RE = {
     "gemm_tn": r"gemm_tn_kernel",
     "bn_apply": r"bn_apply_kernel",
     "bn_bwd": r"bn_bwd_apply_kernel",
-    "upsample_bwd": r"axis_bwd_kernel",
+    "upsample_bwd": r"axis_bwd_kernel|up_nhwc_bwd_kernel",
     "upsample": r"up_nchw|up_nhwc|up_argmax",
     "cross_entropy": r"ce_head2?_kernel|ce_fwd_kernel|ce_pack_targets",
     "conv0_wgrad": r"conv0_wgrad_kernel|ltd_c0_bwd_kernel",
