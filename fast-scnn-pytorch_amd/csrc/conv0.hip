@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
   const int li = lane & 15, lq = lane >> 4;
   int seg, rowb;  // rowb = n * HB + hb
   c0_tile(seg, rowb);
+  stamp(a.stamps, 0);
   const int HB = cdiv(a.Ho, RB);
   const int wo0 = seg * C0_TILE;
   const int n = rowb / HB, ho0 = (rowb - n * HB) * RB;
@@ -164,6 +165,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     fsh[jt] = a.scale ? a.shift[16 * jt + li] : 0.f;
   }
   __syncthreads();
+  stamp(a.stamps, 1);
 
   float tn = 0.f, tmean[2] = {0.f, 0.f}, tm2[2] = {0.f, 0.f};  // the record (wave 0, lq 0)
   for (int r = 0; r < nrows; ++r) {  // (workgroup-uniform)
@@ -205,6 +207,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
           s_out[(wave * 64 + gi * 16 + 4 * lq + q) * OST + 16 * jt + li] = t;
         }
     __syncthreads();
+    stamp(a.stamps, 2);
     {
       constexpr int V = VecW<TO>::V;
       TO* y = (TO*)a.y + (((size_t)n * a.Ho + ho) * a.Wo + wo0) * C0_OUT;
@@ -217,6 +220,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
         *reinterpret_cast<uint4*>(y + (size_t)i * V) = *reinterpret_cast<const uint4*>(&s_out[p * OST + c]);
       }
     }
+    stamp(a.stamps, 3);
     if (a.part == nullptr) continue;
     // ---- per-channel (mean, M2) of the row's npx pixels, from the fp32 registers -------------
     float sum[2] = {0.f, 0.f};
@@ -296,6 +300,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       rec[2 * C0_OUT + c] = tn;
     }
   }
+  stamp(a.stamps, 4);
 }
 
 int conv0_parts(int N, int Ho, int Wo) { return N * cdiv(Ho, C0_RB) * cdiv(Wo, C0_TILE); }
@@ -306,22 +311,24 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
     return E_INVALID;
   }
   dim3 grid(cdiv(a.Wo, C0_TILE), a.N * cdiv(a.Ho, C0_RB));
+  Conv0Args as = a;
+  as.stamps = stamp_region();
   const double px = (double)a.N * a.Ho * a.Wo;
   ProfScope ps(PK_CONV0_FWD, st,
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (y_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
                2.0 * 27 * 32 * px);
   if (y_dtype == DT_F32) {
-    if (a.x_bf16 == 2) conv0_fwd_kernel<float, 2><<<grid, 256, 0, st>>>(a);
-    else if (a.x_bf16) conv0_fwd_kernel<float, 1><<<grid, 256, 0, st>>>(a);
-    else conv0_fwd_kernel<float, 0><<<grid, 256, 0, st>>>(a);
+    if (a.x_bf16 == 2) conv0_fwd_kernel<float, 2><<<grid, 256, 0, st>>>(as);
+    else if (a.x_bf16) conv0_fwd_kernel<float, 1><<<grid, 256, 0, st>>>(as);
+    else conv0_fwd_kernel<float, 0><<<grid, 256, 0, st>>>(as);
   } else if (y_dtype == DT_F16) {
-    if (a.x_bf16 == 2) conv0_fwd_kernel<f16, 2><<<grid, 256, 0, st>>>(a);
-    else if (a.x_bf16) conv0_fwd_kernel<f16, 1><<<grid, 256, 0, st>>>(a);
-    else conv0_fwd_kernel<f16, 0><<<grid, 256, 0, st>>>(a);
+    if (a.x_bf16 == 2) conv0_fwd_kernel<f16, 2><<<grid, 256, 0, st>>>(as);
+    else if (a.x_bf16) conv0_fwd_kernel<f16, 1><<<grid, 256, 0, st>>>(as);
+    else conv0_fwd_kernel<f16, 0><<<grid, 256, 0, st>>>(as);
   } else {
-    if (a.x_bf16 == 2) conv0_fwd_kernel<bf16, 2><<<grid, 256, 0, st>>>(a);
-    else if (a.x_bf16) conv0_fwd_kernel<bf16, 1><<<grid, 256, 0, st>>>(a);
-    else conv0_fwd_kernel<bf16, 0><<<grid, 256, 0, st>>>(a);
+    if (a.x_bf16 == 2) conv0_fwd_kernel<bf16, 2><<<grid, 256, 0, st>>>(as);
+    else if (a.x_bf16) conv0_fwd_kernel<bf16, 1><<<grid, 256, 0, st>>>(as);
+    else conv0_fwd_kernel<bf16, 0><<<grid, 256, 0, st>>>(as);
   }
   return check_launch("conv0_fwd");
 }

@@ -22,6 +22,7 @@ struct Conv0Args {
   int relu;
   void* y;             // NHWC [N,Ho,Wo,32]
   float* part;         // BN partial records [part][3][32] or null
+  unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
 };
 
 struct Conv0WgradArgs {

@@ -292,6 +292,273 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(StemArgs a) {
   stamp(a.stamps, 5);
 }
 
+// ---- row-walking form ---------------------------------------------------------------------
+// A workgroup owns a strip of SW_TW dsconv1 output columns and walks SW_RS output rows down it.
+// Each step needs two new conv0 rows (the third, 2 oh - 1, is the previous step's) and four new
+// image rows (the fifth is the previous step's): conv0 rows are computed once per strip (no
+// vertical halo), the next step's image rows are in flight during the current step, and the
+// rings are small (41 KB fp32: 3 workgroups per CU).  Per step: image rows -> ring, conv0 (MFMA)
+// -> ring, depthwise -> s_dw, pointwise -> HBM; the arithmetic per output is the one-tile
+// kernel's (bit-identical).
+constexpr int SW_TW = 32;                      // dsconv1 output columns per workgroup
+constexpr int SW_RS = 16;                      // dsconv1 output rows walked per workgroup
+constexpr int SW_CC = 2 * SW_TW + 1;           // conv0 columns (65)
+constexpr int SW_IC = 2 * SW_CC + 1;           // image columns (131)
+constexpr int SW_NIR = 5;                      // image ring rows
+constexpr int SW_NCR = 3;                      // conv0 ring rows
+
+template <typename T, int XB>
+__global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
+  constexpr int BF = sizeof(T) == 4 ? 0 : (std::is_same<T, f16>::value ? 2 : 1);
+  using M = C0Mma<BF>;
+  using TI = typename std::conditional<XB != 0, uint16_t, float>::type;
+  constexpr int VI = 16 / sizeof(TI);               // image elements per 16-B vector
+  constexpr int COFF = VI - 2;                      // image column 4 ow0 - 2 in the staged row
+  constexpr int NVC = (SW_IC + COFF + VI - 1) / VI; // vectors per staged image row
+  constexpr int SWD = NVC * VI;                     // staged row width (floats)
+  constexpr int LP4 = (4 * 3 * NVC + 255) / 256;    // loads per thread: 4 image rows
+  constexpr int LP7 = (7 * 3 * NVC + 255) / 256;    // ... 7 image rows (the first step)
+  // image row r lives at slots r % 5 and r % 5 + 5, so the 3 rows 2 r1 .. 2 r1 + 2 of a conv0
+  // row r1 are 3 consecutive slots from (2 r1) % 5: the tap offsets stay per-lane constants
+  __shared__ __attribute__((aligned(16))) float s_img[2 * SW_NIR * 3 * SWD];  // [slot][ci][col]
+  __shared__ __attribute__((aligned(16))) float s_wd[9 * ST_C1];             // [tap][ch]
+  __shared__ __attribute__((aligned(16))) float s_c0[SW_NCR * SW_CC * ST_PS];  // [row % 3][col][ch]
+  __shared__ __attribute__((aligned(16))) float s_dw[SW_TW * ST_PS];        // [o][ch]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  int tw, sg, n;  // strip, row segment, image: XCD-contiguous (speed only)
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const long long T_ = (long long)gx * gy * gridDim.z;
+    long long L = blockIdx.x + (long long)gx * (blockIdx.y + (long long)gy * blockIdx.z);
+    if ((T_ & 7) == 0) L = (L & 7) * (T_ >> 3) + (L >> 3);
+    tw = (int)(L % gx);
+    const long long r = L / gx;
+    sg = (int)(r % gy);
+    n = (int)(r / gy);
+  }
+  stamp(a.stamps, 0);
+  const int ow0 = tw * SW_TW, oh0 = sg * SW_RS;
+  const int c1o = 2 * ow0 - 1;                // conv0 column origin (-1: the depthwise padding)
+  const int cbase = 4 * ow0 - 2 - COFF;       // first staged image column (a vector boundary)
+  const TI* xin = (const TI*)a.x;
+
+  // image rows [r0, r0 + R) of all 3 channels: 16-B vector loads into registers / into the ring
+  auto load_rows = [&](int r0, int R, uint4* raw, int LP) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int i = tid + 256 * k;
+      const int row = i / (3 * NVC), rem = i - row * 3 * NVC;
+      const int ci = rem / NVC, v = rem - ci * NVC;
+      const int ir = r0 + row, ic = cbase + v * VI;
+      const bool ok = row < R && ir >= 0 && ir < a.H && ic >= 0 && ic + VI <= a.W;
+      const size_t off = ok ? (((size_t)n * 3 + ci) * a.H + ir) * a.W + ic : 0;
+      raw[k] = sel4(ok, *reinterpret_cast<const uint4*>(xin + off));
+    }
+  };
+  auto store_rows = [&](int r0, int R, const uint4* raw, int LP) {
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const int i = tid + 256 * k;
+      const int row = i / (3 * NVC), rem = i - row * 3 * NVC;
+      if (row >= R) continue;
+      const int ci = rem / NVC, v = rem - ci * NVC;
+      const int slot = (r0 + row + 4 * SW_NIR) % SW_NIR;  // (r0 >= -2)
+      const TI* e = reinterpret_cast<const TI*>(&raw[k]);
+      float f[VI];
+#pragma unroll
+      for (int j = 0; j < VI; ++j) {
+        if (XB) f[j] = in16<XB>((uint16_t)e[j]);
+        else f[j] = (float)e[j];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float* d = s_img + ((slot + h * SW_NIR) * 3 + ci) * SWD + v * VI;
+#pragma unroll
+        for (int j = 0; j < VI; j += 4)
+          *reinterpret_cast<float4*>(d + j) = make_float4(f[j], f[j + 1], f[j + 2], f[j + 3]);
+      }
+    }
+  };
+  // conv0 B fragments and folded BN (the one-tile kernel's)
+  typename M::Frag bw[2];
+  float fsc[2], fsh[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    float wv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * lq + e;
+      const float t = a.w0[(16 * jt + li) * 27 + (k < 27 ? k : 0)];
+      wv[e] = k < 27 ? t : 0.f;
+    }
+    bw[jt] = M::pack(wv);
+    fsc[jt] = a.sc0[16 * jt + li];
+    fsh[jt] = a.sh0[16 * jt + li];
+  }
+  int koff[8];  // tap k = 8 lq + e -> (kh * 3 + ci) * SWD + kw + COFF from the row's first slot
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * lq + e;
+    const int kk = k < 27 ? k : 0;
+    koff[e] = ((kk % 9) / 3 * 3 + kk / 9) * SWD + kk % 3 + COFF;
+  }
+  for (int i = tid; i < 9 * ST_C1; i += 256) s_wd[i] = a.wd[(i % ST_C1) * 9 + i / ST_C1];
+  // conv0 rows [r0, r0 + NR) x the strip's 65 columns -> conv0 ring (zero outside the map)
+  auto conv0_rows = [&](int r0, auto NRc) {
+    constexpr int NR = decltype(NRc)::value;
+    constexpr int NG = (NR * SW_CC + 15) / 16;
+    constexpr int GPW = (NG + 3) / 4;
+    f32x4 c0v[GPW][2];
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) {
+      const int g = wave + 4 * gi;
+      const int px = 16 * g + li;
+      const int p = px < NR * SW_CC ? px : 0;
+      const int rr = p / SW_CC, cc = p - rr * SW_CC;
+      const float* base = s_img + ((2 * (r0 + rr) + 4 * SW_NIR) % SW_NIR) * 3 * SWD + 2 * cc;
+      float av[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = 8 * lq + e < 27 ? base[koff[e]] : 0.f;
+      const typename M::Frag af = M::pack(av);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (g < NG) M::mma(af, bw[jt], acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = acc[q] * fsc[jt] + fsh[jt];
+          acc[q] = round_as<T>(fmaxf(v, 0.f));
+        }
+        c0v[gi][jt] = acc;
+      }
+    }
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) {
+      const int g = wave + 4 * gi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = 16 * g + 4 * lq + q;
+        if (g >= NG || p >= NR * SW_CC) continue;
+        const int rr = p / SW_CC, cc = p - rr * SW_CC;
+        const int r1 = r0 + rr, c1 = c1o + cc;
+        const bool in = r1 >= 0 && r1 < a.H1 && c1 >= 0 && c1 < a.W1;
+        float* d = s_c0 + (((r1 + 3 * SW_NCR) % SW_NCR) * SW_CC + cc) * ST_PS;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) d[16 * jt + li] = in ? c0v[gi][jt][q] : 0.f;
+      }
+    }
+  };
+
+  // ---- first step's rows: image rows 4 oh0 - 2 .. 4 oh0 + 4, conv0 rows 2 oh0 - 1 .. + 1 ------
+  {
+    uint4 raw[LP7];
+    load_rows(4 * oh0 - 2, 7, raw, LP7);
+    store_rows(4 * oh0 - 2, 7, raw, LP7);
+  }
+  __syncthreads();
+  conv0_rows(2 * oh0 - 1, std::integral_constant<int, 3>());
+  uint4 nxt[LP4];  // the next step's 4 image rows
+  load_rows(4 * oh0 + 5, 4, nxt, LP4);
+  __syncthreads();
+  stamp(a.stamps, 1);
+
+  // per-thread depthwise / pointwise constants
+  const int qd = tid & 7, o = tid >> 3;         // depthwise: channel quad, output column
+  const int pg = wave & 1;                      // pointwise: pixel group (outputs 16 pg ..)
+  const int nt0 = wave < 2 ? 0 : 2, ntn = wave < 2 ? 2 : 1;
+  for (int s = 0; s < SW_RS; ++s) {
+    const int oh = oh0 + s;
+    if (oh >= a.H2) break;  // (workgroup-uniform)
+    if (s > 0) {
+      store_rows(4 * oh + 1, 4, nxt, LP4);
+      if (s + 1 < SW_RS) load_rows(4 * oh + 5, 4, nxt, LP4);
+      __syncthreads();
+      conv0_rows(2 * oh, std::integral_constant<int, 2>());
+      __syncthreads();
+    }
+    // ---- dsconv1.dw of output row oh: conv0 rows 2 oh - 1 .. 2 oh + 1 (taps in row-major order)
+    {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const float* rowp = s_c0 + ((2 * oh - 1 + kh + 3 * SW_NCR) % SW_NCR) * SW_CC * ST_PS;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const float4 v = *reinterpret_cast<const float4*>(&rowp[(2 * o + kw) * ST_PS + 4 * qd]);
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          const float4 w = *reinterpret_cast<const float4*>(&s_wd[(kh * 3 + kw) * ST_C1 + 4 * qd]);
+          const float ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = fmaf(vv[j], ww[j], acc[j]);
+        }
+      }
+      float o4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t = acc[j] * a.scd[4 * qd + j] + a.shd[4 * qd + j];
+        o4[j] = round_as<T>(fmaxf(t, 0.f));
+      }
+      *reinterpret_cast<float4*>(&s_dw[o * ST_PS + 4 * qd]) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+    }
+    __syncthreads();
+    // ---- dsconv1.pw: pixel group pg x column tiles {0, 1} (waves 0, 1) or {2} (waves 2, 3) ---
+    {
+      const int op = 16 * pg + li;
+      const float4 x0 = *reinterpret_cast<const float4*>(&s_dw[op * ST_PS + 8 * lq]);
+      const float4 x1 = *reinterpret_cast<const float4*>(&s_dw[op * ST_PS + 8 * lq + 4]);
+      f32x4 acc[2];
+      if constexpr (sizeof(T) == 4) {
+        uint4 xs[3];
+        gs_split3(make_uint4(__float_as_uint(x0.x), __float_as_uint(x0.y), __float_as_uint(x0.z),
+                             __float_as_uint(x0.w)),
+                  make_uint4(__float_as_uint(x1.x), __float_as_uint(x1.y), __float_as_uint(x1.z),
+                             __float_as_uint(x1.w)), xs);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (u < ntn) {
+            const float* wr = (const float*)a.wp + (size_t)(16 * (nt0 + u) + li) * ST_C1 + 8 * lq;
+            uint4 w3[3];
+            gs_split3(*reinterpret_cast<const uint4*>(wr), *reinterpret_cast<const uint4*>(wr + 4), w3);
+            gs_mma_x3(w3, xs, acc[u]);
+          }
+        }
+      } else {
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const uint4 xb = st_pack8<T>(xv);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (u < ntn) {
+            const uint4 w = *reinterpret_cast<const uint4*>(
+                (const T*)a.wp + (size_t)(16 * (nt0 + u) + li) * ST_C1 + 8 * lq);
+            StPw<T>::run(w, xb, acc[u]);
+          }
+        }
+      }
+      const int ow = ow0 + op;
+      if (ow < a.W2) {
+        T* yp = (T*)a.y + (((size_t)n * a.H2 + oh) * a.W2 + ow) * a.ldy;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (u >= ntn) continue;
+          const int c = 16 * (nt0 + u) + 4 * lq;
+          float o4[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[u][r] * a.scp[c + r] + a.shp[c + r];
+            o4[r] = fmaxf(v, 0.f);
+          }
+          st4v(yp + c, o4);
+        }
+      }
+    }
+  }
+  stamp(a.stamps, 2);
+}
+
 bool stem_ok(const StemArgs& a) {
   const int VI = a.x_dtype ? 8 : 4;
   const int ve = VI == 8 ? 4 : (a.ldy % 4 == 0 ? 4 : 0);  // 4-channel output vectors aligned
@@ -307,9 +574,30 @@ int stem_fwd(const StemArgs& a, int dtype, hipStream_t st) {
               a.H, a.W, a.x_dtype ? 8 : 4);
     return E_UNSUPPORTED;
   }
-  const dim3 grid(cdiv(a.W2, ST_TW), cdiv(a.H2, ST_TH), a.N);
   StemArgs as = a;
   as.stamps = stamp_region();
+  static const bool walk = [] {
+    const char* e = getenv("FSCNN_STEM_WALK");
+    return e && e[0] == '1';
+  }();
+  if (walk) {
+    const dim3 gw(cdiv(a.W2, SW_TW), cdiv(a.H2, SW_RS), a.N);
+    ProfScope pw_(PK_STEM, st, (a.x_dtype ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W +
+                                   (dtype == DT_F32 ? 4.0 : 2.0) * (double)a.N * a.H2 * a.W2 * ST_C2,
+                  0.0);
+#define STEMW(T)                                                                  \
+  do {                                                                            \
+    if (a.x_dtype == 2) stem_walk_kernel<T, 2><<<gw, 256, 0, st>>>(as);           \
+    else if (a.x_dtype == 1) stem_walk_kernel<T, 1><<<gw, 256, 0, st>>>(as);      \
+    else stem_walk_kernel<T, 0><<<gw, 256, 0, st>>>(as);                          \
+  } while (0)
+    if (dtype == DT_F32) STEMW(float);
+    else if (dtype == DT_F16) STEMW(f16);
+    else STEMW(bf16);
+#undef STEMW
+    return check_launch("stem_fwd");
+  }
+  const dim3 grid(cdiv(a.W2, ST_TW), cdiv(a.H2, ST_TH), a.N);
   const double px0 = (double)a.N * a.H1 * a.W1, px2 = (double)a.N * a.H2 * a.W2;
   const int E = dtype == DT_F32 ? 4 : 2;
   ProfScope ps(PK_STEM, st, (a.x_dtype ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (double)E * px2 * ST_C2,
