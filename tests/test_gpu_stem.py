@@ -7,7 +7,8 @@ fp32: conv0 runs on exact fp32 MFMA, the pointwise on the six-product bf16 split
 only the summation order differs (2e-5 of the output magnitude).  bf16 / fp16: the restatement
 rounds the conv0 operands, conv0's output, the depthwise output and the pointwise weights to the
 storage type exactly where the HIP path does, so the difference is accumulation order plus the
-final rounding.  Shapes: cfg5's 480 x 640 slice, ragged maps (partial 4 x 16 output tiles), a
+final rounding.  Shapes: cfg5's 480 x 640 slice, ragged maps (partial 31-column strips and
+16-row segments), a
 16-bit image, an output row stride larger than 48.  Bit-identity with the three unfused
 launches: tests/test_gpu_switches.py::test_stem_fused_bit_identical.
 """
@@ -42,6 +43,8 @@ CASES = [  # (N, H, W, x dtype, ldy)
     (1, 101, 132, torch.float32, 48),   # H2 = 25, W2 = 33: partial tiles in both axes
     (2, 64, 96, torch.bfloat16, 48),    # 16-bit image (16-B vectors of 8)
     (1, 70, 104, torch.float16, 64),    # row stride > 48
+    (1, 270, 520, torch.bfloat16, 48),  # 5 strips (16-bit image vectors at both alignments) x
+                                        # 5 row segments, the last partial
 ]
 
 

@@ -105,19 +105,6 @@ def test_stem_fused_bit_identical(tmp_path):
             k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
 
 
-def test_stem_walk_bit_identical(tmp_path):
-    """The row-walking stem (``FSCNN_STEM_WALK=1``: a workgroup walks 16 output rows down a
-    32-column strip, conv0 rows computed once) is bit-identical to the three unfused launches."""
-    ref = _stem_worker(tmp_path, "FSCNN_STEM_FUSED=0")
-    got = _stem_worker(tmp_path, "FSCNN_STEM_WALK=1")
-    assert int(got["stem_launches"]) == 1
-    for k in ref:
-        if k == "stem_launches":
-            continue
-        assert np.array_equal(ref[k], got[k]), "%s: max |diff| %g" % (
-            k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
-
-
 @pytest.mark.parametrize("switch", ["FSCNN_GRAPHS=1", "FSCNN_SIDE_STREAM=0"])
 def test_switch_train_steps_bit_identical_with_dropout(tmp_path, switch):
     ref = _worker(tmp_path, None)
