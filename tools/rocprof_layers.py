@@ -46,7 +46,7 @@ FAMILY_RE = {
     "bn_finalize": r"bn_(stats_fold_fin|stats_fold|finalize|bwd_fold_fin|bwd_fold|bwd_finalize)_kernel",
     "ppm_branches": r"ppm_(fwd|fwd_lds|bwd)_kernel",
     "ir_block": r"ir_block_kernel",
-    "ltd_stem": r"stem_fwd_kernel",
+    "ltd_stem": r"stem_walk_kernel",
 }
 MARK = re.compile(r"bitwise_not")  # torch's bitwise_not kernel (the phase marker: no step uses it)
 
