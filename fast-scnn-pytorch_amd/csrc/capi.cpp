@@ -161,7 +161,7 @@ extern "C" const char* fscnn_prof_kind_name(int kind) {
                                         "gemm_nt", "gemm_tn", "bn_apply", "bn_bwd", "upsample",
                                         "upsample_bwd", "cross_entropy", "conv0_wgrad",
                                         "bn_bwd_reduce", "bn_finalize", "ppm_branches",
-                                        "ir_block", "ltd_stem"};
+                                        "ir_block", "ltd_stem", "dsconv"};
   return (kind >= 0 && kind < PK_COUNT) ? names[kind] : "?";
 }
 
@@ -733,6 +733,49 @@ int fscnn_block_ltd_fwd(const void* x, int x_dtype, int dtype, int N, int H, int
   a.wp = w_pw; a.scp = scale_p; a.shp = shift_p;
   a.y = y; a.ldy = ldy;
   return stem_fwd(a, dtype, S(stream));
+}
+
+int fscnn_block_dsconv_fwd(const void* x, int dtype, int N, int H, int W, int C, int Co,
+                           const float* w_dw, const float* scale_d, const float* shift_d,
+                           const void* w_pw, const float* scale_p, const float* shift_p, void* y,
+                           int ldy, void* stream) {
+  if (!x || !y || !w_dw || !scale_d || !shift_d || !w_pw || !scale_p || !shift_p) {
+    set_error("fscnn_block_dsconv_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || N <= 0 || H <= 0 || W <= 0) {
+    set_error("fscnn_block_dsconv_fwd: dtype %d N %d H %d W %d", dtype, N, H, W);
+    return E_INVALID;
+  }
+  DsArgs a{};
+  a.x = x; a.N = N; a.H = H; a.W = W; a.C = C; a.Co = Co;
+  a.wd = w_dw; a.scd = scale_d; a.shd = shift_d;
+  a.wp = w_pw; a.scp = scale_p; a.shp = shift_p;
+  a.y = y; a.ldy = ldy;
+  a.rs = ds_rows(N, H, W);
+  return ds_fwd(a, dtype, S(stream));
+}
+
+int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, int C, int Co,
+                               const float* w_dw, const float* scale_d, const float* shift_d,
+                               const void* w_pw, const float* scale_p, const float* shift_p,
+                               const void* res, int ldres, void* y, int ldy, void* stream) {
+  if (!x || !y || !res || !w_dw || !scale_d || !shift_d || !w_pw || !scale_p || !shift_p) {
+    set_error("fscnn_block_dsconv_res_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || N <= 0 || H <= 0 || W <= 0) {
+    set_error("fscnn_block_dsconv_res_fwd: dtype %d N %d H %d W %d", dtype, N, H, W);
+    return E_INVALID;
+  }
+  DsArgs a{};
+  a.x = x; a.N = N; a.H = H; a.W = W; a.C = C; a.Co = Co;
+  a.wd = w_dw; a.scd = scale_d; a.shd = shift_d;
+  a.wp = w_pw; a.scp = scale_p; a.shp = shift_p;
+  a.r = res; a.ldr = ldres;
+  a.y = y; a.ldy = ldy;
+  a.rs = ds_rows(N, H, W);
+  return ds_fwd(a, dtype, S(stream));
 }
 
 }  // extern "C"

@@ -457,7 +457,7 @@ enum Status : int { OK = 0, E_INVALID = -1, E_UNSUPPORTED = -2, E_HIP = -3 };
 enum ProfKind : int {
   PK_NONE = 0, PK_CONV0_FWD, PK_DW_FWD, PK_DW_DGRAD, PK_DW_WGRAD, PK_GEMM_NT, PK_GEMM_TN,
   PK_BN_APPLY, PK_BN_BWD, PK_UP, PK_UP_BWD, PK_CE, PK_CONV0_WGRAD, PK_BN_BWD_RED, PK_BN_FIN,
-  PK_PPM, PK_IR, PK_STEM, PK_COUNT
+  PK_PPM, PK_IR, PK_STEM, PK_DSCONV, PK_COUNT
 };
 constexpr int PK_ALL = 100;  // record every kind (per-launch layer report)
 extern int g_prof_kind;  // kind being recorded (PK_NONE = off)
@@ -482,6 +482,38 @@ struct ProfScope {
 };
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ---- buffer operations: 32-bit offsets, range-checked (an out-of-range lane loads 0 / stores
+// nothing), so edge handling needs no branch and a launch's memory-op count per step is fixed
+constexpr uint32_t BUF_OOB = 0x80000000u;       // a buffer offset past every range
+typedef unsigned int buf_v4u __attribute__((__vector_size__(16)));
+typedef unsigned int buf_v2u __attribute__((__vector_size__(8)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[4],
+                                       float*) {
+  const buf_v4u t = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                   __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[4],
+                                       bf16*) {
+  const buf_v2u t = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                   (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+  __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[4],
+                                       f16*) {
+  const buf_v2u t = {(uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16),
+                   (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16)};
+  __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
+}
 
 // ---- phase stamps (tools/stamp_probe.py; off unless fscnn_debug_stamps set a buffer) ----------
 // Lane 0 of every wave records the 100 MHz wall clock at numbered points of a kernel into

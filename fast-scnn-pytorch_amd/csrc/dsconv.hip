@@ -1,0 +1,343 @@
+// Inference DSConv in one launch: depthwise 3x3 s1 p1 + BN + ReLU, then 1x1 (128 -> 128) + BN
+// (+ a residual) + ReLU, every BatchNorm folded (eval) -- the Classifer's two _DSConv
+// (models/fast_scnn.py:228-231, _DSConv :64-79) and the FeatureFusionModule's dwconv +
+// conv_lower_res with the high-res branch as the residual (:207-218).
+//
+// The unfused eval path writes the depthwise output (128 channels at H/8: 134 MB fp32 at cfg2)
+// and reads it back in the pointwise GEMM, twice per classifier.  Here a workgroup walks a strip
+// of DS_TW output columns down `rs` rows: the three input rows the depthwise window needs sit in
+// an LDS ring (each input row is loaded once per strip, the next one in flight during the current
+// step), the depthwise output of a row goes to LDS already converted to the pointwise B operand
+// (the three bf16 split terms for fp32 plans), and the pointwise weights live in registers
+// (already split): HBM sees the input once and the output once.  The loads and stores are buffer
+// operations (common.hpp BUF_OOB), so every step issues the same memory operations and the wait
+// for the next row leaves the previous stores in flight.
+//
+// Bit-identical to dw_fwd_kernel + gemm_stream(_x3)_kernel by construction: the same depthwise
+// fma chain per output (taps in row-major order from 0, fp32), the same folded-BN fma + ReLU and
+// rounding to the storage type, and the same pointwise MFMA sequence (weights as the A operand,
+// lane (li, lq) holding k = 32 s + 8 lq .. +7, 32-k steps in ascending order, gs_mma_x3 for fp32).
+#include "kernels.hpp"
+
+namespace fscnn {
+
+constexpr int DS_C = 128;              // channels in = depthwise channels = pointwise K
+constexpr int DS_CO = 128;             // pointwise output channels
+constexpr int DS_TW = 16;              // output columns per workgroup (one MFMA pixel group)
+constexpr int DS_RP = DS_TW + 2;       // ring pixels per row (the window's halo)
+constexpr int DS_PP = DS_C + 4;        // ring floats per pixel (padded)
+constexpr int DS_DP = DS_C + 8;        // pointwise operand halves per pixel (padded)
+
+template <typename T>
+struct DsMma;  // one 16-bit MFMA per operand pair (the 16-bit streaming GEMM's GsMma)
+template <>
+struct DsMma<bf16> {
+  static __device__ __forceinline__ void run(const uint4& w, const uint4& x, f32x4& acc) {
+    i16x8 wv, xv;
+    __builtin_memcpy(&wv, &w, 16);
+    __builtin_memcpy(&xv, &x, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, xv, acc, 0, 0, 0);
+  }
+};
+template <>
+struct DsMma<f16> {
+  static __device__ __forceinline__ void run(const uint4& w, const uint4& x, f32x4& acc) {
+    h16x8 wv, xv;
+    __builtin_memcpy(&wv, &w, 16);
+    __builtin_memcpy(&xv, &x, 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wv, xv, acc, 0, 0, 0);
+  }
+};
+template <>
+struct DsMma<float> {
+  static __device__ __forceinline__ void run(const uint4&, const uint4&, f32x4&) {}
+};
+
+template <typename T, bool RES>
+__global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int NP = F32 ? 3 : 1;                  // pointwise operand planes
+  constexpr int VI = 16 / sizeof(T);               // elements per 16-B vector
+  constexpr int VPP = DS_C / VI;                   // vectors per input pixel
+  constexpr int LP = (DS_RP * VPP + 255) / 256;    // row loads per thread
+  __shared__ __attribute__((aligned(16))) float s_ring[3 * DS_RP * DS_PP];   // [row % 3][px][c]
+  __shared__ __attribute__((aligned(16))) uint16_t s_d[NP * DS_TW * DS_DP];  // [plane][px][c]
+  __shared__ __attribute__((aligned(16))) float s_bn[2 * DS_CO];             // pointwise scale, shift
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  int tw, sg, n;  // strip, row segment, image: XCD-contiguous (speed only)
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const long long T_ = (long long)gx * gy * gridDim.z;
+    long long L = blockIdx.x + (long long)gx * (blockIdx.y + (long long)gy * blockIdx.z);
+    if ((T_ & 7) == 0) L = (L & 7) * (T_ >> 3) + (L >> 3);
+    tw = (int)(L % gx);
+    const long long r = L / gx;
+    sg = (int)(r % gy);
+    n = (int)(r / gy);
+  }
+  stamp(a.stamps, 0);
+  const int ow0 = tw * DS_TW, oh0 = sg * a.rs;
+  const size_t img = (size_t)a.H * a.W * DS_C;
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc((const T*)a.x + (size_t)n * img, (uint32_t)(img * sizeof(T)));
+  const size_t ysz = (size_t)a.H * a.W * a.ldy;
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc((T*)a.y + (size_t)n * ysz, (uint32_t)(ysz * sizeof(T)));
+
+  // one input row (the strip's 18 pixels incl. the halo, all channels): per-thread tables
+  uint32_t lvo[LP];  // byte offset of the vector in row 0, or BUF_OOB
+  int lds[LP];       // ring float offset within a slot, or -1
+#pragma unroll
+  for (int k = 0; k < LP; ++k) {
+    const int i = tid + 256 * k;
+    const int px = i / VPP, cv = i - px * VPP;
+    const int col = ow0 - 1 + px;
+    const bool ok = px < DS_RP && col >= 0 && col < a.W;
+    lvo[k] = ok ? (uint32_t)(((size_t)col * DS_C + cv * VI) * sizeof(T)) : BUF_OOB;
+    lds[k] = px < DS_RP ? px * DS_PP + cv * VI : -1;
+  }
+  const uint32_t rowbytes = (uint32_t)((size_t)a.W * DS_C * sizeof(T));
+  auto load_row = [&](int r, uint4* raw) {
+    const bool rok = r >= 0 && r < a.H;
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const uint32_t off = rok && lvo[k] != BUF_OOB ? lvo[k] + (uint32_t)r * rowbytes : BUF_OOB;
+      const buf_v4u t = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      raw[k] = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+  };
+  auto store_row = [&](int r, const uint4* raw) {
+    float* base = s_ring + ((r + 3) % 3) * DS_RP * DS_PP;  // (r >= -1)
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      if (lds[k] < 0) continue;
+      float f[VI];
+      if constexpr (F32) {
+        f[0] = __uint_as_float(raw[k].x); f[1] = __uint_as_float(raw[k].y);
+        f[2] = __uint_as_float(raw[k].z); f[3] = __uint_as_float(raw[k].w);
+      } else {
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&raw[k]);
+#pragma unroll
+        for (int j = 0; j < VI; ++j) f[j] = s16_to<T>(e[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < VI; j += 4)
+        *reinterpret_cast<float4*>(base + lds[k] + j) = make_float4(f[j], f[j + 1], f[j + 2], f[j + 3]);
+    }
+  };
+
+  // depthwise: thread = channel quad qd x output pixels 2 pp, 2 pp + 1; taps and BN in registers
+  const int qd = tid & 31, pp = tid >> 5;
+  float wt[9][4], dsc[4], dsh[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t][j] = a.wd[(4 * qd + j) * 9 + t];
+    dsc[j] = a.scd[4 * qd + j];
+    dsh[j] = a.shd[4 * qd + j];
+  }
+  // pointwise: wave w = output channel tiles 2w, 2w + 1 (weights as the A operand, in registers)
+  uint4 wpr[2][4][NP];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int co = 16 * (2 * wave + u) + li, k = 32 * s + 8 * lq;
+      if constexpr (F32) {
+        const float* wr = (const float*)a.wp + (size_t)co * DS_C + k;
+        gs_split3(*reinterpret_cast<const uint4*>(wr), *reinterpret_cast<const uint4*>(wr + 4), wpr[u][s]);
+      } else {
+        wpr[u][s][0] = *reinterpret_cast<const uint4*>((const T*)a.wp + (size_t)co * DS_C + k);
+      }
+    }
+  for (int i = tid; i < DS_CO; i += 256) {
+    s_bn[i] = a.scp[i];
+    s_bn[DS_CO + i] = a.shp[i];
+  }
+
+  // ---- prologue: rows oh0 - 1, oh0 in the ring, row oh0 + 1 in flight ------------------------
+  uint4 nxt[LP];
+  {
+    uint4 raw[LP];
+    load_row(oh0 - 1, raw);
+    store_row(oh0 - 1, raw);
+    load_row(oh0, raw);
+    store_row(oh0, raw);
+  }
+  load_row(oh0 + 1, nxt);
+  {  // two dropped stores: the loop is entered, as it loops, with 2 stores after the row loads
+    const float z[4] = {0.f, 0.f, 0.f, 0.f};
+    buf_st4(yr, BUF_OOB, z, (T*)nullptr);
+    buf_st4(yr, BUF_OOB + 64, z, (T*)nullptr);
+  }
+  stamp(a.stamps, 1);
+
+  const int oh_end = min(oh0 + a.rs, a.H);
+  constexpr bool res = RES;
+  const __amdgpu_buffer_rsrc_t rr =
+      buf_rsrc(RES ? (const T*)a.r + (size_t)n * a.H * a.W * a.ldr : (const T*)a.x,
+               RES ? (uint32_t)((size_t)a.H * a.W * a.ldr * sizeof(T)) : 0u);
+  for (int oh = oh0; oh < oh_end; ++oh) {
+    // this step's residual, before the row prefetch (so waiting for it does not wait for that)
+    float rv[2][4];
+    if constexpr (RES) {
+      const int ow = ow0 + li;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = 16 * (2 * wave + u) + 4 * lq;
+        const uint32_t off = ow < a.W ? (uint32_t)((((size_t)oh * a.W + ow) * a.ldr + c) * sizeof(T)) : BUF_OOB;
+        if constexpr (F32) {
+          const buf_v4u t = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rv[u][j] = __uint_as_float(t[j]);
+        } else {
+          const buf_v2u t = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
+          rv[u][0] = s16_to<T>((uint16_t)(t[0] & 0xFFFF)); rv[u][1] = s16_to<T>((uint16_t)(t[0] >> 16));
+          rv[u][2] = s16_to<T>((uint16_t)(t[1] & 0xFFFF)); rv[u][3] = s16_to<T>((uint16_t)(t[1] >> 16));
+        }
+      }
+    }
+    store_row(oh + 1, nxt);  // (the slot of row oh - 2: its last reader, dw(oh - 1), is done)
+    load_row(oh + 2, nxt);   // (also past the end: a fixed count per step)
+    __syncthreads();
+    if (oh == oh0 + a.rs / 2) stamp(a.stamps, 2);
+    // ---- depthwise of row oh, two pixels per thread -> s_d as the pointwise B operand --------
+    {
+      float acc[2][4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[p][j] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const float* rowp = s_ring + ((oh - 1 + kh + 3) % 3) * DS_RP * DS_PP + 4 * qd;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {  // ring pixels 2 pp + ci
+          const float4 v = *reinterpret_cast<const float4*>(rowp + (2 * pp + ci) * DS_PP);
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const int kw = ci - p;
+            if (kw < 0 || kw > 2) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[p][j] = fmaf(vv[j], wt[kh * 3 + kw][j], acc[p][j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float o4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = round_as<T>(fmaxf(acc[p][j] * dsc[j] + dsh[j], 0.f));
+        uint16_t* d = s_d + (2 * pp + p) * DS_DP + 4 * qd;
+        if constexpr (F32) {  // gs_split3's terms, one plane each
+          uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t u = __float_as_uint(o4[j]), b0 = u & 0xFFFF0000u;
+            const float r1 = o4[j] - __uint_as_float(b0);
+            const uint32_t b1 = __float_as_uint(r1) & 0xFFFF0000u;
+            const float r2 = r1 - __uint_as_float(b1);
+            p0[j] = b0;
+            p1[j] = b1;
+            p2[j] = __float_as_uint(r2) & 0xFFFF0000u;
+          }
+          *reinterpret_cast<uint2*>(d) = make_uint2((p0[0] >> 16) | p0[1], (p0[2] >> 16) | p0[3]);
+          *reinterpret_cast<uint2*>(d + DS_TW * DS_DP) = make_uint2((p1[0] >> 16) | p1[1], (p1[2] >> 16) | p1[3]);
+          *reinterpret_cast<uint2*>(d + 2 * DS_TW * DS_DP) = make_uint2((p2[0] >> 16) | p2[1], (p2[2] >> 16) | p2[3]);
+        } else {
+          *reinterpret_cast<uint2*>(d) =
+              make_uint2((uint32_t)s16_from<T>(o4[0]) | ((uint32_t)s16_from<T>(o4[1]) << 16),
+                         (uint32_t)s16_from<T>(o4[2]) | ((uint32_t)s16_from<T>(o4[3]) << 16));
+        }
+      }
+    }
+    __syncthreads();
+    if (oh == oh0 + a.rs / 2) stamp(a.stamps, 3);
+    // ---- pointwise: 16 pixels x this wave's 32 output channels, K = 128 in four 32-k steps ----
+    {
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint4 xs[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+          xs[j] = *reinterpret_cast<const uint4*>(s_d + j * DS_TW * DS_DP + li * DS_DP + 32 * s + 8 * lq);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if constexpr (F32) gs_mma_x3(wpr[u][s], xs, acc[u]);
+          else DsMma<T>::run(wpr[u][s][0], xs[0], acc[u]);
+        }
+      }
+      const int ow = ow0 + li;
+      const uint32_t yoff = ow < a.W ? (uint32_t)((((size_t)oh * a.W + ow) * a.ldy) * sizeof(T)) : BUF_OOB;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = 16 * (2 * wave + u) + 4 * lq;
+        const float4 sc = *reinterpret_cast<const float4*>(&s_bn[c]);
+        const float4 sh = *reinterpret_cast<const float4*>(&s_bn[DS_CO + c]);
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+        float o4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[u][r] * scv[r] + shv[r];
+          if constexpr (RES) v += rv[u][r];
+          o4[r] = fmaxf(v, 0.f);
+        }
+        buf_st4(yr, yoff == BUF_OOB ? BUF_OOB : yoff + c * (uint32_t)sizeof(T), o4, (T*)nullptr);
+      }
+    }
+    if (oh == oh0 + a.rs / 2) stamp(a.stamps, 4);
+  }
+  stamp(a.stamps, 5);
+}
+
+bool ds_ok(const DsArgs& a) {
+  return a.N > 0 && a.N < 65536 && a.H > 0 && a.W > 0 && a.C == DS_C && a.Co == DS_CO &&
+         (a.r == nullptr || (a.ldr >= DS_CO && a.ldr % 4 == 0 && ((uintptr_t)a.r & 15) == 0 &&
+                             4LL * a.H * a.W * a.ldr < (long long)BUF_OOB)) &&
+         a.rs >= 1 && cdiv(a.H, a.rs) < 65536 && a.ldy >= DS_CO && a.ldy % 4 == 0 &&
+         ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.y & 15) == 0 &&
+         // per-image buffer ranges below BUF_OOB (32-bit buffer offsets)
+         4LL * a.H * a.W * DS_C < (long long)BUF_OOB && 4LL * a.H * a.W * a.ldy < (long long)BUF_OOB;
+}
+
+// rows walked per workgroup: whole rounds of the 2-per-CU grid where the map allows
+int ds_rows(int N, int H, int W) {
+  const long long slots = 2LL * 256;
+  int best = 8;
+  double best_eff = -1.0;
+  for (int rs = 4; rs <= 16; ++rs) {
+    const long long wg = (long long)N * cdiv(W, DS_TW) * cdiv(H, rs);
+    const long long rounds = (wg + slots - 1) / slots;
+    const double eff = (double)wg / (double)(rounds * slots) * rs / (rs + 2.0);  // (+2: prologue rows)
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = rs; }
+  }
+  return best;
+}
+
+int ds_fwd(const DsArgs& a, int dtype, hipStream_t st) {
+  if (!ds_ok(a)) {
+    set_error("ds_fwd: unsupported shape N=%d H=%d W=%d C=%d Co=%d ldy=%d rs=%d", a.N, a.H, a.W,
+              a.C, a.Co, a.ldy, a.rs);
+    return E_UNSUPPORTED;
+  }
+  DsArgs as = a;
+  as.stamps = stamp_region();
+  const dim3 g(cdiv(a.W, DS_TW), cdiv(a.H, a.rs), a.N);
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  ProfScope ps(PK_DSCONV, st, E * a.N * a.H * a.W * (DS_C + DS_CO + (a.r ? DS_CO : 0)),
+               2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO));
+#define DSK(T)                                                                \
+  do {                                                                        \
+    if (a.r) dsconv_fwd_kernel<T, true><<<g, 256, 0, st>>>(as);               \
+    else dsconv_fwd_kernel<T, false><<<g, 256, 0, st>>>(as);                  \
+  } while (0)
+  if (dtype == DT_F32) DSK(float);
+  else if (dtype == DT_F16) DSK(f16);
+  else DSK(bf16);
+#undef DSK
+  return check_launch("ds_fwd");
+}
+
+}  // namespace fscnn

@@ -422,6 +422,24 @@ struct StemArgs {
 bool stem_ok(const StemArgs& a);
 int stem_fwd(const StemArgs& a, int dtype, hipStream_t st);
 
+// ---- inference DSConv: dw 3x3 s1 p1 + BN + ReLU -> 1x1 + BN + ReLU in one launch (dsconv.hip) --
+struct DsArgs {
+  const void* x;               // NHWC [N,H,W] x C (contiguous rows of C elements), storage dtype
+  int N, H, W, C, Co;          // C = Co = 128 (the Classifer's _DSConv)
+  const float* wd;             // depthwise weights [C][9] fp32
+  const float *scd, *shd;      // folded BN of the depthwise
+  const void* wp;              // pointwise weights [Co][C] in the storage dtype
+  const float *scp, *shp;      // folded BN of the pointwise
+  void* y; int ldy;            // NHWC [N,H,W] x Co (row stride ldy elements)
+  const void* r = nullptr;     // optional residual added after the pointwise BN, before its ReLU
+  int ldr = 0;                 // (the FFM: relu(BN_l(conv_l(dw)) + f), :213-218); may alias y
+  int rs;                      // output rows walked per workgroup (ds_rows)
+  unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
+};
+bool ds_ok(const DsArgs& a);
+int ds_rows(int N, int H, int W);
+int ds_fwd(const DsArgs& a, int dtype, hipStream_t st);
+
 // input gradient of conv0 (autograd of the image through models/fast_scnn.py:153)
 struct Conv0DgradArgs {
   const void* dz;  // NHWC [N,Ho,Wo,32] in the plan dtype (conv0's BN-backward output)

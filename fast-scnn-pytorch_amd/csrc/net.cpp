@@ -953,6 +953,16 @@ struct Exec {
     }();
     return on;
   }
+  // inference DSConv fusion (dsconv.hip: the classifier's two DSConvs, the FFM's dwconv +
+  // conv_lower_res); FSCNN_DSCONV_FUSED=0 runs dw + pw as two launches (the bit-identity test,
+  // tests/test_gpu_switches.py)
+  static bool ds_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("FSCNN_DSCONV_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   int fold_all() {
     FoldTable t{};
     auto add = [&](const BnL& bn, const Unit& u, const ConvL* conv) {
@@ -1117,12 +1127,25 @@ struct Exec {
       u.N = N; u.Hi = pl.H5; u.Wi = pl.W5; u.C = 128; u.Ho = pl.H3; u.Wo = pl.W3;
       u.x = W(pl.po.a); u.ldx = 128; u.y = W(pl.up_low); u.ldy = 128;
       TRY(up_nhwc(u, dt, r.st));
-      TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
       if (!train) {
-        // f = BN_h(conv_h(hr)) ; f = relu(BN_l(conv_l(dw)) + f)
+        // f = BN_h(conv_h(hr)) ; f = relu(BN_l(conv_l(dw)) + f), the dw and conv_l in one
+        // launch (dsconv.hip) when it fits
         TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, raw(W(pl.l2pw.a), 64), false));
-        TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, act(pl.fdw), true, W(pl.f), 128));
+        DsArgs fa{};
+        fa.x = W(pl.up_low); fa.N = N; fa.H = pl.H3; fa.W = pl.W3; fa.C = 128; fa.Co = 128;
+        fa.wd = P(net.ffm_dw.w); fa.scd = Wf(pl.fdw.scale); fa.shd = Wf(pl.fdw.shift);
+        fa.wp = Wg(net.ffm_low); fa.scp = Wf(pl.flow.scale); fa.shp = Wf(pl.flow.shift);
+        fa.y = W(pl.flow.a); fa.ldy = pl.flow.ld; fa.r = W(pl.f); fa.ldr = 128;
+        fa.rs = ds_rows(N, pl.H3, pl.W3);
+        if (ds_enabled() && ds_ok(fa)) {
+          g_prof_tag = "feature_fusion.dwconv + conv_lower_res (fused)";
+          TRY(ds_fwd(fa, dt, r.st));
+        } else {
+          TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+          TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, act(pl.fdw), true, W(pl.f), 128));
+        }
       } else {
+        TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
         g_prof_tag = pl.flow.name.c_str();
         GemmArgs g{};
         const In fin = act(pl.fdw);
@@ -1143,13 +1166,35 @@ struct Exec {
       }
     }
     // ---- Classifier ----
-    TRY(dw(pl.c1dw, net.cls1.dw, net.cls1.bdw, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
-    TRY(pw(pl.c1pw, net.cls1.pw, &net.cls1.bpw, act(pl.c1dw), true));
-    TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+    // inference: each DSConv (dw + BN + ReLU, pw + BN + ReLU) in one launch (dsconv.hip)
+    auto ds_args = [&](const DsL& d, const Unit& udw, const Unit& upw, const void* xin) {
+      DsArgs s{};
+      s.x = xin; s.N = N; s.H = pl.H3; s.W = pl.W3; s.C = 128; s.Co = 128;
+      s.wd = P(d.dw.w); s.scd = Wf(udw.scale); s.shd = Wf(udw.shift);
+      s.wp = Wg(d.pw); s.scp = Wf(upw.scale); s.shp = Wf(upw.shift);
+      s.y = W(upw.a); s.ldy = upw.ld; s.rs = ds_rows(N, pl.H3, pl.W3);
+      return s;
+    };
+    const bool ds_fuse = !train && ds_enabled() && pl.c1pw.ld == 128;
+    const DsArgs ds1 = ds_fuse ? ds_args(net.cls1, pl.c1dw, pl.c1pw, W(pl.f)) : DsArgs{};
+    if (ds_fuse && ds_ok(ds1)) {
+      g_prof_tag = "classifier.dsconv1 (fused)";
+      TRY(ds_fwd(ds1, dt, r.st));
+    } else {
+      TRY(dw(pl.c1dw, net.cls1.dw, net.cls1.bdw, raw(W(pl.f), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+      TRY(pw(pl.c1pw, net.cls1.pw, &net.cls1.bpw, act(pl.c1dw), true));
+    }
     // train with Dropout: the dsconv2 pw BN+ReLU output is only read by the dropout, which
     // applies the BN itself (c2pw.a is never stored: one 128-channel write + read fewer)
     const bool drop_fused = train && r.dropout_p > 0.f;
-    TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, act(pl.c2dw), true, nullptr, 0, !drop_fused));
+    const DsArgs ds2 = ds_fuse ? ds_args(net.cls2, pl.c2dw, pl.c2pw, W(pl.c1pw.a)) : DsArgs{};
+    if (ds_fuse && ds_ok(ds2)) {
+      g_prof_tag = "classifier.dsconv2 (fused)";
+      TRY(ds_fwd(ds2, dt, r.st));
+    } else {
+      TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1));
+      TRY(pw(pl.c2pw, net.cls2.pw, &net.cls2.bpw, act(pl.c2dw), true, nullptr, 0, !drop_fused));
+    }
     const void* cls_in = W(pl.c2pw.a);
     if (drop_fused) {
       DropArgs d{};

@@ -71,36 +71,6 @@ constexpr int SW_CP = SW_CC + 1;               // conv0 ring row pitch (pixel 63
 constexpr int SW_IC = 2 * SW_CC + 1;           // image columns (127)
 constexpr int SW_NIR = 5;                      // image ring rows
 constexpr int SW_NCR = 3;                      // conv0 ring rows
-constexpr uint32_t SW_OOB = 0x80000000u;       // a buffer offset past every range
-typedef unsigned int sw_v4u __attribute__((__vector_size__(16)));
-typedef unsigned int sw_v2u __attribute__((__vector_size__(8)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sw_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t b = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-__device__ __forceinline__ void sw_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[4],
-                                       float*) {
-  const sw_v4u t = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                   __float_as_uint(v[3])};
-  __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
-}
-__device__ __forceinline__ void sw_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[4],
-                                       bf16*) {
-  const sw_v2u t = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                   (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
-  __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
-}
-__device__ __forceinline__ void sw_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[4],
-                                       f16*) {
-  const sw_v2u t = {(uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16),
-                   (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16)};
-  __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
-}
-
 template <typename T, int XB>
 __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
   constexpr int BF = sizeof(T) == 4 ? 0 : (std::is_same<T, f16>::value ? 2 : 1);
@@ -147,9 +117,9 @@ __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
   const int coff = 4 * ow0 - 2 - cbase;               // image column 2 c1o in the staged row
   const size_t plane = (size_t)a.H * a.W;
   const __amdgpu_buffer_rsrc_t xr =
-      sw_rsrc((const TI*)a.x + (size_t)n * 3 * plane, (uint32_t)(3 * plane * sizeof(TI)));
+      buf_rsrc((const TI*)a.x + (size_t)n * 3 * plane, (uint32_t)(3 * plane * sizeof(TI)));
   const size_t ysz = (size_t)a.H2 * a.W2 * a.ldy;
-  const __amdgpu_buffer_rsrc_t yr = sw_rsrc((T*)a.y + (size_t)n * ysz, (uint32_t)(ysz * sizeof(T)));
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc((T*)a.y + (size_t)n * ysz, (uint32_t)(ysz * sizeof(T)));
 
   // image rows [r0, r0 + R) of all 3 channels: 16-B buffer loads into registers / into the ring
   auto load_rows = [&](int r0, int R, uint4* raw, int LP) {
@@ -160,8 +130,8 @@ __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
       const int ci = rem / NVC, v = rem - ci * NVC;
       const int ir = r0 + row, ic = cbase + v * VI;
       const bool ok = row < R && ir >= 0 && ir < a.H && ic >= 0 && ic + VI <= a.W;
-      const uint32_t off = ok ? (uint32_t)(((size_t)ci * a.H + ir) * a.W + ic) * sizeof(TI) : SW_OOB;
-      const sw_v4u t = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      const uint32_t off = ok ? (uint32_t)(((size_t)ci * a.H + ir) * a.W + ic) * sizeof(TI) : BUF_OOB;
+      const buf_v4u t = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
       raw[k] = make_uint4(t[0], t[1], t[2], t[3]);
     }
   };
@@ -295,8 +265,8 @@ __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
     for (int k = 0; k < LP4; ++k) {
       const int ir = r0 + ((lds[k] >> 24) & 7);
       const bool ok = ((lds[k] >> 28) & 1) && ir >= 0 && ir < a.H;
-      const uint32_t off = ok ? lvo[k] + (uint32_t)(r0 * rowbytes) : SW_OOB;
-      const sw_v4u t = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      const uint32_t off = ok ? lvo[k] + (uint32_t)(r0 * rowbytes) : BUF_OOB;
+      const buf_v4u t = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
       raw[k] = make_uint4(t[0], t[1], t[2], t[3]);
     }
   };
@@ -426,8 +396,8 @@ __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
   {  // two dropped stores: the loop is entered, as it loops, with 2 stores after the row loads,
      // so the wait for the rows can leave the stores in flight (vmcnt counts in issue order)
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
-    sw_st4(yr, SW_OOB, z, (T*)nullptr);
-    sw_st4(yr, SW_OOB + 64, z, (T*)nullptr);  // (another address: not merged with the first)
+    buf_st4(yr, BUF_OOB, z, (T*)nullptr);
+    buf_st4(yr, BUF_OOB + 64, z, (T*)nullptr);  // (another address: not merged with the first)
   }
   __syncthreads();
   stamp(a.stamps, 1);
@@ -518,7 +488,7 @@ __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
       const int ow = ow0 + op;
       const uint32_t yoff = op < SW_TW && ow < a.W2
                                 ? (uint32_t)(((size_t)oh * a.W2 + ow) * a.ldy) * sizeof(T)
-                                : SW_OOB;
+                                : BUF_OOB;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {  // (u >= ntn: a dropped store, so every step issues two)
         const int c = u < ntn ? 16 * (nt0 + u) + 4 * lq : 0;
@@ -531,7 +501,7 @@ __global__ __launch_bounds__(256, 3) void stem_walk_kernel(StemArgs a) {
           const float v = acc[u][r] * scv[r] + shv[r];
           o4[r] = fmaxf(v, 0.f);
         }
-        sw_st4(yr, yoff == SW_OOB || u >= ntn ? SW_OOB : yoff + c * (uint32_t)sizeof(T), o4,
+        buf_st4(yr, yoff == BUF_OOB || u >= ntn ? BUF_OOB : yoff + c * (uint32_t)sizeof(T), o4,
                (T*)nullptr);
       }
     }
@@ -547,9 +517,9 @@ bool stem_ok(const StemArgs& a) {
          ve == 4 && a.ldy >= ST_C2 && a.ldy % 4 == 0 &&
          a.H1 == (a.H - 3) / 2 + 1 && a.W1 == (a.W - 3) / 2 + 1 && a.H2 == (a.H1 - 1) / 2 + 1 &&
          a.W2 == (a.W1 - 1) / 2 + 1 && a.N < 65536 && cdiv(a.H2, SW_RS) < 65536 &&
-         // per-image buffer ranges below SW_OOB (32-bit buffer offsets)
-         3LL * a.H * a.W * (a.x_dtype ? 2 : 4) < (long long)SW_OOB &&
-         4LL * a.H2 * a.W2 * a.ldy < (long long)SW_OOB;
+         // per-image buffer ranges below BUF_OOB (32-bit buffer offsets)
+         3LL * a.H * a.W * (a.x_dtype ? 2 : 4) < (long long)BUF_OOB &&
+         4LL * a.H2 * a.W2 * a.ldy < (long long)BUF_OOB;
 }
 
 int stem_fwd(const StemArgs& a, int dtype, hipStream_t st) {

@@ -227,11 +227,35 @@ int fscnn_block_ltd_fwd(const void* x, int x_dtype, int dtype, int N, int H, int
                         const void* w_pw, const float* scale_p, const float* shift_p, void* y,
                         int ldy, void* stream);
 
+/* fscnn_block_dsconv_fwd: an inference _DSConv (models/fast_scnn.py:64-79; the Classifer's
+ * dsconv1 / dsconv2, :228-231) in one launch: y = relu(BN_p(W_p * relu(BN_d(dw3x3_s1_p1(x))))),
+ * every BN folded (scale, shift fp32 per channel).  x NHWC [N][H][W] x C in dtype (rows of C
+ * contiguous elements, 16-B aligned); w_dw [C][9] fp32, w_pw [Co][C] in dtype; y NHWC with row
+ * stride ldy elements (>= Co, multiple of 4, 16-B aligned).  C = Co = 128 (E_UNSUPPORTED
+ * otherwise).  The depthwise output never reaches memory.  Replaces _DSConv's dw conv + BN + ReLU
+ * and pw conv + BN + ReLU (two launches of the unfused eval path); the executor uses it for the
+ * classifier's two DSConvs of every eval plan. */
+int fscnn_block_dsconv_fwd(const void* x, int dtype, int N, int H, int W, int C, int Co,
+                           const float* w_dw, const float* scale_d, const float* shift_d,
+                           const void* w_pw, const float* scale_p, const float* shift_p, void* y,
+                           int ldy, void* stream);
+
+/* fscnn_block_dsconv_res_fwd: the same with a residual added after the pointwise BN, before the
+ * final ReLU: y = relu(BN_p(W_p * relu(BN_d(dw3x3(x)))) + res) -- the FeatureFusionModule's
+ * dwconv + conv_lower_res + the high-res branch (models/fast_scnn.py:207-218).  res NHWC with row
+ * stride ldres (>= Co, multiple of 4, 16-B aligned); res may alias y (each element is read before
+ * it is written, by the same thread). */
+int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, int C, int Co,
+                               const float* w_dw, const float* scale_d, const float* shift_d,
+                               const void* w_pw, const float* scale_p, const float* shift_p,
+                               const void* res, int ldres, void* y, int ldy, void* stream);
+
 /* ---- launch profiler (bench.py roofline, tools/layer_report.py) ----------------------------
  * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 7 bn_apply,
  * 8 bn_bwd (apply), 9 upsample, 10 upsample_bwd, 11 cross_entropy / fused loss head,
  * 12 conv0_wgrad, 13 bn_bwd_reduce, 14 bn_finalize, 15 ppm_branches (the four pyramid-pooling
- * branch convs + BN + ReLU, one launch each way), 16 ir_block (fused inference bottleneck);
+ * branch convs + BN + ReLU, one launch each way), 16 ir_block (fused inference bottleneck),
+ * 17 ltd_stem (fused inference stem), 18 dsconv (fused inference DSConv);
  * 100 = every kind.
  * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
  * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes

@@ -2,8 +2,10 @@
 executor reads FSCNN_STEM_FUSED once).  Eval forwards (no_grad) over the image dtypes and map
 sizes the fused inference stem (csrc/stem.hip) handles -- partial edge tiles included -- saving
 every output, plus the number of stem launches the library's profiler saw in the first case.
+With ``--dsconv``: the same for the fused classifier DSConvs (csrc/dsconv.hip,
+FSCNN_DSCONV_FUSED) over maps whose classifier M = N x H/8 x W/8 >= 4096.
 
-    python tests/_stem_worker.py OUT.npz
+    python tests/_stem_worker.py OUT.npz [--dsconv]
 """
 import ctypes
 import os
@@ -24,9 +26,20 @@ CASES = [  # (name, classes, shape, image dtype, autocast dtype)
     ("fp32_unaligned", 19, (1, 3, 66, 98), "float32", None),  # W % 4 != 0: unfused either way
 ]
 PK_STEM = 17
+# (the classifier runs at H/8 x W/8: M >= 4096 for the unfused pointwise to take the streaming
+# GEMM whose MFMA order the fused DSConv reproduces)
+DS_CASES = [
+    ("fp32", 19, (2, 3, 512, 512), "float32", None),
+    ("fp32_odd", 19, (1, 3, 520, 1048), "float32", None),  # 65 x 131: partial strips and segments
+    ("bf16", 19, (1, 3, 512, 1024), "bfloat16", None),
+    ("fp16_c2", 2, (1, 3, 480, 640), "float16", None),
+    ("autocast16", 19, (1, 3, 520, 1048), "float32", "float16"),
+]
+PK_DSCONV = 18
 
 
-def main(out):
+def main(out, dsconv=False):
+    cases, pk = (DS_CASES, PK_DSCONV) if dsconv else (CASES, PK_STEM)
     import numpy as np
     import torch
     import _fscnn_boot
@@ -36,7 +49,7 @@ def main(out):
     lib = _lib.load()
     dev = torch.device("cuda", 0)
     res = {}
-    for i, (name, nc, shape, xdt, ac) in enumerate(CASES):
+    for i, (name, nc, shape, xdt, ac) in enumerate(cases):
         sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
               arch.portable_state_dict(nc, seed=1, variant="bnrand").items()}
         m = FastSCNN(nc)
@@ -45,7 +58,7 @@ def main(out):
         m._keep_ws = bool(os.environ.get("STEM_DEBUG"))
         x = torch.from_numpy(portable_init.input_tensor(7 + i, shape)).to(dev).to(getattr(torch, xdt))
         if i == 0:
-            _lib.check(lib.fscnn_prof_begin(PK_STEM, 64), "fscnn_prof_begin")
+            _lib.check(lib.fscnn_prof_begin(pk, 64), "fscnn_prof_begin")
         with torch.no_grad():
             if ac:
                 with torch.autocast("cuda", dtype=getattr(torch, ac)):
@@ -69,4 +82,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], "--dsconv" in sys.argv[2:])

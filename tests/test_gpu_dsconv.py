@@ -1,0 +1,115 @@
+"""Fused inference DSConv (csrc/dsconv.hip; models/fast_scnn.py:64-79 _DSConv, the Classifer's
+dsconv1 / dsconv2 at :228-231) through the C ABI (``fscnn_block_dsconv_fwd``) against a plain
+PyTorch fp32 restatement: depthwise 3x3 s1 p1 -> folded BN -> ReLU -> 1x1 conv (128 -> 128) ->
+folded BN -> ReLU.
+
+fp32: the depthwise is an fp32 fma chain, the pointwise the six-product bf16 split (fp32
+products): only the summation order differs (2e-5 of the output magnitude).  bf16 / fp16: the
+restatement rounds the input, the depthwise output and the pointwise weights to the storage type
+exactly where the HIP path does, so the difference is accumulation order plus the final
+rounding.  Shapes: whole and partial 16-column strips, row segments that do not divide the map,
+an output row stride larger than 128.  Bit-identity with the two unfused launches:
+tests/test_gpu_switches.py::test_dsconv_fused_bit_identical.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fast_scnn_pytorch_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * 2 - 1) * scale
+
+
+def _ref(x, wd, wp, bn, dt):
+    q = (lambda t: t) if dt == torch.float32 else (lambda t: t.to(dt).float())  # noqa: E731
+    (sd, hd), (sp, hp) = bn
+    c = lambda t: t[None, :, None, None]  # noqa: E731
+    xc = q(x).permute(0, 3, 1, 2)
+    d = q(F.relu(F.conv2d(xc, wd.reshape(128, 1, 3, 3), padding=1, groups=128) * c(sd) + c(hd)))
+    return F.relu(F.conv2d(d, q(wp)[:, :, None, None]) * c(sp) + c(hp))
+
+
+CASES = [  # (N, H, W, ldy)
+    (2, 24, 48, 128),
+    (1, 37, 53, 128),   # partial strip (53 = 3 x 16 + 5), rows not a multiple of the segment
+    (1, 9, 16, 136),    # row stride > 128
+    (3, 5, 7, 128),     # one partial strip, maps smaller than the window
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W,ldy", CASES)
+def test_dsconv_fwd_vs_torch(dt, N, H, W, ldy):
+    x = rnd(N, H, W, 128, seed=1)
+    wd = rnd(128, 9, seed=3, scale=0.4)
+    wp = rnd(128, 128, seed=4, scale=1.0 / 128 ** 0.5)
+    bn = [(rnd(128, seed=10 + i) * 0.5 + 1.0, rnd(128, seed=20 + i) * 0.2) for i in range(2)]
+    ref = _ref(x, wd, wp, bn, dt)
+    xd = x.to(dt).to(DEV).contiguous()
+    wdd = wd.to(DEV).contiguous()
+    wpd = wp.to(dt).to(DEV).contiguous()
+    bnd = [(s.to(DEV), h.to(DEV)) for s, h in bn]
+    y = torch.full((N, H, W, ldy), float("nan"), dtype=dt, device=DEV)
+    _lib.call("fscnn_block_dsconv_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, 128, 128,
+              _lib.ptr(wdd), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]), _lib.ptr(wpd),
+              _lib.ptr(bnd[1][0]), _lib.ptr(bnd[1][1]), _lib.ptr(y), ldy, _lib.stream_ptr())
+    torch.cuda.synchronize()
+    got = y[..., :128].float().cpu().permute(0, 3, 1, 2)
+    if ldy > 128:  # the padding columns are not written
+        assert torch.isnan(y[..., 128:].float()).all()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    tol = 2e-5 * scale if dt == torch.float32 else 2 ** -7 * scale
+    assert err <= tol, (err, tol, scale)
+    if dt != torch.float32:  # at most a few elements off by more than one output rounding
+        far = ((got - ref).abs() > 2 ** -8 * ref.abs() + 1e-3 * scale).float().mean().item()
+        assert far < 1e-3, far
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_dsconv_fwd_residual_vs_torch(dt):
+    """The FFM form (models/fast_scnn.py:213-218): relu(BN_l(conv_l(relu(BN_d(dw(x))))) + f),
+    the residual f read from the output buffer itself (y aliases f, as in the executor)."""
+    N, H, W = 2, 19, 37
+    x = rnd(N, H, W, 128, seed=5)
+    f = rnd(N, H, W, 128, seed=6)
+    wd = rnd(128, 9, seed=7, scale=0.4)
+    wp = rnd(128, 128, seed=8, scale=1.0 / 128 ** 0.5)
+    bn = [(rnd(128, seed=30 + i) * 0.5 + 1.0, rnd(128, seed=40 + i) * 0.2) for i in range(2)]
+    q = (lambda t: t) if dt == torch.float32 else (lambda t: t.to(dt).float())  # noqa: E731
+    (sd, hd), (sp, hp) = bn
+    c = lambda t: t[None, :, None, None]  # noqa: E731
+    d = q(F.relu(F.conv2d(q(x).permute(0, 3, 1, 2), wd.reshape(128, 1, 3, 3), padding=1,
+                          groups=128) * c(sd) + c(hd)))
+    ref = F.relu(F.conv2d(d, q(wp)[:, :, None, None]) * c(sp) + c(hp) + q(f).permute(0, 3, 1, 2))
+    xd = x.to(dt).to(DEV).contiguous()
+    y = f.to(dt).to(DEV).contiguous()
+    wdd, wpd = wd.to(DEV).contiguous(), wp.to(dt).to(DEV).contiguous()
+    bnd = [(s.to(DEV), h.to(DEV)) for s, h in bn]
+    _lib.call("fscnn_block_dsconv_res_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, 128, 128,
+              _lib.ptr(wdd), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]), _lib.ptr(wpd),
+              _lib.ptr(bnd[1][0]), _lib.ptr(bnd[1][1]), _lib.ptr(y), 128, _lib.ptr(y), 128,
+              _lib.stream_ptr())
+    torch.cuda.synchronize()
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    tol = 2e-5 * scale if dt == torch.float32 else 2 ** -7 * scale
+    assert err <= tol, (err, tol, scale)
+
+
+def test_dsconv_rejects_other_widths():
+    x = torch.zeros(1, 4, 4, 64, device=DEV)
+    w = torch.zeros(128 * 128, device=DEV)
+    y = torch.zeros(1, 4, 4, 128, device=DEV)
+    rc = _lib.load().fscnn_block_dsconv_fwd(_lib.ptr(x), 0, 1, 4, 4, 64, 128,
+                                            *([_lib.ptr(w)] * 6), _lib.ptr(y), 128,
+                                            _lib.stream_ptr())
+    assert rc != 0

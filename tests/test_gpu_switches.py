@@ -3,8 +3,8 @@ non-default path parity-green.  The switches are read once per process, so each 
 fresh child process:
 
 * ``FSCNN_SIDE_STREAM=0`` — every weight gradient on the caller's stream (one stream);
-* ``FSCNN_F32_SPLIT=0``   — exact fp32 MFMA in the eval pointwise GEMMs instead of the
-  three-way bf16 split of each fp32 operand;
+* ``FSCNN_F32_SPLIT=0``   — exact fp32 MFMA in the eval pointwise GEMM launches instead of the
+  three-way bf16 split of each fp32 operand (the fused stem and DSConv always split);
 * ``FSCNN_GRAPHS=1``      — whole forward / backward-stage calls captured into hipGraphs and
   replayed (the dropout seed then travels through a device slot the forward writes);
 * ``FSCNN_LTD_FUSED=0``   — (16-bit train plans) LTD.dsconv1.dw's input gradient stored and
@@ -16,6 +16,9 @@ fresh child process:
   at M >= 4096 low-res pixels in 16-bit plans: test_drop_fused_matches_separate_passes).
 * ``FSCNN_STEM_FUSED=0``  — (inference) conv0, LTD.dsconv1.dw and .pw as three launches instead of
   the fused stem (csrc/stem.hip): bit-identical outputs (test_stem_fused_bit_identical).
+* ``FSCNN_DSCONV_FUSED=0`` — (inference) each classifier DSConv as its depthwise and pointwise
+  launches instead of one fused launch (csrc/dsconv.hip): bit-identical outputs
+  (test_dsconv_fused_bit_identical).
 
 (Round 5 removed the measured-slower variants and their switches: FSCNN_DW_LOOP, FSCNN_GEMM_PF,
 FSCNN_CE_HEAD, FSCNN_CE_PACK, FSCNN_GEMM_MINT.)
@@ -50,7 +53,8 @@ BF16 = ["tests/test_gpu_model.py::test_bf16_forward_within_bf16_budget"]
 CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_GRAPHS=1": TRAIN + EVAL + HEAD16 + ["tests/test_gpu_autograd.py"],
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
-         "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL}
+         "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL,
+         "FSCNN_DSCONV_FUSED=0": EVAL}
 
 
 def _env(switch):
@@ -81,9 +85,11 @@ def _worker(tmp_path, switch, half=None):
     return dict(np.load(out))
 
 
-def _stem_worker(tmp_path, switch):
-    out = str(tmp_path / ("stem_%s.npz" % (switch or "default").replace("=", "_")))
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_stem_worker.py"), out],
+def _stem_worker(tmp_path, switch, dsconv=False):
+    out = str(tmp_path / ("stem_%s%s.npz" % ((switch or "default").replace("=", "_"),
+                                               "_ds" if dsconv else "")))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_stem_worker.py"), out] +
+                       (["--dsconv"] if dsconv else []),
                        cwd=ROOT, env=_env(switch), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     return dict(np.load(out))
@@ -97,6 +103,23 @@ def test_stem_fused_bit_identical(tmp_path):
     ref = _stem_worker(tmp_path, "FSCNN_STEM_FUSED=0")
     got = _stem_worker(tmp_path, None)
     assert int(ref["stem_launches"]) == 0 and int(got["stem_launches"]) == 1
+    for k in ref:
+        if k == "stem_launches":
+            continue
+        assert np.isfinite(got[k]).all(), k
+        assert np.array_equal(ref[k], got[k]), "%s: max |diff| %g" % (
+            k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
+
+
+def test_dsconv_fused_bit_identical(tmp_path):
+    """The fused inference DSConv (depthwise + BN + ReLU and pointwise + BN (+ residual) + ReLU in
+    one launch, csrc/dsconv.hip: the classifier's dsconv1 / dsconv2 and the FFM's dwconv +
+    conv_lower_res) gives bit-identical outputs to the unfused launches: fp32 / bf16 / fp16
+    images, autocast fp16, partial strips and row segments (tests/_stem_worker.py --dsconv).  The
+    default run really took the three fused launches."""
+    ref = _stem_worker(tmp_path, "FSCNN_DSCONV_FUSED=0", dsconv=True)
+    got = _stem_worker(tmp_path, None, dsconv=True)
+    assert int(ref["stem_launches"]) == 0 and int(got["stem_launches"]) == 3
     for k in ref:
         if k == "stem_launches":
             continue
