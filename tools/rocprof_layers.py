@@ -47,6 +47,7 @@ FAMILY_RE = {
     "ppm_branches": r"ppm_(fwd|fwd_lds|bwd)_kernel",
     "ir_block": r"ir_block_kernel",
     "ltd_stem": r"stem_walk_kernel",
+    "dsconv": r"dsconv_fwd_kernel",
 }
 MARK = re.compile(r"bitwise_not")  # torch's bitwise_not kernel (the phase marker: no step uses it)
 
