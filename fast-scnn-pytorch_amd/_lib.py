@@ -116,9 +116,9 @@ SIGNATURES = {
                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "fscnn_block_dsconv_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
-    "fscnn_block_dsconv_res_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
-                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
-                                           c_vp]),
+    "fscnn_block_dsconv_res_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                           c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                           c_vp, c_int, c_vp]),
 }
 
 _lib = None

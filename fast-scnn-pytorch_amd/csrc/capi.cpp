@@ -757,7 +757,7 @@ int fscnn_block_dsconv_fwd(const void* x, int dtype, int N, int H, int W, int C,
 }
 
 int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, int C, int Co,
-                               const float* w_dw, const float* scale_d, const float* shift_d,
+                               int Hi, int Wi, const float* w_dw, const float* scale_d, const float* shift_d,
                                const void* w_pw, const float* scale_p, const float* shift_p,
                                const void* res, int ldres, void* y, int ldy, void* stream) {
   if (!x || !y || !res || !w_dw || !scale_d || !shift_d || !w_pw || !scale_p || !shift_p) {
@@ -773,6 +773,7 @@ int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, in
   a.wd = w_dw; a.scd = scale_d; a.shd = shift_d;
   a.wp = w_pw; a.scp = scale_p; a.shp = shift_p;
   a.r = res; a.ldr = ldres;
+  a.Hi = Hi > 0 ? Hi : 0; a.Wi = Hi > 0 ? Wi : 0;
   a.y = y; a.ldy = ldy;
   a.rs = ds_rows(N, H, W);
   return ds_fwd(a, dtype, S(stream));

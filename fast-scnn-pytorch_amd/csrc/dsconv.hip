@@ -27,6 +27,7 @@ constexpr int DS_TW = 16;              // output columns per workgroup (one MFMA
 constexpr int DS_RP = DS_TW + 2;       // ring pixels per row (the window's halo)
 constexpr int DS_PP = DS_C + 4;        // ring floats per pixel (padded)
 constexpr int DS_DP = DS_C + 8;        // pointwise operand halves per pixel (padded)
+constexpr int DS_UC = 8;               // upsample mode: staged low-resolution columns per strip
 
 template <typename T>
 struct DsMma;  // one 16-bit MFMA per operand pair (the 16-bit streaming GEMM's GsMma)
@@ -53,7 +54,7 @@ struct DsMma<float> {
   static __device__ __forceinline__ void run(const uint4&, const uint4&, f32x4&) {}
 };
 
-template <typename T, bool RES>
+template <typename T, bool RES, bool UP>
 __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int NP = F32 ? 3 : 1;                  // pointwise operand planes
@@ -63,6 +64,9 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   __shared__ __attribute__((aligned(16))) float s_ring[3 * DS_RP * DS_PP];   // [row % 3][px][c]
   __shared__ __attribute__((aligned(16))) uint16_t s_d[NP * DS_TW * DS_DP];  // [plane][px][c]
   __shared__ __attribute__((aligned(16))) float s_bn[2 * DS_CO];             // pointwise scale, shift
+  // upsample mode: the two low-resolution rows x DS_UC columns a ring row interpolates from,
+  // double-buffered ([buf][row][col][c], fp32)
+  __shared__ __attribute__((aligned(16))) float s_stg[UP ? 2 * 2 * DS_UC * DS_C : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -79,7 +83,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   }
   stamp(a.stamps, 0);
   const int ow0 = tw * DS_TW, oh0 = sg * a.rs;
-  const size_t img = (size_t)a.H * a.W * DS_C;
+  const size_t img = UP ? (size_t)a.Hi * a.Wi * DS_C : (size_t)a.H * a.W * DS_C;
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc((const T*)a.x + (size_t)n * img, (uint32_t)(img * sizeof(T)));
   const size_t ysz = (size_t)a.H * a.W * a.ldy;
   const __amdgpu_buffer_rsrc_t yr = buf_rsrc((T*)a.y + (size_t)n * ysz, (uint32_t)(ysz * sizeof(T)));
@@ -126,6 +130,85 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
     }
   };
 
+  // ---- upsample mode: a ring row = bilinear (align_corners) of two staged low-res rows --------
+  constexpr int LPU = (2 * DS_UC * VPP + 255) / 256;  // staging loads per thread
+  const float shs = ac_scale(a.Hi, a.H), sws = ac_scale(a.Wi, a.W);
+  const int jlo = UP ? ac_lerp(max(ow0 - 1, 0), a.Wi, a.W, sws).i0 : 0;  // first staged column
+  uint32_t uvo[UP ? LPU : 1];  // byte offset of the vector in low-res row 0, or BUF_OOB
+  int uls[UP ? LPU : 1];       // staging float offset within a buffer | row << 24, or -1
+  if constexpr (UP) {
+#pragma unroll
+    for (int k = 0; k < LPU; ++k) {
+      const int i = tid + 256 * k;
+      const int rr = i / (DS_UC * VPP), rem = i - rr * DS_UC * VPP;
+      const int j = rem / VPP, cv = rem - j * VPP;
+      const bool ok = rr < 2 && jlo + j < a.Wi;
+      uvo[k] = ok ? (uint32_t)(((size_t)(jlo + j) * DS_C + cv * VI) * sizeof(T)) : BUF_OOB;
+      uls[k] = rr < 2 ? ((rr * DS_UC + j) * DS_C + cv * VI) | (rr << 24) : -1;
+    }
+  }
+  const uint32_t lrowbytes = (uint32_t)((size_t)a.Wi * DS_C * sizeof(T));
+  // the two low-res rows of ring row r -> registers
+  auto load_up = [&](int r, uint4* raw) {
+    const bool rok = r >= 0 && r < a.H;
+    const Lerp lh = ac_lerp(rok ? r : 0, a.Hi, a.H, shs);
+#pragma unroll
+    for (int k = 0; k < LPU; ++k) {
+      const int rsel = (uls[k] >> 24) & 1 ? lh.i1 : lh.i0;
+      const uint32_t off = rok && uls[k] >= 0 && uvo[k] != BUF_OOB ? uvo[k] + (uint32_t)rsel * lrowbytes : BUF_OOB;
+      const buf_v4u t = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      raw[k] = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+  };
+  auto stage_up = [&](int b, const uint4* raw) {
+    float* base = s_stg + b * 2 * DS_UC * DS_C;
+#pragma unroll
+    for (int k = 0; k < LPU; ++k) {
+      if (uls[k] < 0) continue;
+      float f[VI];
+      if constexpr (F32) {
+        f[0] = __uint_as_float(raw[k].x); f[1] = __uint_as_float(raw[k].y);
+        f[2] = __uint_as_float(raw[k].z); f[3] = __uint_as_float(raw[k].w);
+      } else {
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&raw[k]);
+#pragma unroll
+        for (int j = 0; j < VI; ++j) f[j] = s16_to<T>(e[j]);
+      }
+      const int o = uls[k] & 0xFFFFFF;
+#pragma unroll
+      for (int j = 0; j < VI; j += 4)
+        *reinterpret_cast<float4*>(base + o + j) = make_float4(f[j], f[j + 1], f[j + 2], f[j + 3]);
+    }
+  };
+  // ring row r from staging buffer b: up_nhwc's W-then-H lerp2, rounded to the storage type
+  auto interp_up = [&](int r, int b) {
+    const bool rok = r >= 0 && r < a.H;
+    const Lerp lh = ac_lerp(rok ? r : 0, a.Hi, a.H, shs);
+    const float* st = s_stg + b * 2 * DS_UC * DS_C;
+    float* ring = s_ring + ((r + 3) % 3) * DS_RP * DS_PP;
+    for (int i = tid; i < DS_RP * (DS_C / 4); i += 256) {
+      const int px = i / (DS_C / 4), q = i - px * (DS_C / 4);
+      const int col = ow0 - 1 + px;
+      const bool ok = rok && col >= 0 && col < a.W;
+      const Lerp lw = ac_lerp(ok ? col : jlo, a.Wi, a.W, sws);
+      const int j0 = lw.i0 - jlo, j1 = lw.i1 - jlo;
+      const float4 p00 = *reinterpret_cast<const float4*>(st + j0 * DS_C + 4 * q);
+      const float4 p01 = *reinterpret_cast<const float4*>(st + j1 * DS_C + 4 * q);
+      const float4 p10 = *reinterpret_cast<const float4*>(st + (DS_UC + j0) * DS_C + 4 * q);
+      const float4 p11 = *reinterpret_cast<const float4*>(st + (DS_UC + j1) * DS_C + 4 * q);
+      const float a00[4] = {p00.x, p00.y, p00.z, p00.w}, a01[4] = {p01.x, p01.y, p01.z, p01.w};
+      const float a10[4] = {p10.x, p10.y, p10.z, p10.w}, a11[4] = {p11.x, p11.y, p11.z, p11.w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = lerp2(lh.l0, lerp2(lw.l0, a00[j], lw.l1, a01[j]), lh.l1,
+                              lerp2(lw.l0, a10[j], lw.l1, a11[j]));
+        o[j] = ok ? round_as<T>(v) : 0.f;
+      }
+      *reinterpret_cast<float4*>(ring + px * DS_PP + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  };
+
   // depthwise: thread = channel quad qd x output pixels 2 pp, 2 pp + 1; taps and BN in registers
   const int qd = tid & 31, pp = tid >> 5;
   float wt[9][4], dsc[4], dsh[4];
@@ -156,20 +239,37 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   }
 
   // ---- prologue: rows oh0 - 1, oh0 in the ring, row oh0 + 1 in flight ------------------------
-  uint4 nxt[LP];
-  {
+  // (upsample mode: rows oh0 - 1, oh0 interpolated into the ring, row oh0 + 1's low-res rows in
+  // staging buffer (oh0 - 1) & 1, row oh0 + 2's in flight)
+  uint4 nxt[UP ? LPU : LP];
+  if constexpr (UP) {
+    uint4 raw[LPU];
+    load_up(oh0 - 1, raw);
+    stage_up(0, raw);
+    __syncthreads();
+    interp_up(oh0 - 1, 0);
+    load_up(oh0, raw);
+    stage_up(1, raw);
+    __syncthreads();
+    interp_up(oh0, 1);
+    __syncthreads();
+    load_up(oh0 + 1, raw);
+    stage_up((oh0 - 1) & 1, raw);
+    load_up(oh0 + 2, nxt);
+  } else {
     uint4 raw[LP];
     load_row(oh0 - 1, raw);
     store_row(oh0 - 1, raw);
     load_row(oh0, raw);
     store_row(oh0, raw);
+    load_row(oh0 + 1, nxt);
   }
-  load_row(oh0 + 1, nxt);
   {  // two dropped stores: the loop is entered, as it loops, with 2 stores after the row loads
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
     buf_st4(yr, BUF_OOB, z, (T*)nullptr);
     buf_st4(yr, BUF_OOB + 64, z, (T*)nullptr);
   }
+  if constexpr (UP) __syncthreads();  // (staging of row oh0 + 1 before step oh0 interpolates it)
   stamp(a.stamps, 1);
 
   const int oh_end = min(oh0 + a.rs, a.H);
@@ -197,8 +297,14 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
         }
       }
     }
-    store_row(oh + 1, nxt);  // (the slot of row oh - 2: its last reader, dw(oh - 1), is done)
-    load_row(oh + 2, nxt);   // (also past the end: a fixed count per step)
+    if constexpr (UP) {
+      stage_up(oh & 1, nxt);      // row oh + 2's low-res rows (its interpolation: next step)
+      interp_up(oh + 1, (oh - 1) & 1);  // (the slot of row oh - 2: dw(oh - 1) is done)
+      load_up(oh + 3, nxt);       // (also past the end: a fixed count per step)
+    } else {
+      store_row(oh + 1, nxt);  // (the slot of row oh - 2: its last reader, dw(oh - 1), is done)
+      load_row(oh + 2, nxt);   // (also past the end: a fixed count per step)
+    }
     __syncthreads();
     if (oh == oh0 + a.rs / 2) stamp(a.stamps, 2);
     // ---- depthwise of row oh, two pixels per thread -> s_d as the pointwise B operand --------
@@ -292,8 +398,21 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   stamp(a.stamps, 5);
 }
 
+// upsample mode: the low-res columns any strip's 18 ring pixels interpolate from fit DS_UC
+static bool ds_up_fits(const DsArgs& a) {
+  if (a.Hi <= 0) return true;
+  if (a.Wi <= 0 || a.Hi > a.H || a.Wi > a.W) return false;
+  const float sw = ac_scale(a.Wi, a.W);
+  for (int ow0 = 0; ow0 < a.W; ow0 += DS_TW) {
+    const int lo = ac_lerp(std::max(ow0 - 1, 0), a.Wi, a.W, sw).i0;
+    const int hi = ac_lerp(std::min(ow0 + DS_TW, a.W - 1), a.Wi, a.W, sw).i1;
+    if (hi - lo + 1 > DS_UC) return false;
+  }
+  return 4LL * a.Hi * a.Wi * DS_C < (long long)BUF_OOB;
+}
+
 bool ds_ok(const DsArgs& a) {
-  return a.N > 0 && a.N < 65536 && a.H > 0 && a.W > 0 && a.C == DS_C && a.Co == DS_CO &&
+  return ds_up_fits(a) && a.N > 0 && a.N < 65536 && a.H > 0 && a.W > 0 && a.C == DS_C && a.Co == DS_CO &&
          (a.r == nullptr || (a.ldr >= DS_CO && a.ldr % 4 == 0 && ((uintptr_t)a.r & 15) == 0 &&
                              4LL * a.H * a.W * a.ldr < (long long)BUF_OOB)) &&
          a.rs >= 1 && cdiv(a.H, a.rs) < 65536 && a.ldy >= DS_CO && a.ldy % 4 == 0 &&
@@ -326,12 +445,15 @@ int ds_fwd(const DsArgs& a, int dtype, hipStream_t st) {
   as.stamps = stamp_region();
   const dim3 g(cdiv(a.W, DS_TW), cdiv(a.H, a.rs), a.N);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
-  ProfScope ps(PK_DSCONV, st, E * a.N * a.H * a.W * (DS_C + DS_CO + (a.r ? DS_CO : 0)),
+  ProfScope ps(PK_DSCONV, st,
+               E * a.N * ((a.Hi > 0 ? (double)a.Hi * a.Wi : (double)a.H * a.W) * DS_C +
+                          (double)a.H * a.W * (DS_CO + (a.r ? DS_CO : 0))),
                2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO));
 #define DSK(T)                                                                \
   do {                                                                        \
-    if (a.r) dsconv_fwd_kernel<T, true><<<g, 256, 0, st>>>(as);               \
-    else dsconv_fwd_kernel<T, false><<<g, 256, 0, st>>>(as);                  \
+    if (a.r && a.Hi > 0) dsconv_fwd_kernel<T, true, true><<<g, 256, 0, st>>>(as); \
+    else if (a.r) dsconv_fwd_kernel<T, true, false><<<g, 256, 0, st>>>(as);   \
+    else dsconv_fwd_kernel<T, false, false><<<g, 256, 0, st>>>(as);           \
   } while (0)
   if (dtype == DT_F32) DSK(float);
   else if (dtype == DT_F16) DSK(f16);

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void up_nhwc_kernel(UpArgs a) {
   ldv(xb + ((size_t)lh.i1 * a.Wi + lw.i1) * a.ldx, p11);
 #pragma unroll
   for (int j = 0; j < V; ++j)
-    o[j] = lh.l0 * (lw.l0 * p00[j] + lw.l1 * p01[j]) + lh.l1 * (lw.l0 * p10[j] + lw.l1 * p11[j]);
+    o[j] = lerp2(lh.l0, lerp2(lw.l0, p00[j], lw.l1, p01[j]), lh.l1, lerp2(lw.l0, p10[j], lw.l1, p11[j]));
   stv((T*)a.y + pix * a.ldy + cv * V, o);
 }
 

@@ -434,6 +434,9 @@ struct DsArgs {
   const void* r = nullptr;     // optional residual added after the pointwise BN, before its ReLU
   int ldr = 0;                 // (the FFM: relu(BN_l(conv_l(dw)) + f), :213-218); may alias y
   int rs;                      // output rows walked per workgroup (ds_rows)
+  int Hi = 0, Wi = 0;          // > 0: x is [N,Hi,Wi] x C and the depthwise input is its bilinear
+                               // align_corners upsample to H x W (the FFM's F.interpolate, :212),
+                               // formed in LDS, never stored (up_nhwc's arithmetic)
   unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
 };
 bool ds_ok(const DsArgs& a);

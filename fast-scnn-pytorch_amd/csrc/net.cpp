@@ -1126,25 +1126,28 @@ struct Exec {
       UpArgs u{};
       u.N = N; u.Hi = pl.H5; u.Wi = pl.W5; u.C = 128; u.Ho = pl.H3; u.Wo = pl.W3;
       u.x = W(pl.po.a); u.ldx = 128; u.y = W(pl.up_low); u.ldy = 128;
-      TRY(up_nhwc(u, dt, r.st));
       if (!train) {
         // f = BN_h(conv_h(hr)) ; f = relu(BN_l(conv_l(dw)) + f), the dw and conv_l in one
         // launch (dsconv.hip) when it fits
         TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, raw(W(pl.l2pw.a), 64), false));
-        DsArgs fa{};
-        fa.x = W(pl.up_low); fa.N = N; fa.H = pl.H3; fa.W = pl.W3; fa.C = 128; fa.Co = 128;
+        DsArgs fa{};  // the upsample too: the depthwise reads the PPM output through it
+        fa.x = W(pl.po.a); fa.Hi = pl.H5; fa.Wi = pl.W5;
+        fa.N = N; fa.H = pl.H3; fa.W = pl.W3; fa.C = 128; fa.Co = 128;
         fa.wd = P(net.ffm_dw.w); fa.scd = Wf(pl.fdw.scale); fa.shd = Wf(pl.fdw.shift);
         fa.wp = Wg(net.ffm_low); fa.scp = Wf(pl.flow.scale); fa.shp = Wf(pl.flow.shift);
         fa.y = W(pl.flow.a); fa.ldy = pl.flow.ld; fa.r = W(pl.f); fa.ldr = 128;
         fa.rs = ds_rows(N, pl.H3, pl.W3);
         if (ds_enabled() && ds_ok(fa)) {
-          g_prof_tag = "feature_fusion.dwconv + conv_lower_res (fused)";
+          g_prof_tag = "feature_fusion.upsample + dwconv + conv_lower_res (fused)";
           TRY(ds_fwd(fa, dt, r.st));
         } else {
+          g_prof_tag = "feature_fusion.upsample";
+          TRY(up_nhwc(u, dt, r.st));
           TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
           TRY(pw(pl.flow, net.ffm_low, &net.ffm_blow, act(pl.fdw), true, W(pl.f), 128));
         }
       } else {
+        TRY(up_nhwc(u, dt, r.st));
         TRY(dw(pl.fdw, net.ffm_dw, net.ffm_bdw, raw(W(pl.up_low), 128), pl.H3, pl.W3, pl.H3, pl.W3, 1));
         g_prof_tag = pl.flow.name.c_str();
         GemmArgs g{};

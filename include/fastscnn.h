@@ -241,12 +241,15 @@ int fscnn_block_dsconv_fwd(const void* x, int dtype, int N, int H, int W, int C,
                            int ldy, void* stream);
 
 /* fscnn_block_dsconv_res_fwd: the same with a residual added after the pointwise BN, before the
- * final ReLU: y = relu(BN_p(W_p * relu(BN_d(dw3x3(x)))) + res) -- the FeatureFusionModule's
- * dwconv + conv_lower_res + the high-res branch (models/fast_scnn.py:207-218).  res NHWC with row
- * stride ldres (>= Co, multiple of 4, 16-B aligned); res may alias y (each element is read before
- * it is written, by the same thread). */
+ * final ReLU: y = relu(BN_p(W_p * relu(BN_d(dw3x3(up(x))))) + res) -- the FeatureFusionModule's
+ * F.interpolate(scale 4, bilinear, align_corners) + dwconv + conv_lower_res + the high-res branch
+ * (models/fast_scnn.py:207-218).  Hi > 0: x is [N][Hi][Wi] x C and up() its bilinear
+ * align_corners resize to H x W, formed in LDS and never stored (same arithmetic as the unfused
+ * up_nhwc); Hi = 0: up() is the identity and x is [N][H][W] x C.  res NHWC with row stride ldres
+ * (>= Co, multiple of 4, 16-B aligned); res may alias y (each element is read before it is
+ * written, by the same thread). */
 int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, int C, int Co,
-                               const float* w_dw, const float* scale_d, const float* shift_d,
+                               int Hi, int Wi, const float* w_dw, const float* scale_d, const float* shift_d,
                                const void* w_pw, const float* scale_p, const float* shift_p,
                                const void* res, int ldres, void* y, int ldy, void* stream);
 

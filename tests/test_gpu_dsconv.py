@@ -94,7 +94,41 @@ def test_dsconv_fwd_residual_vs_torch(dt):
     wdd, wpd = wd.to(DEV).contiguous(), wp.to(dt).to(DEV).contiguous()
     bnd = [(s.to(DEV), h.to(DEV)) for s, h in bn]
     _lib.call("fscnn_block_dsconv_res_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, 128, 128,
-              _lib.ptr(wdd), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]), _lib.ptr(wpd),
+              0, 0, _lib.ptr(wdd), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]), _lib.ptr(wpd),
+              _lib.ptr(bnd[1][0]), _lib.ptr(bnd[1][1]), _lib.ptr(y), 128, _lib.ptr(y), 128,
+              _lib.stream_ptr())
+    torch.cuda.synchronize()
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    tol = 2e-5 * scale if dt == torch.float32 else 2 ** -7 * scale
+    assert err <= tol, (err, tol, scale)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+@pytest.mark.parametrize("N,Hi,Wi,H,W", [(2, 8, 12, 32, 48), (1, 7, 9, 25, 33), (1, 16, 16, 64, 64)])
+def test_dsconv_upsample_residual_vs_torch(dt, N, Hi, Wi, H, W):
+    """The whole eval FeatureFusionModule low-res branch (models/fast_scnn.py:207-218):
+    relu(BN_l(conv_l(relu(BN_d(dw(up(x)))))) + f) with up = F.interpolate(size (H, W), bilinear,
+    align_corners=True) formed in LDS (the unfused path stores it, rounded to the storage type)."""
+    x = rnd(N, Hi, Wi, 128, seed=11)
+    f = rnd(N, H, W, 128, seed=12)
+    wd = rnd(128, 9, seed=13, scale=0.4)
+    wp = rnd(128, 128, seed=14, scale=1.0 / 128 ** 0.5)
+    bn = [(rnd(128, seed=50 + i) * 0.5 + 1.0, rnd(128, seed=60 + i) * 0.2) for i in range(2)]
+    q = (lambda t: t) if dt == torch.float32 else (lambda t: t.to(dt).float())  # noqa: E731
+    (sd, hd), (sp, hp) = bn
+    c = lambda t: t[None, :, None, None]  # noqa: E731
+    up = q(F.interpolate(q(x).permute(0, 3, 1, 2), size=(H, W), mode="bilinear",
+                         align_corners=True))
+    d = q(F.relu(F.conv2d(up, wd.reshape(128, 1, 3, 3), padding=1, groups=128) * c(sd) + c(hd)))
+    ref = F.relu(F.conv2d(d, q(wp)[:, :, None, None]) * c(sp) + c(hp) + q(f).permute(0, 3, 1, 2))
+    xd = x.to(dt).to(DEV).contiguous()
+    y = f.to(dt).to(DEV).contiguous()
+    wdd, wpd = wd.to(DEV).contiguous(), wp.to(dt).to(DEV).contiguous()
+    bnd = [(s.to(DEV), h.to(DEV)) for s, h in bn]
+    _lib.call("fscnn_block_dsconv_res_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W, 128, 128,
+              Hi, Wi, _lib.ptr(wdd), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]), _lib.ptr(wpd),
               _lib.ptr(bnd[1][0]), _lib.ptr(bnd[1][1]), _lib.ptr(y), 128, _lib.ptr(y), 128,
               _lib.stream_ptr())
     torch.cuda.synchronize()

@@ -113,8 +113,8 @@ def test_stem_fused_bit_identical(tmp_path):
 
 def test_dsconv_fused_bit_identical(tmp_path):
     """The fused inference DSConv (depthwise + BN + ReLU and pointwise + BN (+ residual) + ReLU in
-    one launch, csrc/dsconv.hip: the classifier's dsconv1 / dsconv2 and the FFM's dwconv +
-    conv_lower_res) gives bit-identical outputs to the unfused launches: fp32 / bf16 / fp16
+    one launch, csrc/dsconv.hip: the classifier's dsconv1 / dsconv2 and the FFM's upsample +
+    dwconv + conv_lower_res) gives bit-identical outputs to the unfused launches: fp32 / bf16 / fp16
     images, autocast fp16, partial strips and row segments (tests/_stem_worker.py --dsconv).  The
     default run really took the three fused launches."""
     ref = _stem_worker(tmp_path, "FSCNN_DSCONV_FUSED=0", dsconv=True)
