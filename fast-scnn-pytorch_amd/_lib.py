@@ -112,6 +112,9 @@ SIGNATURES = {
                                    c_vp, c_int, c_vp]),
     "fscnn_pyramid_pool_bwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
                                        c_int, c_vp]),
+    "fscnn_block_ir_s2_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_int, c_vp]),
     "fscnn_block_ltd_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "fscnn_block_dsconv_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,

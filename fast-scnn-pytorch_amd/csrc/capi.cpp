@@ -709,6 +709,30 @@ int fscnn_block_ir_fwd(const void* x, int ldx, int dtype, int N, int H, int W, i
   return ir_block_fwd(a, dtype, S(stream));
 }
 
+int fscnn_block_ir_s2_fwd(const void* x, int ldx, int dtype, int N, int H, int W, int cin,
+                          int expand, int cout, const void* w_expand, const float* w_dw,
+                          const void* w_project, const float* scale_e, const float* shift_e,
+                          const float* scale_d, const float* shift_d, const float* scale_p,
+                          const float* shift_p, void* y, int ldy, void* stream) {
+  if (!x || !y || !w_expand || !w_dw || !w_project || !scale_e || !shift_e || !scale_d ||
+      !shift_d || !scale_p || !shift_p) {
+    set_error("fscnn_block_ir_s2_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || H < 1 || W < 1) {
+    set_error("fscnn_block_ir_s2_fwd: dtype %d H %d W %d", dtype, H, W);
+    return E_INVALID;
+  }
+  IrArgs a{};
+  a.stride = 2; a.Hi = H; a.Wi = W;
+  a.N = N; a.H = (H - 1) / 2 + 1; a.W = (W - 1) / 2 + 1; a.Cin = cin; a.E = expand; a.Cout = cout;
+  a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy;
+  a.we = w_expand; a.wd = w_dw; a.wp = w_project;
+  a.sc_e = scale_e; a.sh_e = shift_e; a.sc_d = scale_d; a.sh_d = shift_d;
+  a.sc_p = scale_p; a.sh_p = shift_p; a.residual = 0;
+  return ir_block_fwd(a, dtype, S(stream));
+}
+
 int fscnn_block_ltd_fwd(const void* x, int x_dtype, int dtype, int N, int H, int W,
                         const float* w_conv, const float* scale_0, const float* shift_0,
                         const float* w_dw, const float* scale_d, const float* shift_d,

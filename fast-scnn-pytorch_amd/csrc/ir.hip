@@ -24,16 +24,25 @@
 
 namespace fscnn {
 
-constexpr int IR_TH = 8, IR_TW = 8;               // output tile
-constexpr int IR_HH = IR_TH + 2, IR_HW = IR_TW + 2;  // haloed input tile
-constexpr int IR_HALO = IR_HH * IR_HW;             // 100 pixels
-constexpr int IR_RT = (IR_HALO + 15) / 16;         // 7 MFMA row tiles
-constexpr int IR_ROWS = IR_RT * 16;                // 112
+// Tiles per stride: stride 1 = an 8 x 8 output tile over a 10 x 10 haloed input tile; stride 2
+// (bottleneck1.0 / 2.0) = a 4 x 8 output tile over a 9 x 17 input tile, whose fp32 split planes
+// and expand chunk still fit LDS (an 8 x 8 stride-2 tile would need 17 x 17 input pixels).
+template <int S>
+struct IrTile {
+  static constexpr int TH = S == 1 ? 8 : 4, TW = 8;          // output tile
+  static constexpr int HH = S * (TH - 1) + 3, HW = S * (TW - 1) + 3;  // haloed input tile
+  static constexpr int HALO = HH * HW;                         // 100 / 153 pixels
+  static constexpr int RT = (HALO + 15) / 16;                  // 7 / 10 MFMA row tiles
+  static constexpr int ROWS = RT * 16;                         // 112 / 160
+  static constexpr int PX = TH * TW;                           // 64 / 32 output pixels
+  static constexpr int XROWS = HALO + 1;  // staged input rows: the halo + a zero row that the
+                                          // MFMA rows past it read
+  static constexpr int RPW = (RT + 1) / 2;                     // expand row tiles per wave
+  static constexpr int NPT = S == 1 ? 2 : 1;                   // depthwise pixels per thread
+  static constexpr int PT = PX / 16;                           // project pixel tiles
+};
 constexpr int IR_EC = 64;                          // expanded channels per chunk
-constexpr int IR_PX = IR_TH * IR_TW;               // 64 output pixels
 constexpr int IR_ELD = IR_EC + 4;                  // fp32 row stride of the expand chunk
-constexpr int IR_XROWS = IR_HALO + 1;              // staged input rows: 100 halo pixels + a zero
-                                                   // row that MFMA rows 100..111 read
 // Operand rows are padded by 16 uint16 (8 dwords): with row strides of 40, 56 or 72 dwords
 // (Cin 64 / 96 / 128, and the 64-channel depthwise chunk) the 16 lanes of every ds_read_b128
 // lane group ({li 0-3, 12-15 of one k-half, li 4-11 of the next}) hit 16 distinct 4-bank slots.
@@ -90,12 +99,13 @@ __device__ __forceinline__ void ir_mma(const uint4 (&a)[IrP<T>::P], const uint4 
 constexpr int IR_PRM = IR_EC * 9 + 4 * IR_EC;  // per-chunk depthwise weights + BN_e / BN_d tables
 
 // LDS bytes of one launch (KS = Cin / 32)
-template <typename T>
+template <typename T, int S>
 __host__ __device__ constexpr size_t ir_lds(int KS) {
-  return (size_t)IrP<T>::P * IR_XROWS * (32 * KS + 16) * 2  // input tile planes
-         + (size_t)IR_ROWS * IR_ELD * 4                       // expand chunk (fp32)
-         + (size_t)IrP<T>::P * IR_PX * (IR_EC + 16) * 2       // depthwise chunk planes
-         + IR_ROWS * 4                                        // halo validity
+  using G = IrTile<S>;
+  return (size_t)IrP<T>::P * G::XROWS * (32 * KS + 16) * 2  // input tile planes
+         + (size_t)G::ROWS * IR_ELD * 4                       // expand chunk (fp32)
+         + (size_t)IrP<T>::P * G::PX * (IR_EC + 16) * 2       // depthwise chunk planes
+         + G::ROWS * 4                                        // halo validity
          + (size_t)2 * IR_PRM * 4;                            // chunk parameters, double-buffered
 }
 
@@ -112,14 +122,17 @@ constexpr int IR_WAVES = IR_THREADS / 64;
 
 // KS: Cin / 32 (2, 3, 4); PPW: project pixel tiles per wave (4 when Cout > 64, else 2);
 // PRE (fp32): the weights come pre-split (a.we3 / a.wp3), no per-chunk split arithmetic
-template <typename T, int KS, int PPW, bool PRE = false>
+template <typename T, int KS, int PPW, bool PRE = false, int S = 1>
 __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
+  using G = IrTile<S>;
+  constexpr int IR_TH = G::TH, IR_TW = G::TW, IR_HW = G::HW, IR_HALO = G::HALO, IR_RT = G::RT;
+  constexpr int IR_ROWS = G::ROWS, IR_PX = G::PX, IR_XROWS = G::XROWS, NPT = G::NPT;
   constexpr int P = IrP<T>::P;
   constexpr int R = sizeof(T) == 4 ? (PRE ? 3 : 2) : 1;  // raw 16-B vectors per 8 weights
   constexpr int CIN = 32 * KS;
   constexpr int XLD = CIN + 16;      // uint16 per input-tile row (conflict-free operand reads)
   constexpr int DLD = IR_EC + 16;    // uint16 per depthwise-chunk row
-  constexpr int RPW = 4;             // expand row tiles per wave (the last half holds 3)
+  constexpr int RPW = G::RPW;        // expand row tiles per wave (stride 1: the last half holds 3)
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   uint16_t* sX = reinterpret_cast<uint16_t*>(s_dyn);                   // [P][101][XLD]
   float* sE = reinterpret_cast<float*>(sX + (size_t)P * IR_XROWS * XLD);  // [112][IR_ELD]
@@ -141,9 +154,10 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
   const int otiles = a.Cout / 16;
   const int ect = wave & 3, erh = (wave >> 2) * RPW;  // expand: channel tile, first row tile
   const int dq = tid & 15, dg = tid >> 4;              // depthwise: channel quad, pixel pair
-  const int doy = dg >> 2, dox = (dg & 3) * 2;
-  const int pot = PPW == 4 ? wave : (wave & 3);        // project: output tile, first pixel tile
-  const int ppt = PPW == 4 ? 0 : 2 * (wave >> 2);
+  const int doy = dg / (IR_TW / NPT), dox = (dg % (IR_TW / NPT)) * NPT;
+  // project: output tile, first pixel tile (all G::PT pixel tiles per wave, or half of them)
+  const int pot = PPW == G::PT ? wave : (wave & 3);
+  const int ppt = PPW == G::PT ? 0 : PPW * (wave >> 2);
   const bool pon = pot < otiles;
 
   // ---- per-chunk loads (issued one chunk ahead) ----------------------------------------------
@@ -223,9 +237,9 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
     for (int i = tid; i < IR_XROWS * VPR; i += IR_THREADS) {
       const int r = i / VPR, v = i - r * VPR;
       const int hy = r / IR_HW, hx = r - hy * IR_HW;
-      const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
-      const bool ok = r < IR_HALO && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-      const size_t off = ok ? (((size_t)n * a.H + gy) * a.W + gx) * a.ldx + v * 8 : 0;
+      const int gy = S * y0 - 1 + hy, gx = S * x0 - 1 + hx;
+      const bool ok = r < IR_HALO && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi;
+      const size_t off = ok ? (((size_t)n * a.Hi + gy) * a.Wi + gx) * a.ldx + v * 8 : 0;
       if constexpr (P == 3) {
         uint4 lo = *reinterpret_cast<const uint4*>((const float*)X + off);
         uint4 hi = *reinterpret_cast<const uint4*>((const float*)X + off + 4);
@@ -268,7 +282,7 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int j = 0; j < RPW; ++j) {
-          const int rt = min(erh + j, IR_RT - 1);  // (waves 4-7 compute tile 6 twice)
+          const int rt = min(erh + j, IR_RT - 1);  // (stride 1: waves 4-7 compute tile 6 twice)
           const int row = min(rt * 16 + li, IR_HALO);  // rows past the halo: the zero row
           uint4 b[P];
 #pragma unroll
@@ -301,16 +315,17 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int k = 0; k < 9; ++k) w[j][k] = prm[(4 * dq + j) * 9 + k];
-      float4 v[3][4];
+      constexpr int NC = S * (NPT - 1) + 3;  // input columns of the thread's window
+      float4 v[3][NC];
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < NC; ++c)
           v[kh][c] = *reinterpret_cast<const float4*>(
-              sE + (size_t)((doy + kh) * IR_HW + dox + c) * IR_ELD + 4 * dq);
-      float acc[2][4];
+              sE + (size_t)((S * doy + kh) * IR_HW + S * dox + c) * IR_ELD + 4 * dq);
+      float acc[NPT][4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < NPT; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
 #pragma unroll
@@ -318,8 +333,8 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const float4 q = v[kh][i + kw];
+          for (int i = 0; i < NPT; ++i) {
+            const float4 q = v[kh][S * i + kw];
             const float qq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(qq[j], w[j][kh * 3 + kw], acc[i][j]);
@@ -328,7 +343,7 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
       const float4 sh4 = *reinterpret_cast<const float4*>(prm + IR_EC * 12 + 4 * dq);
       const float sc[4] = {sc4.x, sc4.y, sc4.z, sc4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NPT; ++i) {
         const int p = doy * IR_TW + dox + i;
         uint16_t h[3][4];
 #pragma unroll
@@ -392,59 +407,78 @@ __global__ __launch_bounds__(IR_THREADS) void ir_block_kernel(IrArgs a) {
   }
 }
 
-bool ir_block_ok(const IrArgs& a, int dtype) {
+bool ir_block_ok(const IrArgs& a0, int dtype) {
+  IrArgs a = a0;
+  if (a.Hi <= 0) { a.Hi = a.H; a.Wi = a.W; }
   const int V = dtype == DT_F32 ? 4 : 8;
   const int KS = a.Cin / 32;
   if (a.Cin % 32 || KS < 2 || KS > 4 || a.E % IR_EC || a.E <= 0 || a.Cout % 16 ||
       a.Cout > 128 || a.Cout <= 0 || a.H < 1 || a.W < 1 || a.N < 1)
     return false;
+  if (a.stride != 1 && a.stride != 2) return false;
+  if (a.stride == 1 ? (a.Hi != a.H || a.Wi != a.W)
+                    : (a.H != (a.Hi - 1) / 2 + 1 || a.W != (a.Wi - 1) / 2 + 1 || a.residual))
+    return false;
   if (a.ldx % V || a.ldy % V || a.ldx < a.Cin || a.ldy < a.Cout) return false;
   if (a.residual && a.Cin != a.Cout) return false;
-  const size_t lds = dtype == DT_F32 ? ir_lds<float>(KS) : ir_lds<bf16>(KS);
+  const size_t lds = a.stride == 1
+      ? (dtype == DT_F32 ? ir_lds<float, 1>(KS) : ir_lds<bf16, 1>(KS))
+      : (dtype == DT_F32 ? ir_lds<float, 2>(KS) : ir_lds<bf16, 2>(KS));
   return lds <= 160 * 1024 - 1024;
 }
 
-template <typename T, int KS>
+template <typename T, int KS, int S>
 static void ir_launch_ks(const IrArgs& a, dim3 grid, hipStream_t st) {
-  const size_t lds = ir_lds<T>(KS);
+  const size_t lds = ir_lds<T, S>(KS);
+  constexpr int PT = IrTile<S>::PT;  // project pixel tiles: all per wave above 64 outputs
   if constexpr (sizeof(T) == 4) {
     if (a.we3 && a.wp3) {
-      if (a.Cout > 64) ir_block_kernel<T, KS, 4, true><<<grid, IR_THREADS, lds, st>>>(a);
-      else ir_block_kernel<T, KS, 2, true><<<grid, IR_THREADS, lds, st>>>(a);
+      if (a.Cout > 64) ir_block_kernel<T, KS, PT, true, S><<<grid, IR_THREADS, lds, st>>>(a);
+      else ir_block_kernel<T, KS, PT / 2, true, S><<<grid, IR_THREADS, lds, st>>>(a);
       return;
     }
   }
-  if (a.Cout > 64) ir_block_kernel<T, KS, 4><<<grid, IR_THREADS, lds, st>>>(a);
-  else ir_block_kernel<T, KS, 2><<<grid, IR_THREADS, lds, st>>>(a);
+  if (a.Cout > 64) ir_block_kernel<T, KS, PT, false, S><<<grid, IR_THREADS, lds, st>>>(a);
+  else ir_block_kernel<T, KS, PT / 2, false, S><<<grid, IR_THREADS, lds, st>>>(a);
+}
+
+template <typename T, int S>
+static void ir_launch_s(const IrArgs& a, dim3 grid, hipStream_t st) {
+  switch (a.Cin / 32) {
+    case 2: ir_launch_ks<T, 2, S>(a, grid, st); break;
+    case 3: ir_launch_ks<T, 3, S>(a, grid, st); break;
+    default: ir_launch_ks<T, 4, S>(a, grid, st); break;
+  }
 }
 
 template <typename T>
 static void ir_launch(const IrArgs& a, dim3 grid, hipStream_t st) {
-  switch (a.Cin / 32) {
-    case 2: ir_launch_ks<T, 2>(a, grid, st); break;
-    case 3: ir_launch_ks<T, 3>(a, grid, st); break;
-    default: ir_launch_ks<T, 4>(a, grid, st); break;
-  }
+  if (a.stride == 2) ir_launch_s<T, 2>(a, grid, st);
+  else ir_launch_s<T, 1>(a, grid, st);
 }
 
-int ir_block_fwd(const IrArgs& a, int dtype, hipStream_t st) {
+int ir_block_fwd(const IrArgs& a0, int dtype, hipStream_t st) {
+  IrArgs a = a0;
+  if (a.Hi <= 0) { a.Hi = a.H; a.Wi = a.W; }
   if (!ir_block_ok(a, dtype)) {
-    set_error("ir_block_fwd: unsupported block (Cin %d E %d Cout %d ldx %d ldy %d residual %d)",
-              a.Cin, a.E, a.Cout, a.ldx, a.ldy, a.residual);
+    set_error("ir_block_fwd: unsupported block (Cin %d E %d Cout %d ldx %d ldy %d residual %d "
+              "stride %d)", a.Cin, a.E, a.Cout, a.ldx, a.ldy, a.residual, a.stride);
     return E_UNSUPPORTED;
   }
-  const long long tiles = (long long)a.N * cdiv(a.H, IR_TH) * cdiv(a.W, IR_TW);
+  const int TH = a.stride == 2 ? IrTile<2>::TH : IrTile<1>::TH;
+  const int TW = a.stride == 2 ? IrTile<2>::TW : IrTile<1>::TW;
+  const long long tiles = (long long)a.N * cdiv(a.H, TH) * cdiv(a.W, TW);
   if (tiles > 0x7fffffffLL) {
     set_error("ir_block_fwd: grid too large");
     return E_UNSUPPORTED;
   }
   const dim3 grid((unsigned)tiles);
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
-  const double M = (double)a.N * a.H * a.W;
+  const double M = (double)a.N * a.H * a.W, Mi = (double)a.N * a.Hi * a.Wi;
   ProfScope ps(PK_IR, st,
-               E * M * (a.Cin + a.Cout * (a.residual ? 2 : 1)) +
+               E * (Mi * a.Cin + M * a.Cout * (a.residual ? 2 : 1)) +
                    E * ((double)a.E * (a.Cin + a.Cout)) + 4.0 * 9 * a.E,
-               2.0 * M * a.E * (a.Cin + a.Cout) + 18.0 * M * a.E);
+               2.0 * (Mi * a.E * a.Cin + M * a.E * a.Cout) + 18.0 * M * a.E);
   if (dtype == DT_F32) ir_launch<float>(a, grid, st);
   else if (dtype == DT_F16) ir_launch<f16>(a, grid, st);
   else ir_launch<bf16>(a, grid, st);

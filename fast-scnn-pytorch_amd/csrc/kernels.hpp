@@ -387,7 +387,9 @@ struct SgdArgs {
 // ---- launchers ----------------------------------------------------------------------------
 // fused stride-1 inverted-residual block, inference (ir.hip; models/fast_scnn.py:95-115)
 struct IrArgs {
-  int N, H, W;                 // map (stride 1: output = input size)
+  int N, H, W;                 // output map (stride 1: = the input map)
+  int stride = 1;              // 1, or 2 (bottleneck1.0 / 2.0: no residual)
+  int Hi = 0, Wi = 0;          // input map (0: = H, W)
   int Cin, E, Cout;            // block input, expanded (6 Cin), output channels
   const void* x; int ldx;      // NHWC block input (storage dtype)
   void* y; int ldy;            // NHWC block output

@@ -163,22 +163,36 @@ int dwout(int h, int s) { return (h - 1) / s + 1; }
 
 }  // namespace
 
+// FSCNN_IR_S2=0: the stride-2 bottlenecks (1.0, 2.0) as three unfused launches in inference
+static bool ir_stride2_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FSCNN_IR_S2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 // shape of bottleneck i as one fused inference launch (ir.hip); false when the block runs as
-// its three unfused units (training plans, stride 2, unsupported shapes)
+// its three unfused units (training plans, unsupported shapes)
 bool ir_block_shape(const Net& net, const Plan& pl, int i, IrArgs& b) {
   const LbL& l = net.lb[i];
-  if (pl.train || l.stride != 1 || i == 0) return false;
+  if (pl.train || (l.stride != 1 && l.stride != 2)) return false;
   b = IrArgs{};
   b.N = pl.N;
+  b.stride = l.stride;
   b.H = i < 3 ? pl.H4 : pl.H5;
   b.W = i < 3 ? pl.W4 : pl.W5;
+  // input map: the previous block's output, or (block 0) the LearningToDownsample output
+  b.Hi = i == 0 ? pl.H3 : (i < 4 ? pl.H4 : pl.H5);
+  b.Wi = i == 0 ? pl.W3 : (i < 4 ? pl.W4 : pl.W5);
   b.Cin = l.cin; b.E = l.cin * 6; b.Cout = l.cout;
-  b.ldx = pl.lbp[i - 1].ld; b.ldy = pl.lbp[i].ld;
-  b.residual = l.cin == l.cout;
-  // one 8 x 8 tile per workgroup: below ~128 tiles (cfg1's 24 x 24 bottleneck3 map is 9 tiles)
-  // the fused launch leaves most CUs idle and the three unfused launches are faster
-  const long long tiles = (long long)b.N * ((b.H + 7) / 8) * ((b.W + 7) / 8);
-  return tiles >= 128 && ir_block_ok(b, pl.dtype);
+  b.ldx = i == 0 ? pl.l2pw.ld : pl.lbp[i - 1].ld; b.ldy = pl.lbp[i].ld;
+  b.residual = l.stride == 1 && l.cin == l.cout;
+  // one output tile per workgroup (8 x 8; stride 2: 4 x 8): below ~128 tiles (cfg1's 24 x 24
+  // bottleneck3 map is 9 tiles) the fused launch leaves most CUs idle and the three unfused
+  // launches are faster
+  const int th = l.stride == 2 ? 4 : 8;
+  const long long tiles = (long long)b.N * ((b.H + th - 1) / th) * ((b.W + 7) / 8);
+  return ir_stride2_enabled() || l.stride == 1 ? tiles >= 128 && ir_block_ok(b, pl.dtype) : false;
 }
 
 namespace {
@@ -1061,7 +1075,7 @@ struct Exec {
       if (ir_block_shape(net, pl, i, b)) {
         // inference: the whole stride-1 block in one launch (ir.hip), the 6x-expanded tensor
         // never leaves LDS
-        b.x = x; b.y = W(pl.lbp[i].a);
+        b.x = x; b.ldx = xld; b.y = W(pl.lbp[i].a);
         b.we = Wg(l.e); b.wd = P(l.d.w); b.wp = Wg(l.p);
         b.sc_e = Wf(pl.lbe[i].scale); b.sh_e = Wf(pl.lbe[i].shift);
         b.sc_d = Wf(pl.lbd[i].scale); b.sh_d = Wf(pl.lbd[i].shift);
@@ -1074,6 +1088,7 @@ struct Exec {
         TRY(ir_block_fwd(b, dt, r.st));
         x = W(pl.lbp[i].a);
         xld = pl.lbp[i].ld;
+        Hc = Ho; Wc = Wo;
         continue;
       }
       TRY(pw(pl.lbe[i], l.e, &l.be, i == 0 ? act(pl.l2pw) : raw(x, xld), true));

@@ -212,6 +212,18 @@ int fscnn_block_ir_fwd(const void* x, int ldx, int dtype, int N, int H, int W, i
                        const float* shift_d, const float* scale_p, const float* shift_p,
                        int residual, void* y, int ldy, void* stream);
 
+/* fscnn_block_ir_s2_fwd: the stride-2 LinearBottleneck (models/fast_scnn.py:95-115 with
+ * stride 2: bottleneck1.0 and bottleneck2.0, no shortcut) in one inference launch:
+ * y = BN_p(W_p * relu(BN_d(dw3x3_s2_p1(relu(BN_e(W_e * x)))))), every BN folded.  x NHWC
+ * [N][H][W] x cin (row stride ldx), y NHWC [N][(H-1)/2+1][(W-1)/2+1] x cout (row stride ldy);
+ * weights and BN tables as fscnn_block_ir_fwd.  The expanded tensor never reaches memory; the
+ * executor uses it for the two stride-2 blocks of every eval plan with >= 128 output tiles. */
+int fscnn_block_ir_s2_fwd(const void* x, int ldx, int dtype, int N, int H, int W, int cin,
+                          int expand, int cout, const void* w_expand, const float* w_dw,
+                          const void* w_project, const float* scale_e, const float* shift_e,
+                          const float* scale_d, const float* shift_d, const float* scale_p,
+                          const float* shift_p, void* y, int ldy, void* stream);
+
 /* fscnn_block_ltd_fwd: the inference LearningToDownsample stem up to dsconv1 in one launch
  * (models/fast_scnn.py:153-154): y = BN_p(W_p * relu(BN_d(dw3x3_s2_p1(relu(BN_0(conv3x3_s2_p0(x)))))))
  * followed by ReLU, every BN folded (scale, shift fp32 per channel).  x NCHW [N][3][H][W] of
