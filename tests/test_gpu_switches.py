@@ -19,6 +19,8 @@ fresh child process:
 * ``FSCNN_DSCONV_FUSED=0`` — (inference) each classifier DSConv as its depthwise and pointwise
   launches instead of one fused launch (csrc/dsconv.hip): bit-identical outputs
   (test_dsconv_fused_bit_identical).
+* ``FSCNN_IR_S2=0``       — (inference) the stride-2 bottlenecks (1.0, 2.0) as their three unfused
+  launches instead of the fused stride-2 block (csrc/ir.hip).
 
 (Round 5 removed the measured-slower variants and their switches: FSCNN_DW_LOOP, FSCNN_GEMM_PF,
 FSCNN_CE_HEAD, FSCNN_CE_PACK, FSCNN_GEMM_MINT.)
@@ -54,7 +56,7 @@ CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_GRAPHS=1": TRAIN + EVAL + HEAD16 + ["tests/test_gpu_autograd.py"],
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
          "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL,
-         "FSCNN_DSCONV_FUSED=0": EVAL}
+         "FSCNN_DSCONV_FUSED=0": EVAL, "FSCNN_IR_S2=0": EVAL}
 
 
 def _env(switch):
