@@ -54,7 +54,18 @@ struct DsMma<float> {
   static __device__ __forceinline__ void run(const uint4&, const uint4&, f32x4&) {}
 };
 
-template <typename T, bool RES, bool UP>
+// one logit element (T) through the buffer (range-checked) path
+__device__ __forceinline__ void cls_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v, float*) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ void cls_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v, bf16*) {
+  __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, 0);
+}
+__device__ __forceinline__ void cls_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v, f16*) {
+  __builtin_amdgcn_raw_buffer_store_b16(f2h(v), r, off, 0, 0);
+}
+
+template <typename T, bool RES, bool UP, bool CLS = false>
 __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int NP = F32 ? 3 : 1;                  // pointwise operand planes
@@ -67,6 +78,10 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   // upsample mode: the two low-resolution rows x DS_UC columns a ring row interpolates from,
   // double-buffered ([buf][row][col][c], fp32)
   __shared__ __attribute__((aligned(16))) float s_stg[UP ? 2 * 2 * DS_UC * DS_C : 4];
+  // classifier mode: its weights as A operand planes ([plane][32 rows][k], rows >= ncls zero)
+  // and bias
+  __shared__ __attribute__((aligned(16))) uint16_t s_cw[CLS ? NP * 32 * DS_DP : 8];
+  __shared__ __attribute__((aligned(16))) float s_cb[CLS ? 32 : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
@@ -85,8 +100,10 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   const int ow0 = tw * DS_TW, oh0 = sg * a.rs;
   const size_t img = UP ? (size_t)a.Hi * a.Wi * DS_C : (size_t)a.H * a.W * DS_C;
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc((const T*)a.x + (size_t)n * img, (uint32_t)(img * sizeof(T)));
-  const size_t ysz = (size_t)a.H * a.W * a.ldy;
-  const __amdgpu_buffer_rsrc_t yr = buf_rsrc((T*)a.y + (size_t)n * ysz, (uint32_t)(ysz * sizeof(T)));
+  const int ldo = CLS ? a.ldl : a.ldy;  // the launch's output: logits (classifier mode) or y
+  const size_t ysz = (size_t)a.H * a.W * ldo;
+  const __amdgpu_buffer_rsrc_t yr =
+      buf_rsrc((T*)(CLS ? a.logits : a.y) + (size_t)n * ysz, (uint32_t)(ysz * sizeof(T)));
 
   // one input row (the strip's 18 pixels incl. the halo, all channels): per-thread tables
   uint32_t lvo[LP];  // byte offset of the vector in row 0, or BUF_OOB
@@ -237,6 +254,26 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
     s_bn[i] = a.scp[i];
     s_bn[DS_CO + i] = a.shp[i];
   }
+  if constexpr (CLS) {  // the classifier weights, split once (fp32) into the A operand planes
+    for (int i = tid; i < 32 * (DS_CO / 8); i += 256) {
+      const int row = i / (DS_CO / 8), k = (i - row * (DS_CO / 8)) * 8;
+      const bool ok = row < a.ncls;
+      uint4 pl[NP];
+      if constexpr (F32) {
+        const float* wr = (const float*)a.wc + (size_t)(ok ? row : 0) * DS_CO + k;
+        const uint4 lo = ok ? *reinterpret_cast<const uint4*>(wr) : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 hi = ok ? *reinterpret_cast<const uint4*>(wr + 4) : make_uint4(0u, 0u, 0u, 0u);
+        gs_split3(lo, hi, pl);
+      } else {
+        pl[0] = ok ? *reinterpret_cast<const uint4*>((const T*)a.wc + (size_t)row * DS_CO + k)
+                   : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        *reinterpret_cast<uint4*>(s_cw + (j * 32 + row) * DS_DP + k) = pl[j];
+    }
+    if (tid < 32) s_cb[tid] = tid < a.ncls ? a.bc[tid] : 0.f;
+  }
 
   // ---- prologue: rows oh0 - 1, oh0 in the ring, row oh0 + 1 in flight ------------------------
   // (upsample mode: rows oh0 - 1, oh0 interpolated into the ring, row oh0 + 1's low-res rows in
@@ -264,10 +301,16 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
     store_row(oh0, raw);
     load_row(oh0 + 1, nxt);
   }
-  {  // two dropped stores: the loop is entered, as it loops, with 2 stores after the row loads
+  {  // dropped stores: the loop is entered, as it loops, with its stores after the row loads
+    // (2 output vectors per step, or 4 logit elements in classifier mode)
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
-    buf_st4(yr, BUF_OOB, z, (T*)nullptr);
-    buf_st4(yr, BUF_OOB + 64, z, (T*)nullptr);
+    if constexpr (CLS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cls_st1(yr, BUF_OOB + 64 * j, 0.f, (T*)nullptr);
+    } else {
+      buf_st4(yr, BUF_OOB, z, (T*)nullptr);
+      buf_st4(yr, BUF_OOB + 64, z, (T*)nullptr);
+    }
   }
   if constexpr (UP) __syncthreads();  // (staging of row oh0 + 1 before step oh0 interpolates it)
   stamp(a.stamps, 1);
@@ -361,6 +404,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
     __syncthreads();
     if (oh == oh0 + a.rs / 2) stamp(a.stamps, 3);
     // ---- pointwise: 16 pixels x this wave's 32 output channels, K = 128 in four 32-k steps ----
+    float ocls[2][4];  // (classifier mode) the pointwise output of this lane
     {
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -390,7 +434,64 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
           if constexpr (RES) v += rv[u][r];
           o4[r] = fmaxf(v, 0.f);
         }
-        buf_st4(yr, yoff == BUF_OOB ? BUF_OOB : yoff + c * (uint32_t)sizeof(T), o4, (T*)nullptr);
+        if constexpr (CLS) {
+          ocls[u][0] = o4[0]; ocls[u][1] = o4[1]; ocls[u][2] = o4[2]; ocls[u][3] = o4[3];
+        } else {
+          buf_st4(yr, yoff == BUF_OOB ? BUF_OOB : yoff + c * (uint32_t)sizeof(T), o4, (T*)nullptr);
+        }
+      }
+    }
+    if constexpr (CLS) {
+      // ---- classifier 1x1 on the pointwise output: its values (rounded as the unfused path
+      // stores them) -> s_d as the classifier's B operand -> 2 waves x 16 classes x 16 pixels
+      __syncthreads();  // every wave's pointwise reads of s_d are done
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = 16 * (2 * wave + u) + 4 * lq;
+        uint16_t* d = s_d + li * DS_DP + c;
+        if constexpr (F32) {
+          uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t uu = __float_as_uint(ocls[u][j]), b0 = uu & 0xFFFF0000u;
+            const float r1 = ocls[u][j] - __uint_as_float(b0);
+            const uint32_t b1 = __float_as_uint(r1) & 0xFFFF0000u;
+            const float r2 = r1 - __uint_as_float(b1);
+            p0[j] = b0;
+            p1[j] = b1;
+            p2[j] = __float_as_uint(r2) & 0xFFFF0000u;
+          }
+          *reinterpret_cast<uint2*>(d) = make_uint2((p0[0] >> 16) | p0[1], (p0[2] >> 16) | p0[3]);
+          *reinterpret_cast<uint2*>(d + DS_TW * DS_DP) = make_uint2((p1[0] >> 16) | p1[1], (p1[2] >> 16) | p1[3]);
+          *reinterpret_cast<uint2*>(d + 2 * DS_TW * DS_DP) = make_uint2((p2[0] >> 16) | p2[1], (p2[2] >> 16) | p2[3]);
+        } else {
+          *reinterpret_cast<uint2*>(d) =
+              make_uint2((uint32_t)s16_from<T>(ocls[u][0]) | ((uint32_t)s16_from<T>(ocls[u][1]) << 16),
+                         (uint32_t)s16_from<T>(ocls[u][2]) | ((uint32_t)s16_from<T>(ocls[u][3]) << 16));
+        }
+      }
+      __syncthreads();
+      const int ot = wave & 1;  // class tile (waves 2, 3 compute tile 0, 1 again: dropped stores)
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint4 xs[NP], ws[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+          xs[j] = *reinterpret_cast<const uint4*>(s_d + j * DS_TW * DS_DP + li * DS_DP + 32 * s + 8 * lq);
+          ws[j] = *reinterpret_cast<const uint4*>(s_cw + (j * 32 + 16 * ot + li) * DS_DP + 32 * s + 8 * lq);
+        }
+        if constexpr (F32) gs_mma_x3(ws, xs, acc);
+        else DsMma<T>::run(ws[0], xs[0], acc);
+      }
+      const int ow = ow0 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * ot + 4 * lq + r;
+        const float v = acc[r] * 1.f + s_cb[co];
+        const bool ok = wave < 2 && ow < a.W && co < a.ncls;
+        cls_st1(yr, ok ? (uint32_t)((((size_t)oh * a.W + ow) * a.ldl + co) * sizeof(T)) : BUF_OOB, v,
+                (T*)nullptr);
       }
     }
     if (oh == oh0 + a.rs / 2) stamp(a.stamps, 4);
@@ -412,6 +513,9 @@ static bool ds_up_fits(const DsArgs& a) {
 }
 
 bool ds_ok(const DsArgs& a) {
+  if (a.wc && (a.r || a.Hi > 0 || !a.bc || !a.logits || a.ncls < 1 || a.ncls > 32 ||
+               a.ldl < a.ncls || 4LL * a.H * a.W * a.ldl >= (long long)BUF_OOB))
+    return false;
   return ds_up_fits(a) && a.N > 0 && a.N < 65536 && a.H > 0 && a.W > 0 && a.C == DS_C && a.Co == DS_CO &&
          (a.r == nullptr || (a.ldr >= DS_CO && a.ldr % 4 == 0 && ((uintptr_t)a.r & 15) == 0 &&
                              4LL * a.H * a.W * a.ldr < (long long)BUF_OOB)) &&
@@ -451,7 +555,8 @@ int ds_fwd(const DsArgs& a, int dtype, hipStream_t st) {
                2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO));
 #define DSK(T)                                                                \
   do {                                                                        \
-    if (a.r && a.Hi > 0) dsconv_fwd_kernel<T, true, true><<<g, 256, 0, st>>>(as); \
+    if (a.wc) dsconv_fwd_kernel<T, false, false, true><<<g, 256, 0, st>>>(as);    \
+    else if (a.r && a.Hi > 0) dsconv_fwd_kernel<T, true, true><<<g, 256, 0, st>>>(as); \
     else if (a.r) dsconv_fwd_kernel<T, true, false><<<g, 256, 0, st>>>(as);   \
     else dsconv_fwd_kernel<T, false, false><<<g, 256, 0, st>>>(as);           \
   } while (0)

@@ -436,6 +436,13 @@ struct DsArgs {
   const void* r = nullptr;     // optional residual added after the pointwise BN, before its ReLU
   int ldr = 0;                 // (the FFM: relu(BN_l(conv_l(dw)) + f), :213-218); may alias y
   int rs;                      // output rows walked per workgroup (ds_rows)
+  // optional classifier 1x1 (+ bias) on the pointwise output (the Classifer's last conv,
+  // :233-236, Dropout the identity in eval): logits [N,H,W] x ncls (row stride ldl) written
+  // instead of y; the pointwise output never reaches memory
+  const void* wc = nullptr;    // [ncls][Co] in the storage dtype (ncls <= 32)
+  const float* bc = nullptr;   // [ncls] fp32 bias
+  int ncls = 0;
+  void* logits = nullptr; int ldl = 0;
   int Hi = 0, Wi = 0;          // > 0: x is [N,Hi,Wi] x C and the depthwise input is its bilinear
                                // align_corners upsample to H x W (the FFM's F.interpolate, :212),
                                // formed in LDS, never stored (up_nhwc's arithmetic)

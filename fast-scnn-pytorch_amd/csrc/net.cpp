@@ -1205,9 +1205,16 @@ struct Exec {
     // train with Dropout: the dsconv2 pw BN+ReLU output is only read by the dropout, which
     // applies the BN itself (c2pw.a is never stored: one 128-channel write + read fewer)
     const bool drop_fused = train && r.dropout_p > 0.f;
-    const DsArgs ds2 = ds_fuse ? ds_args(net.cls2, pl.c2dw, pl.c2pw, W(pl.c1pw.a)) : DsArgs{};
-    if (ds_fuse && ds_ok(ds2)) {
-      g_prof_tag = "classifier.dsconv2 (fused)";
+    // (inference: the classifier conv rides in the same launch -- Dropout is the identity -- and
+    // the dsconv2 output is never stored)
+    DsArgs ds2 = ds_fuse ? ds_args(net.cls2, pl.c2dw, pl.c2pw, W(pl.c1pw.a)) : DsArgs{};
+    if (ds_fuse) {
+      ds2.wc = Wg(net.cls_out); ds2.bc = P(net.cls_out.b); ds2.ncls = net.num_classes;
+      ds2.logits = W(pl.logits); ds2.ldl = pl.Cp;
+    }
+    const bool cls_fused = ds_fuse && ds_ok(ds2);
+    if (cls_fused) {
+      g_prof_tag = "classifier.dsconv2 + conv (fused)";
       TRY(ds_fwd(ds2, dt, r.st));
     } else {
       TRY(dw(pl.c2dw, net.cls2.dw, net.cls2.bdw, act(pl.c1pw), pl.H3, pl.W3, pl.H3, pl.W3, 1));
@@ -1224,7 +1231,7 @@ struct Exec {
       cls_in = W(pl.drop);
     }
     g_prof_tag = "classifier.conv";
-    {
+    if (!cls_fused) {
       GemmArgs g{};
       g.M = (int)pl.c2pw.M; g.N = net.num_classes; g.K = 128; g.A = cls_in; g.lda = 128;
       g.B = Wg(net.cls_out); g.ldb = 128; g.shift = P(net.cls_out.b);
