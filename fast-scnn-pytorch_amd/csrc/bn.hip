@@ -495,6 +495,21 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
 // issued back to back (clamped rows, stores predicated) before their use.  The per-element
 // arithmetic is unchanged, so dz is bit-identical to a one-vector-per-thread pass — that form
 // re-read 6 table vectors (12 16-B loads) for every 2 data loads.
+// the BN-backward output with streaming (non-temporal) stores: its consumer is the next launch,
+// and fewer dirty L2 lines are left for the kernel boundary to write back (r05 A/B: 5.737 / 5.742
+// vs 5.754 / 5.746 ms per cfg3 step)
+__device__ __forceinline__ void stv_o(float* p, const float (&v)[4]) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 t = {v[0], v[1], v[2], v[3]};
+  __builtin_nontemporal_store(t, (f4*)p);
+}
+template <typename T> __device__ __forceinline__ void stv_o(T* p, const float (&v)[8]) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  u4 w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)s16_from<T>(v[2 * i]) | ((uint32_t)s16_from<T>(v[2 * i + 1]) << 16);
+  __builtin_nontemporal_store(w, (u4*)p);
+}
 template <typename T, int MODE, bool TRAIN, bool PAIR, int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, unsigned P) {
   constexpr int V = VecW<T>::V;
@@ -550,7 +565,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, unsigned
           const float xh = (z2[u][j] - p_mn[j]) * p_is[j];
           o2[j] = p_sc[j] * (gv - p_c0[j] - xh * p_c1[j]);
         }
-        stv((T*)a.dz2 + m * a.lddz + c, o2);
+        stv_o((T*)a.dz2 + m * a.lddz + c, o2);
       }
       float o[V];
 #pragma unroll
@@ -565,7 +580,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, unsigned
           o[j] = t_sc[j] * gv;
         }
       }
-      stv((T*)a.dz + m * a.lddz + c, o);
+      stv_o((T*)a.dz + m * a.lddz + c, o);
     }
   }
 }
