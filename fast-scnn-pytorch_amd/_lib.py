@@ -122,6 +122,9 @@ SIGNATURES = {
     "fscnn_block_dsconv_res_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                            c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                            c_vp, c_int, c_vp]),
+    "fscnn_block_ffm_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
+                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_int, c_vp]),
 }
 
 _lib = None

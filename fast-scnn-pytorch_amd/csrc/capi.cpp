@@ -803,6 +803,30 @@ int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, in
   return ds_fwd(a, dtype, S(stream));
 }
 
+int fscnn_block_ffm_fwd(const void* low, int dtype, int N, int Hi, int Wi, int H, int W,
+                        const void* high, int ldhigh, const float* w_dw, const float* scale_d,
+                        const float* shift_d, const void* w_low, const float* scale_l,
+                        const float* shift_l, const void* w_high, const float* scale_h,
+                        const float* shift_h, void* y, int ldy, void* stream) {
+  if (!low || !high || !y || !w_dw || !scale_d || !shift_d || !w_low || !scale_l || !shift_l ||
+      !w_high || !scale_h || !shift_h) {
+    set_error("fscnn_block_ffm_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || N <= 0 || H <= 0 || W <= 0 || Hi <= 0 || Wi <= 0) {
+    set_error("fscnn_block_ffm_fwd: dtype %d N %d Hi %d Wi %d H %d W %d", dtype, N, Hi, Wi, H, W);
+    return E_INVALID;
+  }
+  DsArgs a{};
+  a.x = low; a.N = N; a.H = H; a.W = W; a.C = 128; a.Co = 128; a.Hi = Hi; a.Wi = Wi;
+  a.wd = w_dw; a.scd = scale_d; a.shd = shift_d;
+  a.wp = w_low; a.scp = scale_l; a.shp = shift_l;
+  a.xh = high; a.ldxh = ldhigh; a.wh = w_high; a.sch = scale_h; a.shh = shift_h;
+  a.y = y; a.ldy = ldy;
+  a.rs = ds_rows(N, H, W);
+  return ds_fwd(a, dtype, S(stream));
+}
+
 }  // extern "C"
 
 extern "C" int fscnn_plan_buffer(const fscnn_plan* plan, const char* name, long long* offset,

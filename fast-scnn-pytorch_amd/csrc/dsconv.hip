@@ -13,6 +13,12 @@
 // operations (common.hpp BUF_OOB), so every step issues the same memory operations and the wait
 // for the next row leaves the previous stores in flight.
 //
+// FFM mode (HI): the high-resolution branch (conv_higher_res + BN, :214-215: 64 -> 128 channels at
+// the same H x W) is a second GEMM on the same strip -- a row's 16 high-res pixels are loaded with
+// the step's other loads, stored to LDS as a B operand, multiplied by that branch's weights
+// (registers, pre-split) and used as the residual, so its 128-channel output (134 MB fp32 at cfg2,
+// written and read back) never reaches memory either.
+//
 // Bit-identical to dw_fwd_kernel + gemm_stream(_x3)_kernel by construction: the same depthwise
 // fma chain per output (taps in row-major order from 0, fp32), the same folded-BN fma + ReLU and
 // rounding to the storage type, and the same pointwise MFMA sequence (weights as the A operand,
@@ -28,6 +34,8 @@ constexpr int DS_RP = DS_TW + 2;       // ring pixels per row (the window's halo
 constexpr int DS_PP = DS_C + 4;        // ring floats per pixel (padded)
 constexpr int DS_DP = DS_C + 8;        // pointwise operand halves per pixel (padded)
 constexpr int DS_UC = 8;               // upsample mode: staged low-resolution columns per strip
+constexpr int DS_CH = 64;              // FFM mode: high-resolution branch input channels (K)
+constexpr int DS_HP = DS_CH + 8;       // its operand halves per pixel (padded)
 
 template <typename T>
 struct DsMma;  // one 16-bit MFMA per operand pair (the 16-bit streaming GEMM's GsMma)
@@ -65,7 +73,7 @@ __device__ __forceinline__ void cls_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, 
   __builtin_amdgcn_raw_buffer_store_b16(f2h(v), r, off, 0, 0);
 }
 
-template <typename T, bool RES, bool UP, bool CLS = false>
+template <typename T, bool RES, bool UP, bool CLS = false, bool HI = false>
 __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int NP = F32 ? 3 : 1;                  // pointwise operand planes
@@ -74,7 +82,10 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   constexpr int LP = (DS_RP * VPP + 255) / 256;    // row loads per thread
   __shared__ __attribute__((aligned(16))) float s_ring[3 * DS_RP * DS_PP];   // [row % 3][px][c]
   __shared__ __attribute__((aligned(16))) uint16_t s_d[NP * DS_TW * DS_DP];  // [plane][px][c]
-  __shared__ __attribute__((aligned(16))) float s_bn[2 * DS_CO];             // pointwise scale, shift
+  __shared__ __attribute__((aligned(16))) float s_bn[(HI ? 4 : 2) * DS_CO];  // pointwise (+ high-res) scale, shift
+  // FFM mode: the row's high-res pixels as the second GEMM's B operand ([plane][px][k])
+  __shared__ __attribute__((aligned(16))) uint16_t s_h[HI ? NP * DS_TW * DS_HP : 8];
+  __shared__ __attribute__((aligned(16))) float s_wt[HI && sizeof(T) == 4 ? 9 * DS_C : 4];  // (WT_LDS)
   // upsample mode: the two low-resolution rows x DS_UC columns a ring row interpolates from,
   // double-buffered ([buf][row][col][c], fp32)
   __shared__ __attribute__((aligned(16))) float s_stg[UP ? 2 * 2 * DS_UC * DS_C : 4];
@@ -228,11 +239,22 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
 
   // depthwise: thread = channel quad qd x output pixels 2 pp, 2 pp + 1; taps and BN in registers
   const int qd = tid & 31, pp = tid >> 5;
-  float wt[9][4], dsc[4], dsh[4];
+  // (fp32 FFM mode: the taps in LDS, [9][C], read per kernel row -- the high-res branch's split
+  // weights need their 48 registers)
+  constexpr bool WT_LDS = HI && F32;
+  float wt[WT_LDS ? 1 : 9][4], dsc[4], dsh[4];
+  if constexpr (WT_LDS) {
+    for (int i = tid; i < 9 * DS_C; i += 256) {
+      const int t = i / DS_C, c = i - t * DS_C;
+      s_wt[i] = a.wd[c * 9 + t];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
+    if constexpr (!WT_LDS) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wt[t][j] = a.wd[(4 * qd + j) * 9 + t];
+      for (int t = 0; t < 9; ++t) wt[t][j] = a.wd[(4 * qd + j) * 9 + t];
+    }
     dsc[j] = a.scd[4 * qd + j];
     dsh[j] = a.shd[4 * qd + j];
   }
@@ -253,6 +275,39 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   for (int i = tid; i < DS_CO; i += 256) {
     s_bn[i] = a.scp[i];
     s_bn[DS_CO + i] = a.shp[i];
+    if constexpr (HI) {
+      s_bn[2 * DS_CO + i] = a.sch[i];
+      s_bn[3 * DS_CO + i] = a.shh[i];
+    }
+  }
+  // FFM mode: this thread's 16-B vector of a row's DS_TW high-res pixels (16-bit plans: threads
+  // >= 128 load nothing), and the high-res weights of the wave's output tiles (pre-split)
+  constexpr int VH = DS_CH / VI;  // vectors per high-res pixel
+  const size_t himg = HI ? (size_t)a.H * a.W * a.ldxh : 0;
+  const __amdgpu_buffer_rsrc_t hr =
+      buf_rsrc(HI ? (const T*)a.xh + (size_t)n * himg : (const T*)a.x, (uint32_t)(himg * sizeof(T)));
+  const uint32_t hrowbytes = (uint32_t)((size_t)a.W * a.ldxh * sizeof(T));
+  uint32_t hvo = BUF_OOB;
+  int hls = -1;
+  uint4 wph[2][2][HI ? NP : 1];
+  if constexpr (HI) {
+    const int px = tid / VH, cv = tid - px * VH;
+    if (px < DS_TW) {
+      hls = px * DS_HP + cv * VI;
+      if (ow0 + px < a.W) hvo = (uint32_t)(((size_t)(ow0 + px) * a.ldxh + cv * VI) * sizeof(T));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int co = 16 * (2 * wave + u) + li, k = 32 * s + 8 * lq;
+        if constexpr (F32) {
+          const float* wr = (const float*)a.wh + (size_t)co * DS_CH + k;
+          gs_split3(*reinterpret_cast<const uint4*>(wr), *reinterpret_cast<const uint4*>(wr + 4), wph[u][s]);
+        } else {
+          wph[u][s][0] = *reinterpret_cast<const uint4*>((const T*)a.wh + (size_t)co * DS_CH + k);
+        }
+      }
   }
   if constexpr (CLS) {  // the classifier weights, split once (fp32) into the A operand planes
     for (int i = tid; i < 32 * (DS_CO / 8); i += 256) {
@@ -323,6 +378,12 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
   for (int oh = oh0; oh < oh_end; ++oh) {
     // this step's residual, before the row prefetch (so waiting for it does not wait for that)
     float rv[2][4];
+    uint4 hraw = make_uint4(0u, 0u, 0u, 0u);  // (FFM mode) this thread's high-res vector of row oh
+    if constexpr (HI) {
+      const uint32_t off = hvo != BUF_OOB ? hvo + (uint32_t)oh * hrowbytes : BUF_OOB;
+      const buf_v4u t = __builtin_amdgcn_raw_buffer_load_b128(hr, off, 0, 0);
+      hraw = make_uint4(t[0], t[1], t[2], t[3]);
+    }
     if constexpr (RES) {
       const int ow = ow0 + li;
 #pragma unroll
@@ -359,6 +420,17 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
         for (int j = 0; j < 4; ++j) acc[p][j] = 0.f;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
+        float wk[3][4];
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          if constexpr (WT_LDS) {
+            const float4 t = *reinterpret_cast<const float4*>(s_wt + (kh * 3 + kw) * DS_C + 4 * qd);
+            wk[kw][0] = t.x; wk[kw][1] = t.y; wk[kw][2] = t.z; wk[kw][3] = t.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wk[kw][j] = wt[kh * 3 + kw][j];
+          }
+        }
         const float* rowp = s_ring + ((oh - 1 + kh + 3) % 3) * DS_RP * DS_PP + 4 * qd;
 #pragma unroll
         for (int ci = 0; ci < 4; ++ci) {  // ring pixels 2 pp + ci
@@ -369,7 +441,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
             const int kw = ci - p;
             if (kw < 0 || kw > 2) continue;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[p][j] = fmaf(vv[j], wt[kh * 3 + kw][j], acc[p][j]);
+            for (int j = 0; j < 4; ++j) acc[p][j] = fmaf(vv[j], wk[kw][j], acc[p][j]);
           }
         }
       }
@@ -401,6 +473,31 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
         }
       }
     }
+    if constexpr (HI) {  // the high-res vector -> s_h (the split terms, one plane each, for fp32)
+      if (hls >= 0) {
+        uint16_t* d = s_h + hls;
+        if constexpr (F32) {
+          const uint32_t v4[4] = {hraw.x, hraw.y, hraw.z, hraw.w};
+          uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float f = __uint_as_float(v4[j]);
+            const uint32_t b0 = v4[j] & 0xFFFF0000u;
+            const float r1 = f - __uint_as_float(b0);
+            const uint32_t b1 = __float_as_uint(r1) & 0xFFFF0000u;
+            const float r2 = r1 - __uint_as_float(b1);
+            p0[j] = b0;
+            p1[j] = b1;
+            p2[j] = __float_as_uint(r2) & 0xFFFF0000u;
+          }
+          *reinterpret_cast<uint2*>(d) = make_uint2((p0[0] >> 16) | p0[1], (p0[2] >> 16) | p0[3]);
+          *reinterpret_cast<uint2*>(d + DS_TW * DS_HP) = make_uint2((p1[0] >> 16) | p1[1], (p1[2] >> 16) | p1[3]);
+          *reinterpret_cast<uint2*>(d + 2 * DS_TW * DS_HP) = make_uint2((p2[0] >> 16) | p2[1], (p2[2] >> 16) | p2[3]);
+        } else {
+          *reinterpret_cast<uint4*>(d) = hraw;
+        }
+      }
+    }
     __syncthreads();
     if (oh == oh0 + a.rs / 2) stamp(a.stamps, 3);
     // ---- pointwise: 16 pixels x this wave's 32 output channels, K = 128 in four 32-k steps ----
@@ -419,6 +516,46 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
           else DsMma<T>::run(wpr[u][s][0], xs[0], acc[u]);
         }
       }
+      if constexpr (HI) {  // the high-res branch: BN_h(W_h * xh), rounded as the unfused path stores it
+        f32x4 ah[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          uint4 xs[NP];
+#pragma unroll
+          for (int j = 0; j < NP; ++j)
+            xs[j] = *reinterpret_cast<const uint4*>(s_h + j * DS_TW * DS_HP + li * DS_HP + 32 * s + 8 * lq);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            if constexpr (F32) gs_mma_x3(wph[u][s], xs, ah[u]);
+            else DsMma<T>::run(wph[u][s][0], xs[0], ah[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = 16 * (2 * wave + u) + 4 * lq;
+          const float4 sc = *reinterpret_cast<const float4*>(&s_bn[2 * DS_CO + c]);
+          const float4 sh = *reinterpret_cast<const float4*>(&s_bn[3 * DS_CO + c]);
+          const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+          float hv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hv[r] = ah[u][r] * scv[r] + shv[r];
+          if constexpr (F32) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rv[u][r] = hv[r];
+          } else {
+            // the fp32 value first, then its 16-bit rounding, as the unfused GEMM stores it (left
+            // alone, the compiler fuses the two into v_fma_mix: one rounding instead of two)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(hv[r]));
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+              const uint32_t pk = (uint32_t)s16_from<T>(hv[r]) | ((uint32_t)s16_from<T>(hv[r + 1]) << 16);
+              rv[u][r] = s16_to<T>((uint16_t)(pk & 0xFFFFu));
+              rv[u][r + 1] = s16_to<T>((uint16_t)(pk >> 16));
+            }
+          }
+        }
+      }
       const int ow = ow0 + li;
       const uint32_t yoff = ow < a.W ? (uint32_t)((((size_t)oh * a.W + ow) * a.ldy) * sizeof(T)) : BUF_OOB;
 #pragma unroll
@@ -431,7 +568,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[u][r] * scv[r] + shv[r];
-          if constexpr (RES) v += rv[u][r];
+          if constexpr (RES || HI) v += rv[u][r];
           o4[r] = fmaxf(v, 0.f);
         }
         if constexpr (CLS) {
@@ -513,6 +650,9 @@ static bool ds_up_fits(const DsArgs& a) {
 }
 
 bool ds_ok(const DsArgs& a) {
+  if (a.xh && (a.r || a.wc || a.Hi <= 0 || !a.wh || !a.sch || !a.shh || a.ldxh < DS_CH || a.ldxh % 8 ||
+               ((uintptr_t)a.xh & 15) || ((uintptr_t)a.wh & 15) || 4LL * a.H * a.W * a.ldxh >= (long long)BUF_OOB))
+    return false;
   if (a.wc && (a.r || a.Hi > 0 || !a.bc || !a.logits || a.ncls < 1 || a.ncls > 32 ||
                a.ldl < a.ncls || 4LL * a.H * a.W * a.ldl >= (long long)BUF_OOB))
     return false;
@@ -551,11 +691,12 @@ int ds_fwd(const DsArgs& a, int dtype, hipStream_t st) {
   const double E = dtype == DT_F32 ? 4.0 : 2.0;
   ProfScope ps(PK_DSCONV, st,
                E * a.N * ((a.Hi > 0 ? (double)a.Hi * a.Wi : (double)a.H * a.W) * DS_C +
-                          (double)a.H * a.W * (DS_CO + (a.r ? DS_CO : 0))),
-               2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO));
+                          (double)a.H * a.W * (DS_CO + (a.r ? DS_CO : 0) + (a.xh ? DS_CH : 0))),
+               2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO + (a.xh ? (double)DS_CH * DS_CO : 0.0)));
 #define DSK(T)                                                                \
   do {                                                                        \
     if (a.wc) dsconv_fwd_kernel<T, false, false, true><<<g, 256, 0, st>>>(as);    \
+    else if (a.xh) dsconv_fwd_kernel<T, false, true, false, true><<<g, 256, 0, st>>>(as); \
     else if (a.r && a.Hi > 0) dsconv_fwd_kernel<T, true, true><<<g, 256, 0, st>>>(as); \
     else if (a.r) dsconv_fwd_kernel<T, true, false><<<g, 256, 0, st>>>(as);   \
     else dsconv_fwd_kernel<T, false, false><<<g, 256, 0, st>>>(as);           \

@@ -435,6 +435,7 @@ struct DsArgs {
   void* y; int ldy;            // NHWC [N,H,W] x Co (row stride ldy elements)
   const void* r = nullptr;     // optional residual added after the pointwise BN, before its ReLU
   int ldr = 0;                 // (the FFM: relu(BN_l(conv_l(dw)) + f), :213-218); may alias y
+                               // (or xh below)
   int rs;                      // output rows walked per workgroup (ds_rows)
   // optional classifier 1x1 (+ bias) on the pointwise output (the Classifer's last conv,
   // :233-236, Dropout the identity in eval): logits [N,H,W] x ncls (row stride ldl) written
@@ -446,6 +447,13 @@ struct DsArgs {
   int Hi = 0, Wi = 0;          // > 0: x is [N,Hi,Wi] x C and the depthwise input is its bilinear
                                // align_corners upsample to H x W (the FFM's F.interpolate, :212),
                                // formed in LDS, never stored (up_nhwc's arithmetic)
+  // optional high-resolution branch computed in the launch and used as the residual (the FFM's
+  // conv_higher_res + BN, :214-215; requires Hi > 0 and r == nullptr): BN_h(W_h * xh), its
+  // 128-channel output never stored
+  const void* xh = nullptr;    // NHWC [N,H,W] x 64 (row stride ldxh elements), storage dtype
+  int ldxh = 0;
+  const void* wh = nullptr;    // [Co][64] in the storage dtype
+  const float *sch = nullptr, *shh = nullptr;  // folded BN of the high-res branch
   unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
 };
 bool ds_ok(const DsArgs& a);

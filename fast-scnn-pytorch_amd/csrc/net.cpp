@@ -977,6 +977,15 @@ struct Exec {
     }();
     return on;
   }
+  // FSCNN_FFM_HI=0: the FFM's high-res branch runs as its own GEMM (the fused launch then adds its
+  // stored output as a residual)
+  static bool ffm_hi_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("FSCNN_FFM_HI");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   int fold_all() {
     FoldTable t{};
     auto add = [&](const BnL& bn, const Unit& u, const ConvL* conv) {
@@ -1144,15 +1153,24 @@ struct Exec {
       if (!train) {
         // f = BN_h(conv_h(hr)) ; f = relu(BN_l(conv_l(dw)) + f), the dw and conv_l in one
         // launch (dsconv.hip) when it fits
-        TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, raw(W(pl.l2pw.a), 64), false));
         DsArgs fa{};  // the upsample too: the depthwise reads the PPM output through it
         fa.x = W(pl.po.a); fa.Hi = pl.H5; fa.Wi = pl.W5;
         fa.N = N; fa.H = pl.H3; fa.W = pl.W3; fa.C = 128; fa.Co = 128;
         fa.wd = P(net.ffm_dw.w); fa.scd = Wf(pl.fdw.scale); fa.shd = Wf(pl.fdw.shift);
         fa.wp = Wg(net.ffm_low); fa.scp = Wf(pl.flow.scale); fa.shp = Wf(pl.flow.shift);
-        fa.y = W(pl.flow.a); fa.ldy = pl.flow.ld; fa.r = W(pl.f); fa.ldr = 128;
+        fa.y = W(pl.flow.a); fa.ldy = pl.flow.ld;
         fa.rs = ds_rows(N, pl.H3, pl.W3);
-        if (ds_enabled() && ds_ok(fa)) {
+        // and the high-res branch (conv_higher_res + BN) as a second GEMM in the same launch
+        DsArgs fh = fa;
+        fh.xh = W(pl.l2pw.a); fh.ldxh = 64; fh.wh = Wg(net.ffm_high);
+        fh.sch = Wf(pl.fhigh.scale); fh.shh = Wf(pl.fhigh.shift);
+        fa.r = W(pl.f); fa.ldr = 128;
+        const bool hi_fused = ds_enabled() && ffm_hi_enabled() && ds_ok(fh);
+        if (!hi_fused) TRY(pw(pl.fhigh, net.ffm_high, &net.ffm_bhigh, raw(W(pl.l2pw.a), 64), false));
+        if (hi_fused) {
+          g_prof_tag = "feature_fusion (upsample + dwconv + conv_lower_res + conv_higher_res, fused)";
+          TRY(ds_fwd(fh, dt, r.st));
+        } else if (ds_enabled() && ds_ok(fa)) {
           g_prof_tag = "feature_fusion.upsample + dwconv + conv_lower_res (fused)";
           TRY(ds_fwd(fa, dt, r.st));
         } else {

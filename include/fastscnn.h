@@ -265,6 +265,22 @@ int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, in
                                const void* w_pw, const float* scale_p, const float* shift_p,
                                const void* res, int ldres, void* y, int ldy, void* stream);
 
+/* fscnn_block_ffm_fwd: the inference FeatureFusionModule (models/fast_scnn.py:200-218) in one
+ * launch: y = relu(BN_l(W_l * relu(BN_d(dw3x3(up(low))))) + BN_h(W_h * high)).  low NHWC
+ * [N][Hi][Wi] x 128 (the global feature extractor's output; up() its bilinear align_corners resize
+ * to H x W, formed in LDS); high NHWC [N][H][W] x 64 with row stride ldhigh (>= 64, multiple of
+ * 8, 16-B aligned; LearningToDownsample's output); w_dw [128][9] fp32, w_low [128][128] and
+ * w_high [128][64] in dtype; every BN folded to (scale, shift) fp32.  Neither the upsampled
+ * input, the depthwise output nor the high-res branch's output reaches memory.  Replaces
+ * F.interpolate + dwconv + conv_lower_res + conv_higher_res + add + ReLU (four launches of the
+ * unfused eval path); the executor uses it for the FFM of every eval plan (FSCNN_FFM_HI=0 keeps
+ * the high-res branch as its own GEMM and fscnn_block_dsconv_res_fwd), bit-identical to them. */
+int fscnn_block_ffm_fwd(const void* low, int dtype, int N, int Hi, int Wi, int H, int W,
+                        const void* high, int ldhigh, const float* w_dw, const float* scale_d,
+                        const float* shift_d, const void* w_low, const float* scale_l,
+                        const float* shift_l, const void* w_high, const float* scale_h,
+                        const float* shift_h, void* y, int ldy, void* stream);
+
 /* ---- launch profiler (bench.py roofline, tools/layer_report.py) ----------------------------
  * kind: 1 conv0_fwd, 2 dw_fwd, 3 dw_dgrad, 4 dw_wgrad, 5 gemm_nt, 6 gemm_tn, 7 bn_apply,
  * 8 bn_bwd (apply), 9 upsample, 10 upsample_bwd, 11 cross_entropy / fused loss head,

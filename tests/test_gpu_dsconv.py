@@ -1,5 +1,6 @@
 """Fused inference DSConv (csrc/dsconv.hip; models/fast_scnn.py:64-79 _DSConv, the Classifer's
-dsconv1 / dsconv2 at :228-231) through the C ABI (``fscnn_block_dsconv_fwd``) against a plain
+dsconv1 / dsconv2 at :228-231, and the FeatureFusionModule, :200-218) through the C ABI
+(``fscnn_block_dsconv_fwd`` / ``_res_fwd``, ``fscnn_block_ffm_fwd``) against a plain
 PyTorch fp32 restatement: depthwise 3x3 s1 p1 -> folded BN -> ReLU -> 1x1 conv (128 -> 128) ->
 folded BN -> ReLU.
 
@@ -138,6 +139,48 @@ def test_dsconv_upsample_residual_vs_torch(dt, N, Hi, Wi, H, W):
     tol = 2e-5 * scale if dt == torch.float32 else 2 ** -7 * scale
     assert err <= tol, (err, tol, scale)
 
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,Hi,Wi,H,W,ldh", [(2, 8, 12, 32, 48, 64), (1, 7, 9, 25, 33, 72),
+                                             (1, 16, 16, 64, 64, 64)])
+def test_ffm_fwd_vs_torch(dt, N, Hi, Wi, H, W, ldh):
+    """The whole eval FeatureFusionModule (models/fast_scnn.py:200-218) in one launch
+    (``fscnn_block_ffm_fwd``): relu(BN_l(conv_l(relu(BN_d(dw(up(low)))))) + BN_h(conv_h(high)))
+    -- the high-res branch is a second GEMM on the same strip, rounded to the storage type where
+    the unfused path stores it; partial strips, a high-res row stride above 64."""
+    low = rnd(N, Hi, Wi, 128, seed=15)
+    high = rnd(N, H, W, ldh, seed=16)
+    wd = rnd(128, 9, seed=17, scale=0.4)
+    wl = rnd(128, 128, seed=18, scale=1.0 / 128 ** 0.5)
+    wh = rnd(128, 64, seed=19, scale=1.0 / 64 ** 0.5)
+    bn = [(rnd(128, seed=70 + i) * 0.5 + 1.0, rnd(128, seed=80 + i) * 0.2) for i in range(3)]
+    q = (lambda t: t) if dt == torch.float32 else (lambda t: t.to(dt).float())  # noqa: E731
+    (sd, hd), (sl, hl), (sh, hh) = bn
+    c = lambda t: t[None, :, None, None]  # noqa: E731
+    up = q(F.interpolate(q(low).permute(0, 3, 1, 2), size=(H, W), mode="bilinear",
+                         align_corners=True))
+    d = q(F.relu(F.conv2d(up, wd.reshape(128, 1, 3, 3), padding=1, groups=128) * c(sd) + c(hd)))
+    fh = q(F.conv2d(q(high[..., :64]).permute(0, 3, 1, 2), q(wh)[:, :, None, None]) * c(sh) + c(hh))
+    ref = F.relu(F.conv2d(d, q(wl)[:, :, None, None]) * c(sl) + c(hl) + fh)
+    lowd, highd = low.to(dt).to(DEV).contiguous(), high.to(dt).to(DEV).contiguous()
+    wdd = wd.to(DEV).contiguous()
+    wld, whd = wl.to(dt).to(DEV).contiguous(), wh.to(dt).to(DEV).contiguous()
+    bnd = [(s.to(DEV), h.to(DEV)) for s, h in bn]
+    y = torch.full((N, H, W, 128), float("nan"), dtype=dt, device=DEV)
+    _lib.call("fscnn_block_ffm_fwd", _lib.ptr(lowd), _lib.dtype_code(dt), N, Hi, Wi, H, W,
+              _lib.ptr(highd), ldh, _lib.ptr(wdd), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]),
+              _lib.ptr(wld), _lib.ptr(bnd[1][0]), _lib.ptr(bnd[1][1]), _lib.ptr(whd),
+              _lib.ptr(bnd[2][0]), _lib.ptr(bnd[2][1]), _lib.ptr(y), 128, _lib.stream_ptr())
+    torch.cuda.synchronize()
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    tol = 2e-5 * scale if dt == torch.float32 else 2 ** -7 * scale
+    assert err <= tol, (err, tol, scale)
+    if dt != torch.float32:
+        far = ((got - ref).abs() > 2 ** -8 * ref.abs() + 1e-3 * scale).float().mean().item()
+        assert far < 1e-3, far
 
 def test_dsconv_rejects_other_widths():
     x = torch.zeros(1, 4, 4, 64, device=DEV)

@@ -21,6 +21,9 @@ fresh child process:
   (test_dsconv_fused_bit_identical).
 * ``FSCNN_IR_S2=0``       — (inference) the stride-2 bottlenecks (1.0, 2.0) as their three unfused
   launches instead of the fused stride-2 block (csrc/ir.hip).
+* ``FSCNN_FFM_HI=0``      — (inference) the FFM's high-res branch (conv_higher_res + BN) as its own
+  GEMM, added as a stored residual by the fused launch, instead of a second GEMM inside it
+  (test_ffm_hi_fused_bit_identical).
 
 (Round 5 removed the measured-slower variants and their switches: FSCNN_DW_LOOP, FSCNN_GEMM_PF,
 FSCNN_CE_HEAD, FSCNN_CE_PACK, FSCNN_GEMM_MINT.)
@@ -56,7 +59,7 @@ CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_GRAPHS=1": TRAIN + EVAL + HEAD16 + ["tests/test_gpu_autograd.py"],
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
          "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL,
-         "FSCNN_DSCONV_FUSED=0": EVAL, "FSCNN_IR_S2=0": EVAL}
+         "FSCNN_DSCONV_FUSED=0": EVAL, "FSCNN_IR_S2=0": EVAL, "FSCNN_FFM_HI=0": EVAL}
 
 
 def _env(switch):
@@ -116,12 +119,26 @@ def test_stem_fused_bit_identical(tmp_path):
 def test_dsconv_fused_bit_identical(tmp_path):
     """The fused inference DSConv (depthwise + BN + ReLU and pointwise + BN (+ residual) + ReLU in
     one launch, csrc/dsconv.hip: the classifier's dsconv1 / dsconv2 and the FFM's upsample +
-    dwconv + conv_lower_res) gives bit-identical outputs to the unfused launches: fp32 / bf16 / fp16
+    dwconv + conv_lower_res + conv_higher_res) gives bit-identical outputs to the unfused launches: fp32 / bf16 / fp16
     images, autocast fp16, partial strips and row segments (tests/_stem_worker.py --dsconv).  The
     default run really took the three fused launches."""
     ref = _stem_worker(tmp_path, "FSCNN_DSCONV_FUSED=0", dsconv=True)
     got = _stem_worker(tmp_path, None, dsconv=True)
     assert int(ref["stem_launches"]) == 0 and int(got["stem_launches"]) == 3
+    for k in ref:
+        if k == "stem_launches":
+            continue
+        assert np.isfinite(got[k]).all(), k
+        assert np.array_equal(ref[k], got[k]), "%s: max |diff| %g" % (
+            k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
+
+
+def test_ffm_hi_fused_bit_identical(tmp_path):
+    """The FFM's high-res branch computed inside the fused launch (a second GEMM on the strip)
+    gives bit-identical outputs to its own GEMM launch + the stored residual (FSCNN_FFM_HI=0)."""
+    ref = _stem_worker(tmp_path, "FSCNN_FFM_HI=0", dsconv=True)
+    got = _stem_worker(tmp_path, None, dsconv=True)
+    assert int(ref["stem_launches"]) == 3 and int(got["stem_launches"]) == 3
     for k in ref:
         if k == "stem_launches":
             continue
