@@ -190,3 +190,19 @@ def test_dsconv_rejects_other_widths():
                                             *([_lib.ptr(w)] * 6), _lib.ptr(y), 128,
                                             _lib.stream_ptr())
     assert rc != 0
+
+
+def test_ffm_rejects_bad_high_stride():
+    """fscnn_block_ffm_fwd needs the high-res rows as whole 16-B vectors (ldhigh >= 64, a multiple
+    of 8): anything else is refused (E_UNSUPPORTED), nothing is launched."""
+    low = torch.zeros(1, 4, 4, 128, device=DEV)
+    high = torch.zeros(1, 16, 16, 64, device=DEV)
+    w = torch.zeros(128 * 128, device=DEV)
+    y = torch.full((1, 16, 16, 128), 7.0, device=DEV)
+    for ldh in (60, 68):
+        rc = _lib.load().fscnn_block_ffm_fwd(_lib.ptr(low), 0, 1, 4, 4, 16, 16, _lib.ptr(high), ldh,
+                                             *([_lib.ptr(w)] * 9), _lib.ptr(y), 128,
+                                             _lib.stream_ptr())
+        assert rc != 0
+    torch.cuda.synchronize()
+    assert (y == 7.0).all()
