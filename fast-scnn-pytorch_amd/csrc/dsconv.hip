@@ -208,18 +208,38 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
         *reinterpret_cast<float4*>(base + o + j) = make_float4(f[j], f[j + 1], f[j + 2], f[j + 3]);
     }
   };
-  // ring row r from staging buffer b: up_nhwc's W-then-H lerp2, rounded to the storage type
+  // ring row r from staging buffer b: up_nhwc's W-then-H lerp2, rounded to the storage type.
+  // A thread's items (ring pixel, channel quad) are the same every step: their column taps are
+  // computed once (staged columns j0 | j1 << 8 | in-map << 16, and the two weights).
+  constexpr int NUI = (DS_RP * (DS_C / 4) + 255) / 256;  // interpolation items per thread
+  int ucj[UP ? NUI : 1];
+  float ucl0[UP ? NUI : 1], ucl1[UP ? NUI : 1];
+  if constexpr (UP) {
+#pragma unroll
+    for (int k = 0; k < NUI; ++k) {
+      const int i = tid + 256 * k;
+      const int px = i / (DS_C / 4);
+      const int col = ow0 - 1 + px;
+      const bool ok = col >= 0 && col < a.W;
+      const Lerp lw = ac_lerp(ok ? col : jlo, a.Wi, a.W, sws);
+      ucj[k] = (lw.i0 - jlo) | ((lw.i1 - jlo) << 8) | (ok ? 1 << 16 : 0);
+      ucl0[k] = lw.l0;
+      ucl1[k] = lw.l1;
+    }
+  }
   auto interp_up = [&](int r, int b) {
     const bool rok = r >= 0 && r < a.H;
     const Lerp lh = ac_lerp(rok ? r : 0, a.Hi, a.H, shs);
     const float* st = s_stg + b * 2 * DS_UC * DS_C;
     float* ring = s_ring + ((r + 3) % 3) * DS_RP * DS_PP;
-    for (int i = tid; i < DS_RP * (DS_C / 4); i += 256) {
+#pragma unroll
+    for (int k = 0; k < NUI; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= DS_RP * (DS_C / 4)) continue;
       const int px = i / (DS_C / 4), q = i - px * (DS_C / 4);
-      const int col = ow0 - 1 + px;
-      const bool ok = rok && col >= 0 && col < a.W;
-      const Lerp lw = ac_lerp(ok ? col : jlo, a.Wi, a.W, sws);
-      const int j0 = lw.i0 - jlo, j1 = lw.i1 - jlo;
+      const bool ok = rok && (ucj[k] >> 16);
+      const int j0 = ucj[k] & 0xFF, j1 = (ucj[k] >> 8) & 0xFF;
+      const float l0 = ucl0[k], l1 = ucl1[k];
       const float4 p00 = *reinterpret_cast<const float4*>(st + j0 * DS_C + 4 * q);
       const float4 p01 = *reinterpret_cast<const float4*>(st + j1 * DS_C + 4 * q);
       const float4 p10 = *reinterpret_cast<const float4*>(st + (DS_UC + j0) * DS_C + 4 * q);
@@ -229,8 +249,8 @@ __global__ __launch_bounds__(256, 2) void dsconv_fwd_kernel(DsArgs a) {
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float v = lerp2(lh.l0, lerp2(lw.l0, a00[j], lw.l1, a01[j]), lh.l1,
-                              lerp2(lw.l0, a10[j], lw.l1, a11[j]));
+        const float v = lerp2(lh.l0, lerp2(l0, a00[j], l1, a01[j]), lh.l1,
+                              lerp2(l0, a10[j], l1, a11[j]));
         o[j] = ok ? round_as<T>(v) : 0.f;
       }
       *reinterpret_cast<float4*>(ring + px * DS_PP + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
