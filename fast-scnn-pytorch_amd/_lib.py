@@ -122,6 +122,8 @@ SIGNATURES = {
     "fscnn_block_dsconv_res_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                            c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                            c_vp, c_int, c_vp]),
+    "fscnn_block_cls_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int] + [c_vp] * 14 + [c_int, c_vp, c_vp,
+                                                                              c_int, c_vp]),
     "fscnn_block_ffm_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                     c_int, c_vp]),

@@ -803,6 +803,42 @@ int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, in
   return ds_fwd(a, dtype, S(stream));
 }
 
+int fscnn_block_cls_fwd(const void* x, int dtype, int N, int H, int W, const float* w_dw1,
+                        const float* scale_d1, const float* shift_d1, const void* w_pw1,
+                        const float* scale_p1, const float* shift_p1, const float* w_dw2,
+                        const float* scale_d2, const float* shift_d2, const void* w_pw2,
+                        const float* scale_p2, const float* shift_p2, const void* w_cls,
+                        const float* b_cls, int ncls, void* tmp, void* logits, int ldl,
+                        void* stream) {
+  if (!x || !tmp || !logits || !w_dw1 || !scale_d1 || !shift_d1 || !w_pw1 || !scale_p1 ||
+      !shift_p1 || !w_dw2 || !scale_d2 || !shift_d2 || !w_pw2 || !scale_p2 || !shift_p2 || !w_cls ||
+      !b_cls) {
+    set_error("fscnn_block_cls_fwd: null argument");
+    return E_INVALID;
+  }
+  if (dtype < DT_F32 || dtype > DT_F16 || N <= 0 || H <= 0 || W <= 0) {
+    set_error("fscnn_block_cls_fwd: dtype %d N %d H %d W %d", dtype, N, H, W);
+    return E_INVALID;
+  }
+  DsArgs a{};  // dsconv1 -> tmp
+  a.x = x; a.N = N; a.H = H; a.W = W; a.C = 128; a.Co = 128;
+  a.wd = w_dw1; a.scd = scale_d1; a.shd = shift_d1;
+  a.wp = w_pw1; a.scp = scale_p1; a.shp = shift_p1;
+  a.y = tmp; a.ldy = 128;
+  a.rs = ds_rows(N, H, W);
+  DsArgs b = a;  // dsconv2 + the classifier conv -> logits
+  b.x = tmp;
+  b.wd = w_dw2; b.scd = scale_d2; b.shd = shift_d2;
+  b.wp = w_pw2; b.scp = scale_p2; b.shp = shift_p2;
+  b.wc = w_cls; b.bc = b_cls; b.ncls = ncls; b.logits = logits; b.ldl = ldl;
+  if (!ds_ok(a) || !ds_ok(b)) {
+    set_error("fscnn_block_cls_fwd: unsupported shape N=%d H=%d W=%d ncls=%d ldl=%d", N, H, W, ncls, ldl);
+    return E_UNSUPPORTED;
+  }
+  const int rc = ds_fwd(a, dtype, S(stream));
+  return rc ? rc : ds_fwd(b, dtype, S(stream));
+}
+
 int fscnn_block_ffm_fwd(const void* low, int dtype, int N, int Hi, int Wi, int H, int W,
                         const void* high, int ldhigh, const float* w_dw, const float* scale_d,
                         const float* shift_d, const void* w_low, const float* scale_l,

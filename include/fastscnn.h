@@ -265,6 +265,22 @@ int fscnn_block_dsconv_res_fwd(const void* x, int dtype, int N, int H, int W, in
                                const void* w_pw, const float* scale_p, const float* shift_p,
                                const void* res, int ldres, void* y, int ldy, void* stream);
 
+/* fscnn_block_cls_fwd: the inference Classifer (models/fast_scnn.py:221-237; Dropout is the
+ * identity in eval) in two launches: tmp = dsconv1(x) (fscnn_block_dsconv_fwd), then dsconv2 and
+ * the 1x1 classifier conv (+ bias) in one launch whose 128-channel dsconv2 output never reaches
+ * memory: logits = W_cls * dsconv2(tmp) + b_cls.  x and tmp NHWC [N][H][W] x 128 in dtype
+ * (16-B aligned); w_dw* [128][9] fp32, w_pw* [128][128] and w_cls [ncls][128] in dtype, b_cls
+ * [ncls] fp32, every BN folded to (scale, shift) fp32; logits NHWC [N][H][W] x ncls with row
+ * stride ldl (>= ncls; ncls <= 32), only the first ncls columns written.  Replaces the
+ * Classifer's dw / pw / dw / pw / conv launches of the unfused eval path; bit-identical to them. */
+int fscnn_block_cls_fwd(const void* x, int dtype, int N, int H, int W, const float* w_dw1,
+                        const float* scale_d1, const float* shift_d1, const void* w_pw1,
+                        const float* scale_p1, const float* shift_p1, const float* w_dw2,
+                        const float* scale_d2, const float* shift_d2, const void* w_pw2,
+                        const float* scale_p2, const float* shift_p2, const void* w_cls,
+                        const float* b_cls, int ncls, void* tmp, void* logits, int ldl,
+                        void* stream);
+
 /* fscnn_block_ffm_fwd: the inference FeatureFusionModule (models/fast_scnn.py:200-218) in one
  * launch: y = relu(BN_l(W_l * relu(BN_d(dw3x3(up(low))))) + BN_h(W_h * high)).  low NHWC
  * [N][Hi][Wi] x 128 (the global feature extractor's output; up() its bilinear align_corners resize

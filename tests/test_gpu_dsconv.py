@@ -182,6 +182,44 @@ def test_ffm_fwd_vs_torch(dt, N, Hi, Wi, H, W, ldh):
         far = ((got - ref).abs() > 2 ** -8 * ref.abs() + 1e-3 * scale).float().mean().item()
         assert far < 1e-3, far
 
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W,ncls,ldl", [(2, 24, 48, 19, 19), (1, 37, 53, 2, 8)])
+def test_cls_fwd_vs_torch(dt, N, H, W, ncls, ldl):
+    """The whole eval Classifer (models/fast_scnn.py:221-237) through ``fscnn_block_cls_fwd``:
+    conv_cls(dsconv2(dsconv1(x))) + bias, dsconv2's output never stored; logits row stride
+    above ncls (the padding columns untouched)."""
+    x = rnd(N, H, W, 128, seed=21)
+    w = [rnd(128, 9, seed=22, scale=0.4), rnd(128, 128, seed=23, scale=128 ** -0.5),
+         rnd(128, 9, seed=24, scale=0.4), rnd(128, 128, seed=25, scale=128 ** -0.5)]
+    wc = rnd(ncls, 128, seed=26, scale=128 ** -0.5)
+    bc = rnd(ncls, seed=27, scale=0.1)
+    bn = [(rnd(128, seed=90 + i) * 0.5 + 1.0, rnd(128, seed=95 + i) * 0.2) for i in range(4)]
+    q = (lambda t: t) if dt == torch.float32 else (lambda t: t.to(dt).float())  # noqa: E731
+    h1 = q(_ref(x, w[0], w[1], bn[0:2], dt)).permute(0, 2, 3, 1)
+    h2 = q(_ref(h1, w[2], w[3], bn[2:4], dt))
+    ref = F.conv2d(h2, q(wc)[:, :, None, None]) + bc[None, :, None, None]
+    xd = x.to(dt).to(DEV).contiguous()
+    wd = [w[0].to(DEV), w[1].to(dt).to(DEV), w[2].to(DEV), w[3].to(dt).to(DEV)]
+    bnd = [(s_.to(DEV), h_.to(DEV)) for s_, h_ in bn]
+    tmp = torch.empty(N, H, W, 128, dtype=dt, device=DEV)
+    lg = torch.full((N, H, W, ldl), float("nan"), dtype=dt, device=DEV)
+    wcd, bcd = wc.to(dt).to(DEV).contiguous(), bc.to(DEV).contiguous()
+    _lib.call("fscnn_block_cls_fwd", _lib.ptr(xd), _lib.dtype_code(dt), N, H, W,
+              _lib.ptr(wd[0]), _lib.ptr(bnd[0][0]), _lib.ptr(bnd[0][1]), _lib.ptr(wd[1]),
+              _lib.ptr(bnd[1][0]), _lib.ptr(bnd[1][1]), _lib.ptr(wd[2]), _lib.ptr(bnd[2][0]),
+              _lib.ptr(bnd[2][1]), _lib.ptr(wd[3]), _lib.ptr(bnd[3][0]), _lib.ptr(bnd[3][1]),
+              _lib.ptr(wcd), _lib.ptr(bcd), ncls, _lib.ptr(tmp), _lib.ptr(lg), ldl,
+              _lib.stream_ptr())
+    torch.cuda.synchronize()
+    got = lg[..., :ncls].float().cpu().permute(0, 3, 1, 2)
+    if ldl > ncls:
+        assert torch.isnan(lg[..., ncls:].float()).all()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    tol = 2e-5 * scale if dt == torch.float32 else 2 ** -6 * scale
+    assert err <= tol, (err, tol, scale)
+
 def test_dsconv_rejects_other_widths():
     x = torch.zeros(1, 4, 4, 64, device=DEV)
     w = torch.zeros(128 * 128, device=DEV)
