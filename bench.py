@@ -12,8 +12,9 @@ overlapped with the staged backward; weak scaling (8 images per GPU).
 
     python bench.py [--gpus N --steps K --warmup W]
 
-Rank 0 prints ONE JSON line.  Extra objects: roofline of the dominant kernel family (HIP events
-on its launch stream over the timed region, algorithmic bytes per SURVEY.md §8(d)),
+Rank 0 prints ONE JSON line.  Extra objects: roofline of the dominant kernel family (kernel time
+from HIP events bound to each of its dispatches, hipExtLaunchKernelGGL, over the last tenth of the
+timed region; algorithmic bytes per SURVEY.md §8(d)),
 cpu_baseline (the oracle restatement timed on this host's cores on a bounded sample), and the
 forward-only fp32 inference rate (cfg2) for the north-star forward target.
 """
@@ -101,7 +102,9 @@ def cpu_model():
     return "unknown"
 
 
-def prof(lib, kind, fn, max_launches):
+def prof(lib, kind, fn, max_launches, per_launch=False):
+    """Kernel time (ms), launches, algorithmic bytes and flops of one kernel family over fn();
+    per_launch: also [(layer, us, bytes, flops)] in issue order."""
     import torch
     from fast_scnn_pytorch_amd import _lib
     _lib.check(lib.fscnn_prof_begin(kind, max_launches), "fscnn_prof_begin")
@@ -110,7 +113,27 @@ def prof(lib, kind, fn, max_launches):
     ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
     _lib.check(lib.fscnn_prof_end(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b),
                                   ctypes.byref(f)), "fscnn_prof_end")
-    return ms.value, n.value, b.value, f.value
+    if not per_launch:
+        return ms.value, n.value, b.value, f.value
+    recs = []
+    for i in range(n.value):
+        k, t, by, fl, tag = (ctypes.c_int(), ctypes.c_float(), ctypes.c_double(), ctypes.c_double(),
+                             ctypes.c_char_p())
+        _lib.check(lib.fscnn_prof_launch(i, ctypes.byref(k), ctypes.byref(t), ctypes.byref(by),
+                                         ctypes.byref(fl), ctypes.byref(tag)), "fscnn_prof_launch")
+        recs.append((tag.value.decode(), t.value * 1e3, by.value, fl.value))
+    return ms.value, n.value, b.value, f.value, recs
+
+
+def family_report(recs, peak_gbs):
+    """Per-family HBM fraction from kernel time, and each launch's layer / us / fraction."""
+    us = sum(r[1] for r in recs)
+    by = sum(r[2] for r in recs)
+    gbs = by / (us * 1e-6) / 1e9 if us > 0 else 0.0
+    return {"launches": len(recs), "us": round(us, 1), "GBps": round(gbs, 1),
+            "hbm_frac": round(gbs / peak_gbs, 4),
+            "layers": [[r[0], round(r[1], 1), round(r[2] / (r[1] * 1e-6) / 1e9 / peak_gbs, 3)
+                        if r[1] > 0 else 0.0] for r in recs]}
 
 
 def cpu_baseline(args):
@@ -345,10 +368,10 @@ def main():
         kind = max(PROF_KINDS, key=lambda k: census[PROF_KINDS[k]])
     barrier()
 
-    # ---- timed region: K steps; HIP events bracket the dominant family's launches in the last
-    # tenth of the timed steps (each timing event costs its stream ~7 us of idle time on MI355X:
-    # ~0.7 ms per profiled step for the 52-launch gemm_nt family, so profiling a quarter of the
-    # steps inflated ms_per_step by ~0.12 ms; the events are created before the region)
+    # ---- timed region: K steps; the dominant family's dispatches in the last tenth of the timed
+    # steps carry kernel-bound HIP events (hipExtLaunchKernelGGL: each event pair holds its
+    # dispatch's own start / end timestamps, the kernel time rocprofv3 reports; no marker
+    # packets on the stream); the events are created before the region
     nprof = max(1, args.steps // 10)
     _lib.check(lib.fscnn_prof_begin(kind, 512 * nprof), "fscnn_prof_begin")
     ms, n, b, f = (ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double())
@@ -396,6 +419,12 @@ def main():
             mfma_util[pname] = {"launches": pn, "ms": round(pms, 4), "tflops": round(tfs, 2),
                                 "peak_tflops": MFMA_PEAK_TFS[args.dtype],
                                 "frac": round(tfs / MFMA_PEAK_TFS[args.dtype], 4)}
+    # the train step's depthwise families (forward, input gradient, weight gradient) from kernel
+    # time, each launch named by its layer (north_star's depthwise >= 60 % of HBM target)
+    depthwise = {}
+    for pk, pname in ((2, "dw_fwd"), (3, "dw_dgrad"), (4, "dw_wgrad")):
+        res = prof(lib, pk, step, 4096, per_launch=True)
+        depthwise[pname] = family_report(res[4], HBM_PEAK_GBS)
     barrier()
 
     value = world * B * args.steps / elapsed
@@ -415,8 +444,9 @@ def main():
     roof.update({"kernel": kname, "launches": n.value, "avg_launch_us": round(avg_ms * 1e3, 2),
                  "algo_bytes_per_launch": round(bytes_per_launch),
                  "algo_flops_per_launch": round(flops_per_launch), "traffic": None})
-    roof["timing"] = ("HIP events around each launch on its own stream over the last tenth of "
-                      "the timed steps (each event pair adds its stream's ~7 us event latency)")
+    roof["timing"] = ("kernel time: HIP events bound to each dispatch of the family "
+                      "(hipExtLaunchKernelGGL start / stop timestamps) over the last tenth of "
+                      "the timed steps")
     # HBM traffic per launch from the PMC counters of a committed profiling run (rocprofv3 --pmc
     # cannot run inside this process); labelled with its file and round
     pmc = os.path.join(ROOT, "profiles", "pmc_%s_%s.json" % (kname, args.dtype))
@@ -452,8 +482,10 @@ def main():
                                  "max": round(step_ms[-1], 3), "n": len(step_ms),
                                  "timing": "HIP events per step boundary on the caller's stream, "
                                            "%d steps after the timed region (rank 0)" % len(step_ms)},
-        "mfma_utilisation": dict(mfma_util, note="1x1-conv GEMM families, HIP-event time over one "
+        "mfma_utilisation": dict(mfma_util, note="1x1-conv GEMM families, kernel time over one "
                                  "profiled step each; algorithmic flops 2*M*N*K per launch"),
+        "depthwise_train": dict(depthwise, note="cfg3 train step, kernel time over one profiled "
+                                "step per family; layers: [module, us, HBM fraction]"),
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (portable counter-based generator; random-init weights, default law)",
         "config": {"workload": ("cfg3 train step: fwd + CE(ignore -1) + bwd + fused SGD" + (" (unfused CE)" if args.unfused_loss else " (fused low-res upsample+CE head)")),
@@ -478,9 +510,9 @@ def main():
                                            for b, e in model.native().stage_ranges]
     if census:
         result["kernel_ms_per_step_census"] = census
-        result["census_note"] = ("HIP-event kernel time per family over one profiled step each; "
-                                 "the families overlap on two streams and every event idles its "
-                                 "stream ~7 us, so the sum is not a breakdown of ms_per_step")
+        result["census_note"] = ("kernel time per family over one profiled step each (events "
+                                 "bound to the dispatches); the families overlap on two streams, "
+                                 "so the sum is not a breakdown of ms_per_step")
 
     # forward-only inference (rank 0, N=1 only): cfg2 fp32 (north-star forward target), cfg1
     # (demo.py: 1 x 3 x 768 x 768, latency) and cfg5 (TuSimple 32 x 3 x 480 x 640, C=2)
@@ -500,14 +532,23 @@ def main():
             return (time.perf_counter() - t1) / nrep
 
         fe = fwd_rate(model, x32, max(5, args.steps // 2))
+        # the fused inference blocks' matrix work (algorithmic flops of expand / depthwise /
+        # project, conv0 / pointwise, dw / pw) per kernel time, against the fp32 matrix spec and
+        # against the ceiling of the six-product split-bf16 form they run (2.5 PF / 6)
+        fused = {}
         with torch.no_grad():
-            fms, fn, fb, ff = prof(lib, 2, lambda: model(x32), 256)
-        dw_gbs = fb / max(fn, 1) / (fms / max(fn, 1) * 1e-3) / 1e9 if fms > 0 else 0
+            for pk, pname in ((16, "ir_block"), (18, "dsconv"), (17, "ltd_stem")):
+                fms, fn, fb, ff = prof(lib, pk, lambda: model(x32), 256)
+                if fms > 0:
+                    tfs = ff / (fms * 1e-3) / 1e12
+                    fused[pname] = {"launches": fn, "us": round(fms * 1e3, 1),
+                                    "tflops": round(tfs, 1),
+                                    "frac_fp32_matrix": round(tfs / MFMA_PEAK_TFS["fp32"], 3),
+                                    "frac_split_bf16": round(tfs / (MFMA_PEAK_TFS["bf16"] / 6), 3)}
         result["forward_fp32"] = {"value": round(B / fe, 2), "unit": "images/s",
                                   "ms_per_batch": round(1e3 * fe, 3),
                                   "config": "cfg2 eval fp32 %dx3x%dx%d" % (B, H, W),
-                                  "dw_fwd_GBps": round(dw_gbs, 1),
-                                  "dw_fwd_hbm_frac": round(dw_gbs / HBM_PEAK_GBS, 4)}
+                                  "fused_blocks_mfma": fused}
         x1 = torch.from_numpy(portable_init.input_tensor(1, (1, 3, 768, 768))).to(dev)
         f1 = fwd_rate(model, x1, 20)
         result["forward_cfg1"] = {"value": round(1 / f1, 2), "unit": "images/s",

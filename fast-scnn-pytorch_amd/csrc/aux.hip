@@ -78,8 +78,8 @@ int im2col3(const Im2ColArgs& a, int dtype, hipStream_t st) {
     return E_INVALID;
   }
   const unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) im2col3_kernel<uint32_t><<<grid, 256, 0, st>>>(a);
-  else im2col3_kernel<uint16_t><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(im2col3_kernel<uint32_t>, grid, 256, 0, st, a);
+  else prof_launch(im2col3_kernel<uint16_t>, grid, 256, 0, st, a);
   return check_launch("im2col3");
 }
 
@@ -90,9 +90,9 @@ int col2im3(const Col2ImArgs& a, int dtype, hipStream_t st) {
     return E_INVALID;
   }
   const unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) col2im3_kernel<float><<<grid, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) col2im3_kernel<f16><<<grid, 256, 0, st>>>(a);
-  else col2im3_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(col2im3_kernel<float>, grid, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(col2im3_kernel<f16>, grid, 256, 0, st, a);
+  else prof_launch(col2im3_kernel<bf16>, grid, 256, 0, st, a);
   return check_launch("col2im3");
 }
 

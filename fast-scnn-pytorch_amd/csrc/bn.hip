@@ -34,7 +34,7 @@ int bn_fold(const FoldTable& t, hipStream_t st) {
     set_error("bn_fold: bad table size %d", t.n);
     return E_INVALID;
   }
-  bn_fold_kernel<<<t.n, 256, 0, st>>>(t);
+  prof_launch(bn_fold_kernel, t.n, 256, 0, st, t);
   return check_launch("bn_fold");
 }
 
@@ -169,12 +169,12 @@ int bn_finalize(const BnFinalizeArgs& a, hipStream_t st) {
   if (a.P > BN_Q) {
     Q = BN_Q;
     if (a.counters) {
-      bn_stats_fold_fin_kernel<<<dim3(cdiv(a.C, 64), Q), blk, 0, st>>>(a, Q, a.counters);
+      prof_launch(bn_stats_fold_fin_kernel, dim3(cdiv(a.C, 64), Q), blk, 0, st, a, Q, a.counters);
       return check_launch("bn_finalize");
     }
-    bn_stats_fold_kernel<<<dim3(cdiv(a.C, 64), Q), blk, 0, st>>>(a.part, a.P, a.C, Q);
+    prof_launch(bn_stats_fold_kernel, dim3(cdiv(a.C, 64), Q), blk, 0, st, a.part, a.P, a.C, Q);
   }
-  bn_finalize_kernel<<<cdiv(a.C, 64), blk, 0, st>>>(a, Q);
+  prof_launch(bn_finalize_kernel, cdiv(a.C, 64), blk, 0, st, a, Q);
   return check_launch("bn_finalize");
 }
 
@@ -220,9 +220,9 @@ int bn_apply(const BnApplyArgs& a, int dtype, hipStream_t st) {
                    (2 + (a.z2 ? 1 : 0) + (a.res ? 1 : 0)),
                0.0);
   unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) bn_apply_kernel<float><<<grid, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) bn_apply_kernel<f16><<<grid, 256, 0, st>>>(a);
-  else bn_apply_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(bn_apply_kernel<float>, grid, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(bn_apply_kernel<f16>, grid, 256, 0, st, a);
+  else prof_launch(bn_apply_kernel<bf16>, grid, 256, 0, st, a);
   return check_launch("bn_apply");
 }
 
@@ -355,12 +355,12 @@ int bn_bwd_reduce(const BnBwdArgs& a, int dtype, hipStream_t st) {
       set_error("bn_bwd_reduce: a paired BN needs the mask mode and its own records / statistics");
       return E_INVALID;
     }
-    if (dtype == DT_F32) bn_bwd_reduce_kernel<float, 1, true><<<grid, block, shm, st>>>(b);
-    else if (dtype == DT_F16) bn_bwd_reduce_kernel<f16, 1, true><<<grid, block, shm, st>>>(b);
-    else bn_bwd_reduce_kernel<bf16, 1, true><<<grid, block, shm, st>>>(b);
+    if (dtype == DT_F32) prof_launch(bn_bwd_reduce_kernel<float, 1, true>, grid, block, shm, st, b);
+    else if (dtype == DT_F16) prof_launch(bn_bwd_reduce_kernel<f16, 1, true>, grid, block, shm, st, b);
+    else prof_launch(bn_bwd_reduce_kernel<bf16, 1, true>, grid, block, shm, st, b);
     return check_launch("bn_bwd_reduce");
   }
-#define BN_RED(T, M) bn_bwd_reduce_kernel<T, M><<<grid, block, shm, st>>>(b)
+#define BN_RED(T, M) prof_launch(bn_bwd_reduce_kernel<T, M>, grid, block, shm, st, b)
   if (dtype == DT_F32) {
     if (mode == 0) BN_RED(float, 0); else if (mode == 1) BN_RED(float, 1); else BN_RED(float, 2);
   } else if (dtype == DT_F16) {
@@ -477,13 +477,13 @@ int bn_bwd_finalize(float* part, int P, int C, double count, float* dgamma, floa
   if (P > BN_Q) {
     Q = BN_Q;
     if (counters) {
-      bn_bwd_fold_fin_kernel<<<dim3(cdiv(C, 64), Q), blk, 0, st>>>(part, P, C, Q, count, dgamma,
+      prof_launch(bn_bwd_fold_fin_kernel, dim3(cdiv(C, 64), Q), blk, 0, st, part, P, C, Q, count, dgamma,
                                                                   dbeta, coef, counters, tab);
       return check_launch("bn_bwd_finalize");
     }
-    bn_bwd_fold_kernel<<<dim3(cdiv(C, 64), Q), blk, 0, st>>>(part, P, C, Q);
+    prof_launch(bn_bwd_fold_kernel, dim3(cdiv(C, 64), Q), blk, 0, st, part, P, C, Q);
   }
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), blk, 0, st>>>(part, Q, C, count, dgamma, dbeta, coef, tab);
+  prof_launch(bn_bwd_finalize_kernel, cdiv(C, 64), blk, 0, st, part, Q, C, count, dgamma, dbeta, coef, tab);
   return check_launch("bn_bwd_finalize");
 }
 
@@ -589,15 +589,15 @@ template <typename T, int U>
 static void bn_bwd_apply_launch_u(const BnBwdArgs& a, unsigned P, hipStream_t st) {
   const int mode = a.relu_z ? 2 : (a.mask ? 1 : 0);
   const unsigned grid = (unsigned)(((long long)P * (a.C / VecW<T>::V) + 255) / 256);
-  if (a.z2) bn_bwd_apply_kernel<T, 1, true, true, (U > 2 ? 2 : U)><<<grid, 256, 0, st>>>(a, P);
+  if (a.z2) prof_launch(bn_bwd_apply_kernel<T, 1, true, true, (U > 2 ? 2 : U)>, grid, 256, 0, st, a, P);
   else if (a.coef) {
-    if (mode == 0) bn_bwd_apply_kernel<T, 0, true, false, U><<<grid, 256, 0, st>>>(a, P);
-    else if (mode == 1) bn_bwd_apply_kernel<T, 1, true, false, U><<<grid, 256, 0, st>>>(a, P);
-    else bn_bwd_apply_kernel<T, 2, true, false, U><<<grid, 256, 0, st>>>(a, P);
+    if (mode == 0) prof_launch(bn_bwd_apply_kernel<T, 0, true, false, U>, grid, 256, 0, st, a, P);
+    else if (mode == 1) prof_launch(bn_bwd_apply_kernel<T, 1, true, false, U>, grid, 256, 0, st, a, P);
+    else prof_launch(bn_bwd_apply_kernel<T, 2, true, false, U>, grid, 256, 0, st, a, P);
   } else {
-    if (mode == 0) bn_bwd_apply_kernel<T, 0, false, false, U><<<grid, 256, 0, st>>>(a, P);
-    else if (mode == 1) bn_bwd_apply_kernel<T, 1, false, false, U><<<grid, 256, 0, st>>>(a, P);
-    else bn_bwd_apply_kernel<T, 2, false, false, U><<<grid, 256, 0, st>>>(a, P);
+    if (mode == 0) prof_launch(bn_bwd_apply_kernel<T, 0, false, false, U>, grid, 256, 0, st, a, P);
+    else if (mode == 1) prof_launch(bn_bwd_apply_kernel<T, 1, false, false, U>, grid, 256, 0, st, a, P);
+    else prof_launch(bn_bwd_apply_kernel<T, 2, false, false, U>, grid, 256, 0, st, a, P);
   }
 }
 

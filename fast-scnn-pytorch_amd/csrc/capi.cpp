@@ -43,16 +43,34 @@ struct ProfState {
   double bytes = 0, flops = 0;
   long long launches = 0;
   bool overflow = false;
+  bool armed = false, taken = false;  // the open scope's events (prof_start / prof_take_ext)
+  hipStream_t arm_st = nullptr;
 } g_prof;
 }  // namespace
 
+// A scope arms its event pair for the first prof_launch inside it (kernel-bound events); a scope
+// whose launch does not take them (none issued) falls back to marker events around the scope.
 void prof_start(hipStream_t st) {
   if (g_prof.used + 2 > g_prof.ev.size()) { g_prof.overflow = true; return; }
-  (void)hipEventRecord(g_prof.ev[g_prof.used], st);
+  g_prof.armed = true;
+  g_prof.taken = false;
+  g_prof.arm_st = st;
+}
+bool prof_take_ext(hipEvent_t& e0, hipEvent_t& e1) {
+  if (!g_prof.armed || g_prof.taken) return false;
+  e0 = g_prof.ev[g_prof.used];
+  e1 = g_prof.ev[g_prof.used + 1];
+  g_prof.taken = true;
+  return true;
 }
 void prof_stop(hipStream_t st, int kind, double bytes, double flops) {
   if (g_prof.used + 2 > g_prof.ev.size()) return;
-  (void)hipEventRecord(g_prof.ev[g_prof.used + 1], st);
+  const bool taken = g_prof.armed && g_prof.taken;
+  g_prof.armed = false;
+  if (!taken) {  // no kernel launched in the scope: a zero-length marker pair
+    (void)hipEventRecord(g_prof.ev[g_prof.used], st);
+    (void)hipEventRecord(g_prof.ev[g_prof.used + 1], st);
+  }
   g_prof.used += 2;
   g_prof.kind.push_back(kind);
   g_prof.tag.emplace_back(g_prof_tag ? g_prof_tag : "");

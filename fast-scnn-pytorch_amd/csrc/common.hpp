@@ -7,6 +7,7 @@
 // free of the E[x^2]-E[x]^2 cancellation.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
@@ -480,6 +481,21 @@ struct ProfScope {
     if (on) prof_stop(st, kind, bytes, flops);
   }
 };
+
+// Every kernel launch goes through prof_launch.  Inside a recording ProfScope the scope's first
+// launch is issued by hipExtLaunchKernelGGL with the scope's event pair bound to the dispatch
+// itself: the events carry the kernel's own start / end timestamps (what rocprofv3's kernel trace
+// reads), not marker packets around it (each of which idles the stream ~7 us).  Otherwise it is a
+// plain launch.
+bool prof_take_ext(hipEvent_t& e0, hipEvent_t& e1);
+template <typename F, typename... A>
+inline void prof_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, A... args) {
+  hipEvent_t e0, e1;
+  if (prof_take_ext(e0, e1))
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, e0, e1, 0u, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+}
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 

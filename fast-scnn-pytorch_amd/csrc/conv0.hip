@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     }
     stamp(a.stamps, 3);
     if (a.part == nullptr) continue;
-    // ---- per-channel (mean, M2) of the row's npx pixels, from the fp32 registers -------------
+    // ---- per-channel (mean, M2) of the row's npx pixels: the values as stored (rounded to TO) --
     float sum[2] = {0.f, 0.f};
 #pragma unroll
     for (int gi = 0; gi < 4; ++gi)
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       for (int q = 0; q < 4; ++q) {
         const bool ok = wave * 64 + gi * 16 + 4 * lq + q < npx;
 #pragma unroll
-        for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? acc[gi][jt][q] : 0.f;
+        for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? round_as<TO>(acc[gi][jt][q]) : 0.f;
       }
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
         const bool ok = wave * 64 + gi * 16 + 4 * lq + q < npx;
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
-          const float d = acc[gi][jt][q] - mean[jt];
+          const float d = round_as<TO>(acc[gi][jt][q]) - mean[jt];
           m2[jt] += ok ? d * d : 0.f;
         }
       }
@@ -318,17 +318,17 @@ int conv0_fwd(const Conv0Args& a, int y_dtype, hipStream_t st) {
                (a.x_bf16 ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W + (y_dtype == DT_F32 ? 4.0 : 2.0) * px * 32,
                2.0 * 27 * 32 * px);
   if (y_dtype == DT_F32) {
-    if (a.x_bf16 == 2) conv0_fwd_kernel<float, 2><<<grid, 256, 0, st>>>(as);
-    else if (a.x_bf16) conv0_fwd_kernel<float, 1><<<grid, 256, 0, st>>>(as);
-    else conv0_fwd_kernel<float, 0><<<grid, 256, 0, st>>>(as);
+    if (a.x_bf16 == 2) prof_launch(conv0_fwd_kernel<float, 2>, grid, 256, 0, st, as);
+    else if (a.x_bf16) prof_launch(conv0_fwd_kernel<float, 1>, grid, 256, 0, st, as);
+    else prof_launch(conv0_fwd_kernel<float, 0>, grid, 256, 0, st, as);
   } else if (y_dtype == DT_F16) {
-    if (a.x_bf16 == 2) conv0_fwd_kernel<f16, 2><<<grid, 256, 0, st>>>(as);
-    else if (a.x_bf16) conv0_fwd_kernel<f16, 1><<<grid, 256, 0, st>>>(as);
-    else conv0_fwd_kernel<f16, 0><<<grid, 256, 0, st>>>(as);
+    if (a.x_bf16 == 2) prof_launch(conv0_fwd_kernel<f16, 2>, grid, 256, 0, st, as);
+    else if (a.x_bf16) prof_launch(conv0_fwd_kernel<f16, 1>, grid, 256, 0, st, as);
+    else prof_launch(conv0_fwd_kernel<f16, 0>, grid, 256, 0, st, as);
   } else {
-    if (a.x_bf16 == 2) conv0_fwd_kernel<bf16, 2><<<grid, 256, 0, st>>>(as);
-    else if (a.x_bf16) conv0_fwd_kernel<bf16, 1><<<grid, 256, 0, st>>>(as);
-    else conv0_fwd_kernel<bf16, 0><<<grid, 256, 0, st>>>(as);
+    if (a.x_bf16 == 2) prof_launch(conv0_fwd_kernel<bf16, 2>, grid, 256, 0, st, as);
+    else if (a.x_bf16) prof_launch(conv0_fwd_kernel<bf16, 1>, grid, 256, 0, st, as);
+    else prof_launch(conv0_fwd_kernel<bf16, 0>, grid, 256, 0, st, as);
   }
   return check_launch("conv0_fwd");
 }
@@ -548,13 +548,13 @@ int conv0_wgrad(const Conv0WgradArgs& a, int dz_dtype, hipStream_t st) {
 #define CW_LAUNCH(T)                                                                  \
   do {                                                                                \
     if (dx) {                                                                         \
-      if (a.x_bf16 == 2) conv0_wgrad_kernel<T, 2, true><<<P, 256, 0, st>>>(a);        \
-      else if (a.x_bf16) conv0_wgrad_kernel<T, 1, true><<<P, 256, 0, st>>>(a);        \
-      else conv0_wgrad_kernel<T, 0, true><<<P, 256, 0, st>>>(a);                      \
+      if (a.x_bf16 == 2) prof_launch(conv0_wgrad_kernel<T, 2, true>, P, 256, 0, st, a);        \
+      else if (a.x_bf16) prof_launch(conv0_wgrad_kernel<T, 1, true>, P, 256, 0, st, a);        \
+      else prof_launch(conv0_wgrad_kernel<T, 0, true>, P, 256, 0, st, a);                      \
     } else {                                                                          \
-      if (a.x_bf16 == 2) conv0_wgrad_kernel<T, 2><<<P, 256, 0, st>>>(a);              \
-      else if (a.x_bf16) conv0_wgrad_kernel<T, 1><<<P, 256, 0, st>>>(a);              \
-      else conv0_wgrad_kernel<T, 0><<<P, 256, 0, st>>>(a);                            \
+      if (a.x_bf16 == 2) prof_launch(conv0_wgrad_kernel<T, 2>, P, 256, 0, st, a);              \
+      else if (a.x_bf16) prof_launch(conv0_wgrad_kernel<T, 1>, P, 256, 0, st, a);              \
+      else prof_launch(conv0_wgrad_kernel<T, 0>, P, 256, 0, st, a);                            \
     }                                                                                 \
   } while (0)
   if (dz_dtype == DT_F32) CW_LAUNCH(float);
@@ -629,9 +629,9 @@ int conv0_dgrad(const Conv0DgradArgs& a, int dz_dtype, hipStream_t st) {
   const int blocks = cdiv((long long)a.N * a.H * a.W, 256);
 #define C0D_LAUNCH(T)                                                                          \
   do {                                                                                         \
-    if (a.dx_dtype == DT_BF16) conv0_dgrad_kernel<T, bf16><<<blocks, 256, 0, st>>>(a);         \
-    else if (a.dx_dtype == DT_F16) conv0_dgrad_kernel<T, f16><<<blocks, 256, 0, st>>>(a);      \
-    else conv0_dgrad_kernel<T, float><<<blocks, 256, 0, st>>>(a);                              \
+    if (a.dx_dtype == DT_BF16) prof_launch(conv0_dgrad_kernel<T, bf16>, blocks, 256, 0, st, a);         \
+    else if (a.dx_dtype == DT_F16) prof_launch(conv0_dgrad_kernel<T, f16>, blocks, 256, 0, st, a);      \
+    else prof_launch(conv0_dgrad_kernel<T, float>, blocks, 256, 0, st, a);                              \
   } while (0)
   if (dz_dtype == DT_F32) C0D_LAUNCH(float);
   else if (dz_dtype == DT_F16) C0D_LAUNCH(f16);
@@ -997,7 +997,7 @@ int ltd_c0_bwd(const LtdC0BwdArgs& a, int dtype, hipStream_t st) {
                  2.0 * ((double)a.N * a.Ho * a.Wo * 32 + px * 32) +
                      (a.x_dtype ? 2.0 : 4.0) * a.N * 3.0 * a.XH * a.XW + 36.0 * 32,
                  18.0 * (double)a.N * a.Ho * a.Wo * 32 + 4.0 * 27 * 32 * px);
-#define LC_LAUNCH(T, XB) ltd_c0_bwd_kernel<T, XB><<<P, 256, 0, st>>>(a)
+#define LC_LAUNCH(T, XB) prof_launch(ltd_c0_bwd_kernel<T, XB>, P, 256, 0, st, a)
 #define LC_LAUNCH_X(T)                            \
   do {                                            \
     if (a.x_dtype == 2) LC_LAUNCH(T, 2);          \
@@ -1027,7 +1027,7 @@ __global__ void conv0_wgrad_combine_kernel(const float* s, const float* tab, con
 
 int conv0_wgrad_combine(const float* sums, const float* tab, const float* mean, float* dw,
                         hipStream_t st) {
-  conv0_wgrad_combine_kernel<<<cdiv(864, 256), 256, 0, st>>>(sums, tab, mean, dw);
+  prof_launch(conv0_wgrad_combine_kernel, cdiv(864, 256), 256, 0, st, sums, tab, mean, dw);
   return check_launch("conv0_wgrad_combine");
 }
 

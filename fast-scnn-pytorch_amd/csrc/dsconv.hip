@@ -670,6 +670,11 @@ static bool ds_up_fits(const DsArgs& a) {
 }
 
 bool ds_ok(const DsArgs& a) {
+  // upsample mode (Hi > 0) is the FFM form only: its low-res input is read through the upsample
+  // ring, which the plain strip kernel (no r / xh) does not have
+  if (a.Hi > 0 && !a.r && !a.xh) return false;
+  // the kernels read / write these with 16-B vector accesses
+  if (((uintptr_t)a.wp & 15) || ((uintptr_t)a.wc & 15) || ((uintptr_t)a.logits & 15)) return false;
   if (a.xh && (a.r || a.wc || a.Hi <= 0 || !a.wh || !a.sch || !a.shh || a.ldxh < DS_CH || a.ldxh % 8 ||
                ((uintptr_t)a.xh & 15) || ((uintptr_t)a.wh & 15) || 4LL * a.H * a.W * a.ldxh >= (long long)BUF_OOB))
     return false;
@@ -712,14 +717,15 @@ int ds_fwd(const DsArgs& a, int dtype, hipStream_t st) {
   ProfScope ps(PK_DSCONV, st,
                E * a.N * ((a.Hi > 0 ? (double)a.Hi * a.Wi : (double)a.H * a.W) * DS_C +
                           (double)a.H * a.W * (DS_CO + (a.r ? DS_CO : 0) + (a.xh ? DS_CH : 0))),
-               2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO + (a.xh ? (double)DS_CH * DS_CO : 0.0)));
+               2.0 * a.N * a.H * a.W * (9.0 * DS_C + (double)DS_C * DS_CO + (a.xh ? (double)DS_CH * DS_CO : 0.0) +
+                                        (a.wc ? (double)DS_CO * a.ncls : 0.0)));
 #define DSK(T)                                                                \
   do {                                                                        \
-    if (a.wc) dsconv_fwd_kernel<T, false, false, true><<<g, 256, 0, st>>>(as);    \
-    else if (a.xh) dsconv_fwd_kernel<T, false, true, false, true><<<g, 256, 0, st>>>(as); \
-    else if (a.r && a.Hi > 0) dsconv_fwd_kernel<T, true, true><<<g, 256, 0, st>>>(as); \
-    else if (a.r) dsconv_fwd_kernel<T, true, false><<<g, 256, 0, st>>>(as);   \
-    else dsconv_fwd_kernel<T, false, false><<<g, 256, 0, st>>>(as);           \
+    if (a.wc) prof_launch(dsconv_fwd_kernel<T, false, false, true>, g, 256, 0, st, as);    \
+    else if (a.xh) prof_launch(dsconv_fwd_kernel<T, false, true, false, true>, g, 256, 0, st, as); \
+    else if (a.r && a.Hi > 0) prof_launch(dsconv_fwd_kernel<T, true, true>, g, 256, 0, st, as); \
+    else if (a.r) prof_launch(dsconv_fwd_kernel<T, true, false>, g, 256, 0, st, as);   \
+    else prof_launch(dsconv_fwd_kernel<T, false, false>, g, 256, 0, st, as);           \
   } while (0)
   if (dtype == DT_F32) DSK(float);
   else if (dtype == DT_F16) DSK(f16);

@@ -289,7 +289,8 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
     return;
   }
   if (a.part == nullptr) return;
-  // ---- per-channel (mean, M2, count) over the tile (train-mode BN statistics) ---------------
+  // ---- per-channel (mean, M2, count) over the tile (train-mode BN statistics of the values as
+  // stored: the BN normalises the rounded z, as the reference's autocast BN does) --------------
   const int trows = min(G::TH, a.Ho - th0), tcols = min(G::TW, a.Wo - tw0);
   const float cnt = (float)(trows * tcols);
   float mean[4];
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
 #pragma unroll
     for (int r = 0; r < G::HS; ++r)
 #pragma unroll
-      for (int p = 0; p < G::WS; ++p) sum += (r < nrow && p < ncol) ? acc[r][p][j] : 0.f;
+      for (int p = 0; p < G::WS; ++p) sum += (r < nrow && p < ncol) ? round_as<T>(acc[r][p][j]) : 0.f;
     s_red[(grp * QB + q) * 4 + j] = sum;
   }
   __syncthreads();
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
     for (int r = 0; r < G::HS; ++r)
 #pragma unroll
       for (int p = 0; p < G::WS; ++p) {
-        const float d = acc[r][p][j] - mean[j];
+        const float d = round_as<T>(acc[r][p][j]) - mean[j];
         m2 += (r < nrow && p < ncol) ? d * d : 0.f;
       }
     s_red[(grp * QB + q) * 4 + j] = m2;
@@ -375,17 +376,17 @@ int dw_parts(int N, int Ho, int Wo, int C, int dtype, int stride) {
 template <typename T, bool FLIP, bool IT, bool BR>
 static void dw_launch_fwd_t(const DwArgs& a, dim3 grid, int nthr, int cbv, hipStream_t st) {
   if constexpr (BR) {  // stride-1 dgrad with BN-backward partials
-    if (a.tail_ink) dw_fwd_kernel<T, 1, true, false, true, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
-    else dw_fwd_kernel<T, 1, true, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
+    if (a.tail_ink) prof_launch(dw_fwd_kernel<T, 1, true, false, true, true>, grid, nthr, dw_shm<T, 1>(cbv), st, a, cbv);
+    else prof_launch(dw_fwd_kernel<T, 1, true, false, true>, grid, nthr, dw_shm<T, 1>(cbv), st, a, cbv);
     return;
   }
   if (!FLIP && a.tail_ink) {  // train forward with the in-kernel BN finish
-    if (a.stride == 1) dw_fwd_kernel<T, 1, false, IT, false, true><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
-    else dw_fwd_kernel<T, 2, false, IT, false, true><<<grid, nthr, dw_shm<T, 2>(cbv), st>>>(a, cbv);
+    if (a.stride == 1) prof_launch(dw_fwd_kernel<T, 1, false, IT, false, true>, grid, nthr, dw_shm<T, 1>(cbv), st, a, cbv);
+    else prof_launch(dw_fwd_kernel<T, 2, false, IT, false, true>, grid, nthr, dw_shm<T, 2>(cbv), st, a, cbv);
     return;
   }
-  if (a.stride == 1) dw_fwd_kernel<T, 1, FLIP, IT><<<grid, nthr, dw_shm<T, 1>(cbv), st>>>(a, cbv);
-  else dw_fwd_kernel<T, 2, FLIP, IT><<<grid, nthr, dw_shm<T, 2>(cbv), st>>>(a, cbv);
+  if (a.stride == 1) prof_launch(dw_fwd_kernel<T, 1, FLIP, IT>, grid, nthr, dw_shm<T, 1>(cbv), st, a, cbv);
+  else prof_launch(dw_fwd_kernel<T, 2, FLIP, IT>, grid, nthr, dw_shm<T, 2>(cbv), st, a, cbv);
 }
 
 template <bool FLIP, bool IT, bool BR = false>
@@ -672,8 +673,8 @@ int dw_dgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
     if (fin) P = (int)(grid.y * grid.z);
 #define DWD2(T)                                                                 \
   do {                                                                          \
-    if (br) dw_dgrad_s2_kernel<T, true><<<grid, block, 0, st>>>(b, rpw);              \
-    else dw_dgrad_s2_kernel<T, false><<<grid, block, 0, st>>>(b, rpw);               \
+    if (br) prof_launch(dw_dgrad_s2_kernel<T, true>, grid, block, 0, st, b, rpw);              \
+    else prof_launch(dw_dgrad_s2_kernel<T, false>, grid, block, 0, st, b, rpw);               \
   } while (0)
     if (dtype == DT_F32) DWD2(float);
     else if (dtype == DT_F16) DWD2(f16);
@@ -827,8 +828,8 @@ int dw_wgrad(const DwBwdArgs& a, int dtype, hipStream_t st) {
   const int nthr = cbv * 32;
 #define DWW_LAUNCH(T, S)                                                                      \
   do {                                                                                        \
-    if (a.x_scale) dw_wgrad_kernel<T, S, true><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb); \
-    else dw_wgrad_kernel<T, S, false><<<grid, nthr, dw_shm<T, S>(cbv), st>>>(a, cbv, tpb);          \
+    if (a.x_scale) prof_launch(dw_wgrad_kernel<T, S, true>, grid, nthr, dw_shm<T, S>(cbv), st, a, cbv, tpb); \
+    else prof_launch(dw_wgrad_kernel<T, S, false>, grid, nthr, dw_shm<T, S>(cbv), st, a, cbv, tpb);          \
   } while (0)
   if (dtype == DT_F32) {
     if (a.stride == 1) DWW_LAUNCH(float, 1);

@@ -436,7 +436,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
   }
   if (a.part == nullptr) return;
 
-  // ---- train-mode BN statistics of the output tile (per column: mean, M2, count) ----------
+  // ---- train-mode BN statistics of the output tile as stored (per column: mean, M2, count) -
   const int valid_rows = min(G_BM, a.M - m0);
   float mean_c[NT];
 #pragma unroll
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
-        s += (m < a.M) ? acc[mt][nt][r] : 0.f;
+        s += (m < a.M) ? round_as<T>(acc[mt][nt][r]) : 0.f;
       }
     s += __shfl_xor(s, 16);
     s += __shfl_xor(s, 32);
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
-        float d = acc[mt][nt][r] - mean_c[nt];
+        float d = round_as<T>(acc[mt][nt][r]) - mean_c[nt];
         s += (m < a.M) ? d * d : 0.f;
       }
     s += __shfl_xor(s, 16);
@@ -517,11 +517,11 @@ int gemm_nt_parts(const GemmArgs& a, int dtype) {
 template <typename T, bool BT, bool BS, bool AT, bool X3, bool TL>
 static void launch_nt_tl(const GemmArgs& a, int nt, dim3 grid, size_t shm, hipStream_t st) {
   switch (nt) {
-    case 2: gemm_nt_kernel<T, 2, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
-    case 3: gemm_nt_kernel<T, 3, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
-    case 4: gemm_nt_kernel<T, 4, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
-    case 6: gemm_nt_kernel<T, 6, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
-    default: gemm_nt_kernel<T, 8, BT, BS, AT, X3, TL><<<grid, 256, shm, st>>>(a); break;
+    case 2: prof_launch(gemm_nt_kernel<T, 2, BT, BS, AT, X3, TL>, grid, 256, shm, st, a); break;
+    case 3: prof_launch(gemm_nt_kernel<T, 3, BT, BS, AT, X3, TL>, grid, 256, shm, st, a); break;
+    case 4: prof_launch(gemm_nt_kernel<T, 4, BT, BS, AT, X3, TL>, grid, 256, shm, st, a); break;
+    case 6: prof_launch(gemm_nt_kernel<T, 6, BT, BS, AT, X3, TL>, grid, 256, shm, st, a); break;
+    default: prof_launch(gemm_nt_kernel<T, 8, BT, BS, AT, X3, TL>, grid, 256, shm, st, a); break;
   }
 }
 
@@ -869,8 +869,8 @@ int gemm_tn(GemmTnArgs a, int splits, int dtype, hipStream_t st) {
   }
 #define TN_LAUNCH(T)                                        \
   do {                                                      \
-    if (xt) gemm_tn_kernel<T, true><<<grid, 256, 0, st>>>(a); \
-    else gemm_tn_kernel<T, false><<<grid, 256, 0, st>>>(a);   \
+    if (xt) prof_launch(gemm_tn_kernel<T, true>, grid, 256, 0, st, a); \
+    else prof_launch(gemm_tn_kernel<T, false>, grid, 256, 0, st, a);   \
   } while (0)
   if (dtype == DT_F32) TN_LAUNCH(float);
   else if (dtype == DT_F16) TN_LAUNCH(f16);
@@ -931,10 +931,10 @@ int reduce_slabs_ex(float* slab, int S, long long stride, long long count, float
   int S2 = S;
   if (S > RED_Q) {
     dim3 g1(cdiv(n, 256), RED_Q);
-    reduce_fold_kernel<<<g1, 256, 0, st>>>(slab, S, RED_Q, stride, n);
+    prof_launch(reduce_fold_kernel, g1, 256, 0, st, slab, S, RED_Q, stride, n);
     S2 = RED_Q;
   }
-  reduce_final_kernel<<<cdiv(n, 256), 256, 0, st>>>(slab, S2, stride, n, out, accumulate, C9);
+  prof_launch(reduce_final_kernel, cdiv(n, 256), 256, 0, st, slab, S2, stride, n, out, accumulate, C9);
   return check_launch("reduce_slabs");
 }
 
@@ -1018,8 +1018,8 @@ int reduce_slabs_multi(const RedTable& tin, hipStream_t st) {
     f.n++;
     f.blk0[f.n] = f.blocks;
   }
-  if (f.n) reduce_fold_multi_kernel<<<f.blocks, 256, 0, st>>>(f);
-  reduce_final_multi_kernel<<<t.blocks, 256, 0, st>>>(t);
+  if (f.n) prof_launch(reduce_fold_multi_kernel, f.blocks, 256, 0, st, f);
+  prof_launch(reduce_final_multi_kernel, t.blocks, 256, 0, st, t);
   return check_launch("reduce_slabs_multi");
 }
 
@@ -1058,9 +1058,9 @@ int colsum(const void* D, int M, int N, int ld, float* part, int dtype, hipStrea
   int P = colsum_parts(M);
   int rpb = cdiv(M, P);
   dim3 grid(cdiv(N, 64), P);
-  if (dtype == DT_F32) colsum_kernel<float><<<grid, 256, 0, st>>>((const float*)D, M, N, ld, rpb, part);
-  else if (dtype == DT_F16) colsum_kernel<f16><<<grid, 256, 0, st>>>((const f16*)D, M, N, ld, rpb, part);
-  else colsum_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)D, M, N, ld, rpb, part);
+  if (dtype == DT_F32) prof_launch(colsum_kernel<float>, grid, 256, 0, st, (const float*)D, M, N, ld, rpb, part);
+  else if (dtype == DT_F16) prof_launch(colsum_kernel<f16>, grid, 256, 0, st, (const f16*)D, M, N, ld, rpb, part);
+  else prof_launch(colsum_kernel<bf16>, grid, 256, 0, st, (const bf16*)D, M, N, ld, rpb, part);
   return check_launch("colsum");
 }
 

@@ -448,8 +448,8 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[mt][nt][r] * scv[r] + shv[r];
-            if constexpr (ST) {  // statistics of the unrounded value (gemm_nt's convention)
-              const float d = mok ? v - shf[r] : 0.f;
+            if constexpr (ST) {  // statistics of the value as stored (gemm_nt's convention)
+              const float d = mok ? round_as<T>(v) - shf[r] : 0.f;
               s1[nt][r] += d;
               s2[nt][r] += d * d;
             }
@@ -843,25 +843,25 @@ static void gs_launch_ks(const GemmArgs& a, int ks, dim3 grid, size_t lds, int b
   constexpr bool WIDE = SUMS && NT > 4;  // wide statistics tiles: K <= 2 k-steps only
   constexpr bool DEEP = sizeof(T) == 2 && NT <= 4 && !TAIL;
   switch (ks) {
-    case 1: gemm_stream_kernel<T, NT, 1, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
-    case 2: gemm_stream_kernel<T, NT, 2, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg); break;
+    case 1: prof_launch(gemm_stream_kernel<T, NT, 1, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg); break;
+    case 2: prof_launch(gemm_stream_kernel<T, NT, 2, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg); break;
     case 3:
-      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 3, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      if constexpr (!WIDE) prof_launch(gemm_stream_kernel<T, NT, 3, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
       break;
     case 4:
-      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 4, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      if constexpr (!WIDE) prof_launch(gemm_stream_kernel<T, NT, 4, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
       break;
     case 6:
-      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 6, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      if constexpr (!WIDE) prof_launch(gemm_stream_kernel<T, NT, 6, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
       break;
     case 8:
-      if constexpr (!WIDE) gemm_stream_kernel<T, NT, 8, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+      if constexpr (!WIDE) prof_launch(gemm_stream_kernel<T, NT, 8, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
       break;
     default:  // deep K: 16-bit, <= 4 column tiles, no scalar tail
       if constexpr (DEEP) {
-        if (ks == 12) gemm_stream_kernel<T, NT, 12, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
-        else if (ks == 16) gemm_stream_kernel<T, NT, 16, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
-        else gemm_stream_kernel<T, NT, 18, TAIL, AT, ST, BS><<<grid, 256, lds, st>>>(a, bpg);
+        if (ks == 12) prof_launch(gemm_stream_kernel<T, NT, 12, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
+        else if (ks == 16) prof_launch(gemm_stream_kernel<T, NT, 16, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
+        else prof_launch(gemm_stream_kernel<T, NT, 18, TAIL, AT, ST, BS>, grid, 256, lds, st, a, bpg);
       }
       break;
   }
@@ -921,7 +921,7 @@ static bool gs_x3_launch(const GemmArgs& a, hipStream_t st) {
   if (bpg > need) bpg = need;
   if (bpg < 1) bpg = 1;
   const dim3 grid((unsigned)(groups * bpg));
-#define X3(NT, KS, TL) gemm_stream_x3_kernel<NT, KS, TL><<<grid, 256, lds, st>>>(a, bpg)
+#define X3(NT, KS, TL) prof_launch(gemm_stream_x3_kernel<NT, KS, TL>, grid, 256, lds, st, a, bpg)
 #define X3K(NT, TL)                         \
   switch (ks) {                             \
     case 1: X3(NT, 1, TL); break;           \

@@ -655,7 +655,7 @@ int ce_pack_targets(const long long* t, long long n, int C, long long ignore_ind
   if (n == 0) return OK;
   ProfScope ps(PK_CE, st, 9.0 * (double)n, 0.0);
   const long long blocks = (n + 2047) / 2048;
-  ce_pack_targets_kernel<<<(unsigned)blocks, 256, 0, st>>>(t, n, C, ignore_index, out);
+  prof_launch(ce_pack_targets_kernel, (unsigned)blocks, 256, 0, st, t, n, C, ignore_index, out);
   return check_launch("ce_pack_targets");
 }
 
@@ -708,33 +708,33 @@ int ce_head(const CeHeadArgs& a, float* out2, int dtype, hipStream_t st) {
       CeHeadArgs as = a;
       as.stamps = stamp_region();
       if (a.C == 19) {
-        if (dtype == DT_F16) ce_head2_kernel<f16, 19><<<grid, HD_T, 0, st>>>(as);
-        else ce_head2_kernel<bf16, 19><<<grid, HD_T, 0, st>>>(as);
+        if (dtype == DT_F16) prof_launch(ce_head2_kernel<f16, 19>, grid, HD_T, 0, st, as);
+        else prof_launch(ce_head2_kernel<bf16, 19>, grid, HD_T, 0, st, as);
       } else {
-        if (dtype == DT_F16) ce_head2_kernel<f16, 2><<<grid, HD_T, 0, st>>>(as);
-        else ce_head2_kernel<bf16, 2><<<grid, HD_T, 0, st>>>(as);
+        if (dtype == DT_F16) prof_launch(ce_head2_kernel<f16, 2>, grid, HD_T, 0, st, as);
+        else prof_launch(ce_head2_kernel<bf16, 2>, grid, HD_T, 0, st, as);
       }
     } else if (a.C == 19) {
-      if (f32) ce_head_kernel<float, 19, true><<<grid, HD_T, 0, st>>>(a);
-      else if (dtype == DT_F16) ce_head_kernel<f16, 19, true><<<grid, HD_T, 0, st>>>(a);
-      else ce_head_kernel<bf16, 19, true><<<grid, HD_T, 0, st>>>(a);
+      if (f32) prof_launch(ce_head_kernel<float, 19, true>, grid, HD_T, 0, st, a);
+      else if (dtype == DT_F16) prof_launch(ce_head_kernel<f16, 19, true>, grid, HD_T, 0, st, a);
+      else prof_launch(ce_head_kernel<bf16, 19, true>, grid, HD_T, 0, st, a);
     } else if (a.C == 2) {
-      if (f32) ce_head_kernel<float, 2, true><<<grid, HD_T, 0, st>>>(a);
-      else if (dtype == DT_F16) ce_head_kernel<f16, 2, true><<<grid, HD_T, 0, st>>>(a);
-      else ce_head_kernel<bf16, 2, true><<<grid, HD_T, 0, st>>>(a);
+      if (f32) prof_launch(ce_head_kernel<float, 2, true>, grid, HD_T, 0, st, a);
+      else if (dtype == DT_F16) prof_launch(ce_head_kernel<f16, 2, true>, grid, HD_T, 0, st, a);
+      else prof_launch(ce_head_kernel<bf16, 2, true>, grid, HD_T, 0, st, a);
     } else if (a.C <= 8) {
-      if (f32) ce_head_kernel<float, 8, false><<<grid, HD_T, 0, st>>>(a);
-      else if (dtype == DT_F16) ce_head_kernel<f16, 8, false><<<grid, HD_T, 0, st>>>(a);
-      else ce_head_kernel<bf16, 8, false><<<grid, HD_T, 0, st>>>(a);
+      if (f32) prof_launch(ce_head_kernel<float, 8, false>, grid, HD_T, 0, st, a);
+      else if (dtype == DT_F16) prof_launch(ce_head_kernel<f16, 8, false>, grid, HD_T, 0, st, a);
+      else prof_launch(ce_head_kernel<bf16, 8, false>, grid, HD_T, 0, st, a);
     } else {
-      if (f32) ce_head_kernel<float, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
-      else if (dtype == DT_F16) ce_head_kernel<f16, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
-      else ce_head_kernel<bf16, HD_CMAX, false><<<grid, HD_T, 0, st>>>(a);
+      if (f32) prof_launch(ce_head_kernel<float, HD_CMAX, false>, grid, HD_T, 0, st, a);
+      else if (dtype == DT_F16) prof_launch(ce_head_kernel<f16, HD_CMAX, false>, grid, HD_T, 0, st, a);
+      else prof_launch(ce_head_kernel<bf16, HD_CMAX, false>, grid, HD_T, 0, st, a);
     }
     int rc = check_launch("ce_head");
     if (rc) return rc;
   }
-  ce_head_finalize_kernel<<<1, 256, 0, st>>>(a.part, ce_head_parts(a.N, a.Hl, a.Wl), out2);
+  prof_launch(ce_head_finalize_kernel, 1, 256, 0, st, a.part, ce_head_parts(a.N, a.Hl, a.Wl), out2);
   return check_launch("ce_head_finalize");
 }
 
@@ -754,11 +754,11 @@ int ce_head_scale(const float* g_raw, void* g, long long M, int C, int ld, const
                   const float* out2, int dtype, hipStream_t st) {
   const int total = (int)(M * ld);
   if (dtype == DT_F32)
-    ce_head_scale_kernel<float><<<cdiv(total, 256), 256, 0, st>>>(g_raw, (float*)g, (int)M, C, ld, gout, out2);
+    prof_launch(ce_head_scale_kernel<float>, cdiv(total, 256), 256, 0, st, g_raw, (float*)g, (int)M, C, ld, gout, out2);
   else if (dtype == DT_F16)
-    ce_head_scale_kernel<f16><<<cdiv(total, 256), 256, 0, st>>>(g_raw, (f16*)g, (int)M, C, ld, gout, out2);
+    prof_launch(ce_head_scale_kernel<f16>, cdiv(total, 256), 256, 0, st, g_raw, (f16*)g, (int)M, C, ld, gout, out2);
   else
-    ce_head_scale_kernel<bf16><<<cdiv(total, 256), 256, 0, st>>>(g_raw, (bf16*)g, (int)M, C, ld, gout, out2);
+    prof_launch(ce_head_scale_kernel<bf16>, cdiv(total, 256), 256, 0, st, g_raw, (bf16*)g, (int)M, C, ld, gout, out2);
   return check_launch("ce_head_scale");
 }
 

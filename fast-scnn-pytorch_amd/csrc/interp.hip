@@ -48,9 +48,9 @@ int up_nhwc(const UpArgs& a, int dtype, hipStream_t st) {
   }
   long long total = (long long)a.N * a.Ho * a.Wo * (a.C / V);
   unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) up_nhwc_kernel<float><<<grid, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) up_nhwc_kernel<f16><<<grid, 256, 0, st>>>(a);
-  else up_nhwc_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(up_nhwc_kernel<float>, grid, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(up_nhwc_kernel<f16>, grid, 256, 0, st, a);
+  else prof_launch(up_nhwc_kernel<bf16>, grid, 256, 0, st, a);
   return check_launch("up_nhwc");
 }
 
@@ -198,8 +198,8 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
     const bool vec = a.Wo % 4 == 0;
 #define UPR_LAUNCH(TI, TO)                                                              \
   do {                                                                                  \
-    if (vec) up_nchw_rows_kernel<TI, TO, true><<<g, UPR_THREADS, lds, st>>>(a);         \
-    else up_nchw_rows_kernel<TI, TO, false><<<g, UPR_THREADS, lds, st>>>(a);            \
+    if (vec) prof_launch(up_nchw_rows_kernel<TI, TO, true>, g, UPR_THREADS, lds, st, a);         \
+    else prof_launch(up_nchw_rows_kernel<TI, TO, false>, g, UPR_THREADS, lds, st, a);            \
   } while (0)
     if (in_dtype == DT_F32 && out_dtype == DT_F32) UPR_LAUNCH(float, float);
     else if (in_dtype == DT_F16 && out_dtype == DT_F16) UPR_LAUNCH(f16, f16);
@@ -213,15 +213,15 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
 #undef UPR_LAUNCH
     return check_launch("up_nchw");
   }
-  if (in_dtype == DT_F32 && out_dtype == DT_F32) up_nchw_kernel<float, float, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_F16 && out_dtype == DT_F16) up_nchw_kernel<f16, f16, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_F16 && out_dtype == DT_F32) up_nchw_kernel<f16, float, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_F16) up_nchw_kernel<f16, bf16, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_BF16 && out_dtype == DT_F16) up_nchw_kernel<bf16, f16, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_F32 && out_dtype == DT_F16) up_nchw_kernel<float, f16, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) up_nchw_kernel<bf16, bf16, 0><<<grid, 256, 0, st>>>(a);
-  else if (in_dtype == DT_BF16 && out_dtype == DT_F32) up_nchw_kernel<bf16, float, 0><<<grid, 256, 0, st>>>(a);
-  else up_nchw_kernel<float, bf16, 0><<<grid, 256, 0, st>>>(a);
+  if (in_dtype == DT_F32 && out_dtype == DT_F32) prof_launch(up_nchw_kernel<float, float, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_F16 && out_dtype == DT_F16) prof_launch(up_nchw_kernel<f16, f16, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_F16 && out_dtype == DT_F32) prof_launch(up_nchw_kernel<f16, float, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_F16) prof_launch(up_nchw_kernel<f16, bf16, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_BF16 && out_dtype == DT_F16) prof_launch(up_nchw_kernel<bf16, f16, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_F32 && out_dtype == DT_F16) prof_launch(up_nchw_kernel<float, f16, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_BF16 && out_dtype == DT_BF16) prof_launch(up_nchw_kernel<bf16, bf16, 0>, grid, 256, 0, st, a);
+  else if (in_dtype == DT_BF16 && out_dtype == DT_F32) prof_launch(up_nchw_kernel<bf16, float, 0>, grid, 256, 0, st, a);
+  else prof_launch(up_nchw_kernel<float, bf16, 0>, grid, 256, 0, st, a);
   return check_launch("up_nchw");
 }
 
@@ -310,14 +310,14 @@ int up_argmax(const UpArgs& a, int in_dtype, void* labels, int label_u8, hipStre
   }
   dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)cdiv(a.Ho, UPR_R), (unsigned)a.N);
   if (in_dtype == DT_F32) {
-    if (label_u8) up_argmax_kernel<float, uint8_t><<<g, UPR_THREADS, lds, st>>>(a, (uint8_t*)labels);
-    else up_argmax_kernel<float, long long><<<g, UPR_THREADS, lds, st>>>(a, (long long*)labels);
+    if (label_u8) prof_launch(up_argmax_kernel<float, uint8_t>, g, UPR_THREADS, lds, st, a, (uint8_t*)labels);
+    else prof_launch(up_argmax_kernel<float, long long>, g, UPR_THREADS, lds, st, a, (long long*)labels);
   } else if (in_dtype == DT_F16) {
-    if (label_u8) up_argmax_kernel<f16, uint8_t><<<g, UPR_THREADS, lds, st>>>(a, (uint8_t*)labels);
-    else up_argmax_kernel<f16, long long><<<g, UPR_THREADS, lds, st>>>(a, (long long*)labels);
+    if (label_u8) prof_launch(up_argmax_kernel<f16, uint8_t>, g, UPR_THREADS, lds, st, a, (uint8_t*)labels);
+    else prof_launch(up_argmax_kernel<f16, long long>, g, UPR_THREADS, lds, st, a, (long long*)labels);
   } else {
-    if (label_u8) up_argmax_kernel<bf16, uint8_t><<<g, UPR_THREADS, lds, st>>>(a, (uint8_t*)labels);
-    else up_argmax_kernel<bf16, long long><<<g, UPR_THREADS, lds, st>>>(a, (long long*)labels);
+    if (label_u8) prof_launch(up_argmax_kernel<bf16, uint8_t>, g, UPR_THREADS, lds, st, a, (uint8_t*)labels);
+    else prof_launch(up_argmax_kernel<bf16, long long>, g, UPR_THREADS, lds, st, a, (long long*)labels);
   }
   return check_launch("up_argmax");
 }
@@ -411,8 +411,8 @@ int axis_bwd(const AxisBwdArgs& a, int g_dtype, int d_dtype, hipStream_t st) {
   dim3 grid((unsigned)((per_i / vx + 255) / 256), a.Lin);
 #define AXB(TG, TD)                                                          \
   do {                                                                       \
-    if (vec) axis_bwd_kernel<TG, TD, 4><<<grid, 256, 0, st>>>(a);            \
-    else axis_bwd_kernel<TG, TD, 1><<<grid, 256, 0, st>>>(a);                \
+    if (vec) prof_launch(axis_bwd_kernel<TG, TD, 4>, grid, 256, 0, st, a);            \
+    else prof_launch(axis_bwd_kernel<TG, TD, 1>, grid, 256, 0, st, a);                \
   } while (0)
   if (g_dtype == DT_F32 && d_dtype == DT_F32) AXB(float, float);
   else if (g_dtype == DT_BF16 && d_dtype == DT_BF16) AXB(bf16, bf16);
@@ -503,9 +503,9 @@ int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
     return E_UNSUPPORTED;
   }
   dim3 grid(50, a.N);
-  if (dtype == DT_F32) pyramid_pool_kernel<float><<<grid, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) pyramid_pool_kernel<f16><<<grid, 256, 0, st>>>(a);
-  else pyramid_pool_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(pyramid_pool_kernel<float>, grid, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(pyramid_pool_kernel<f16>, grid, 256, 0, st, a);
+  else prof_launch(pyramid_pool_kernel<bf16>, grid, 256, 0, st, a);
   return check_launch("pyramid_pool");
 }
 
@@ -567,9 +567,9 @@ int pyramid_pool_bwd(const PoolBwdArgs& a, int dtype, hipStream_t st) {
   }
   long long total = (long long)a.N * a.H * a.W * (a.C / V);
   unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) pyramid_pool_bwd_kernel<float><<<grid, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) pyramid_pool_bwd_kernel<f16><<<grid, 256, 0, st>>>(a);
-  else pyramid_pool_bwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(pyramid_pool_bwd_kernel<float>, grid, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(pyramid_pool_bwd_kernel<f16>, grid, 256, 0, st, a);
+  else prof_launch(pyramid_pool_bwd_kernel<bf16>, grid, 256, 0, st, a);
   return check_launch("pyramid_pool_bwd");
 }
 
@@ -617,9 +617,9 @@ int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
   }
   long long total = (long long)a.N * a.H * a.W * (4 * a.CF / V);
   unsigned grid = (unsigned)((total + 255) / 256);
-  if (dtype == DT_F32) ppm_up_fwd_kernel<float><<<grid, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) ppm_up_fwd_kernel<f16><<<grid, 256, 0, st>>>(a);
-  else ppm_up_fwd_kernel<bf16><<<grid, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(ppm_up_fwd_kernel<float>, grid, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(ppm_up_fwd_kernel<f16>, grid, 256, 0, st, a);
+  else prof_launch(ppm_up_fwd_kernel<bf16>, grid, 256, 0, st, a);
   return check_launch("ppm_up_fwd");
 }
 
@@ -711,15 +711,16 @@ __global__ __launch_bounds__(PPB_THREADS) void ppm_up_bwd_kernel(PpmUpArgs a, vo
 
 int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
-  if (a.CF <= 0 || a.CF > 32 || a.CF % V || a.ldy % V || a.coff % V || a.H > PPB_MAXH ||
-      a.N > 65535) {
+  // the row mapping hands rest / (CF / V) rows to a pass: CF / V must divide the 64 lanes
+  if (a.CF <= 0 || a.CF > 32 || a.CF % V || (PPB_THREADS / PPB_SEG) % (a.CF / V) || a.ldy % V ||
+      a.coff % V || a.H > PPB_MAXH || a.N > 65535) {
     set_error("ppm_up_bwd: CF=%d H=%d unsupported", a.CF, a.H);
     return E_UNSUPPORTED;
   }
   dim3 grid(4, a.N);
-  if (dtype == DT_F32) ppm_up_bwd_kernel<float><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
-  else if (dtype == DT_F16) ppm_up_bwd_kernel<f16><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
-  else ppm_up_bwd_kernel<bf16><<<grid, PPB_THREADS, 0, st>>>(a, dfeats);
+  if (dtype == DT_F32) prof_launch(ppm_up_bwd_kernel<float>, grid, PPB_THREADS, 0, st, a, dfeats);
+  else if (dtype == DT_F16) prof_launch(ppm_up_bwd_kernel<f16>, grid, PPB_THREADS, 0, st, a, dfeats);
+  else prof_launch(ppm_up_bwd_kernel<bf16>, grid, PPB_THREADS, 0, st, a, dfeats);
   return check_launch("ppm_up_bwd");
 }
 

@@ -433,13 +433,13 @@ static void ir_launch_ks(const IrArgs& a, dim3 grid, hipStream_t st) {
   constexpr int PT = IrTile<S>::PT;  // project pixel tiles: all per wave above 64 outputs
   if constexpr (sizeof(T) == 4) {
     if (a.we3 && a.wp3) {
-      if (a.Cout > 64) ir_block_kernel<T, KS, PT, true, S><<<grid, IR_THREADS, lds, st>>>(a);
-      else ir_block_kernel<T, KS, PT / 2, true, S><<<grid, IR_THREADS, lds, st>>>(a);
+      if (a.Cout > 64) prof_launch(ir_block_kernel<T, KS, PT, true, S>, grid, IR_THREADS, lds, st, a);
+      else prof_launch(ir_block_kernel<T, KS, PT / 2, true, S>, grid, IR_THREADS, lds, st, a);
       return;
     }
   }
-  if (a.Cout > 64) ir_block_kernel<T, KS, PT, false, S><<<grid, IR_THREADS, lds, st>>>(a);
-  else ir_block_kernel<T, KS, PT / 2, false, S><<<grid, IR_THREADS, lds, st>>>(a);
+  if (a.Cout > 64) prof_launch(ir_block_kernel<T, KS, PT, false, S>, grid, IR_THREADS, lds, st, a);
+  else prof_launch(ir_block_kernel<T, KS, PT / 2, false, S>, grid, IR_THREADS, lds, st, a);
 }
 
 template <typename T, int S>

@@ -75,12 +75,12 @@ int ce_parts(int N, long long HW) { return (int)(((long long)N * HW + 255) / 256
 
 int ce_fwd(const CeArgs& a, float* out, int dtype, hipStream_t st) {
   int P = ce_parts(a.N, a.HW);
-  if (dtype == DT_F32) ce_fwd_kernel<float><<<P, 256, 0, st>>>(a);
-  else if (dtype == DT_F16) ce_fwd_kernel<f16><<<P, 256, 0, st>>>(a);
-  else ce_fwd_kernel<bf16><<<P, 256, 0, st>>>(a);
+  if (dtype == DT_F32) prof_launch(ce_fwd_kernel<float>, P, 256, 0, st, a);
+  else if (dtype == DT_F16) prof_launch(ce_fwd_kernel<f16>, P, 256, 0, st, a);
+  else prof_launch(ce_fwd_kernel<bf16>, P, 256, 0, st, a);
   int rc = check_launch("ce_fwd");
   if (rc) return rc;
-  ce_finalize_kernel<<<1, 256, 0, st>>>(a.part, P, out);
+  prof_launch(ce_finalize_kernel, 1, 256, 0, st, a.part, P, out);
   return check_launch("ce_finalize");
 }
 
@@ -112,9 +112,9 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(CeArgs a, const float* gout
 
 int ce_bwd(const CeArgs& a, const float* gout, const float* stats, int dtype, hipStream_t st) {
   int P = ce_parts(a.N, a.HW);
-  if (dtype == DT_F32) ce_bwd_kernel<float><<<P, 256, 0, st>>>(a, gout, stats);
-  else if (dtype == DT_F16) ce_bwd_kernel<f16><<<P, 256, 0, st>>>(a, gout, stats);
-  else ce_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, gout, stats);
+  if (dtype == DT_F32) prof_launch(ce_bwd_kernel<float>, P, 256, 0, st, a, gout, stats);
+  else if (dtype == DT_F16) prof_launch(ce_bwd_kernel<f16>, P, 256, 0, st, a, gout, stats);
+  else prof_launch(ce_bwd_kernel<bf16>, P, 256, 0, st, a, gout, stats);
   return check_launch("ce_bwd");
 }
 
@@ -156,9 +156,9 @@ __global__ __launch_bounds__(256) void ohem_prob_kernel(CeArgs a, float thresh, 
 int ohem_prob(const CeArgs& a, float thresh, float* prob, unsigned long long* counts, int dtype,
               hipStream_t st) {
   const int P = ce_parts(a.N, a.HW);
-  if (dtype == DT_F32) ohem_prob_kernel<float><<<P, 256, 0, st>>>(a, thresh, prob, counts);
-  else if (dtype == DT_F16) ohem_prob_kernel<f16><<<P, 256, 0, st>>>(a, thresh, prob, counts);
-  else ohem_prob_kernel<bf16><<<P, 256, 0, st>>>(a, thresh, prob, counts);
+  if (dtype == DT_F32) prof_launch(ohem_prob_kernel<float>, P, 256, 0, st, a, thresh, prob, counts);
+  else if (dtype == DT_F16) prof_launch(ohem_prob_kernel<f16>, P, 256, 0, st, a, thresh, prob, counts);
+  else prof_launch(ohem_prob_kernel<bf16>, P, 256, 0, st, a, thresh, prob, counts);
   return check_launch("ohem_prob");
 }
 
@@ -287,15 +287,15 @@ int ohem_threshold_dev(const float* key, long long n, const unsigned long long* 
     return E_INVALID;
   }
   OhemSel* s = reinterpret_cast<OhemSel*>(work + 2048);
-  ohem_sel_init_kernel<<<1, 256, 0, st>>>(counts, min_kept, thresh, s, work, thr);
+  prof_launch(ohem_sel_init_kernel, 1, 256, 0, st, counts, min_kept, thresh, s, work, thr);
   static const int shifts[3] = {21, 10, 0}, widths[3] = {11, 11, 10};
   const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 2048);
   for (int d = 0; d < 3; ++d) {
     const unsigned bins = 1u << widths[d];
-    ohem_sel_hist_kernel<<<grid, 256, 0, st>>>(key, n, shifts[d], bins, s, work);
-    ohem_sel_pick_kernel<<<1, 256, 0, st>>>(s, work, bins, widths[d], shifts[d]);
+    prof_launch(ohem_sel_hist_kernel, grid, 256, 0, st, key, n, shifts[d], bins, s, work);
+    prof_launch(ohem_sel_pick_kernel, 1, 256, 0, st, s, work, bins, widths[d], shifts[d]);
   }
-  ohem_sel_final_kernel<<<1, 64, 0, st>>>(s, thr);
+  prof_launch(ohem_sel_final_kernel, 1, 64, 0, st, s, thr);
   return check_launch("ohem_threshold");
 }
 
@@ -446,11 +446,11 @@ int dice_loss_fwd(const void* logits, int dtype, const long long* target, int N,
   }
   DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};
   const int P = ce_parts(N, HW);
-  if (dtype == DT_F32) dice_fwd_kernel<float><<<P, 256, 0, st>>>(a, part);
-  else if (dtype == DT_F16) dice_fwd_kernel<f16><<<P, 256, 0, st>>>(a, part);
-  else dice_fwd_kernel<bf16><<<P, 256, 0, st>>>(a, part);
+  if (dtype == DT_F32) prof_launch(dice_fwd_kernel<float>, P, 256, 0, st, a, part);
+  else if (dtype == DT_F16) prof_launch(dice_fwd_kernel<f16>, P, 256, 0, st, a, part);
+  else prof_launch(dice_fwd_kernel<bf16>, P, 256, 0, st, a, part);
   if (int rc = check_launch("dice_fwd")) return rc;
-  dice_finalize_kernel<<<1, 256, 0, st>>>(part, P, stats);
+  prof_launch(dice_finalize_kernel, 1, 256, 0, st, part, P, stats);
   return check_launch("dice_finalize");
 }
 
@@ -459,9 +459,9 @@ int dice_loss_bwd(const void* logits, int dtype, const long long* target, int N,
                   float smooth, float wd, float wf, void* dlogits, hipStream_t st) {
   DiceArgs a{logits, target, N, HW, C, alpha, gamma, focal};
   const int P = ce_parts(N, HW);
-  if (dtype == DT_F32) dice_bwd_kernel<float><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
-  else if (dtype == DT_F16) dice_bwd_kernel<f16><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
-  else dice_bwd_kernel<bf16><<<P, 256, 0, st>>>(a, stats, gout, smooth, wd, wf, dlogits);
+  if (dtype == DT_F32) prof_launch(dice_bwd_kernel<float>, P, 256, 0, st, a, stats, gout, smooth, wd, wf, dlogits);
+  else if (dtype == DT_F16) prof_launch(dice_bwd_kernel<f16>, P, 256, 0, st, a, stats, gout, smooth, wd, wf, dlogits);
+  else prof_launch(dice_bwd_kernel<bf16>, P, 256, 0, st, a, stats, gout, smooth, wd, wf, dlogits);
   return check_launch("dice_bwd");
 }
 
@@ -526,9 +526,9 @@ int dropout(const DropArgs& a, int dtype, hipStream_t st) {
   const unsigned P = chan_sweep((long long)a.N * a.H * a.W, a.C / V);
   const unsigned grid = (unsigned)(((long long)P * (a.C / V) + 255) / 256);
   uint32_t thr = dropout_threshold(a.p);
-  if (dtype == DT_F32) dropout_kernel<float><<<grid, 256, 0, st>>>(a, thr, P);
-  else if (dtype == DT_F16) dropout_kernel<f16><<<grid, 256, 0, st>>>(a, thr, P);
-  else dropout_kernel<bf16><<<grid, 256, 0, st>>>(a, thr, P);
+  if (dtype == DT_F32) prof_launch(dropout_kernel<float>, grid, 256, 0, st, a, thr, P);
+  else if (dtype == DT_F16) prof_launch(dropout_kernel<f16>, grid, 256, 0, st, a, thr, P);
+  else prof_launch(dropout_kernel<bf16>, grid, 256, 0, st, a, thr, P);
   return check_launch("dropout");
 }
 
@@ -585,8 +585,8 @@ int seg_metric(const void* pred, int pred_u8, const long long* target, long long
   const long long blocks = (n + 255) / 256;
   const unsigned grid = (unsigned)(blocks < 1024 ? blocks : 1024);
   unsigned long long* c = reinterpret_cast<unsigned long long*>(counts);
-  if (pred_u8) seg_metric_kernel<uint8_t><<<grid, 256, 0, st>>>((const uint8_t*)pred, target, n, C, c);
-  else seg_metric_kernel<long long><<<grid, 256, 0, st>>>((const long long*)pred, target, n, C, c);
+  if (pred_u8) prof_launch(seg_metric_kernel<uint8_t>, grid, 256, 0, st, (const uint8_t*)pred, target, n, C, c);
+  else prof_launch(seg_metric_kernel<long long>, grid, 256, 0, st, (const long long*)pred, target, n, C, c);
   return check_launch("seg_metric");
 }
 
@@ -634,10 +634,10 @@ int normalize_u8(const uint8_t* x, int N, int H, int W, const float* mean, const
   const long long npix4 = (long long)N * HW / 4;
   const unsigned grid = (unsigned)((npix4 + 255) / 256);
   if (out_dtype == DT_F32)
-    normalize_u8_kernel<float><<<grid, 256, 0, st>>>(x, npix4, HW, mean[0], mean[1], mean[2],
+    prof_launch(normalize_u8_kernel<float>, grid, 256, 0, st, x, npix4, HW, mean[0], mean[1], mean[2],
                                                      std[0], std[1], std[2], (float*)y);
   else
-    normalize_u8_kernel<bf16><<<grid, 256, 0, st>>>(x, npix4, HW, mean[0], mean[1], mean[2],
+    prof_launch(normalize_u8_kernel<bf16>, grid, 256, 0, st, x, npix4, HW, mean[0], mean[1], mean[2],
                                                     std[0], std[1], std[2], (bf16*)y);
   return check_launch("normalize_u8");
 }
@@ -663,7 +663,7 @@ int remap_labels(const uint8_t* in, long long n, const long long* lut, int lut_s
     return E_INVALID;
   }
   if (n == 0) return OK;
-  remap_labels_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(in, n, lut, lut_size, offset,
+  prof_launch(remap_labels_kernel, (unsigned)((n + 255) / 256), 256, 0, st, in, n, lut, lut_size, offset,
                                                                     invalid, out);
   return check_launch("remap_labels");
 }
@@ -671,7 +671,7 @@ int remap_labels(const uint8_t* in, long long n, const long long* lut, int lut_s
 __global__ void set_u64_kernel(uint64_t* p, uint64_t v) { *p = v; }
 
 int set_u64(uint64_t* p, uint64_t v, hipStream_t st) {
-  set_u64_kernel<<<1, 1, 0, st>>>(p, v);
+  prof_launch(set_u64_kernel, 1, 1, 0, st, p, v);
   return check_launch("set_u64");
 }
 
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(SgdArgs a) {
 
 int sgd(const SgdArgs& a, hipStream_t st) {
   unsigned grid = (unsigned)((a.n + 1023) / 1024);
-  sgd_kernel<<<grid, 256, 0, st>>>(a);
+  prof_launch(sgd_kernel, grid, 256, 0, st, a);
   return check_launch("sgd");
 }
 
@@ -772,9 +772,9 @@ int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t
       return E_INVALID;
     }
   const unsigned grid = (unsigned)std::min<long long>((t.total + 2047) / 2048, 4096);
-  if (dtype == DT_F32) weights_prep_kernel<float><<<grid, 256, 0, st>>>(t, P, (float*)dst);
-  else if (dtype == DT_F16) weights_prep_kernel<f16><<<grid, 256, 0, st>>>(t, P, (f16*)dst);
-  else weights_prep_kernel<bf16><<<grid, 256, 0, st>>>(t, P, (bf16*)dst);
+  if (dtype == DT_F32) prof_launch(weights_prep_kernel<float>, grid, 256, 0, st, t, P, (float*)dst);
+  else if (dtype == DT_F16) prof_launch(weights_prep_kernel<f16>, grid, 256, 0, st, t, P, (f16*)dst);
+  else prof_launch(weights_prep_kernel<bf16>, grid, 256, 0, st, t, P, (bf16*)dst);
   return check_launch("weights_prep");
 }
 
@@ -784,7 +784,7 @@ __global__ void cast_f32_bf16_kernel(const float* x, uint16_t* y, long long n) {
   if (i < n) y[i] = f2bf(x[i]);
 }
 int cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st) {
-  cast_f32_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(x, (uint16_t*)y, n);
+  prof_launch(cast_f32_bf16_kernel, (unsigned)((n + 255) / 256), 256, 0, st, x, (uint16_t*)y, n);
   return check_launch("cast_f32_bf16");
 }
 
@@ -794,7 +794,7 @@ __global__ void fill_kernel(float* x, long long n, float v) {
 }
 int fill_f32(float* x, long long n, float v, hipStream_t st) {
   if (n <= 0) return OK;
-  fill_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(x, n, v);
+  prof_launch(fill_kernel, (unsigned)((n + 255) / 256), 256, 0, st, x, n, v);
   return check_launch("fill");
 }
 

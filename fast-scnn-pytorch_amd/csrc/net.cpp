@@ -2039,6 +2039,13 @@ int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to)
     set_error("input gradient dtype code must be 0 (fp32), 1 (bf16) or 2 (fp16)");
     return E_INVALID;
   }
+  if (r.gloss && pl.train != 1) {
+    // the fused loss head's gradient exists only after fscnn_forward_loss, which needs a
+    // training plan (train = 1): an eval-autograd plan (train = 2) never wrote it
+    set_error("net_backward: grad_loss / loss2 need a training plan (train=1), got train=%d",
+              pl.train);
+    return E_INVALID;
+  }
   return run_graphed(pl, run_key(1, stage_from, stage_to, r), r.st, [&](hipStream_t st) -> int {
     RunArgs rr = r;
     rr.st = st;

@@ -7,7 +7,7 @@
 // BatchNorm reductions are block-local: forward = conv, batch statistics (fp64, fixed order), the
 // finish of bn_finish.hpp (running statistics included), ReLU apply; backward = the BN-backward sums
 // + finish, dz, weight gradient (stored into the fp32 gradient arena) and input gradient.
-// Arithmetic follows the general path: z rounded to the storage type, statistics of the unrounded
+// Arithmetic follows the general path: z rounded to the storage type, statistics of that stored
 // value, y = relu(fmaf(z_stored, scale, shift)) (bn_apply), dz = scale*(g - c0 - xhat*c1) rounded
 // to the storage type before both GEMMs read it (bn_bwd_apply).
 #include "bn_finish.hpp"
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_kernel(PpmFwdArgs a) {
 #pragma unroll
       for (int j = 0; j < V; ++j) acc = fmaf(xv[j], wr[k + j], acc);
     }
-    s_z[m * PPM_C + n] = acc;
+    s_z[m * PPM_C + n] = round_as<T>(acc);  // the stored value (statistics and apply)
     st1(Z + (size_t)m * PPM_C + n, acc);
   }
   __syncthreads();
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_lds_kernel(PpmFwdArgs a) {
 #pragma unroll
       for (int j = 0; j < V; ++j) acc = fmaf(xv[j], wr[k + j], acc);
     }
-    s_z[m * PPM_C + n] = acc;
+    s_z[m * PPM_C + n] = round_as<T>(acc);  // the stored value (statistics and apply)
     st1(Z + (size_t)m * PPM_C + n, acc);
   }
   __syncthreads();
@@ -327,13 +327,13 @@ int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st) {
                2.0 * a.K * PPM_C * rows);
   if (dtype != DT_F32 && a.K == PPM_K && maxM <= 288) {
     const size_t l2 = (size_t)maxM * PPM_C * 4 + (size_t)maxM * PPM_K * 2;
-    if (dtype == DT_F16) ppm_fwd_lds_kernel<f16><<<a.nb, PPM_T, l2, st>>>(a);
-    else ppm_fwd_lds_kernel<bf16><<<a.nb, PPM_T, l2, st>>>(a);
+    if (dtype == DT_F16) prof_launch(ppm_fwd_lds_kernel<f16>, a.nb, PPM_T, l2, st, a);
+    else prof_launch(ppm_fwd_lds_kernel<bf16>, a.nb, PPM_T, l2, st, a);
     return check_launch("ppm_branches_fwd");
   }
-  if (dtype == DT_F32) ppm_fwd_kernel<float><<<a.nb, PPM_T, lds, st>>>(a);
-  else if (dtype == DT_F16) ppm_fwd_kernel<f16><<<a.nb, PPM_T, lds, st>>>(a);
-  else ppm_fwd_kernel<bf16><<<a.nb, PPM_T, lds, st>>>(a);
+  if (dtype == DT_F32) prof_launch(ppm_fwd_kernel<float>, a.nb, PPM_T, lds, st, a);
+  else if (dtype == DT_F16) prof_launch(ppm_fwd_kernel<f16>, a.nb, PPM_T, lds, st, a);
+  else prof_launch(ppm_fwd_kernel<bf16>, a.nb, PPM_T, lds, st, a);
   return check_launch("ppm_branches_fwd");
 }
 
@@ -350,9 +350,9 @@ int ppm_branches_bwd(const PpmBwdArgs& a, int dtype, hipStream_t st) {
   b.wg0[0] = 0;
   for (int i = 0; i < a.nb; ++i) b.wg0[i + 1] = b.wg0[i] + std::max(1, std::min(16, a.b[i].M / 32));
   const int nwg = b.wg0[a.nb];
-  if (dtype == DT_F32) ppm_bwd_kernel<float><<<nwg, PPM_T, lds, st>>>(b);
-  else if (dtype == DT_F16) ppm_bwd_kernel<f16><<<nwg, PPM_T, lds, st>>>(b);
-  else ppm_bwd_kernel<bf16><<<nwg, PPM_T, lds, st>>>(b);
+  if (dtype == DT_F32) prof_launch(ppm_bwd_kernel<float>, nwg, PPM_T, lds, st, b);
+  else if (dtype == DT_F16) prof_launch(ppm_bwd_kernel<f16>, nwg, PPM_T, lds, st, b);
+  else prof_launch(ppm_bwd_kernel<bf16>, nwg, PPM_T, lds, st, b);
   return check_launch("ppm_branches_bwd");
 }
 

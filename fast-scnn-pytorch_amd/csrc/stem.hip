@@ -514,6 +514,7 @@ bool stem_ok(const StemArgs& a) {
   const int VI = a.x_dtype ? 8 : 4;
   const int ve = VI == 8 ? 4 : (a.ldy % 4 == 0 ? 4 : 0);  // 4-channel output vectors aligned
   return a.N > 0 && a.H >= 3 && a.W >= 3 && a.W % VI == 0 && ((uintptr_t)a.x & 15) == 0 &&
+         ((uintptr_t)a.y & 15) == 0 && ((uintptr_t)a.wp & 15) == 0 &&
          ve == 4 && a.ldy >= ST_C2 && a.ldy % 4 == 0 &&
          a.H1 == (a.H - 3) / 2 + 1 && a.W1 == (a.W - 3) / 2 + 1 && a.H2 == (a.H1 - 1) / 2 + 1 &&
          a.W2 == (a.W1 - 1) / 2 + 1 && a.N < 65536 && cdiv(a.H2, SW_RS) < 65536 &&
@@ -533,12 +534,13 @@ int stem_fwd(const StemArgs& a, int dtype, hipStream_t st) {
   const dim3 gw(cdiv(a.W2, SW_TW), cdiv(a.H2, SW_RS), a.N);
   ProfScope pw_(PK_STEM, st, (a.x_dtype ? 2.0 : 4.0) * a.N * 3.0 * a.H * a.W +
                                  (dtype == DT_F32 ? 4.0 : 2.0) * (double)a.N * a.H2 * a.W2 * ST_C2,
-                0.0);
+                // conv0 (27 -> 32), the depthwise 3 x 3 (32) and the pointwise 32 -> 48
+                2.0 * a.N * (27.0 * 32 * a.H1 * a.W1 + (9.0 * 32 + 32.0 * ST_C2) * a.H2 * a.W2));
 #define STEMW(T)                                                            \
   do {                                                                      \
-    if (a.x_dtype == 2) stem_walk_kernel<T, 2><<<gw, 256, 0, st>>>(as);      \
-    else if (a.x_dtype == 1) stem_walk_kernel<T, 1><<<gw, 256, 0, st>>>(as); \
-    else stem_walk_kernel<T, 0><<<gw, 256, 0, st>>>(as);                     \
+    if (a.x_dtype == 2) prof_launch(stem_walk_kernel<T, 2>, gw, 256, 0, st, as);      \
+    else if (a.x_dtype == 1) prof_launch(stem_walk_kernel<T, 1>, gw, 256, 0, st, as); \
+    else prof_launch(stem_walk_kernel<T, 0>, gw, 256, 0, st, as);                     \
   } while (0)
   if (dtype == DT_F32) STEMW(float);
   else if (dtype == DT_F16) STEMW(f16);

@@ -253,6 +253,9 @@ class _FastSCNNFunction(torch.autograd.Function):
         else:
             outs, _, _, dt, xc = model._run_forward(x, MODE_EVAL, ar=ar)
             ctx.mode, ctx.ws, ctx.seed, ctx.dt = MODE_EVAL_GRAD, None, 0, dt
+            # the backward recomputes this forward from the running statistics: remember their
+            # version (a train-mode forward or a load_state_dict in between bumps it)
+            ctx.r_version = ar["R"]._version
         ctx.x_dtype = x.dtype
         # the converted dense NCHW fp32/bf16 copy the forward read, not the caller's tensor: the
         # conv0 weight gradient re-reads it as dense NCHW (channels_last / fp16 / expanded inputs)
@@ -265,6 +268,11 @@ class _FastSCNNFunction(torch.autograd.Function):
         gaux = gouts[1] if len(gouts) > 1 else None
         model, ws = ctx.model, ctx.ws
         if ctx.mode == MODE_EVAL_GRAD:
+            if ctx.ar["R"]._version != ctx.r_version:
+                raise RuntimeError(
+                    "one of the variables needed for gradient computation has been modified by an "
+                    "inplace operation: the BatchNorm running statistics changed (a train-mode "
+                    "forward or a state_dict load) between this eval-mode forward and its backward")
             # (in the forward's arithmetic: autocast is not active where autograd runs backward)
             _, ws, _, _, _ = model._run_forward(x, MODE_EVAL_GRAD, ar=ctx.ar, dt=ctx.dt)
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
@@ -286,9 +294,11 @@ class _FastSCNNLossFunction(torch.autograd.Function):
         ctx.ws, ctx.seed, ctx.dt, ctx.loss2 = ws, seed, dt, loss2
         ctx.x_dtype = x.dtype
         ctx.save_for_backward(xc, *params)
-        # a view of the (mean, count) pair the head wrote: the backward reads the count from
-        # loss2 itself, which autograd never writes, so no copy is needed
-        return loss2[0]
+        # the mean of the (mean, count) pair the head wrote, as a tensor sharing its storage but
+        # not an autograd view (a view created here would refuse the in-place ops the reference's
+        # loss tensor allows: loss /= accum_steps); the backward reads only the count, loss2[1]
+        out = torch.empty((), dtype=loss2.dtype, device=loss2.device)
+        return out.set_(loss2.untyped_storage(), loss2.storage_offset(), (), ())
 
     @staticmethod
     def backward(ctx, gloss):
@@ -541,6 +551,9 @@ class FastSCNN(nn.Module):
                           _lib.ptr(out), _lib.dtype_code(out_dt), *rest[1:])
         if train:
             self._writeback(ar)
+            # the running statistics changed: an eval-mode graph recorded before this forward
+            # must not backpropagate through them (_FastSCNNFunction.backward checks)
+            torch.autograd.graph.increment_version(ar["R"])
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return ((out, aux_out) if self.aux else (out,)), ws, seed, dt, x
@@ -629,6 +642,7 @@ class FastSCNN(nn.Module):
                       _lib.ptr(ar["R"]), _lib.ptr(ar["NBT"]), _lib.ptr(ws), _lib.c_ull(seed),
                       _lib.c_float(p), _lib.c_float(self._momentum()), _lib.stream_ptr(x.device))
         self._writeback(ar)
+        torch.autograd.graph.increment_version(ar["R"])
         if getattr(self, "_keep_ws", False):
             self._debug = {"plan": plan, "ws": ws, "dt": dt}
         return loss2, ws, seed, dt, x

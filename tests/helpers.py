@@ -80,29 +80,53 @@ def oracle_half_emulated(sd, x, nc, dtype=torch.float16):
         F.conv2d, F.batch_norm, F.interpolate = oc, ob, oi
 
 
-def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True, dtype=torch.bfloat16):
+def oracle_bf16_train_emulated(sd, x, t, nc, drop_seed, emulate=True, dtype=torch.bfloat16,
+                               relu_masks=None, record=False, round_out=False,
+                               round_blocks=False, round_all=False):
     """One train step (forward, CE(ignore -1), backward) of the oracle: fp64 when ``emulate`` is
     False, else fp32 with every conv input / weight / output rounded to ``dtype`` (bf16: cfg3's
     storage precision; fp16: train.py:269's autocast) — and, because autograd casts gradients
     back through those roundings, every conv input / output gradient rounded to ``dtype`` as
-    well.  Returns (loss, {name: fp64 grad})."""
+    well.  Returns (loss, {name: fp64 grad}); with ``record`` also the recorded activations.
+    ``relu_masks``: evaluate under given ReLU masks (oracle ``_Ctx.relu``).  ``round_out``: the
+    module's output, the full-resolution logits, is itself ``dtype`` (a 16-bit model returns
+    16-bit logits, models/fast_scnn.py:40 under autocast), so it and its gradient are rounded.
+    ``round_blocks``: every LinearBottleneck's output (after the shortcut add,
+    models/fast_scnn.py:112-114) and its gradient rounded as well — the one activation a 16-bit
+    implementation stores that is not a conv input or output (the residual stream).
+    ``round_all``: 16-bit storage of every op output, as torch.autocast runs the reference in
+    16 bits (train.py:269): conv, BatchNorm, interpolate and adaptive-pool outputs and the
+    LinearBottleneck sums (implies ``round_blocks``), each with its gradient."""
     import torch.nn.functional as F
     from oracle import fast_scnn_ref as ref
     dt = torch.float32 if emulate else torch.float64
     s = {k: (v.detach().clone().to(dt).requires_grad_(True)
              if v.is_floating_point() and "running" not in k else
              (v.to(dt) if v.is_floating_point() else v)) for k, v in sd.items()}
-    oc = F.conv2d
+    oc, ob = F.conv2d, ref._bottleneck
+    obn, oi, op = F.batch_norm, F.interpolate, F.adaptive_avg_pool2d
     if emulate:
         q = lambda v: v.to(dtype).float()  # noqa: E731
         F.conv2d = lambda a, w, b=None, *r, **k: q(oc(q(a), q(w), b, *r, **k))
+        if round_blocks or round_all:
+            ref._bottleneck = lambda *a, **k: q(ob(*a, **k))
+        if round_all:
+            F.batch_norm = lambda *a, **k: q(obn(*a, **k))
+            F.interpolate = lambda *a, **k: q(oi(*a, **k))
+            F.adaptive_avg_pool2d = lambda *a, **k: q(op(*a, **k))
     try:
-        outs, _, _ = ref.forward(s, x.to(dt), nc, training=True, dropout_seed=drop_seed)
-        loss = ref.cross_entropy(outs[0], t)
+        outs, _, acts = ref.forward(s, x.to(dt), nc, training=True, dropout_seed=drop_seed,
+                                    relu_masks=relu_masks, record=record)
+        out = outs[0].to(dtype).float() if (emulate and round_out) else outs[0]
+        loss = ref.cross_entropy(out, t)
         loss.backward()
     finally:
-        F.conv2d = oc
-    return loss.item(), {k: v.grad.double() for k, v in s.items() if v.grad is not None}
+        F.conv2d, ref._bottleneck = oc, ob
+        F.batch_norm, F.interpolate, F.adaptive_avg_pool2d = obn, oi, op
+    grads = {k: v.grad.double() for k, v in s.items() if v.grad is not None}
+    if record:
+        return loss.item(), grads, acts
+    return loss.item(), grads
 
 
 def argmax_agreement(logits, ref_argmax, ref_logits=None, margin_tol=1e-4):

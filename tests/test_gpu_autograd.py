@@ -213,3 +213,47 @@ def test_grad_arena_fully_written():
             res[(mode, fill == 0.0)] = torch.cat([p.grad.flatten() for p in m.parameters()])
         assert torch.isfinite(res[(mode, False)]).all(), mode
         assert torch.equal(res[(mode, False)], res[(mode, True)]), mode
+
+
+def test_forward_loss_allows_inplace_ops_on_the_loss():
+    """train.py-style gradient accumulation divides the loss in place (``loss /= accum``); the
+    reference's loss tensor allows it, so the fused head's must too, with the gradient scaled."""
+    sd = portable_sd(19, variant="bnrand")
+    x = torch.from_numpy(np.random.default_rng(3).uniform(-1.5, 1.5, (2, 3, 96, 160))
+                         .astype(np.float32)).to(DEV)
+    t = torch.from_numpy(np.random.default_rng(4).integers(-1, 19, (2, 96, 160))).to(DEV)
+    m = make_model(sd, 19).train()
+    m._dropout_seed = 7
+    l1 = m.forward_loss(x, t)
+    l1.backward()
+    g1 = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    m.load_state_dict(sd)
+    l2 = m.forward_loss(x, t)
+    v = l2.item()
+    l2 /= 4.0
+    l2 += 0.0
+    assert abs(l2.item() - v / 4.0) <= 1e-7 * abs(v)
+    l2.backward()
+    for k, p in m.named_parameters():
+        torch.testing.assert_close(p.grad, g1[k] / 4.0, rtol=1e-5, atol=1e-9, msg=k)
+
+
+def test_eval_backward_refuses_changed_running_stats():
+    """The eval-mode backward recomputes the forward from the running statistics; a train-mode
+    forward in between changes them, so (as the reference's saved native_batch_norm inputs
+    would) the backward raises instead of returning gradients of other BN constants."""
+    sd = portable_sd(19, variant="bnrand")
+    x = torch.from_numpy(np.random.default_rng(5).uniform(-1.5, 1.5, (2, 3, 64, 96))
+                         .astype(np.float32)).to(DEV)
+    m = make_model(sd, 19).eval()
+    out = m(x)[0]
+    m.train()
+    with torch.no_grad():
+        m(x)
+    m.eval()
+    with pytest.raises(RuntimeError, match="inplace operation"):
+        out.sum().backward()
+    # untouched statistics: the same graph shape backpropagates
+    out = m(x)[0]
+    out.sum().backward()

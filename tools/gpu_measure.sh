@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
-# Round-5 measurement set: full GPU suite, smoke, the bench line, rocprofv3 kernel stats + one
+# Round measurement set: full GPU suite, smoke, the bench line, rocprofv3 kernel stats + one
 # train step trace, the family kernel times the bench reads, PMC HBM traffic, per-layer tables.
-#   tools/gpu_r05_final.sh <tag>
+#   tools/gpu_measure.sh <tag>
 set -uo pipefail
-TAG=${1:-r05}
+TAG=${1:-r06}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/$TAG
