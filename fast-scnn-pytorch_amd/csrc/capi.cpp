@@ -1,4 +1,5 @@
 // extern "C" boundary of libfastscnn_hip.so (declared in include/fastscnn.h).
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>

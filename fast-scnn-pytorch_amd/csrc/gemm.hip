@@ -557,6 +557,11 @@ int gemm_nt(const GemmArgs& a, int dtype, hipStream_t st) {
     set_error("gemm_nt: empty problem M=%d N=%d K=%d", a.M, a.N, a.K);
     return E_INVALID;
   }
+  // C null: a statistics-only pass (the BN records of an output that is recomputed, not stored)
+  if (!a.C && !(a.part && !a.R && !a.bpart && gemm_stream_ok(a, dtype))) {
+    set_error("gemm_nt: no output (statistics only) needs the streaming kernel with statistics");
+    return E_UNSUPPORTED;
+  }
   if (a.lda % V || (uintptr_t)a.A % 16 || (uintptr_t)a.B % 16 || a.ldb % V) {
     set_error("gemm_nt: operands must be 16-B aligned with ld multiple of %d (lda=%d ldb=%d)", V,
               a.lda, a.ldb);

@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
               o[r] = dropout_keep(dseed, nchw, a.drop_thr) ? round_as<T>(o[r]) * dscale : 0.f;
             }
           }
-          if (mok) st4v(Cp + mr * a.ldc + n0 + nl, o);
+          if (mok && Cp) st4v(Cp + mr * a.ldc + n0 + nl, o);  // (C null: statistics only)
           if constexpr (BS) {  // partials of the value as stored, masked by that BN's ReLU
             const float4 bm = *reinterpret_cast<const float4*>(sbc + nl);
             const float4 bv = *reinterpret_cast<const float4*>(sbc + BN + nl);
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(GemmArgs a, int bpg
             if (n >= a.N) continue;
             float v = acc[mt][nt][r] * ssc[nl + r] + ssc[BN + nl + r];
             if (Rp) v += ld1(Rp + (size_t)m * a.ldr + n);
-            st1(Cp + (size_t)m * a.ldc + n, a.relu ? fmaxf(v, 0.f) : v);
+            if (Cp) st1(Cp + (size_t)m * a.ldc + n, a.relu ? fmaxf(v, 0.f) : v);
           }
         }
       }

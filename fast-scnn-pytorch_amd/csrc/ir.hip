@@ -485,4 +485,321 @@ int ir_block_fwd(const IrArgs& a0, int dtype, hipStream_t st) {
   return check_launch("ir_block_fwd");
 }
 
+// ================================================================================================
+// Training form of the bottleneck's first two layers (models/fast_scnn.py:102-107: expand
+// _ConvBNReLU + depthwise _DWConv's conv), recomputing the 6x-expanded tensor instead of storing
+// it.  Train-mode BatchNorm needs the expand output's batch statistics before anything can be
+// normalised, so the expand runs twice: a statistics-only pass (the streaming GEMM with no output
+// stores, gemm_stream.hip) finishes BN_e, then this launch recomputes the expand per tile, applies
+// BN_e + ReLU in LDS and runs the depthwise 3x3 on it, storing only the depthwise's pre-BN output
+// (the unfused path's dw z, bit-identical: same MFMA k order as the streaming GEMM, same rounding
+// of the expand output to the storage type, bn_apply's relu(fmaf(z, scale, shift)) rounded to the
+// storage type, the depthwise's tap order) and one (mean, M2, count) record per workgroup and
+// channel for BN_d (statistics of the stored values).  The 201 MB (bottleneck1.0, cfg3) expand
+// output is neither written nor read back; the backward recomputes it (net.cpp).
+// 16-bit plans only (bf16 / fp16: one MFMA per operand pair).
+// ================================================================================================
+constexpr int IRT_PRM = IR_EC * 9 + 2 * IR_EC;  // per-chunk depthwise weights + BN_e (scale, shift)
+
+template <typename T, int S>
+__host__ __device__ constexpr size_t ir_train_lds(int KS) {
+  using G = IrTile<S>;
+  return (size_t)G::XROWS * (32 * KS + 16) * 2  // input tile
+         + (size_t)G::ROWS * IR_ELD * 4           // expand chunk (fp32)
+         + G::ROWS * 4                            // halo validity
+         + (size_t)2 * IRT_PRM * 4                // chunk parameters, double-buffered
+         + (size_t)IR_WAVES * IR_EC * 4 + IR_EC * 4;  // statistics rows + channel means
+}
+
+template <typename T, int KS, int S>
+__global__ __launch_bounds__(IR_THREADS) void ir_train_fwd_kernel(IrArgs a) {
+  using G = IrTile<S>;
+  constexpr int IR_TH = G::TH, IR_TW = G::TW, IR_HW = G::HW, IR_HALO = G::HALO, IR_RT = G::RT;
+  constexpr int IR_ROWS = G::ROWS, IR_XROWS = G::XROWS, NPT = G::NPT;
+  constexpr int CIN = 32 * KS;
+  constexpr int XLD = CIN + 16;
+  constexpr int RPW = G::RPW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  uint16_t* sX = reinterpret_cast<uint16_t*>(s_dyn);                      // [101][XLD]
+  float* sE = reinterpret_cast<float*>(sX + (size_t)IR_XROWS * XLD);      // [ROWS][IR_ELD]
+  float* sV = sE + IR_ROWS * IR_ELD;                                      // [ROWS] 1 = in image
+  float* sPrm = sV + IR_ROWS;                                             // [2][IRT_PRM]
+  float* sRed = sPrm + 2 * IRT_PRM;                                       // [8 waves][64]
+  float* sMean = sRed + IR_WAVES * IR_EC;                                 // [64]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lq = lane >> 4;
+  const int tiles_x = cdiv(a.W, IR_TW), tiles_y = cdiv(a.H, IR_TH);
+  int t = blockIdx.x;
+  const int n = t / (tiles_x * tiles_y);
+  t -= n * tiles_x * tiles_y;
+  const int y0 = (t / tiles_x) * IR_TH, x0 = (t % tiles_x) * IR_TW;
+  const T* X = (const T*)a.x;
+  const T* We = (const T*)a.we;
+  const int ect = wave & 3, erh = (wave >> 2) * RPW;
+  const int dq = tid & 15, dg = tid >> 4;
+  const int doy = dg / (IR_TW / NPT), dox = (dg % (IR_TW / NPT)) * NPT;
+  // valid output pixels of the tile (the BN_d record's count) and of this thread
+  const int vh = min(IR_TH, a.H - y0), vw = min(IR_TW, a.W - x0);
+  const float cnt = (float)(vh * vw);
+  bool pv[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) pv[i] = doy < vh && dox + i < vw;
+
+  uint4 rwe[KS];
+  float rprm[2];
+  auto fetch_we = [&](int e0) {
+    const int erow = e0 + ect * 16 + li;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      rwe[s] = *reinterpret_cast<const uint4*>(We + (size_t)erow * CIN + 32 * s + 8 * lq);
+  };
+  // parameter entries tid and tid + 512: entry i < 576 is wd[e0 * 9 + i], then BN_e scale, shift
+  const float* psrc[2];
+  int pmul[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * IR_THREADS;
+    if (i < IR_EC * 9) {
+      psrc[u] = a.wd + i;
+      pmul[u] = 9;
+    } else {
+      const int j = min(i, IRT_PRM - 1) - IR_EC * 9, tab = j / IR_EC, c = j - tab * IR_EC;
+      psrc[u] = (tab == 0 ? a.sc_e : a.sh_e) + c;
+      pmul[u] = 1;
+    }
+  }
+  auto fetch_prm = [&](int e0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) rprm[u] = psrc[u][(size_t)e0 * pmul[u]];
+  };
+  auto put_prm = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * IR_THREADS;
+      if (i < IRT_PRM) sPrm[buf * IRT_PRM + i] = rprm[u];
+    }
+  };
+
+  fetch_we(0);
+  fetch_prm(0);
+  put_prm(0);
+  // ---- stage the haloed input tile (the producer's lazily applied BN + ReLU when given) -------
+  {
+    constexpr int VPR = CIN / 8;
+    for (int i = tid; i < IR_XROWS * VPR; i += IR_THREADS) {
+      const int r = i / VPR, v = i - r * VPR;
+      const int hy = r / IR_HW, hx = r - hy * IR_HW;
+      const int gy = S * y0 - 1 + hy, gx = S * x0 - 1 + hx;
+      const bool ok = r < IR_HALO && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi;
+      const size_t off = ok ? (((size_t)n * a.Hi + gy) * a.Wi + gx) * a.ldx + v * 8 : 0;
+      uint4 q = *reinterpret_cast<const uint4*>(X + off);
+      if (a.x_scale) q = bnrelu_vec<T>(q, a.x_scale + v * 8, a.x_shift + v * 8);
+      *reinterpret_cast<uint4*>(sX + (size_t)r * XLD + v * 8) = sel4(ok, q);
+      if (v == 0) sV[r] = ok ? 1.f : 0.f;
+    }
+    for (int r = IR_XROWS + tid; r < IR_ROWS; r += IR_THREADS) sV[r] = 0.f;
+  }
+
+  T* Y = (T*)a.y;
+  const int nchunks = a.E / IR_EC;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int e0 = ch * IR_EC;
+    const float* prm = sPrm + (ch & 1) * IRT_PRM;
+    uint4 we[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) we[s] = rwe[s];
+    if (ch + 1 < nchunks) {
+      fetch_we(e0 + IR_EC);  // in flight during this chunk
+      fetch_prm(e0 + IR_EC);
+    }
+    __syncthreads();  // input tile + this chunk's parameters staged; sE free
+    // ---- expand, rounded to the storage type (the unfused z), BN_e + ReLU, halo zeroed ----------
+    {
+      f32x4 acc[RPW];
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+          const int rt = min(erh + j, IR_RT - 1);
+          const int row = min(rt * 16 + li, IR_HALO);
+          uint4 b[1];
+          b[0] = *reinterpret_cast<const uint4*>(sX + (size_t)row * XLD + 32 * s + 8 * lq);
+          uint4 w1[1] = {we[s]};
+          ir_mma<T>(w1, b, acc[j]);
+        }
+      const int c = ect * 16 + 4 * lq;
+      const float4 sc = *reinterpret_cast<const float4*>(prm + IR_EC * 9 + c);
+      const float4 sh = *reinterpret_cast<const float4*>(prm + IR_EC * 10 + c);
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        const int rt = min(erh + j, IR_RT - 1);
+        const int px = rt * 16 + li;
+        const float valid = sV[px];
+        float4 o;
+        o.x = valid * round_as<T>(fmaxf(fmaf(round_as<T>(acc[j][0]), sc.x, sh.x), 0.f));
+        o.y = valid * round_as<T>(fmaxf(fmaf(round_as<T>(acc[j][1]), sc.y, sh.y), 0.f));
+        o.z = valid * round_as<T>(fmaxf(fmaf(round_as<T>(acc[j][2]), sc.z, sh.z), 0.f));
+        o.w = valid * round_as<T>(fmaxf(fmaf(round_as<T>(acc[j][3]), sc.w, sh.w), 0.f));
+        *reinterpret_cast<float4*>(sE + (size_t)px * IR_ELD + c) = o;
+      }
+    }
+    __syncthreads();
+    // ---- depthwise 3x3 of the chunk: pre-BN output stored, its statistics per channel ---------
+    float v[NPT][4];
+    {
+      float w[4][9];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) w[j][k] = prm[(4 * dq + j) * 9 + k];
+      constexpr int NC = S * (NPT - 1) + 3;
+      float4 xv[3][NC];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          xv[kh][c] = *reinterpret_cast<const float4*>(
+              sE + (size_t)((S * doy + kh) * IR_HW + S * dox + c) * IR_ELD + 4 * dq);
+      float acc[NPT][4];
+#pragma unroll
+      for (int i = 0; i < NPT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int i = 0; i < NPT; ++i) {
+            const float4 q = xv[kh][S * i + kw];
+            const float qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(qq[j], w[j][kh * 3 + kw], acc[i][j]);
+          }
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] = round_as<T>(acc[i][j]);
+        if (pv[i]) {
+          const size_t pix = ((size_t)n * a.H + y0 + doy) * a.W + x0 + dox + i;
+          st4v(Y + pix * a.ldy + e0 + 4 * dq, v[i]);
+        }
+      }
+    }
+    if (ch + 1 < nchunks) put_prm((ch + 1) & 1);  // (its last readers finished chunk ch - 1)
+    // ---- BN_d record of the chunk: mean over the tile's valid pixels, then M2 ------------------
+    float s4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) s += pv[i] ? v[i][j] : 0.f;
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      s4[j] = s;
+    }
+    if (lq == 0) *reinterpret_cast<float4*>(sRed + wave * IR_EC + 4 * dq) = make_float4(s4[0], s4[1], s4[2], s4[3]);
+    __syncthreads();
+    if (tid < IR_EC) {
+      float s = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < IR_WAVES; ++w8) s += sRed[w8 * IR_EC + tid];
+      sMean[tid] = s / cnt;
+    }
+    __syncthreads();
+    {
+      const float4 mu = *reinterpret_cast<const float4*>(sMean + 4 * dq);
+      const float m4[4] = {mu.x, mu.y, mu.z, mu.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+          const float d = v[i][j] - m4[j];
+          s += pv[i] ? d * d : 0.f;
+        }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        s4[j] = s;
+      }
+    }
+    __syncthreads();  // every thread read sMean / the sums rows
+    if (lq == 0) *reinterpret_cast<float4*>(sRed + wave * IR_EC + 4 * dq) = make_float4(s4[0], s4[1], s4[2], s4[3]);
+    __syncthreads();
+    if (tid < IR_EC) {
+      float m2 = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < IR_WAVES; ++w8) m2 += sRed[w8 * IR_EC + tid];
+      float* rec = a.part + (size_t)blockIdx.x * 3 * a.E + e0 + tid;
+      rec[0] = sMean[tid];
+      rec[a.E] = m2;
+      rec[2 * a.E] = cnt;
+    }
+  }
+}
+
+bool ir_train_ok(const IrArgs& a0, int dtype) {
+  IrArgs a = a0;
+  if (a.Hi <= 0) { a.Hi = a.H; a.Wi = a.W; }
+  if (dtype != DT_BF16 && dtype != DT_F16) return false;
+  const int KS = a.Cin / 32;
+  if (a.Cin % 32 || KS < 2 || KS > 4 || a.E % IR_EC || a.E <= 0 || a.H < 1 || a.W < 1 ||
+      a.N < 1 || !a.part || !a.sc_e || !a.sh_e || !a.wd || !a.we || !a.x || !a.y)
+    return false;
+  if (a.stride != 1 && a.stride != 2) return false;
+  if (a.stride == 1 ? (a.Hi != a.H || a.Wi != a.W)
+                    : (a.H != (a.Hi - 1) / 2 + 1 || a.W != (a.Wi - 1) / 2 + 1))
+    return false;
+  if (a.ldx % 8 || a.ldx < a.Cin || a.ldy < a.E || a.ldy % 4) return false;
+  if (((uintptr_t)a.x & 15) || ((uintptr_t)a.we & 15) || ((uintptr_t)a.y & 7)) return false;
+  if ((a.x_scale == nullptr) != (a.x_shift == nullptr)) return false;
+  const size_t lds = a.stride == 1 ? ir_train_lds<bf16, 1>(KS) : ir_train_lds<bf16, 2>(KS);
+  return lds <= 160 * 1024 - 1024;
+}
+
+long long ir_train_parts(int N, int H, int W, int stride) {
+  const int TH = stride == 2 ? IrTile<2>::TH : IrTile<1>::TH, TW = stride == 2 ? IrTile<2>::TW : IrTile<1>::TW;
+  return (long long)N * cdiv(H, TH) * cdiv(W, TW);
+}
+
+template <typename T, int S>
+static void ir_train_launch_s(const IrArgs& a, dim3 grid, hipStream_t st) {
+  switch (a.Cin / 32) {
+    case 2: prof_launch(ir_train_fwd_kernel<T, 2, S>, grid, IR_THREADS, ir_train_lds<T, S>(2), st, a); break;
+    case 3: prof_launch(ir_train_fwd_kernel<T, 3, S>, grid, IR_THREADS, ir_train_lds<T, S>(3), st, a); break;
+    default: prof_launch(ir_train_fwd_kernel<T, 4, S>, grid, IR_THREADS, ir_train_lds<T, S>(4), st, a); break;
+  }
+}
+
+int ir_train_fwd(const IrArgs& a0, int dtype, hipStream_t st) {
+  IrArgs a = a0;
+  if (a.Hi <= 0) { a.Hi = a.H; a.Wi = a.W; }
+  if (!ir_train_ok(a, dtype)) {
+    set_error("ir_train_fwd: unsupported block (dtype %d Cin %d E %d ldx %d ldy %d stride %d)",
+              dtype, a.Cin, a.E, a.ldx, a.ldy, a.stride);
+    return E_UNSUPPORTED;
+  }
+  const long long tiles = ir_train_parts(a.N, a.H, a.W, a.stride);
+  if (tiles > 0x7fffffffLL) {
+    set_error("ir_train_fwd: grid too large");
+    return E_UNSUPPORTED;
+  }
+  const dim3 grid((unsigned)tiles);
+  const double M = (double)a.N * a.H * a.W, Mi = (double)a.N * a.Hi * a.Wi;
+  ProfScope ps(PK_IR, st, 2.0 * (Mi * a.Cin + M * a.E) + 2.0 * a.E * a.Cin + 4.0 * 9 * a.E,
+               2.0 * Mi * a.E * a.Cin + 18.0 * M * a.E);
+  if (dtype == DT_F16) {
+    if (a.stride == 2) ir_train_launch_s<f16, 2>(a, grid, st);
+    else ir_train_launch_s<f16, 1>(a, grid, st);
+  } else {
+    if (a.stride == 2) ir_train_launch_s<bf16, 2>(a, grid, st);
+    else ir_train_launch_s<bf16, 1>(a, grid, st);
+  }
+  return check_launch("ir_train_fwd");
+}
+
 }  // namespace fscnn

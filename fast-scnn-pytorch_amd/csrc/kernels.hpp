@@ -402,9 +402,18 @@ struct IrArgs {
   // ([3][E][Cin], [3][Cout][E]; weights_prep mode 3), or null (the kernel splits them)
   const uint16_t* we3 = nullptr;
   const uint16_t* wp3 = nullptr;
+  // training form (ir_train_fwd: expand recomputed + depthwise, no project): the input's lazily
+  // applied BN + ReLU (or null), sc_e / sh_e = BN_e's batch-statistics table, y = the depthwise's
+  // pre-BN output [N,H,W][ldy] and part = its BN records [tiles][3][E]
+  const float* x_scale = nullptr;
+  const float* x_shift = nullptr;
+  float* part = nullptr;
 };
 bool ir_block_ok(const IrArgs& a, int dtype);
 int ir_block_fwd(const IrArgs& a, int dtype, hipStream_t st);
+bool ir_train_ok(const IrArgs& a, int dtype);
+long long ir_train_parts(int N, int H, int W, int stride);
+int ir_train_fwd(const IrArgs& a, int dtype, hipStream_t st);
 
 // inference LearningToDownsample stem (stem.hip): conv0 + BN + ReLU -> dsconv1.dw + BN + ReLU ->
 // dsconv1.pw + BN + ReLU in one launch (models/fast_scnn.py:153-154), BatchNorms folded

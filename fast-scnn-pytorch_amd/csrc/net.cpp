@@ -195,9 +195,16 @@ bool ir_block_shape(const Net& net, const Plan& pl, int i, IrArgs& b) {
   return ir_stride2_enabled() || l.stride == 1 ? tiles >= 128 && ir_block_ok(b, pl.dtype) : false;
 }
 
-namespace {
-
-}  // namespace
+// FSCNN_IR_TRAIN: training plans recompute the 6x-expanded tensor of these bottlenecks instead
+// of storing it (ir.hip ir_train_fwd + a statistics-only expand pass; the backward recomputes it):
+// 0 none, 1 bottleneck1 (default: the 201 / 50 / 50 MB tensors at cfg3), 2 every bottleneck
+static int ir_train_blocks() {
+  static const int v = [] {
+    const char* e = getenv("FSCNN_IR_TRAIN");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 
 int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& pl) {
   if (N < 1 || H < 3 || W < 3) {
@@ -261,7 +268,9 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
     int Ho = i < 3 ? pl.H4 : pl.H5, Wo = i < 3 ? pl.W4 : pl.W5;
     int e = l.cin * 6;
     unit(pl.lbe[i], Min, e, gemm_parts((int)Min));
-    unit(pl.lbd[i], Mout, e, dw_parts(N, Ho, Wo, e, dtype, l.stride));
+    // (the training form of ir.hip writes one BN_d record per output tile)
+    unit(pl.lbd[i], Mout, e, std::max<int>(dw_parts(N, Ho, Wo, e, dtype, l.stride),
+                                          (int)ir_train_parts(N, Ho, Wo, l.stride)));
     if (i == 8) unit(pl.lbp[i], Mout, l.cout, gemm_parts((int)Mout), pl.concat, 256);
     else unit(pl.lbp[i], Mout, l.cout, gemm_parts((int)Mout));
   }
@@ -1100,8 +1109,14 @@ struct Exec {
         Hc = Ho; Wc = Wo;
         continue;
       }
-      TRY(pw(pl.lbe[i], l.e, &l.be, i == 0 ? act(pl.l2pw) : raw(x, xld), true));
-      TRY(dw(pl.lbd[i], l.d, l.bd, act(pl.lbe[i]), Hc, Wc, Ho, Wo, l.stride));
+      IrArgs tb;
+      const In xin = i == 0 ? act(pl.l2pw) : raw(x, xld);
+      if (irt_shape(i, xin, tb)) {
+        TRY(irt_forward(i, xin, tb));
+      } else {
+        TRY(pw(pl.lbe[i], l.e, &l.be, xin, true));
+        TRY(dw(pl.lbd[i], l.d, l.bd, act(pl.lbe[i]), Hc, Wc, Ho, Wo, l.stride));
+      }
       bool shortcut = l.stride == 1 && l.cin == l.cout;
       TRY(pw(pl.lbp[i], l.p, &l.bp, act(pl.lbd[i]), false, shortcut ? x : nullptr,
              shortcut ? xld : 0));
@@ -1282,6 +1297,68 @@ struct Exec {
     u.N = N; u.Hi = pl.H3; u.Wi = pl.W3; u.C = net.num_classes; u.Ho = pl.H; u.Wo = pl.W;
     u.x = W(pl.logits); u.ldx = pl.Cp; u.y = r.out; u.ldy = 0;
     return up_nchw(u, dt, r.out_dtype, r.st);
+  }
+
+  // ---- training bottleneck with the expanded tensor recomputed (ir.hip ir_train_fwd) ----------
+  // (models/fast_scnn.py:102-107) 16-bit training plans, the blocks ir_train_blocks() selects
+  bool irt_shape(int i, const In& xin, IrArgs& b) const {
+    const int sel = ir_train_blocks();
+    if (pl.train != 1 || frozen || dt == DT_F32 || sel == 0 || (sel == 1 && i >= 3)) return false;
+    const LbL& l = net.lb[i];
+    b = IrArgs{};
+    b.N = pl.N; b.stride = l.stride;
+    b.H = i < 3 ? pl.H4 : pl.H5; b.W = i < 3 ? pl.W4 : pl.W5;
+    b.Hi = i == 0 ? pl.H3 : (i < 4 ? pl.H4 : pl.H5);
+    b.Wi = i == 0 ? pl.W3 : (i < 4 ? pl.W4 : pl.W5);
+    b.Cin = l.cin; b.E = l.cin * 6; b.Cout = l.cout;
+    b.x = xin.p; b.ldx = xin.ld; b.x_scale = xin.sc; b.x_shift = xin.sh;
+    b.we = Wg(l.e); b.wd = P(l.d.w);
+    b.sc_e = Wf(pl.lbe[i].scale); b.sh_e = Wf(pl.lbe[i].shift);
+    b.y = W(pl.lbd[i].z); b.ldy = b.E; b.part = Wf(pl.lbd[i].part);
+    // the statistics-only pass needs the streaming GEMM (M >= 4096 pixels)
+    GemmArgs g = expand_args(i, xin);
+    g.part = Wf(pl.lbe[i].part);
+    return ir_train_parts(b.N, b.H, b.W, b.stride) <= pl.lbd[i].nparts && ir_train_ok(b, dt) &&
+           gemm_stream_ok(g, dt);
+  }
+  // the expand conv as a GEMM over the block input (statistics only, or the recompute)
+  GemmArgs expand_args(int i, const In& xin) const {
+    const LbL& l = net.lb[i];
+    const Unit& ue = pl.lbe[i];
+    GemmArgs g{};
+    g.M = (int)ue.M; g.N = ue.C; g.K = l.cin;
+    g.A = xin.p; g.lda = xin.ld; g.a_scale = xin.sc; g.a_shift = xin.sh;
+    g.B = Wg(l.e); g.ldb = l.cin;
+    g.shift = P(l.e.b);
+    g.ldc = ue.C;
+    return g;
+  }
+  int irt_forward(int i, const In& xin, IrArgs& b) {
+    const LbL& l = net.lb[i];
+    const Unit &ue = pl.lbe[i], &ud = pl.lbd[i];
+    // BN_e's batch statistics: the expand GEMM with no output (its records + in-kernel finish)
+    g_prof_tag = ue.name.c_str();
+    GemmArgs g = expand_args(i, xin);
+    g.C = nullptr;
+    gemm_fin(g, ue, l.be);
+    TRY(gemm_nt(g, dt, r.st));
+    // expand recomputed per tile -> BN_e + ReLU -> depthwise: only its pre-BN output stored
+    g_prof_tag = ud.name.c_str();
+    TRY(ir_train_fwd(b, dt, r.st));
+    BnFinalizeArgs f = fin_args(ud, l.bd);
+    f.P = (int)ir_train_parts(b.N, b.H, b.W, b.stride);
+    return bn_finalize(f, r.st);
+  }
+  // the backward's copy of the expand output the forward never stored: the same GEMM (same MFMA
+  // k order, rounded to the storage type) as the statistics pass, with its output
+  int irt_recompute(int i) {
+    const In xin = i == 0 ? act(pl.l2pw) : raw(W(pl.lbp[i - 1].a), pl.lbp[i - 1].ld);
+    IrArgs tb;
+    if (!irt_shape(i, xin, tb)) return OK;
+    g_prof_tag = pl.lbe[i].name.c_str();
+    GemmArgs g = expand_args(i, xin);
+    g.C = W(pl.lbe[i].z);
+    return gemm_nt(g, dt, r.st);
   }
 
   // FFM conv_higher_res (models/fast_scnn.py:202) + its BN statistics (train): on the side
@@ -1766,6 +1843,7 @@ struct Exec {
     int gxld = i == 0 ? 64 : pl.lbp[i - 1].ga_ld;
     bool shortcut = l.stride == 1 && l.cin == l.cout;
     const int e = l.cin * 6;
+    TRY(irt_recompute(i));  // (the expanded tensor, when the forward did not store it)
     // up's dy was produced by block i+1's expand dgrad with fused partials (not for the last
     // block: its dy is the PPM concat gradient)
     Dz d;

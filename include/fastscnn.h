@@ -304,8 +304,9 @@ int fscnn_block_ffm_fwd(const void* low, int dtype, int N, int Hi, int Wi, int H
  * branch convs + BN + ReLU, one launch each way), 16 ir_block (fused inference bottleneck),
  * 17 ltd_stem (fused inference stem), 18 dsconv (fused inference DSConv);
  * 100 = every kind.
- * Between begin and end every launch of that kernel family is bracketed by hipEvents on its own
- * stream; end synchronises and returns summed kernel ms, launch count and the algorithmic bytes
+ * Between begin and end every launch of that kernel family is bracketed by hipEvents bound to its
+ * dispatch (hipExtLaunchKernelGGL); end synchronises and returns summed kernel ms,
+ * launch count and the algorithmic bytes
  * and flops of those launches (SURVEY.md §8(d) formulas); fscnn_prof_launch then returns launch
  * i's kind, ms, bytes, flops and layer (reference module name; issue order). */
 int fscnn_prof_begin(int kind, int max_launches);
