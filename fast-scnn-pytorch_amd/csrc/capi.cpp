@@ -1,5 +1,7 @@
 // extern "C" boundary of libfastscnn_hip.so (declared in include/fastscnn.h).
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -48,6 +50,33 @@ struct ProfState {
   hipStream_t arm_st = nullptr;
 } g_prof;
 }  // namespace
+
+bool g_host_prof = [] {
+  const char* e = getenv("FSCNN_HOST_PROF");
+  return e && e[0] == '1';
+}();
+namespace {
+struct HostProf {
+  double us[4] = {0, 0, 0, 0};
+  long long n[4] = {0, 0, 0, 0};
+  ~HostProf() {
+    if (!g_host_prof) return;
+    static const char* names[4] = {"kernel launches", "side-stream forks", "side-stream joins",
+                                   "C entry points (total)"};
+    for (int i = 0; i < 4; ++i)
+      fprintf(stderr, "FSCNN_HOST_PROF %-24s %10lld calls %12.1f us  (%.2f us each)\n", names[i],
+              n[i], us[i], n[i] ? us[i] / n[i] : 0.0);
+  }
+} g_hostp;
+}  // namespace
+double host_now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void host_prof_add(int what, double us) {
+  g_hostp.us[what] += us;
+  g_hostp.n[what]++;
+}
 
 // A scope arms its event pair for the first prof_launch inside it (kernel-bound events); a scope
 // whose launch does not take them (none issued) falls back to marker events around the scope.

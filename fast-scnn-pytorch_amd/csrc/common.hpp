@@ -488,13 +488,19 @@ struct ProfScope {
 // reads), not marker packets around it (each of which idles the stream ~7 us).  Otherwise it is a
 // plain launch.
 bool prof_take_ext(hipEvent_t& e0, hipEvent_t& e1);
+// FSCNN_HOST_PROF=1 (diagnostics): host time spent in launches / stream forks, printed at exit
+extern bool g_host_prof;
+void host_prof_add(int what, double us);
+double host_now_us();
 template <typename F, typename... A>
 inline void prof_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, A... args) {
   hipEvent_t e0, e1;
+  const double t0 = g_host_prof ? host_now_us() : 0.0;
   if (prof_take_ext(e0, e1))
     hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, e0, e1, 0u, args...);
   else
     hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+  if (g_host_prof) host_prof_add(0, host_now_us() - t0);
 }
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -222,7 +222,12 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
     }
     stamp(a.stamps, 3);
     if (a.part == nullptr) continue;
-    // ---- per-channel (mean, M2) of the row's npx pixels: the values as stored (rounded to TO) --
+    // ---- per-channel (mean, M2) of the row's npx pixels: the values as stored (16-bit: read back
+    // from the staged output tile, so the fp32 accumulators die at the store) ------------------
+    auto stored = [&](int gi, int jt, int q) -> float {
+      if constexpr (BF) return s16_to<TO>(s_out[(wave * 64 + gi * 16 + 4 * lq + q) * OST + 16 * jt + li].x);
+      else return acc[gi][jt][q];
+    };
     float sum[2] = {0.f, 0.f};
 #pragma unroll
     for (int gi = 0; gi < 4; ++gi)
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
       for (int q = 0; q < 4; ++q) {
         const bool ok = wave * 64 + gi * 16 + 4 * lq + q < npx;
 #pragma unroll
-        for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? round_as<TO>(acc[gi][jt][q]) : 0.f;
+        for (int jt = 0; jt < 2; ++jt) sum[jt] += ok ? stored(gi, jt, q) : 0.f;
       }
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(Conv0Args a) {
         const bool ok = wave * 64 + gi * 16 + 4 * lq + q < npx;
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt) {
-          const float d = round_as<TO>(acc[gi][jt][q]) - mean[jt];
+          const float d = stored(gi, jt, q) - mean[jt];
           m2[jt] += ok ? d * d : 0.f;
         }
       }

@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
         for (int j = 0; j < 4; ++j) {
           const float t = acc[r][p][j] * sc[j] + sh[j];
           o[j] = a.relu ? fmaxf(t, 0.f) : t;
-          acc[r][p][j] = o[j];
+          acc[r][p][j] = round_as<T>(o[j]);  // (the statistics below: of the stored value)
         }
         quad_st(yb + (size_t)p * a.C, o);
       }
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
 #pragma unroll
     for (int r = 0; r < G::HS; ++r)
 #pragma unroll
-      for (int p = 0; p < G::WS; ++p) sum += (r < nrow && p < ncol) ? round_as<T>(acc[r][p][j]) : 0.f;
+      for (int p = 0; p < G::WS; ++p) sum += (r < nrow && p < ncol) ? acc[r][p][j] : 0.f;
     s_red[(grp * QB + q) * 4 + j] = sum;
   }
   __syncthreads();
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256, 3) void dw_fwd_kernel(DwArgs a, int cbv) {
     for (int r = 0; r < G::HS; ++r)
 #pragma unroll
       for (int p = 0; p < G::WS; ++p) {
-        const float d = round_as<T>(acc[r][p][j]) - mean[j];
+        const float d = acc[r][p][j] - mean[j];
         m2 += (r < nrow && p < ncol) ? d * d : 0.f;
       }
     s_red[(grp * QB + q) * 4 + j] = m2;

@@ -438,6 +438,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 
   // ---- train-mode BN statistics of the output tile as stored (per column: mean, M2, count) -
   const int valid_rows = min(G_BM, a.M - m0);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = round_as<T>(acc[mt][nt][r]);
   float mean_c[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -447,7 +453,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
-        s += (m < a.M) ? round_as<T>(acc[mt][nt][r]) : 0.f;
+        s += (m < a.M) ? acc[mt][nt][r] : 0.f;
       }
     s += __shfl_xor(s, 16);
     s += __shfl_xor(s, 32);
@@ -468,7 +474,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int m = m0 + wave * 32 + mt * 16 + lq * 4 + r;
-        float d = round_as<T>(acc[mt][nt][r]) - mean_c[nt];
+        float d = acc[mt][nt][r] - mean_c[nt];
         s += (m < a.M) ? d * d : 0.f;
       }
     s += __shfl_xor(s, 16);

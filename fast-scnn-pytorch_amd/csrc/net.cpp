@@ -197,11 +197,15 @@ bool ir_block_shape(const Net& net, const Plan& pl, int i, IrArgs& b) {
 
 // FSCNN_IR_TRAIN: training plans recompute the 6x-expanded tensor of these bottlenecks instead
 // of storing it (ir.hip ir_train_fwd + a statistics-only expand pass; the backward recomputes it):
-// 0 none, 1 bottleneck1 (default: the 201 / 50 / 50 MB tensors at cfg3), 2 every bottleneck
+// 0 none (default), 1 bottleneck1 (the 201 / 50 / 50 MB tensors at cfg3), 2 every bottleneck.
+// Measured r06 (cfg3 bf16, same box, two pairs): 6.028 / 6.035 ms per step with bottleneck1
+// recomputed vs 5.815 / 5.815 stored -- the statistics-only expand costs 76 of the stored
+// expand's 103 us (its epilogue's statistics, not its stores, dominate), the fused tile kernel
+// 113 us against the depthwise's 91, and the backward's recompute another 137 us
 static int ir_train_blocks() {
   static const int v = [] {
     const char* e = getenv("FSCNN_IR_TRAIN");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -598,13 +602,19 @@ struct SideStream {
   }
   // the side stream waits for everything enqueued on `main` so far
   bool fork_from(hipStream_t main) {
+    const double t0 = g_host_prof ? host_now_us() : 0.0;
     std::lock_guard<std::mutex> lock(mu);
-    return hipEventRecord(fork, main) == hipSuccess && hipStreamWaitEvent(s, fork, 0) == hipSuccess;
+    const bool ok = hipEventRecord(fork, main) == hipSuccess && hipStreamWaitEvent(s, fork, 0) == hipSuccess;
+    if (g_host_prof) host_prof_add(1, host_now_us() - t0);
+    return ok;
   }
   // `main` waits for everything enqueued on the side stream so far
   bool join_into(hipStream_t main) {
+    const double t0 = g_host_prof ? host_now_us() : 0.0;
     std::lock_guard<std::mutex> lock(mu);
-    return hipEventRecord(join, s) == hipSuccess && hipStreamWaitEvent(main, join, 0) == hipSuccess;
+    const bool ok = hipEventRecord(join, s) == hipSuccess && hipStreamWaitEvent(main, join, 0) == hipSuccess;
+    if (g_host_prof) host_prof_add(2, host_now_us() - t0);
+    return ok;
   }
   ~SideStream() {
     hipEvent_t ev[2] = {fork, join};
@@ -2068,7 +2078,14 @@ int run_graphed(const Plan& pl, std::vector<uint64_t> key, hipStream_t st, F&& b
 
 }  // namespace
 
+int net_forward_impl(const Plan& pl, const RunArgs& r);
 int net_forward(const Plan& pl, const RunArgs& r) {
+  const double t0 = g_host_prof ? host_now_us() : 0.0;
+  const int rc = net_forward_impl(pl, r);
+  if (g_host_prof) host_prof_add(3, host_now_us() - t0);
+  return rc;
+}
+int net_forward_impl(const Plan& pl, const RunArgs& r) {
   if (r.x_dtype < DT_F32 || r.x_dtype > DT_F16 || r.out_dtype < DT_F32 || r.out_dtype > DT_F16) {
     set_error("fscnn_forward: input / output dtype codes must be 0 (fp32), 1 (bf16) or 2 (fp16)");
     return E_INVALID;
@@ -2099,7 +2116,14 @@ int net_forward(const Plan& pl, const RunArgs& r) {
 
 // stages: 0 = head (upsample, classifier, FFM, PPM), 1 = bottleneck3, 2 = bottleneck2,
 //         3 = bottleneck1 + LearningToDownsample
+int net_backward_impl(const Plan& pl, const RunArgs& r, int stage_from, int stage_to);
 int net_backward(const Plan& pl, const RunArgs& r, int stage_from, int stage_to) {
+  const double t0 = g_host_prof ? host_now_us() : 0.0;
+  const int rc = net_backward_impl(pl, r, stage_from, stage_to);
+  if (g_host_prof) host_prof_add(3, host_now_us() - t0);
+  return rc;
+}
+int net_backward_impl(const Plan& pl, const RunArgs& r, int stage_from, int stage_to) {
   if (!pl.train) {
     set_error("net_backward: the plan was built for inference (train=0)");
     return E_INVALID;
