@@ -10,6 +10,7 @@ the kernel-only durations bench.py reports beside its event-timed roofline.
 """
 import csv
 import json
+import re
 import sys
 
 FAMILIES = [
@@ -29,6 +30,10 @@ FAMILIES = [
 
 def family(name):
     short = name.split("<")[0].split("(")[0].replace("void ", "").replace("fscnn::", "")
+    if short == "dw_fwd_kernel":
+        # dw_fwd_kernel<T, S, FLIP, ...>: FLIP = the stride-1 input gradient (dw_dgrad family)
+        m = re.search(r"dw_fwd_kernel<[^,]+, ?\d, ?(true|false)", name)
+        return "dw_dgrad" if m and m.group(1) == "true" else "dw_fwd"
     for fam, keys in FAMILIES:
         if any(short.startswith(k) for k in keys):
             return fam
