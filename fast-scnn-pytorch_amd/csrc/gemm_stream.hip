@@ -730,9 +730,26 @@ static bool gs_x3_on() {
   return on;
 }
 
+// The largest column tile count of the statistics forms above N = 64: 4.  Their per-lane
+// shifted sums (8 NT registers) put the NT = 6 form at 256 VGPRs (2 waves per SIMD); measured
+// r06, cfg3 bf16, same box, two pairs: cap 4 5.777 / 5.771 ms per step, NT = 6 (the previous
+// choice for N % 96 == 0) 5.786 / 5.780, cap 3 5.841 / 5.808, cap 2 5.860 / 5.863.
+// FSCNN_GS_ST_NT overrides it (tuning A/B; 0: no cap).
+static int gs_st_nt_cap() {
+  static const int v = [] {
+    const char* e = getenv("FSCNN_GS_ST_NT");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 static int gs_pick_nt(const GemmArgs& a, int ks) {
   const int N = a.N;
   if (N <= 32) return 2;
+  if (a.part && ks <= 8 && N > 64 && gs_st_nt_cap() > 0) {
+    for (int nt = gs_st_nt_cap(); nt >= 2; --nt)
+      if (N % (16 * nt) == 0) return nt;
+  }
   if (ks > 8) return N % 64 == 0 ? 4 : (N % 48 == 0 ? 3 : 4);  // deep K: weights [<=64][K] in LDS
   if (N <= 48) return 3;
   if (N <= 64 || a.bpart) return 4;
