@@ -440,17 +440,19 @@ __host__ __device__ __forceinline__ int pp_start(int i, int in, int k) { return 
 __host__ __device__ __forceinline__ int pp_end(int i, int in, int k) { return ((i + 1) * in + k - 1) / k; }
 
 
-// one workgroup per (bin, image): CV = C/V channel vectors x PG = 256/CV pixel groups; every
-// thread walks its pixels of the window with 8 vector loads in flight per batch; the pixel
-// groups are combined in fixed order through LDS.
+// one workgroup per (bin, image, slice of CVL channel vectors): PG = 256/CVL pixel groups, every
+// thread walks its pixels of the window with 8 vector loads in flight per batch; the pixel groups
+// are combined by a fixed-order tree through LDS.  (r06: a workgroup per (bin, image) over all C
+// left the 2048-pixel 1x1 bins on 8 CUs walking 32 dependent load batches: 34 us at cfg2, 19 us
+// at cfg3; slices of 4 vectors put 8x / 4x as many workgroups on every bin.)
 template <typename T>
-__global__ __launch_bounds__(256) void pyramid_pool_kernel(PoolArgs a) {
+__global__ __launch_bounds__(256) void pyramid_pool_kernel(PoolArgs a, int CVL) {
   constexpr int V = VecW<T>::V;
   __shared__ float red[256 * V];
   const int b = blockIdx.x, n = blockIdx.y;
-  const int CV = a.C / V;
-  const int PG = 256 / CV;
-  const int cv = threadIdx.x % CV, g = threadIdx.x / CV;
+  const int PG = 256 / CVL;
+  const int cl = threadIdx.x % CVL, g = threadIdx.x / CVL;
+  const int cv = blockIdx.z * CVL + cl;
   int k, bi, bj;
   pp_bin(b, k, bi, bj);
   const int h0 = pp_start(bi, a.H, k), h1 = pp_end(bi, a.H, k);
@@ -483,29 +485,35 @@ __global__ __launch_bounds__(256) void pyramid_pool_kernel(PoolArgs a) {
 #pragma unroll
   for (int j = 0; j < V; ++j) red[threadIdx.x * V + j] = s[j];
   __syncthreads();
+  for (int st = PG >> 1; st > 0; st >>= 1) {  // PG is a power of two (host-checked)
+    if (g < st) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) red[threadIdx.x * V + j] += red[(threadIdx.x + st * CVL) * V + j];
+    }
+    __syncthreads();
+  }
   if (g == 0) {
     float o[V];
 #pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = 0.f;
-    for (int gg = 0; gg < PG; ++gg)
-#pragma unroll
-      for (int j = 0; j < V; ++j) o[j] += red[(gg * CV + cv) * V + j];
-#pragma unroll
-    for (int j = 0; j < V; ++j) o[j] *= inv;
+    for (int j = 0; j < V; ++j) o[j] = red[threadIdx.x * V + j] * inv;
     stv((T*)a.pooled + ((size_t)b * a.N + n) * a.C + cv * V, o);
   }
 }
 
 int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
-  if (a.C % V || a.C / V > 256 || a.ldx % V) {
+  const int CV = a.C / V;
+  // channel-vector slice per workgroup: 4 when it divides CV, else the whole row (<= 256, a
+  // power of two so the pixel groups halve evenly)
+  const int CVL = CV % 4 == 0 ? 4 : CV;
+  if (a.C % V || CV > 256 || (CVL & (CVL - 1)) || a.ldx % V) {
     set_error("pyramid_pool: C=%d ldx=%d", a.C, a.ldx);
     return E_UNSUPPORTED;
   }
-  dim3 grid(50, a.N);
-  if (dtype == DT_F32) prof_launch(pyramid_pool_kernel<float>, grid, 256, 0, st, a);
-  else if (dtype == DT_F16) prof_launch(pyramid_pool_kernel<f16>, grid, 256, 0, st, a);
-  else prof_launch(pyramid_pool_kernel<bf16>, grid, 256, 0, st, a);
+  dim3 grid(50, a.N, CV / CVL);
+  if (dtype == DT_F32) prof_launch(pyramid_pool_kernel<float>, grid, 256, 0, st, a, CVL);
+  else if (dtype == DT_F16) prof_launch(pyramid_pool_kernel<f16>, grid, 256, 0, st, a, CVL);
+  else prof_launch(pyramid_pool_kernel<bf16>, grid, 256, 0, st, a, CVL);
   return check_launch("pyramid_pool");
 }
 

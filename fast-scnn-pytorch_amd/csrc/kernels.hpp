@@ -280,7 +280,8 @@ struct PpmUpArgs {
   void* y; int ldy; int coff;
 };
 
-// PPM branch convs of the training step, one workgroup per branch (ppm.hip)
+// PPM branch convs in one launch (ppm.hip): training, one workgroup per branch; inference, one
+// wave per 16-row tile
 struct PpmBranchFwd {
   BnFinalizeArgs f;  // gamma / beta / running statistics -> mean / invstd / scale / shift
   const void* x;     // pooled rows [M][K]
@@ -292,6 +293,7 @@ struct PpmBranchFwd {
 struct PpmFwdArgs {
   PpmBranchFwd b[4];
   int nb, K, C;
+  int eval = 0;  // inference: y = relu(z * f.scale + f.shift) (folded BN), no z, no statistics
 };
 struct PpmBranchBwd {
   const void* dy; int lddy;  // gradient of y

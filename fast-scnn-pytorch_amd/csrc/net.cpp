@@ -986,6 +986,15 @@ struct Exec {
     }();
     return on;
   }
+  // inference PPM branch convs in one launch (ppm.hip); FSCNN_PPM_FUSED=0 runs the four pointwise
+  // launches (the bit-identity test, tests/test_gpu_switches.py)
+  static bool ppm_eval_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("FSCNN_PPM_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   // inference DSConv fusion (dsconv.hip: the classifier's two DSConvs, the FFM's dwconv +
   // conv_lower_res); FSCNN_DSCONV_FUSED=0 runs dw + pw as two launches (the bit-identity test,
   // tests/test_gpu_switches.py)
@@ -1154,6 +1163,21 @@ struct Exec {
           b.x = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
           b.w = Wg(net.ppm_c[i]);
           b.z = W(u.z); b.y = W(u.a); b.ldy = u.ld; b.M = (int)u.M;
+        }
+        TRY(ppm_branches_fwd(f, dt, r.st));
+      } else if (!train && ppm_eval_enabled()) {
+        // inference: the four branch convs + folded BN + ReLU as one launch of 16-row tiles,
+        // bit-identical to the four pointwise launches (FSCNN_PPM_FUSED=0)
+        g_prof_tag = "global_feature_extractor.ppm.conv1-4";
+        PpmFwdArgs f{};
+        f.nb = 4; f.K = 128; f.C = 32; f.eval = 1;
+        for (int i = 0; i < 4; ++i) {
+          const Unit& u = pl.ppk[i];
+          PpmBranchFwd& b = f.b[i];
+          b.f.scale = Wf(u.scale); b.f.shift = Wf(u.shift);
+          b.x = (char*)W(pl.pooled) + (size_t)base[i] * N * 128 * E;
+          b.w = Wg(net.ppm_c[i]);
+          b.y = W(u.a); b.ldy = u.ld; b.M = (int)u.M;
         }
         TRY(ppm_branches_fwd(f, dt, r.st));
       } else {

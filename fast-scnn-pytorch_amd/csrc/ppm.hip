@@ -13,6 +13,7 @@
 #include "bn_finish.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace fscnn {
 
@@ -96,59 +97,99 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_kernel(PpmFwdArgs a) {
     st1(Y + (size_t)m * b.ldy + n, fmaxf(fmaf(round_as<T>(s_z[m * PPM_C + n]), sc, sh), 0.f));
 }
 
-// 16-bit plans, K = 128 (the PPM input): the branch's whole pooled input X [M][128] is staged in
-// LDS with one batch of 16-B loads per thread and each thread keeps its channel's 128 weights in
-// registers, so the row walk reads only LDS (the kernel above walks its rows as a chain of
-// dependent L2 round trips: 34 us for the four branches at cfg3).  Same per-row fmaf order (k
-// ascending), so the values are identical.
-constexpr int PPM_K = 128;
+// ---- matrix-core forms (r06) ---------------------------------------------------------------
+// One 16-row x 32-col tile of z = X W^T per wave on the matrix cores, in the k order of the tiled
+// GEMM (gemm.hip gemm_nt_kernel), so the inference form is bit-identical to the four pointwise
+// launches it replaces: chunks of 32 (fp32) / 64 (16-bit) k; fp32 inference runs the three-term
+// bf16 split of both operands per chunk (X3: lane group lq supplies vectors lq and lq + 4), fp32
+// training exact v_mfma_f32_16x16x4_f32 and 16-bit v_mfma_f32_16x16x32 in halves h = 0, 1 (lane
+// group lq supplies vector lq + 4h).  Lanes load their fragments straight from global memory: the
+// pooled rows and the 32 x 128 weights are read once per tile and stay in L2.  (The FMA forms
+// walked a branch's rows on one CU: ppm_fwd_lds 27.5 us per cfg3 step, four pointwise launches
+// 33 us at cfg2; a branch is at most 18 tiles.)
 template <typename T>
-__global__ __launch_bounds__(PPM_T) void ppm_fwd_lds_kernel(PpmFwdArgs a) {
-  constexpr int V = VecW<T>::V;
+constexpr int ppm_kc() { return 8 * VecW<T>::V; }  // k per chunk
+
+template <typename T, bool X3>
+__device__ __forceinline__ void ppm_tile(const T* xr, const T* Wt, int K, int li, int lq,
+                                         f32x4 (&acc)[2]) {
+  constexpr int V = VecW<T>::V, KC = ppm_kc<T>();
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* wr[2] = {Wt + (size_t)li * K, Wt + (size_t)(16 + li) * K};
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    if constexpr (X3) {
+      uint4 a3[3];
+      gs_split3(*reinterpret_cast<const uint4*>(xr + k0 + lq * V),
+                *reinterpret_cast<const uint4*>(xr + k0 + (lq + 4) * V), a3);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        uint4 b3[3];
+        gs_split3(*reinterpret_cast<const uint4*>(wr[nt] + k0 + lq * V),
+                  *reinterpret_cast<const uint4*>(wr[nt] + k0 + (lq + 4) * V), b3);
+        gs_mma_x3(a3, b3, acc[nt]);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ko = k0 + (lq + 4 * h) * V;
+        const uint4 av = *reinterpret_cast<const uint4*>(xr + ko);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const uint4 bv = *reinterpret_cast<const uint4*>(wr[nt] + ko);
+          if constexpr (sizeof(T) == 4) {
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.x), __uint_as_float(bv.x), acc[nt], 0, 0, 0);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.y), __uint_as_float(bv.y), acc[nt], 0, 0, 0);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.z), __uint_as_float(bv.z), acc[nt], 0, 0, 0);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.w), __uint_as_float(bv.w), acc[nt], 0, 0, 0);
+          } else if constexpr (std::is_same<T, f16>::value) {
+            h16x8 a8, b8;
+            __builtin_memcpy(&a8, &av, 16);
+            __builtin_memcpy(&b8, &bv, 16);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, acc[nt], 0, 0, 0);
+          } else {
+            i16x8 a8, b8;
+            __builtin_memcpy(&a8, &av, 16);
+            __builtin_memcpy(&b8, &bv, 16);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, acc[nt], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+}
+
+// training: one workgroup per branch (its batch statistics stay block-local); wave w takes row
+// tiles w, w + 8, ...; then the statistics / finish / apply of ppm_fwd_kernel over the stored z
+template <typename T>
+__global__ __launch_bounds__(PPM_T) void ppm_fwd_mma_kernel(PpmFwdArgs a) {
   const PpmBranchFwd& b = a.b[blockIdx.x];
-  const int M = b.M, tid = threadIdx.x;
-  const int n = tid & 31, sl = tid >> 5;
+  const int M = b.M, K = a.K, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, li = lane & 15, lq = lane >> 4;
   extern __shared__ float sm[];
-  float* s_z = sm;                                              // [M][C], unrounded conv output
-  T* s_x = reinterpret_cast<T*>(s_z + (size_t)M * PPM_C);       // [M][K]
+  float* s_z = sm;  // [M][C], the stored (rounded) conv output
   __shared__ double s_r[2][PPM_T];
   __shared__ float s_ss[2][PPM_C];
   const T* X = (const T*)b.x;
-  {
-    const int nv = M * PPM_K / V;
-    constexpr int LPT = 288 * PPM_K / 8 / PPM_T;  // 9: the largest branch (M <= 288 checked)
-    uint4 raw[LPT];
-#pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int i = tid + u * PPM_T;
-      raw[u] = *reinterpret_cast<const uint4*>(X + (size_t)(i < nv ? i : 0) * V);
-    }
-#pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int i = tid + u * PPM_T;
-      if (i < nv) *reinterpret_cast<uint4*>(s_x + (size_t)i * V) = raw[u];
-    }
-  }
-  float wr[PPM_K];
-  const T* Wt = (const T*)b.w + (size_t)n * PPM_K;
-#pragma unroll
-  for (int k = 0; k < PPM_K; k += V) ldv(Wt + k, *reinterpret_cast<float(*)[V]>(&wr[k]));
-  __syncthreads();
+  const T* Wt = (const T*)b.w;
   T* Z = (T*)b.z;
-  for (int m = sl; m < M; m += 16) {
-    const T* xr = s_x + (size_t)m * PPM_K;
-    float acc = 0.f;
+  for (int t = wave; t * 16 < M; t += PPM_T / 64) {
+    const int r = t * 16 + li;
+    f32x4 acc[2];
+    ppm_tile<T, false>(X + (size_t)(r < M ? r : 0) * K, Wt, K, li, lq, acc);
 #pragma unroll
-    for (int k = 0; k < PPM_K; k += V) {
-      float xv[V];
-      ldv(xr + k, xv);
+    for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int j = 0; j < V; ++j) acc = fmaf(xv[j], wr[k + j], acc);
-    }
-    s_z[m * PPM_C + n] = round_as<T>(acc);  // the stored value (statistics and apply)
-    st1(Z + (size_t)m * PPM_C + n, acc);
+      for (int q = 0; q < 4; ++q) {
+        const int m = t * 16 + lq * 4 + q, c = nt * 16 + li;
+        if (m < M) {
+          s_z[m * PPM_C + c] = round_as<T>(acc[nt][q]);
+          st1(Z + (size_t)m * PPM_C + c, acc[nt][q]);
+        }
+      }
   }
   __syncthreads();
+  const int n = tid & 31, sl = tid >> 5;
   double t1 = 0.0, t2 = 0.0;
   for (int m = sl; m < M; m += 16) {
     const double v = s_z[m * PPM_C + n];
@@ -172,7 +213,33 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_lds_kernel(PpmFwdArgs a) {
   T* Y = (T*)b.y;
   const float sc = s_ss[0][n], sh = s_ss[1][n];
   for (int m = sl; m < M; m += 16)
-    st1(Y + (size_t)m * b.ldy + n, fmaxf(fmaf(round_as<T>(s_z[m * PPM_C + n]), sc, sh), 0.f));
+    st1(Y + (size_t)m * b.ldy + n, fmaxf(fmaf(s_z[m * PPM_C + n], sc, sh), 0.f));
+}
+
+// inference: one wave per 16-row tile of any branch, y = relu(z * scale + shift) with the folded
+// eval BN (b.f.scale / b.f.shift as inputs), the tiled GEMM's epilogue arithmetic
+template <typename T>
+__global__ __launch_bounds__(64) void ppm_eval_mma_kernel(PpmFwdArgs a) {
+  int t = blockIdx.x, bi = 0;
+  while (bi + 1 < a.nb && t >= (a.b[bi].M + 15) / 16) t -= (a.b[bi++].M + 15) / 16;
+  const PpmBranchFwd& b = a.b[bi];
+  const int M = b.M, K = a.K, lane = threadIdx.x, li = lane & 15, lq = lane >> 4;
+  const int r = t * 16 + li;
+  f32x4 acc[2];
+  ppm_tile<T, sizeof(T) == 4>((const T*)b.x + (size_t)(r < M ? r : 0) * K, (const T*)b.w, K, li,
+                              lq, acc);
+  T* Y = (T*)b.y;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int c = nt * 16 + li;
+    const float sc = b.f.scale[c], sh = b.f.shift[c];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = t * 16 + lq * 4 + q;
+      const float v = acc[nt][q] * sc + sh;
+      if (m < M) st1(Y + (size_t)m * b.ldy + c, fmaxf(v, 0.f));
+    }
+  }
 }
 
 // G workgroups per branch (a.wg0): each recomputes the branch's BN-backward sums and dz (tiny,
@@ -319,18 +386,36 @@ bool ppm_branches_ok(int maxM, int K, int dtype) {
 int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st) {
   int maxM = 0;
   for (int i = 0; i < a.nb; ++i) maxM = a.b[i].M > maxM ? a.b[i].M : maxM;
-  if (!ppm_check(a.nb, a.K, a.C, maxM, dtype)) return E_INVALID;
-  const size_t lds = (size_t)PPM_C * (a.K + 1) * 4 + (size_t)maxM * PPM_C * 4;
+  const int kc = dtype == DT_F32 ? 32 : 64;
   double rows = 0.0;
   for (int i = 0; i < a.nb; ++i) rows += a.b[i].M;
-  ProfScope ps(PK_PPM, st, rows * (a.K + 2.0 * PPM_C) * (dtype == DT_F32 ? 4 : 2),
-               2.0 * a.K * PPM_C * rows);
-  if (dtype != DT_F32 && a.K == PPM_K && maxM <= 288) {
-    const size_t l2 = (size_t)maxM * PPM_C * 4 + (size_t)maxM * PPM_K * 2;
-    if (dtype == DT_F16) prof_launch(ppm_fwd_lds_kernel<f16>, a.nb, PPM_T, l2, st, a);
-    else prof_launch(ppm_fwd_lds_kernel<bf16>, a.nb, PPM_T, l2, st, a);
+  if (a.eval) {  // inference: no statistics, any M; the matrix-core form only
+    if (a.nb < 1 || a.nb > 4 || a.C != PPM_C || a.K < kc || a.K % kc || maxM < 1 ||
+        dtype < DT_F32 || dtype > DT_F16) {
+      set_error("ppm_branches_fwd (eval): nb=%d K=%d C=%d M=%d dtype=%d not supported", a.nb, a.K,
+                a.C, maxM, dtype);
+      return E_UNSUPPORTED;
+    }
+    unsigned tiles = 0;
+    for (int i = 0; i < a.nb; ++i) tiles += (unsigned)((a.b[i].M + 15) / 16);
+    ProfScope ps(PK_PPM, st, rows * (a.K + PPM_C) * (dtype == DT_F32 ? 4 : 2),
+                 2.0 * a.K * PPM_C * rows);
+    if (dtype == DT_F32) prof_launch(ppm_eval_mma_kernel<float>, tiles, 64, 0, st, a);
+    else if (dtype == DT_F16) prof_launch(ppm_eval_mma_kernel<f16>, tiles, 64, 0, st, a);
+    else prof_launch(ppm_eval_mma_kernel<bf16>, tiles, 64, 0, st, a);
     return check_launch("ppm_branches_fwd");
   }
+  if (!ppm_check(a.nb, a.K, a.C, maxM, dtype)) return E_INVALID;
+  ProfScope ps(PK_PPM, st, rows * (a.K + 2.0 * PPM_C) * (dtype == DT_F32 ? 4 : 2),
+               2.0 * a.K * PPM_C * rows);
+  if (a.K % kc == 0) {
+    const size_t l2 = (size_t)maxM * PPM_C * 4;
+    if (dtype == DT_F32) prof_launch(ppm_fwd_mma_kernel<float>, a.nb, PPM_T, l2, st, a);
+    else if (dtype == DT_F16) prof_launch(ppm_fwd_mma_kernel<f16>, a.nb, PPM_T, l2, st, a);
+    else prof_launch(ppm_fwd_mma_kernel<bf16>, a.nb, PPM_T, l2, st, a);
+    return check_launch("ppm_branches_fwd");
+  }
+  const size_t lds = (size_t)PPM_C * (a.K + 1) * 4 + (size_t)maxM * PPM_C * 4;
   if (dtype == DT_F32) prof_launch(ppm_fwd_kernel<float>, a.nb, PPM_T, lds, st, a);
   else if (dtype == DT_F16) prof_launch(ppm_fwd_kernel<f16>, a.nb, PPM_T, lds, st, a);
   else prof_launch(ppm_fwd_kernel<bf16>, a.nb, PPM_T, lds, st, a);

@@ -3,9 +3,11 @@ executor reads FSCNN_STEM_FUSED once).  Eval forwards (no_grad) over the image d
 sizes the fused inference stem (csrc/stem.hip) handles -- partial edge tiles included -- saving
 every output, plus the number of stem launches the library's profiler saw in the first case.
 With ``--dsconv``: the same for the fused classifier DSConvs (csrc/dsconv.hip,
-FSCNN_DSCONV_FUSED) over maps whose classifier M = N x H/8 x W/8 >= 4096.
+FSCNN_DSCONV_FUSED) over maps whose classifier M = N x H/8 x W/8 >= 4096.  With ``--ppm``: the
+inference PPM branch convs in one launch (csrc/ppm.hip, FSCNN_PPM_FUSED) over batches whose bins
+leave partial 16-row tiles.
 
-    python tests/_stem_worker.py OUT.npz [--dsconv]
+    python tests/_stem_worker.py OUT.npz [--dsconv | --ppm]
 """
 import ctypes
 import os
@@ -36,10 +38,21 @@ DS_CASES = [
     ("autocast16", 19, (1, 3, 520, 1048), "float32", "float16"),
 ]
 PK_DSCONV = 18
+# (the PPM branches have M = k*k*N rows < 4096, where the unfused pointwise takes the tiled GEMM
+# whose k order the fused launch reproduces)
+PPM_CASES = [
+    ("fp32", 19, (2, 3, 256, 512), "float32", None),
+    ("fp32_n3", 19, (3, 3, 320, 416), "float32", None),  # 3 / 12 / 27 / 108 rows
+    ("fp32_n8", 19, (8, 3, 256, 256), "float32", None),  # 8 / 32 / 72 / 288 rows (cfg2's bins)
+    ("bf16", 19, (3, 3, 192, 256), "bfloat16", None),
+    ("fp16_c2", 2, (5, 3, 480, 640), "float16", None),
+    ("autocast16", 19, (2, 3, 256, 320), "float32", "float16"),
+]
+PK_PPM = 15
 
 
-def main(out, dsconv=False):
-    cases, pk = (DS_CASES, PK_DSCONV) if dsconv else (CASES, PK_STEM)
+def main(out, dsconv=False, ppm=False):
+    cases, pk = (DS_CASES, PK_DSCONV) if dsconv else ((PPM_CASES, PK_PPM) if ppm else (CASES, PK_STEM))
     import numpy as np
     import torch
     import _fscnn_boot
@@ -82,4 +95,4 @@ def main(out, dsconv=False):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], "--dsconv" in sys.argv[2:])
+    main(sys.argv[1], "--dsconv" in sys.argv[2:], "--ppm" in sys.argv[2:])

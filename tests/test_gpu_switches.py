@@ -24,6 +24,9 @@ fresh child process:
 * ``FSCNN_FFM_HI=0``      — (inference) the FFM's high-res branch (conv_higher_res + BN) as its own
   GEMM, added as a stored residual by the fused launch, instead of a second GEMM inside it
   (test_ffm_hi_fused_bit_identical).
+* ``FSCNN_PPM_FUSED=0``   — (inference) the four PPM branch convs as four pointwise launches instead
+  of one launch of 16-row matrix-core tiles (csrc/ppm.hip): bit-identical outputs
+  (test_ppm_fused_bit_identical).
 
 (Round 5 removed the measured-slower variants and their switches: FSCNN_DW_LOOP, FSCNN_GEMM_PF,
 FSCNN_CE_HEAD, FSCNN_CE_PACK, FSCNN_GEMM_MINT.)
@@ -60,6 +63,7 @@ CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
          "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL,
          "FSCNN_DSCONV_FUSED=0": EVAL, "FSCNN_IR_S2=0": EVAL, "FSCNN_FFM_HI=0": EVAL,
+         "FSCNN_PPM_FUSED=0": EVAL,
          "FSCNN_IR_TRAIN=1": TRAIN[-1:] + ["tests/test_gpu_bf16_train.py"],
          "FSCNN_IR_TRAIN=2": TRAIN[-1:] + ["tests/test_gpu_bf16_train.py"]}
 
@@ -92,11 +96,11 @@ def _worker(tmp_path, switch, half=None):
     return dict(np.load(out))
 
 
-def _stem_worker(tmp_path, switch, dsconv=False):
+def _stem_worker(tmp_path, switch, dsconv=False, ppm=False):
     out = str(tmp_path / ("stem_%s%s.npz" % ((switch or "default").replace("=", "_"),
-                                               "_ds" if dsconv else "")))
+                                               "_ds" if dsconv else ("_ppm" if ppm else ""))))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_stem_worker.py"), out] +
-                       (["--dsconv"] if dsconv else []),
+                       (["--dsconv"] if dsconv else []) + (["--ppm"] if ppm else []),
                        cwd=ROOT, env=_env(switch), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     return dict(np.load(out))
@@ -141,6 +145,22 @@ def test_ffm_hi_fused_bit_identical(tmp_path):
     ref = _stem_worker(tmp_path, "FSCNN_FFM_HI=0", dsconv=True)
     got = _stem_worker(tmp_path, None, dsconv=True)
     assert int(ref["stem_launches"]) == 3 and int(got["stem_launches"]) == 3
+    for k in ref:
+        if k == "stem_launches":
+            continue
+        assert np.isfinite(got[k]).all(), k
+        assert np.array_equal(ref[k], got[k]), "%s: max |diff| %g" % (
+            k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
+
+
+def test_ppm_fused_bit_identical(tmp_path):
+    """The inference PPM branch convs (conv1..conv4 + folded BN + ReLU) as one launch of 16-row
+    matrix-core tiles give bit-identical outputs to the four pointwise GEMM launches: fp32 (the
+    three-term split) / bf16 / fp16 / autocast fp16, bins of 1..288 rows with partial tiles
+    (tests/_stem_worker.py --ppm).  The default run really took the one launch."""
+    ref = _stem_worker(tmp_path, "FSCNN_PPM_FUSED=0", ppm=True)
+    got = _stem_worker(tmp_path, None, ppm=True)
+    assert int(ref["stem_launches"]) == 0 and int(got["stem_launches"]) == 1
     for k in ref:
         if k == "stem_launches":
             continue
