@@ -10,26 +10,40 @@ constexpr float BN_EPS = 1e-5f;
 
 // forward: fp64 sums over the merged records, n = sum count, s1 = sum n*mean,
 // s2 = sum (M2 + n*mean^2) -> mean / invstd / scale / shift and aten's running-stat update
-// (unbiased variance n/(n-1), momentum) of channel c
-__device__ __forceinline__ void bn_fwd_finish(const BnFinalizeArgs& a, int c, double n, double s1,
-                                              double s2) {
+// (unbiased variance n/(n-1), momentum) of channel c.  Every input is loaded before the first
+// store: a load after a store through a pointer that may alias it is its own memory round trip,
+// and this runs at the very end of a producer (r06: gamma, beta, rmean, rvar were up to four
+// dependent round trips behind the stores).  Returns (scale, shift).
+__device__ __forceinline__ float2 bn_fwd_finish(const BnFinalizeArgs& a, int c, double n,
+                                                double s1, double s2) {
+  const float g = a.gamma[c], be = a.beta[c];
+  const double bias = a.bias ? (double)a.bias[c] : 0.0;
+  float rm = 0.f, rv = 0.f;
+  if (a.rmean) {
+    rm = a.rmean[c];
+    rv = a.rvar[c];
+  }
+  const bool bump = a.nbt && c == 0;
+  const long long nb = bump ? a.nbt[0] : 0;
   const double mu = n > 0.0 ? s1 / n : 0.0;
   const double m2 = n > 0.0 ? fmax(s2 - n * mu * mu, 0.0) : 0.0;
-  const double mean = mu + (a.bias ? (double)a.bias[c] : 0.0);
+  const double mean = mu + bias;
   const double var = n > 0 ? m2 / n : 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)BN_EPS));
-  const float scale = a.gamma[c] * invstd;
+  const float scale = g * invstd;
+  const float shift = be - (float)mean * scale;
   a.mean[c] = (float)mean;
   a.invstd[c] = invstd;
   a.scale[c] = scale;
-  a.shift[c] = a.beta[c] - (float)mean * scale;
+  a.shift[c] = shift;
   if (a.rmean) {
     const float m = a.momentum;
-    a.rmean[c] = (1.f - m) * a.rmean[c] + m * (float)mean;
+    a.rmean[c] = (1.f - m) * rm + m * (float)mean;
     const float unb = n > 1 ? (float)(m2 / (n - 1.0)) : (float)var;
-    a.rvar[c] = (1.f - m) * a.rvar[c] + m * unb;
+    a.rvar[c] = (1.f - m) * rv + m * unb;
   }
-  if (a.nbt && c == 0) a.nbt[0] += 1;
+  if (bump) a.nbt[0] = nb + 1;
+  return make_float2(scale, shift);
 }
 
 // backward: s1 = sum dy_r, s2 = sum dy_r * xhat of channel c (C channels) -> dbeta, dgamma, the
@@ -37,10 +51,18 @@ __device__ __forceinline__ void bn_fwd_finish(const BnFinalizeArgs& a, int c, do
 // dz = scale*(dy_r - c0 - (z - mean)*invstd*c1) = al*dy_r + gz*z + be
 // count == BN_FROZEN_COUNT: a BN normalised with its running statistics (eval-mode autograd,
 // models/fast_scnn.py in .eval() with grad enabled): mean and invstd are constants, so the batch
-// terms vanish (c0 = c1 = 0) and dz = scale * dy_r; dgamma / dbeta keep their sums
+// terms vanish (c0 = c1 = 0) and dz = scale * dy_r; dgamma / dbeta keep their sums.  (Inputs
+// loaded before the first store, as in bn_fwd_finish.)
 __device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2, double count,
                                               float* dgamma, float* dbeta, float* coef,
                                               const BnBwdTab& t) {
+  float sc = 0.f, isd = 0.f, mu = 0.f, sh = 1.f;
+  if (t.tab) {
+    sc = t.scale[c];
+    isd = t.invstd[c];
+    mu = t.mean[c];
+    if (t.relu) sh = t.shift[c];
+  }
   if (dbeta) dbeta[c] = (float)s1;
   if (dgamma) dgamma[c] = (float)s2;
   const bool frozen = count == BN_FROZEN_COUNT;
@@ -48,16 +70,15 @@ __device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2
   coef[c] = c0;
   coef[C + c] = c1;
   if (t.tab) {
-    const float sc = t.scale[c];
-    const float gz = -sc * c1 * t.invstd[c];
+    const float gz = -sc * c1 * isd;
     float4 v;
     v.x = sc;
-    v.y = -sc * c0 - gz * t.mean[c];
+    v.y = -sc * c0 - gz * mu;
     v.z = gz;
     v.w = t.relu ? sc : 0.f;
     float* e = t.tab + (size_t)c * BWDX_STRIDE;
     *reinterpret_cast<float4*>(e) = v;
-    e[4] = t.relu ? t.shift[c] : 1.f;
+    e[4] = sh;
   }
 }
 

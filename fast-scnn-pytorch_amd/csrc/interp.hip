@@ -503,8 +503,9 @@ __global__ __launch_bounds__(256) void pyramid_pool_kernel(PoolArgs a, int CVL) 
 int pyramid_pool(const PoolArgs& a, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   const int CV = a.C / V;
-  // channel-vector slice per workgroup: 4 when it divides CV, else the whole row (<= 256, a
-  // power of two so the pixel groups halve evenly)
+  // channel-vector slice per workgroup: 4 vectors when that divides CV (eight fp32 / four 16-bit
+  // slices of C = 128; two-vector 16-bit slices measured 13.8 vs 10.3 us at cfg3), else the whole
+  // row (<= 256, a power of two so the pixel groups halve evenly)
   const int CVL = CV % 4 == 0 ? 4 : CV;
   if (a.C % V || CV > 256 || (CVL & (CVL - 1)) || a.ldx % V) {
     set_error("pyramid_pool: C=%d ldx=%d", a.C, a.ldx);
@@ -632,32 +633,33 @@ int ppm_up_fwd(const PpmUpArgs& a, int dtype, hipStream_t st) {
 }
 
 // backward: dfeats[bin][n][c] = sum_{h,w} wy(h,bi) wx(w,bj) dy[n,h,w,coff+lv*CF+c]  (gather)
-// Separable, one workgroup per (level, image): phase 1 reduces every row of the level's dy slice
+// Separable, one workgroup per (level, image, 16-B channel vector -- r06: per (level, image) the
+// 32 workgroups of cfg3 took 22.7 us): phase 1 reduces every row of the level's dy slice
 // onto the k column bins (rows[h][bj][c] = sum_w wx(w,bj) dy[h,w,c]), phase 2 folds the rows onto
 // the k row bins (one thread per (c, bin)), fixed order throughout.  Phase 1: a thread takes one
 // 16-B channel vector of one row and the columns w = s, s + 8, ... of its segment s (8 segments on
 // 8 adjacent lanes): its <= 8 vector loads per batch are all in flight at once (one memory round
-// trip for W <= 64), and the 8 segments' bin sums meet in a fixed xor butterfly.
+// trip for W <= 64; 64 rows per pass), and the 8 segments' bin sums meet in a fixed xor butterfly.
 constexpr int PPB_THREADS = 512;
-constexpr int PPB_MAXH = 80;  // LDS rows[H][6][CF<=32] fp32
+constexpr int PPB_MAXH = 80;  // LDS rows[H][6][8] fp32
 constexpr int PPB_SEG = 8;    // column segments (adjacent lanes)
 
 template <typename T>
 __global__ __launch_bounds__(PPB_THREADS) void ppm_up_bwd_kernel(PpmUpArgs a, void* dfeats) {
   constexpr int V = VecW<T>::V;
-  __shared__ float rows[PPB_MAXH * 6 * 32];
+  __shared__ float rows[PPB_MAXH * 6 * 8];  // [h][bj][one channel vector]
   const int lv = blockIdx.x, n = blockIdx.y;
   const int k = PP_LEVELS[lv];
   const int base = lv == 0 ? 0 : (lv == 1 ? 1 : (lv == 2 ? 5 : 14));
   const float sh = ac_scale(k, a.H), sw = ac_scale(k, a.W);
-  const int CF = a.CF, CV = CF / V;
+  const int CF = a.CF;
   const int sg = threadIdx.x % PPB_SEG, rest = threadIdx.x / PPB_SEG;
-  const int cv = rest % CV;
-  const int RP = PPB_THREADS / PPB_SEG / CV;  // rows per pass
+  const int cv = blockIdx.z;  // this workgroup's 16-B channel vector
+  constexpr int RP = PPB_THREADS / PPB_SEG;  // rows per pass
   const T* gp = (const T*)a.y + (size_t)n * a.H * a.W * a.ldy + a.coff + lv * CF + cv * V;
   // (the pass loop is uniform across the wave's 8-lane segment groups: RP rows per pass)
   for (int h0 = 0; h0 < a.H; h0 += RP) {
-    const int h = h0 + rest / CV;
+    const int h = h0 + rest;
     const bool hok = h < a.H;
     float acc[6][V];
 #pragma unroll
@@ -700,32 +702,32 @@ __global__ __launch_bounds__(PPB_THREADS) void ppm_up_bwd_kernel(PpmUpArgs a, vo
       for (int bj = 0; bj < 6; ++bj)
         if (bj < k) {
 #pragma unroll
-          for (int e = 0; e < V; ++e) rows[(h * 6 + bj) * 32 + cv * V + e] = acc[bj][e];
+          for (int e = 0; e < V; ++e) rows[(h * 6 + bj) * 8 + e] = acc[bj][e];
         }
     }
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < k * k * CF; t += PPB_THREADS) {
-    const int cc = t % CF, bin = t / CF, bi = bin / k, bj = bin - bi * k;
+  for (int t = threadIdx.x; t < k * k * V; t += PPB_THREADS) {
+    const int e = t % V, bin = t / V, bi = bin / k, bj = bin - bi * k;
     float s = 0.f;
     for (int h = 0; h < a.H; ++h) {
       const Lerp lh = ac_lerp(h, k, a.H, sh);
       const float wy = (lh.i0 == bi ? lh.l0 : 0.f) + (lh.i1 == bi ? lh.l1 : 0.f);
-      s += wy * rows[(h * 6 + bj) * 32 + cc];
+      s += wy * rows[(h * 6 + bj) * 8 + e];
     }
-    st1((T*)dfeats + ((size_t)(base + bin) * a.N + n) * CF + cc, s);
+    st1((T*)dfeats + ((size_t)(base + bin) * a.N + n) * CF + cv * V + e, s);
   }
 }
 
 int ppm_up_bwd(const PpmUpArgs& a, void* dfeats, int dtype, hipStream_t st) {
   const int V = dtype == DT_F32 ? 4 : 8;
   // the row mapping hands rest / (CF / V) rows to a pass: CF / V must divide the 64 lanes
-  if (a.CF <= 0 || a.CF > 32 || a.CF % V || (PPB_THREADS / PPB_SEG) % (a.CF / V) || a.ldy % V ||
-      a.coff % V || a.H > PPB_MAXH || a.N > 65535) {
+  if (a.CF <= 0 || a.CF > 32 || a.CF % V || a.ldy % V || a.coff % V || a.H > PPB_MAXH ||
+      a.N > 65535) {
     set_error("ppm_up_bwd: CF=%d H=%d unsupported", a.CF, a.H);
     return E_UNSUPPORTED;
   }
-  dim3 grid(4, a.N);
+  dim3 grid(4, a.N, a.CF / V);
   if (dtype == DT_F32) prof_launch(ppm_up_bwd_kernel<float>, grid, PPB_THREADS, 0, st, a, dfeats);
   else if (dtype == DT_F16) prof_launch(ppm_up_bwd_kernel<f16>, grid, PPB_THREADS, 0, st, a, dfeats);
   else prof_launch(ppm_up_bwd_kernel<bf16>, grid, PPB_THREADS, 0, st, a, dfeats);

@@ -294,6 +294,7 @@ struct PpmFwdArgs {
   PpmBranchFwd b[4];
   int nb, K, C;
   int eval = 0;  // inference: y = relu(z * f.scale + f.shift) (folded BN), no z, no statistics
+  unsigned long long* stamps = nullptr;  // phase stamps (tools/stamp_probe.py)
 };
 struct PpmBranchBwd {
   const void* dy; int lddy;  // gradient of y
@@ -312,6 +313,7 @@ struct PpmBwdArgs {
   PpmBranchBwd b[4];
   int nb, K, C;
   int wg0[5] = {0, 0, 0, 0, 0};  // (set by the launcher) first workgroup of each branch
+  unsigned long long* stamps = nullptr;  // phase stamps (tools/stamp_probe.py)
 };
 
 struct CeArgs {

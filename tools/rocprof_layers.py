@@ -44,7 +44,7 @@ FAMILY_RE = {
     "conv0_wgrad": r"conv0_wgrad_kernel|ltd_c0_bwd_kernel",
     "bn_bwd_reduce": r"bn_bwd_reduce_kernel",
     "bn_finalize": r"bn_(stats_fold_fin|stats_fold|finalize|bwd_fold_fin|bwd_fold|bwd_finalize)_kernel",
-    "ppm_branches": r"ppm_(fwd|fwd_lds|bwd)_kernel",
+    "ppm_branches": r"ppm_(fwd|fwd_mma|eval_mma|bwd)_kernel",
     "ir_block": r"ir_block_kernel|ir_train_fwd_kernel",
     "ltd_stem": r"stem_walk_kernel",
     "dsconv": r"dsconv_fwd_kernel",
