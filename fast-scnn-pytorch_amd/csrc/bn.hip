@@ -106,6 +106,8 @@ __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q
   __shared__ double sh[3][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = chunk * 64 + cx;
+  BnFwdIn in;  // the finish's inputs, in flight with the record loads
+  if (ty == 0 && c < a.C) in = bn_fwd_load(a, c);
   double n = 0.0, s1 = 0.0, s2 = 0.0;
   if (c < a.C) {
     constexpr int U = BN_Q / BN_TY;
@@ -139,7 +141,7 @@ __device__ __forceinline__ void bn_finalize_chunk(const BnFinalizeArgs& a, int Q
     s1 += sh[1][t][cx];
     s2 += sh[2][t][cx];
   }
-  bn_fwd_finish(a, c, n, s1, s2);
+  bn_fwd_finish(a, c, n, s1, s2, in);
 }
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(BnFinalizeArgs a, int Q) {
@@ -421,6 +423,8 @@ __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, 
   __shared__ double sh[2][BN_TY][64];
   const int cx = threadIdx.x, ty = threadIdx.y;
   const int c = chunk * 64 + cx;
+  BnBwdIn in;  // the finish's inputs, in flight with the record loads
+  if (ty == 0 && c < C) in = bn_bwd_load(t, c);
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     constexpr int U = BN_Q / BN_TY;
@@ -449,7 +453,7 @@ __device__ __forceinline__ void bn_bwd_finalize_chunk(const float* part, int Q, 
     s1 += sh[0][t][cx];
     s2 += sh[1][t][cx];
   }
-  bn_bwd_finish(c, C, s1, s2, count, dgamma, dbeta, coef, t);
+  bn_bwd_finish(c, C, s1, s2, count, dgamma, dbeta, coef, t, in);
 }
 
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* part, int Q, int C,

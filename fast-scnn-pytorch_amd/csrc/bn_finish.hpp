@@ -10,40 +10,53 @@ constexpr float BN_EPS = 1e-5f;
 
 // forward: fp64 sums over the merged records, n = sum count, s1 = sum n*mean,
 // s2 = sum (M2 + n*mean^2) -> mean / invstd / scale / shift and aten's running-stat update
-// (unbiased variance n/(n-1), momentum) of channel c.  Every input is loaded before the first
-// store: a load after a store through a pointer that may alias it is its own memory round trip,
-// and this runs at the very end of a producer (r06: gamma, beta, rmean, rvar were up to four
-// dependent round trips behind the stores).  Returns (scale, shift).
-__device__ __forceinline__ float2 bn_fwd_finish(const BnFinalizeArgs& a, int c, double n,
-                                                double s1, double s2) {
-  const float g = a.gamma[c], be = a.beta[c];
-  const double bias = a.bias ? (double)a.bias[c] : 0.0;
-  float rm = 0.f, rv = 0.f;
+// (unbiased variance n/(n-1), momentum) of channel c.  The per-channel inputs are loaded apart
+// (bn_fwd_load) so an in-kernel finisher can issue them before its last fold: a load after a
+// store through a pointer that may alias it is its own memory round trip, and this runs at the
+// very end of a producer (r06: gamma, beta, rmean, rvar were up to four dependent round trips
+// behind the stores).  Returns (scale, shift).
+struct BnFwdIn {
+  float g = 0.f, be = 0.f, rm = 0.f, rv = 0.f;
+  double bias = 0.0;
+  long long nb = 0;
+};
+__device__ __forceinline__ BnFwdIn bn_fwd_load(const BnFinalizeArgs& a, int c) {
+  BnFwdIn r;
+  r.g = a.gamma[c];
+  r.be = a.beta[c];
+  r.bias = a.bias ? (double)a.bias[c] : 0.0;
   if (a.rmean) {
-    rm = a.rmean[c];
-    rv = a.rvar[c];
+    r.rm = a.rmean[c];
+    r.rv = a.rvar[c];
   }
-  const bool bump = a.nbt && c == 0;
-  const long long nb = bump ? a.nbt[0] : 0;
+  if (a.nbt && c == 0) r.nb = a.nbt[0];
+  return r;
+}
+__device__ __forceinline__ float2 bn_fwd_finish(const BnFinalizeArgs& a, int c, double n,
+                                                double s1, double s2, const BnFwdIn& in) {
   const double mu = n > 0.0 ? s1 / n : 0.0;
   const double m2 = n > 0.0 ? fmax(s2 - n * mu * mu, 0.0) : 0.0;
-  const double mean = mu + bias;
+  const double mean = mu + in.bias;
   const double var = n > 0 ? m2 / n : 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)BN_EPS));
-  const float scale = g * invstd;
-  const float shift = be - (float)mean * scale;
+  const float scale = in.g * invstd;
+  const float shift = in.be - (float)mean * scale;
   a.mean[c] = (float)mean;
   a.invstd[c] = invstd;
   a.scale[c] = scale;
   a.shift[c] = shift;
   if (a.rmean) {
     const float m = a.momentum;
-    a.rmean[c] = (1.f - m) * rm + m * (float)mean;
+    a.rmean[c] = (1.f - m) * in.rm + m * (float)mean;
     const float unb = n > 1 ? (float)(m2 / (n - 1.0)) : (float)var;
-    a.rvar[c] = (1.f - m) * rv + m * unb;
+    a.rvar[c] = (1.f - m) * in.rv + m * unb;
   }
-  if (bump) a.nbt[0] = nb + 1;
+  if (a.nbt && c == 0) a.nbt[0] = in.nb + 1;
   return make_float2(scale, shift);
+}
+__device__ __forceinline__ float2 bn_fwd_finish(const BnFinalizeArgs& a, int c, double n,
+                                                double s1, double s2) {
+  return bn_fwd_finish(a, c, n, s1, s2, bn_fwd_load(a, c));
 }
 
 // backward: s1 = sum dy_r, s2 = sum dy_r * xhat of channel c (C channels) -> dbeta, dgamma, the
@@ -52,17 +65,23 @@ __device__ __forceinline__ float2 bn_fwd_finish(const BnFinalizeArgs& a, int c, 
 // count == BN_FROZEN_COUNT: a BN normalised with its running statistics (eval-mode autograd,
 // models/fast_scnn.py in .eval() with grad enabled): mean and invstd are constants, so the batch
 // terms vanish (c0 = c1 = 0) and dz = scale * dy_r; dgamma / dbeta keep their sums.  (Inputs
-// loaded before the first store, as in bn_fwd_finish.)
+// loaded apart, as in the forward.)
+struct BnBwdIn {
+  float sc = 0.f, isd = 0.f, mu = 0.f, sh = 1.f;
+};
+__device__ __forceinline__ BnBwdIn bn_bwd_load(const BnBwdTab& t, int c) {
+  BnBwdIn r;
+  if (t.tab) {
+    r.sc = t.scale[c];
+    r.isd = t.invstd[c];
+    r.mu = t.mean[c];
+    if (t.relu) r.sh = t.shift[c];
+  }
+  return r;
+}
 __device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2, double count,
                                               float* dgamma, float* dbeta, float* coef,
-                                              const BnBwdTab& t) {
-  float sc = 0.f, isd = 0.f, mu = 0.f, sh = 1.f;
-  if (t.tab) {
-    sc = t.scale[c];
-    isd = t.invstd[c];
-    mu = t.mean[c];
-    if (t.relu) sh = t.shift[c];
-  }
+                                              const BnBwdTab& t, const BnBwdIn& in) {
   if (dbeta) dbeta[c] = (float)s1;
   if (dgamma) dgamma[c] = (float)s2;
   const bool frozen = count == BN_FROZEN_COUNT;
@@ -70,16 +89,21 @@ __device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2
   coef[c] = c0;
   coef[C + c] = c1;
   if (t.tab) {
-    const float gz = -sc * c1 * isd;
+    const float gz = -in.sc * c1 * in.isd;
     float4 v;
-    v.x = sc;
-    v.y = -sc * c0 - gz * mu;
+    v.x = in.sc;
+    v.y = -in.sc * c0 - gz * in.mu;
     v.z = gz;
-    v.w = t.relu ? sc : 0.f;
+    v.w = t.relu ? in.sc : 0.f;
     float* e = t.tab + (size_t)c * BWDX_STRIDE;
     *reinterpret_cast<float4*>(e) = v;
-    e[4] = sh;
+    e[4] = in.sh;
   }
+}
+__device__ __forceinline__ void bn_bwd_finish(int c, int C, double s1, double s2, double count,
+                                              float* dgamma, float* dbeta, float* coef,
+                                              const BnBwdTab& t) {
+  bn_bwd_finish(c, C, s1, s2, count, dgamma, dbeta, coef, t, bn_bwd_load(t, c));
 }
 
 // ---- generic in-kernel finish over per-workgroup records ----------------------------------
@@ -214,11 +238,18 @@ __device__ inline void tail_complete(float* part, int P, int N, int p, int c0, i
   if (!arrive_last(ctr + chunk, (unsigned)nteam)) return;
   for (int cb = 0; cb < nc; cb += nthr) {
     const int ncb = min(nthr, nc - cb), n = c0 + cb + tid;
+    const bool own = tid < ncb && n < N;
+    BnFwdIn fin;  // the finish's inputs in flight with the fold's loads
+    BnBwdIn bin;
+    if (own) {
+      if constexpr (FWD) fin = bn_fwd_load(t.fwd, n);
+      else bin = bn_bwd_load(t.tab, n);
+    }
     double s[3];
     tail_fold<FWD, true>(nullptr, t.tsum, N, c0 + cb, ncb, 0, nteam, lds, s);
-    if (tid < ncb && n < N) {
-      if constexpr (FWD) bn_fwd_finish(t.fwd, n, s[0], s[1], s[2]);
-      else bn_bwd_finish(n, N, s[1], s[2], t.count, t.dgamma, t.dbeta, t.coef, t.tab);
+    if (own) {
+      if constexpr (FWD) bn_fwd_finish(t.fwd, n, s[0], s[1], s[2], fin);
+      else bn_bwd_finish(n, N, s[1], s[2], t.count, t.dgamma, t.dbeta, t.coef, t.tab, bin);
     }
   }
   reset_counter(ctr + chunk);

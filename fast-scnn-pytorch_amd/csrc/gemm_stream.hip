@@ -162,6 +162,14 @@ __device__ inline void gs_finish(const GemmArgs& a, int g, int bi, int n0, int B
   const int tid = threadIdx.x, col = tid % BN, n = n0 + col;
   const bool owner = tid < BN && n < a.N;  // slice 0 holds the folded sums
   if (!arrive_last(ctr + GS_CTR_TEAMS + g * nteam + team, (unsigned)tsize)) return;
+  // the finish's per-channel inputs, in flight with the team fold (one round trip off the chain
+  // of the group's last workgroup)
+  BnFwdIn fin;
+  BnBwdIn bin;
+  if (owner) {
+    if constexpr (FWD) fin = bn_fwd_load(a.tail.fwd, n);
+    else bin = bn_bwd_load(a.tail.tab, n);
+  }
   double s[3];
   gs_fold<FWD>(a, n0, BN, team * GS_TEAM, tsize, 1, s);
   if (owner) {  // the team record replaces slot team * GS_TEAM (every other reader is done)
@@ -182,9 +190,9 @@ __device__ inline void gs_finish(const GemmArgs& a, int g, int bi, int n0, int B
   if (!arrive_last(ctr + g, (unsigned)nteam)) return;
   gs_fold<FWD>(a, n0, BN, 0, nteam, GS_TEAM, s);
   if (owner) {
-    if constexpr (FWD) bn_fwd_finish(a.tail.fwd, n, s[0], s[1], s[2]);
+    if constexpr (FWD) bn_fwd_finish(a.tail.fwd, n, s[0], s[1], s[2], fin);
     else bn_bwd_finish(n, a.N, s[1], s[2], a.tail.count, a.tail.dgamma, a.tail.dbeta,
-                       a.tail.coef, a.tail.tab);
+                       a.tail.coef, a.tail.tab, bin);
   }
   reset_counter(ctr + g);
 }

@@ -643,6 +643,7 @@ struct PrepTable {
   int n = 0;
   long long total = 0;
   long long start[PREP_MAXJOBS + 1] = {};
+  int cstart[PREP_MAXJOBS + 1] = {};  // (set by weights_prep) first 2048-element chunk of each job
   PrepJob j[PREP_MAXJOBS];
 };
 int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t st);

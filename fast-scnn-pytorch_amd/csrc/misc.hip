@@ -706,51 +706,67 @@ int sgd(const SgdArgs& a, hipStream_t st) {
 // arena P: the plain cast of the whole arena (bf16 steps) and, for every dense conv, W^T
 // [cin*k*k][ld] zero-padded past cout (the dgrad's non-transposed B operand).  Element i of the
 // flattened job table belongs to the job whose [start, start') range holds it.
-// A block-iteration covers 2048 consecutive elements (8 per thread, 256 apart): the job is found
-// once per thread by binary search and then advanced as the index grows; 32-bit index arithmetic
-// within a job (host-checked).  (r05: the per-element search and 64-bit divisions had made this
-// ~17 us per step for ~3.4 M elements.)
+// One workgroup per 2048-element chunk of one job (t.cstart: the chunks of job k are
+// [cstart[k], cstart[k+1])), found by a workgroup-uniform binary search, so the job record is read
+// once per workgroup and the thread's 8 elements (256 apart) are independent loads in flight
+// together; 32-bit index arithmetic within a job (host-checked).  (r06: a flat element range
+// with the job searched and advanced per thread was a chain of dependent table and data loads,
+// 17-19 us per step for ~3.4 M elements.)
 constexpr int PREP_PER = 8;
+constexpr int PREP_CHUNK = 256 * PREP_PER;
 template <typename T>
 __global__ __launch_bounds__(256) void weights_prep_kernel(PrepTable t, const float* P, T* dst) {
-  constexpr long long CH = 256LL * PREP_PER;
-  for (long long c0 = (long long)blockIdx.x * CH; c0 < t.total; c0 += (long long)gridDim.x * CH) {
-    long long i = c0 + threadIdx.x;
-    if (i >= t.total) break;
-    int lo = 0, hi = t.n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (t.start[mid] <= i) lo = mid;
-      else hi = mid - 1;
+  const int b = blockIdx.x;
+  int lo = 0, hi = t.n - 1;
+  while (lo < hi) {  // last job whose first chunk <= b (uniform)
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.cstart[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const PrepJob& J = t.j[lo];
+  const int len = (int)(t.start[lo + 1] - t.start[lo]);
+  const int i0 = (b - t.cstart[lo]) * PREP_CHUNK + threadIdx.x;
+  if (J.trans == 3) {  // one term of the bf16 truncation split, planes [3][R][Cc]
+    const int plane = J.R * J.Cc;
+    float f[PREP_PER];
+#pragma unroll
+    for (int e = 0; e < PREP_PER; ++e) {
+      const int idx = i0 + 256 * e, ic = idx < len ? idx : 0;
+      const int p = ic >= plane ? (ic >= 2 * plane ? 2 : 1) : 0;
+      f[e] = P[J.src + (ic - p * plane)];
     }
-    for (int e = 0; e < PREP_PER && i < t.total; ++e, i += 256) {
-      while (t.start[lo + 1] <= i) ++lo;
-      const PrepJob& J = t.j[lo];
-      const int idx = (int)(i - t.start[lo]);
-      if (J.trans == 3) {  // one term of the bf16 truncation split, planes [3][R][Cc]
-        const int plane = J.R * J.Cc;
-        const int p = idx >= plane ? (idx >= 2 * plane ? 2 : 1) : 0;
-        const float f = P[J.src + (idx - p * plane)];
-        const uint32_t h0 = __float_as_uint(f) & 0xFFFF0000u;
-        const float r1 = f - __uint_as_float(h0);
-        const uint32_t h1 = __float_as_uint(r1) & 0xFFFF0000u;
-        const float r2 = r1 - __uint_as_float(h1);
-        const uint32_t term = p == 0 ? h0 : (p == 1 ? h1 : __float_as_uint(r2) & 0xFFFF0000u);
-        reinterpret_cast<uint16_t*>(dst)[J.dst + idx] = (uint16_t)(term >> 16);
-        continue;
-      }
-      float v;
-      if (J.trans == 2) {
-        v = 0.f;  // zero fill (counters)
-      } else if (J.trans) {
-        const int n = idx / J.ld;
-        const int k = idx - n * J.ld;
-        v = k < J.R ? P[J.src + (long long)k * J.Cc + n] : 0.f;
-      } else {
-        v = P[J.src + idx];
-      }
-      st1(dst + J.dst + idx, v);
+#pragma unroll
+    for (int e = 0; e < PREP_PER; ++e) {
+      const int idx = i0 + 256 * e;
+      if (idx >= len) break;
+      const int p = idx >= plane ? (idx >= 2 * plane ? 2 : 1) : 0;
+      const uint32_t h0 = __float_as_uint(f[e]) & 0xFFFF0000u;
+      const float r1 = f[e] - __uint_as_float(h0);
+      const uint32_t h1 = __float_as_uint(r1) & 0xFFFF0000u;
+      const float r2 = r1 - __uint_as_float(h1);
+      const uint32_t term = p == 0 ? h0 : (p == 1 ? h1 : __float_as_uint(r2) & 0xFFFF0000u);
+      reinterpret_cast<uint16_t*>(dst)[J.dst + idx] = (uint16_t)(term >> 16);
     }
+    return;
+  }
+  float v[PREP_PER];
+#pragma unroll
+  for (int e = 0; e < PREP_PER; ++e) {
+    const int idx = i0 + 256 * e, ic = idx < len ? idx : 0;
+    if (J.trans == 2) {
+      v[e] = 0.f;  // zero fill (counters)
+    } else if (J.trans) {
+      const int n = ic / J.ld;
+      const int k = ic - n * J.ld;
+      v[e] = k < J.R ? P[J.src + (long long)(k < J.R ? k : 0) * J.Cc + n] : 0.f;
+    } else {
+      v[e] = P[J.src + ic];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < PREP_PER; ++e) {
+    const int idx = i0 + 256 * e;
+    if (idx < len) st1(dst + J.dst + idx, v[e]);
   }
 }
 
@@ -771,7 +787,11 @@ int weights_prep(PrepTable& t, const float* P, void* dst, int dtype, hipStream_t
       set_error("weights_prep: job %d has %lld elements", k, t.start[k + 1] - t.start[k]);
       return E_INVALID;
     }
-  const unsigned grid = (unsigned)std::min<long long>((t.total + 2047) / 2048, 4096);
+  t.cstart[0] = 0;
+  for (int k = 0; k < t.n; ++k)
+    t.cstart[k + 1] = t.cstart[k] + (int)((t.start[k + 1] - t.start[k] + PREP_CHUNK - 1) / PREP_CHUNK);
+  const unsigned grid = (unsigned)t.cstart[t.n];
+  if (grid == 0) return OK;
   if (dtype == DT_F32) prof_launch(weights_prep_kernel<float>, grid, 256, 0, st, t, P, (float*)dst);
   else if (dtype == DT_F16) prof_launch(weights_prep_kernel<f16>, grid, 256, 0, st, t, P, (f16*)dst);
   else prof_launch(weights_prep_kernel<bf16>, grid, 256, 0, st, t, P, (bf16*)dst);
