@@ -734,4 +734,173 @@ int ds_fwd(const DsArgs& a, int dtype, hipStream_t st) {
   return check_launch("ds_fwd");
 }
 
+// ---- LearningToDownsample.dsconv2 (inference): depthwise 3x3 s2 (48 ch) + BN + ReLU and
+// pointwise 48 -> 64 + BN + ReLU in one launch (models/fast_scnn.py:155, _DSConv :64-79) ------
+// The unfused eval path writes the depthwise output (48 channels at H/8: 50 MB fp32 at cfg2) and
+// reads it back in the pointwise GEMM.  Here a workgroup owns 4 output rows x 16 columns: the
+// depthwise outputs (every tap loaded from L2/L1: a stride-2 window shares a third of its input
+// with its neighbour) go to LDS as the pointwise B operand, K zero-padded 48 -> 64, and each wave
+// multiplies one 16-pixel group by the 64 x 64 weights (LDS, split into three bf16 terms for
+// fp32 plans).  Bit-identical to dw_fwd_kernel<T, 2> + the streaming pointwise GEMM
+// (gemm_stream_x3_kernel fp32 / gemm_stream_kernel 16-bit, M >= 4096): the same depthwise fma
+// chain per output (taps row-major, zero-padded taps included), the same folded-BN fma + ReLU and
+// rounding to the storage type, the same MFMA sequence (weights as the A operand, lane (li, lq)
+// holding k = 32 s + 8 lq .. +7, s ascending) and epilogue.
+constexpr int D2_C = 48, D2_CO = 64, D2_TW = 16, D2_R = 4, D2_PX = D2_TW * D2_R;
+constexpr int D2_KV = 8;            // 16-B operand vectors per weight row (K padded to 64)
+constexpr int D2_WST = D2_KV + 1;   // padded LDS row stride (vectors)
+constexpr int D2_DP = 64 + 8;       // depthwise output row (elements, padded) in LDS
+
+template <typename T>
+__global__ __launch_bounds__(256) void ds2_fwd_kernel(Ds2Args a) {
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int NP = F32 ? 3 : 1;
+  __shared__ __attribute__((aligned(16))) uint4 s_w[NP * D2_CO * D2_WST];  // [plane][co][k vec]
+  __shared__ __attribute__((aligned(16))) T s_d[D2_PX * D2_DP];            // [px][k], k >= 48: 0
+  __shared__ __attribute__((aligned(16))) float s_wd[9 * D2_C];            // [tap][c]
+  __shared__ float s_bn[2 * D2_C + 2 * D2_CO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int ow0 = blockIdx.x * D2_TW, oh0 = blockIdx.y * D2_R, n = blockIdx.z;
+  stamp(a.stamps, 0);
+  // pointwise weights: [co][48] storage dtype -> operand vectors (fp32: three truncation planes)
+  for (int i = tid; i < D2_CO * D2_KV; i += 256) {
+    const int r = i / D2_KV, v = i - r * D2_KV, k = v * 8;
+    const bool ok = k < D2_C;
+    const T* src = (const T*)a.wp + (size_t)r * D2_C + (ok ? k : 0);
+    if constexpr (F32) {
+      uint4 lo4 = *reinterpret_cast<const uint4*>(src), hi4 = *reinterpret_cast<const uint4*>(src + 4);
+      if (!ok) lo4 = hi4 = make_uint4(0u, 0u, 0u, 0u);
+      uint4 t[3];
+      gs_split3(lo4, hi4, t);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) s_w[(j * D2_CO + r) * D2_WST + v] = t[j];
+    } else {
+      const uint4 t = *reinterpret_cast<const uint4*>(src);
+      s_w[r * D2_WST + v] = ok ? t : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  for (int i = tid; i < 9 * D2_C; i += 256) s_wd[(i % 9) * D2_C + i / 9] = a.wd[i];
+  if (tid < D2_C) {
+    s_bn[tid] = a.scd[tid];
+    s_bn[D2_C + tid] = a.shd[tid];
+  }
+  if (tid < D2_CO) {
+    s_bn[2 * D2_C + tid] = a.scp[tid];
+    s_bn[2 * D2_C + D2_CO + tid] = a.shp[tid];
+  }
+  // the K padding of the depthwise operand (k = 48 .. 63) is zero
+  for (int i = tid; i < D2_PX * 16; i += 256) st1(s_d + (i >> 4) * D2_DP + D2_C + (i & 15), 0.f);
+  __syncthreads();
+  // ---- depthwise: 64 pixels x 12 channel quads, 3 per thread; all 27 loads in flight ----------
+  const T* X = (const T*)a.x + (size_t)n * a.H * a.W * D2_C;
+  float xv[3][9][4];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int id = tid + 256 * u, px = id / 12, cq = id - px * 12;
+    const int oh = oh0 + px / D2_TW, ow = ow0 + (px & (D2_TW - 1));
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
+        const bool ok = oh < a.Ho && ow < a.Wo && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+        const size_t off = ok ? ((size_t)ih * a.W + iw) * D2_C + 4 * cq : 0;
+        float v[4];
+        ld4v(X + off, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[u][kh * 3 + kw][j] = ok ? v[j] : 0.f;
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int id = tid + 256 * u, px = id / 12, cq = id - px * 12;
+    const int c0 = 4 * cq;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w4 = *reinterpret_cast<const float4*>(s_wd + t * D2_C + c0);
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv[u][t][j], wv[j], acc[j]);
+    }
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = acc[j] * s_bn[c0 + j] + s_bn[D2_C + c0 + j];
+      o[j] = fmaxf(t, 0.f);
+    }
+    st4v(s_d + px * D2_DP + c0, o);
+  }
+  __syncthreads();
+  stamp(a.stamps, 1);
+  // ---- pointwise: wave w = output row oh0 + w, lane li = column ow0 + li ------------------------
+  const int px = wave * D2_TW + li;
+  f32x4 acc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int k = 32 * s + 8 * lq;
+    if constexpr (F32) {
+      const float* d = reinterpret_cast<const float*>(s_d) + px * D2_DP + k;
+      uint4 xs[3];
+      gs_split3(*reinterpret_cast<const uint4*>(d), *reinterpret_cast<const uint4*>(d + 4), xs);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        uint4 w[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) w[j] = s_w[(j * D2_CO + nt * 16 + li) * D2_WST + 4 * s + lq];
+        gs_mma_x3(w, xs, acc[nt]);
+      }
+    } else {
+      const uint4 xs = *reinterpret_cast<const uint4*>(s_d + px * D2_DP + k);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        DsMma<T>::run(s_w[(nt * 16 + li) * D2_WST + 4 * s + lq], xs, acc[nt]);
+    }
+  }
+  const int oh = oh0 + wave, ow = ow0 + li;
+  if (oh < a.Ho && ow < a.Wo) {
+    T* y = (T*)a.y + (((size_t)n * a.Ho + oh) * a.Wo + ow) * a.ldy;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int nl = nt * 16 + 4 * lq;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[nt][r] * s_bn[2 * D2_C + nl + r] + s_bn[2 * D2_C + D2_CO + nl + r];
+        o[r] = fmaxf(v, 0.f);
+      }
+      st4v(y + nl, o);
+    }
+  }
+  stamp(a.stamps, 2);
+}
+
+bool ds2_ok(const Ds2Args& a) {
+  return a.N > 0 && a.N < 65536 && a.H > 0 && a.W > 0 && a.Ho == (a.H - 1) / 2 + 1 &&
+         a.Wo == (a.W - 1) / 2 + 1 && cdiv(a.Ho, D2_R) < 65536 && a.ldy >= D2_CO && a.ldy % 4 == 0 &&
+         ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.y & 15) == 0 && ((uintptr_t)a.wp & 15) == 0 &&
+         a.wd && a.scd && a.shd && a.scp && a.shp;
+}
+
+int ds2_fwd(const Ds2Args& a, int dtype, hipStream_t st) {
+  if (!ds2_ok(a)) {
+    set_error("ds2_fwd: unsupported shape N=%d H=%d W=%d -> %dx%d ldy=%d", a.N, a.H, a.W, a.Ho,
+              a.Wo, a.ldy);
+    return E_UNSUPPORTED;
+  }
+  Ds2Args as = a;
+  as.stamps = stamp_region();
+  const dim3 g(cdiv(a.Wo, D2_TW), cdiv(a.Ho, D2_R), a.N);
+  const double E = dtype == DT_F32 ? 4.0 : 2.0;
+  ProfScope ps(PK_DSCONV, st, E * a.N * ((double)a.H * a.W * D2_C + (double)a.Ho * a.Wo * D2_CO),
+               2.0 * a.N * a.Ho * a.Wo * (9.0 * D2_C + (double)D2_C * D2_CO));
+  if (dtype == DT_F32) prof_launch(ds2_fwd_kernel<float>, g, 256, 0, st, as);
+  else if (dtype == DT_F16) prof_launch(ds2_fwd_kernel<f16>, g, 256, 0, st, as);
+  else prof_launch(ds2_fwd_kernel<bf16>, g, 256, 0, st, as);
+  return check_launch("ds2_fwd");
+}
+
 }  // namespace fscnn

@@ -470,6 +470,20 @@ struct DsArgs {
   unsigned long long* stamps = nullptr;  // (set by the launcher) phase stamps
 };
 bool ds_ok(const DsArgs& a);
+// inference LearningToDownsample.dsconv2 (dsconv.hip ds2_fwd): depthwise 3x3 s2 p1 over 48
+// channels + folded BN + ReLU, pointwise 48 -> 64 + folded BN + ReLU, one launch
+struct Ds2Args {
+  const void* x;             // NHWC [N,H,W] x 48, contiguous, storage dtype
+  int N, H, W, Ho, Wo;
+  const float* wd;           // depthwise weights [48][9] fp32
+  const float *scd, *shd;    // its folded BN
+  const void* wp;            // pointwise weights [64][48], storage dtype
+  const float *scp, *shp;    // its folded BN
+  void* y; int ldy;          // NHWC [N,Ho,Wo] x 64 (row stride ldy)
+  unsigned long long* stamps = nullptr;
+};
+bool ds2_ok(const Ds2Args& a);
+int ds2_fwd(const Ds2Args& a, int dtype, hipStream_t st);
 int ds_rows(int N, int H, int W);
 int ds_fwd(const DsArgs& a, int dtype, hipStream_t st);
 

@@ -986,6 +986,16 @@ struct Exec {
     }();
     return on;
   }
+  // inference LearningToDownsample.dsconv2 in one launch (dsconv.hip ds2_fwd);
+  // FSCNN_LTD2_FUSED=0 runs its depthwise and pointwise launches (the bit-identity test,
+  // tests/test_gpu_switches.py)
+  static bool ltd2_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("FSCNN_LTD2_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   // inference PPM branch convs in one launch (ppm.hip); FSCNN_PPM_FUSED=0 runs the four pointwise
   // launches (the bit-identity test, tests/test_gpu_switches.py)
   static bool ppm_eval_enabled() {
@@ -1078,8 +1088,23 @@ struct Exec {
       TRY(dw(pl.l1dw, net.ltd1.dw, net.ltd1.bdw, act(pl.c0), pl.H1, pl.W1, pl.H2, pl.W2, 2));
       TRY(pw(pl.l1pw, net.ltd1.pw, &net.ltd1.bpw, act(pl.l1dw), true));
     }
-    TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, act(pl.l1pw), pl.H2, pl.W2, pl.H3, pl.W3, 2));
-    TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, act(pl.l2dw), true));
+    {
+      // inference: dsconv2's depthwise s2 + pointwise in one launch (dsconv.hip ds2_fwd), its
+      // 48-channel depthwise output never stored; FSCNN_LTD2_FUSED=0 runs the two launches
+      Ds2Args d2{};
+      const In xin = act(pl.l1pw);
+      d2.x = xin.p; d2.N = N; d2.H = pl.H2; d2.W = pl.W2; d2.Ho = pl.H3; d2.Wo = pl.W3;
+      d2.wd = P(net.ltd2.dw.w); d2.scd = Wf(pl.l2dw.scale); d2.shd = Wf(pl.l2dw.shift);
+      d2.wp = Wg(net.ltd2.pw); d2.scp = Wf(pl.l2pw.scale); d2.shp = Wf(pl.l2pw.shift);
+      d2.y = W(pl.l2pw.a); d2.ldy = pl.l2pw.ld;
+      if (!train && ltd2_enabled() && !xin.sc && xin.ld == 48 && ds2_ok(d2)) {
+        g_prof_tag = "learning_to_downsample.dsconv2 (dw + pw, fused)";
+        TRY(ds2_fwd(d2, dt, r.st));
+      } else {
+        TRY(dw(pl.l2dw, net.ltd2.dw, net.ltd2.bdw, xin, pl.H2, pl.W2, pl.H3, pl.W3, 2));
+        TRY(pw(pl.l2pw, net.ltd2.pw, &net.ltd2.bpw, act(pl.l2dw), true));
+      }
+    }
     // train: the FeatureFusionModule's high-res branch (conv_higher_res + its BN statistics, on
     // the LTD output only) runs on the side stream beside the latency-bound global feature
     // extractor; its BN finish uses the backward's counters and its own team-sum scratch, so it

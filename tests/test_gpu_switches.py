@@ -24,6 +24,9 @@ fresh child process:
 * ``FSCNN_FFM_HI=0``      — (inference) the FFM's high-res branch (conv_higher_res + BN) as its own
   GEMM, added as a stored residual by the fused launch, instead of a second GEMM inside it
   (test_ffm_hi_fused_bit_identical).
+* ``FSCNN_LTD2_FUSED=0``  — (inference) LearningToDownsample.dsconv2 as its depthwise and pointwise
+  launches instead of one (csrc/dsconv.hip ds2_fwd): bit-identical outputs
+  (test_ltd2_fused_bit_identical).
 * ``FSCNN_PPM_FUSED=0``   — (inference) the four PPM branch convs as four pointwise launches instead
   of one launch of 16-row matrix-core tiles (csrc/ppm.hip): bit-identical outputs
   (test_ppm_fused_bit_identical).
@@ -63,7 +66,7 @@ CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
          "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL,
          "FSCNN_DSCONV_FUSED=0": EVAL, "FSCNN_IR_S2=0": EVAL, "FSCNN_FFM_HI=0": EVAL,
-         "FSCNN_PPM_FUSED=0": EVAL,
+         "FSCNN_PPM_FUSED=0": EVAL, "FSCNN_LTD2_FUSED=0": EVAL,
          "FSCNN_IR_TRAIN=1": TRAIN[-1:] + ["tests/test_gpu_bf16_train.py"],
          "FSCNN_IR_TRAIN=2": TRAIN[-1:] + ["tests/test_gpu_bf16_train.py"]}
 
@@ -130,7 +133,8 @@ def test_dsconv_fused_bit_identical(tmp_path):
     default run really took the three fused launches."""
     ref = _stem_worker(tmp_path, "FSCNN_DSCONV_FUSED=0", dsconv=True)
     got = _stem_worker(tmp_path, None, dsconv=True)
-    assert int(ref["stem_launches"]) == 0 and int(got["stem_launches"]) == 3
+    # (+1 in both: LearningToDownsample.dsconv2's fused launch, FSCNN_LTD2_FUSED)
+    assert int(ref["stem_launches"]) == 1 and int(got["stem_launches"]) == 4
     for k in ref:
         if k == "stem_launches":
             continue
@@ -144,7 +148,25 @@ def test_ffm_hi_fused_bit_identical(tmp_path):
     gives bit-identical outputs to its own GEMM launch + the stored residual (FSCNN_FFM_HI=0)."""
     ref = _stem_worker(tmp_path, "FSCNN_FFM_HI=0", dsconv=True)
     got = _stem_worker(tmp_path, None, dsconv=True)
-    assert int(ref["stem_launches"]) == 3 and int(got["stem_launches"]) == 3
+    assert int(ref["stem_launches"]) == 4 and int(got["stem_launches"]) == 4
+    for k in ref:
+        if k == "stem_launches":
+            continue
+        assert np.isfinite(got[k]).all(), k
+        assert np.array_equal(ref[k], got[k]), "%s: max |diff| %g" % (
+            k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
+
+
+def test_ltd2_fused_bit_identical(tmp_path):
+    """LearningToDownsample.dsconv2 in one launch (depthwise 3x3 s2 + BN + ReLU, pointwise
+    48 -> 64 + BN + ReLU; csrc/dsconv.hip ds2_fwd) gives bit-identical outputs to its depthwise
+    and pointwise launches: fp32 / bf16 / fp16 images, autocast fp16, partial 4 x 16 tiles
+    (tests/_stem_worker.py --dsconv: the maps give >= 4096 dsconv2 pixels, where the unfused
+    pointwise takes the streaming GEMM whose MFMA order the fused launch reproduces).  The
+    default run really took the fused launch (4 DSConv launches against 3)."""
+    ref = _stem_worker(tmp_path, "FSCNN_LTD2_FUSED=0", dsconv=True)
+    got = _stem_worker(tmp_path, None, dsconv=True)
+    assert int(ref["stem_launches"]) == 3 and int(got["stem_launches"]) == 4
     for k in ref:
         if k == "stem_launches":
             continue

@@ -47,7 +47,7 @@ FAMILY_RE = {
     "ppm_branches": r"ppm_(fwd|fwd_mma|eval_mma|bwd)_kernel",
     "ir_block": r"ir_block_kernel|ir_train_fwd_kernel",
     "ltd_stem": r"stem_walk_kernel",
-    "dsconv": r"dsconv_fwd_kernel",
+    "dsconv": r"dsconv_fwd_kernel|ds2_fwd_kernel",
 }
 MARK = re.compile(r"bitwise_not")  # torch's bitwise_not kernel (the phase marker: no step uses it)
 
