@@ -539,8 +539,10 @@ int plan_build(const Net& net, int N, int H, int W, int dtype, int train, Plan& 
 // The backward's weight gradients (gemm_tn, colsum, depthwise / conv0 wgrad) only feed the
 // deferred slab reduction at the end of their stage, so they run on a second stream, beside
 // the dgrad -> BN-backward chain that carries the critical path: many of those launches are
-// latency-bound and leave HBM idle.  Every event recorded on a stream costs that stream ~7 us
-// of idle time on MI355X (measured: 61 such gaps = 0.43 ms of a 7.05 ms step), so events are
+// latency-bound and leave HBM idle.  Every event recorded on a stream costs that stream ~5-7 us
+// of idle time on MI355X (measured: 61 such gaps = 0.43 ms of a 7.05 ms step; r06: two extra
+// forks per flush +0.41 ms per step; forking every 2nd / 3rd flush +0.28 / +0.35 ms: the wgrads
+// start later), less without the events' system-scope fence (SideStream::init), so events are
 // kept to one fork per wgrad launch (Exec::side_launch) and one join before the stage's slab
 // reduction: every BN-backward output dz and operand table a wgrad reads has its own slot in
 // the step's arenas (no reuse, so no release events; 7.08 -> 7.00 ms/step).
@@ -593,9 +595,22 @@ struct SideStream {
     } else if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       return false;
     }
+    // fork / join events without the system-scope fence: a default event record writes back and
+    // invalidates the L2s (host visibility) and the next kernels start cold.  Both ends of these
+    // events are kernels of this device, whose dispatch packets carry their own agent-scope
+    // acquire / release (the cross-XCD coherence every same-stream kernel pair already relies
+    // on), and no host code inspects them.  Measured r06: 5.585 / 5.599 vs 5.677 / 5.692 ms per
+    // cfg3 step (same box; device-scope-release events 5.693 / 5.696); every side-stream path stays
+    // bit-identical to one stream (test_switch_train_steps_bit_identical_with_dropout).
+    // FSCNN_SIDE_FENCE=1 restores the default (fenced) events.
+    static const unsigned evf = [] {
+      const char* e = getenv("FSCNN_SIDE_FENCE");
+      return (unsigned)hipEventDisableTiming |
+             (e && e[0] == '1' ? 0u : (unsigned)hipEventDisableSystemFence);
+    }();
     hipEvent_t* ev[2] = {&fork, &join};
     for (auto* e : ev)
-      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
+      if (hipEventCreateWithFlags(e, evf) != hipSuccess) return false;
     ready = true;
     failed = false;
     return true;

@@ -11,6 +11,8 @@ fresh child process:
   conv0's weight gradient its own launch, instead of the fused ltd_c0_bwd pass;
 * ``FSCNN_SIDE_PRIO=0``   — the weight-gradient side stream as a plain stream instead of one at
   the device's lowest priority;
+* ``FSCNN_SIDE_FENCE=1``  — the side stream's fork / join events with the default system-scope
+  fence (the default drops it: both ends are kernels of the device); train steps bit-identical;
 * ``FSCNN_DROP_FUSED=0``  — the classifier's Dropout backward and dsconv2 pw's BN-backward reduce
   as their own passes instead of in the classifier conv's dgrad epilogue (the fused form runs only
   at M >= 4096 low-res pixels in 16-bit plans: test_drop_fused_matches_separate_passes).
@@ -64,6 +66,7 @@ BF16 = ["tests/test_gpu_model.py::test_bf16_forward_within_bf16_budget"]
 CASES = {"FSCNN_SIDE_STREAM=0": TRAIN, "FSCNN_F32_SPLIT=0": EVAL,
          "FSCNN_GRAPHS=1": TRAIN + EVAL + HEAD16 + ["tests/test_gpu_autograd.py"],
          "FSCNN_LTD_FUSED=0": TRAIN[-1:] + BF16, "FSCNN_SIDE_PRIO=0": TRAIN[:1],
+         "FSCNN_SIDE_FENCE=1": TRAIN[:1],
          "FSCNN_DROP_FUSED=0": TRAIN[:1] + HEAD16, "FSCNN_STEM_FUSED=0": EVAL,
          "FSCNN_DSCONV_FUSED=0": EVAL, "FSCNN_IR_S2=0": EVAL, "FSCNN_FFM_HI=0": EVAL,
          "FSCNN_PPM_FUSED=0": EVAL, "FSCNN_LTD2_FUSED=0": EVAL,
@@ -191,7 +194,7 @@ def test_ppm_fused_bit_identical(tmp_path):
             k, float(np.abs(ref[k].astype(np.float64) - got[k]).max()))
 
 
-@pytest.mark.parametrize("switch", ["FSCNN_GRAPHS=1", "FSCNN_SIDE_STREAM=0"])
+@pytest.mark.parametrize("switch", ["FSCNN_GRAPHS=1", "FSCNN_SIDE_STREAM=0", "FSCNN_SIDE_FENCE=1"])
 def test_switch_train_steps_bit_identical_with_dropout(tmp_path, switch):
     ref = _worker(tmp_path, None)
     got = _worker(tmp_path, switch)
