@@ -83,15 +83,16 @@ __global__ __launch_bounds__(256) void up_nchw_kernel(UpArgs a) {
 }
 
 // Row-group form (the 1.27 GB fp32 write of cfg2 is the whole cost, so stores are what matter):
-// a workgroup owns UPR_R consecutive output rows of image n and UPR_COLS columns.  The source
+// a workgroup owns UPR_RS consecutive output rows of image n and UPR_COLS columns.  The source
 // rows they read, [i0(first row), i1(last row)] (at most `rows` of them, bounded on the host), are
 // staged once in LDS class-major [row][C][Wi+1] in fp32; then every thread produces 4
-// consecutive columns of each class plane of each of the UPR_R rows and writes them with 16-B
+// consecutive columns of each class plane of each of the UPR_RS rows and writes them with 16-B
 // (fp32) / 8-B (bf16) non-temporal stores.  Same weights and the same W-then-H expression as aten,
 // so the fp32 result is bit-identical to the per-pixel kernel above.
 constexpr int UPR_THREADS = 512;
 constexpr int UPR_COLS = 4 * UPR_THREADS;
-constexpr int UPR_R = 8;
+constexpr int UPR_R = 8;   // output rows per workgroup of up_argmax
+constexpr int UPR_RS = 4;  // ... of up_nchw_rows (the logits upsample)
 constexpr int UPR_MAXROWS = 4;  // staged source rows per group (host-checked)
 
 typedef float upr_f4 __attribute__((ext_vector_type(4)));
@@ -111,22 +112,40 @@ __device__ __forceinline__ void st4_nt(f16* p, const float (&v)[4]) {
   __builtin_nontemporal_store(t, (upr_u2*)p);
 }
 
-template <typename TI, typename TO, bool VEC>
+template <typename TI, typename TO, bool VEC, int RR>
 __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
   extern __shared__ float s_rows[];  // [rows][C][Wi + 1] (padded: the staging stores walk c)
-  const int ho0 = blockIdx.y * UPR_R, n = blockIdx.z;
-  const int ho1 = min(ho0 + UPR_R, a.Ho) - 1;
+  const int ho0 = blockIdx.y * RR, n = blockIdx.z;
+  const int ho1 = min(ho0 + RR, a.Ho) - 1;
   const float sh = ac_scale(a.Hi, a.Ho);
   const int lo = ac_lerp(ho0, a.Hi, a.Ho, sh).i0;
   const int nrows = ac_lerp(ho1, a.Hi, a.Ho, sh).i1 - lo + 1;  // <= host bound
   const int WP = a.Wi + 1, CWP = a.C * WP, CW = a.C * a.Wi;
   const TI* xb = (const TI*)a.x + ((size_t)n * a.Hi + lo) * a.Wi * a.ldx;
-  // stage: element e = (r, wi, c) with c fastest in global memory (NHWC), class-major in LDS
-  for (int e = threadIdx.x; e < nrows * CW; e += UPR_THREADS) {
-    const int r = e / CW;
-    const int rem = e - r * CW;
-    const int wi = rem / a.C, c = rem - wi * a.C;
-    s_rows[r * CWP + c * WP + wi] = ld1(xb + ((size_t)r * a.Wi + wi) * a.ldx + c);
+  // stage: element e = (r, wi, c) with c fastest in global memory (NHWC), class-major in LDS;
+  // 8 loads per thread in flight per batch (one element per iteration was a chain of memory
+  // round trips before the first store of the workgroup)
+  const int ne = nrows * CW;
+  for (int e0 = threadIdx.x; e0 < ne; e0 += 8 * UPR_THREADS) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * UPR_THREADS, ec = e < ne ? e : e0;
+      const int r = ec / CW;
+      const int rem = ec - r * CW;
+      const int wi = rem / a.C, c = rem - wi * a.C;
+      v[u] = ld1(xb + ((size_t)r * a.Wi + wi) * a.ldx + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * UPR_THREADS;
+      if (e < ne) {
+        const int r = e / CW;
+        const int rem = e - r * CW;
+        const int wi = rem / a.C, c = rem - wi * a.C;
+        s_rows[r * CWP + c * WP + wi] = v[u];
+      }
+    }
   }
   __syncthreads();
   const int wo0 = blockIdx.x * UPR_COLS + threadIdx.x * 4;
@@ -139,7 +158,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
   TO* yb = (TO*)a.y + (size_t)n * a.C * plane + wo0;
   for (int c = 0; c < a.C; ++c) {
     // W-interpolation of each staged source row for this thread's 4 columns (aten's inner
-    // bracket), computed once and shared by the UPR_R output rows
+    // bracket), computed once and shared by the RR output rows
     float wr[UPR_MAXROWS][4];
 #pragma unroll
     for (int r = 0; r < UPR_MAXROWS; ++r) {
@@ -174,7 +193,7 @@ __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
 }
 
 // largest number of source rows any UPR_R-row group reads (host copy of the kernel's bound)
-static int upr_max_rows(int Hi, int Ho) {
+static int upr_max_rows(int Hi, int Ho, int UPR_R = fscnn::UPR_R) {
   const float sh = ac_scale(Hi, Ho);
   int mx = 0;
   for (int g0 = 0; g0 < Ho; g0 += UPR_R) {
@@ -192,14 +211,17 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
                (in_dtype == DT_F32 ? 4.0 : 2.0) * a.N * a.C * a.Hi * a.Wi +
                    (out_dtype == DT_F32 ? 4.0 : 2.0) * (double)a.N * a.C * a.Ho * a.Wo,
                7.0 * a.N * a.C * a.Ho * a.Wo);
-  const size_t lds = (size_t)upr_max_rows(a.Hi, a.Ho) * a.C * (a.Wi + 1) * sizeof(float);
-  if (lds <= 64 * 1024 && a.N <= 65535 && upr_max_rows(a.Hi, a.Ho) <= UPR_MAXROWS) {
-    dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)cdiv(a.Ho, UPR_R), (unsigned)a.N);
+  // 4 output rows per workgroup: 2048 workgroups at cfg2 (r06 rocprof: 254 vs 262 us with 8 rows,
+  // 255 with 2; 16 / 24 rows leave the chip underfilled, +350 us)
+  constexpr int RR = UPR_RS;
+  const size_t lds = (size_t)upr_max_rows(a.Hi, a.Ho, RR) * a.C * (a.Wi + 1) * sizeof(float);
+  if (lds <= 64 * 1024 && a.N <= 65535 && upr_max_rows(a.Hi, a.Ho, RR) <= UPR_MAXROWS) {
+    dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)cdiv(a.Ho, RR), (unsigned)a.N);
     const bool vec = a.Wo % 4 == 0;
 #define UPR_LAUNCH(TI, TO)                                                              \
   do {                                                                                  \
-    if (vec) prof_launch(up_nchw_rows_kernel<TI, TO, true>, g, UPR_THREADS, lds, st, a);         \
-    else prof_launch(up_nchw_rows_kernel<TI, TO, false>, g, UPR_THREADS, lds, st, a);            \
+    if (vec) prof_launch(up_nchw_rows_kernel<TI, TO, true, RR>, g, UPR_THREADS, lds, st, a);     \
+    else prof_launch(up_nchw_rows_kernel<TI, TO, false, RR>, g, UPR_THREADS, lds, st, a);        \
   } while (0)
     if (in_dtype == DT_F32 && out_dtype == DT_F32) UPR_LAUNCH(float, float);
     else if (in_dtype == DT_F16 && out_dtype == DT_F16) UPR_LAUNCH(f16, f16);
