@@ -550,7 +550,7 @@ int reduce_slabs_ex(float* slab, int S, long long stride, long long count, float
                     int accumulate, int C9, hipStream_t st);
 // Deferred weight-gradient reductions: the slab reductions of a backward stage are queued and run
 // by two launches (fold + final) over the whole job table instead of two per weight tensor.
-constexpr int RED_MAXJOBS = 48;
+constexpr int RED_MAXJOBS = 64;  // a whole step's weight-gradient jobs (one multi-stage call)
 struct RedJob {
   float* slab;   // [S][stride] partials (consumed)
   float* out;

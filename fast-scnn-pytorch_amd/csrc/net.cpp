@@ -858,7 +858,7 @@ struct Exec {
   }
   int defer_reduce(float* slab, int S, long long count, float* out, int C9) {
     if (red.n == RED_MAXJOBS) {  // (a stage has <= ~20 jobs; flushing here would let later
-      set_error("defer_reduce: more than %d jobs in one stage", RED_MAXJOBS);  // slabs overlap)
+      set_error("defer_reduce: more than %d jobs in one call", RED_MAXJOBS);  // slabs overlap)
       return E_INVALID;
     }
     if (count <= 0 || count > 0x7fffffff) {
@@ -2228,7 +2228,11 @@ int net_backward_impl(const Plan& pl, const RunArgs& r, int stage_from, int stag
           TRY(ex.backward_ltd());
           break;
       }
-      TRY(ex.flush_reduce());  // the stage's gradient bucket is complete after this
+      // the stage's gradient bucket is complete after its reduction; a call covering several
+      // stages (no per-stage consumer between them: fast_scnn.py without a grad_stage_hook)
+      // reduces every stage's slabs once at its end, so the main stream never waits for the
+      // side stream's weight gradients mid-step (the slab arena holds the whole step's slabs)
+      if (s == stage_to) TRY(ex.flush_reduce());
     }
     return ex.join();  // the caller's stream sees every gradient
   });

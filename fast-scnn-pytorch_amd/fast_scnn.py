@@ -682,38 +682,45 @@ class FastSCNN(nn.Module):
         if getattr(self, "_keep_ws", False):
             self._debug["bws"] = bws
         hook = self.grad_stage_hook
-        for s in range(4):
+        if hook is None:
+            # one native call for the four stages: their weight-gradient reductions run once at
+            # its end, so the main stream does not wait for the side stream between stages
             with torch.cuda.device(x.device):
-                self._backward_stage(plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p,
-                                     dx)
-            if hook is not None:
+                self._backward_stage(plan, (0, 3), gout, gaux, gloss, loss2, x, ar, G, ws, bws,
+                                     seed, p, dx)
+        else:
+            for s in range(4):
+                with torch.cuda.device(x.device):
+                    self._backward_stage(plan, (s, s), gout, gaux, gloss, loss2, x, ar, G, ws,
+                                         bws, seed, p, dx)
                 b, e = nat.stage_ranges[s]
                 hook(s, G, b, e)
         return [G[off:off + numel].view(prm.shape)
                 for prm, (_, off, numel) in zip(ar["params"], nat.params)]
 
-    def _backward_stage(self, plan, s, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p,
+    def _backward_stage(self, plan, stages, gout, gaux, gloss, loss2, x, ar, G, ws, bws, seed, p,
                         dx=None):
+        s0, s1 = stages  # backward stages s0 .. s1 (0: head ... 3: LearningToDownsample)
         if dx is not None:  # the general entry point: also writes the input gradient (stage 3)
             _lib.call("fscnn_backward_dx", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(gloss),
                       _lib.ptr(loss2), _lib.ptr(x), _lib.dtype_code(x.dtype), _lib.ptr(dx),
                       _lib.dtype_code(dx.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s0, s1,
                       _lib.stream_ptr(x.device))
         elif gloss is None and self.aux:
             _lib.call("fscnn_backward_aux", plan, _lib.ptr(gout), _lib.ptr(gaux), _lib.ptr(x),
                       _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s0, s1,
                       _lib.stream_ptr(x.device))
         elif gloss is None:
             _lib.call("fscnn_backward", plan, _lib.ptr(gout), _lib.ptr(x),
                       _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s0, s1,
                       _lib.stream_ptr(x.device))
         else:
             _lib.call("fscnn_backward_loss", plan, _lib.ptr(gloss), _lib.ptr(loss2), _lib.ptr(x),
                       _lib.dtype_code(x.dtype), _lib.ptr(ar["P"]), _lib.ptr(G), _lib.ptr(ws),
-                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s, s,
+                      _lib.ptr(bws), _lib.c_ull(seed), _lib.c_float(p), s0, s1,
                       _lib.stream_ptr(x.device))
 
     def _needs_graph(self, x):
