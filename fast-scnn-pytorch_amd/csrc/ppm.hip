@@ -238,38 +238,66 @@ __global__ __launch_bounds__(PPM_T) void ppm_fwd_mma_kernel(PpmFwdArgs a) {
   stamp(a.stamps, 4);
 }
 
-// inference: one wave per 16-row tile of any branch, y = relu(z * scale + shift) with the folded
-// eval BN (b.f.scale / b.f.shift as inputs), the tiled GEMM's epilogue arithmetic
+// inference: two waves per 16-row tile of any branch, wave w the 16 output channels 16w .. 16w+15
+// (each wave's MFMA sequence is the pair form's for its column tile: the same values), y =
+// relu(z * scale + shift) with the folded eval BN (b.f.scale / b.f.shift as inputs), the tiled
+// GEMM's epilogue arithmetic
+template <typename T, bool X3>
+__device__ __forceinline__ void ppm_mma1(const PpmFrag<T>& a, const PpmFrag<T>& b, f32x4& acc) {
+  constexpr int NCH = PpmFrag<T>::NCH;
+  acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if constexpr (X3) {
+      uint4 a3[3], b3[3];
+      gs_split3(a.v[c][0], a.v[c][1], a3);
+      gs_split3(b.v[c][0], b.v[c][1], b3);
+      gs_mma_x3(a3, b3, acc);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint4 av = a.v[c][h], bv = b.v[c][h];
+        if constexpr (sizeof(T) == 4) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.x), __uint_as_float(bv.x), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.y), __uint_as_float(bv.y), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.z), __uint_as_float(bv.z), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.w), __uint_as_float(bv.w), acc, 0, 0, 0);
+        } else if constexpr (std::is_same<T, f16>::value) {
+          h16x8 a8, b8;
+          __builtin_memcpy(&a8, &av, 16);
+          __builtin_memcpy(&b8, &bv, 16);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, acc, 0, 0, 0);
+        } else {
+          i16x8 a8, b8;
+          __builtin_memcpy(&a8, &av, 16);
+          __builtin_memcpy(&b8, &bv, 16);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, acc, 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
 template <typename T>
-__global__ __launch_bounds__(64) void ppm_eval_mma_kernel(PpmFwdArgs a) {
+__global__ __launch_bounds__(128) void ppm_eval_mma_kernel(PpmFwdArgs a) {
   int t = blockIdx.x, bi = 0;
   while (bi + 1 < a.nb && t >= (a.b[bi].M + 15) / 16) t -= (a.b[bi++].M + 15) / 16;
   const PpmBranchFwd& b = a.b[bi];
-  const int M = b.M, lane = threadIdx.x, li = lane & 15, lq = lane >> 4;
+  const int M = b.M, lane = threadIdx.x & 63, nt = threadIdx.x >> 6, li = lane & 15, lq = lane >> 4;
   const int r = t * 16 + li;
-  const T* Wt = (const T*)b.w;
-  PpmFrag<T> bw[2], af;
-  bw[0].load(Wt + (size_t)li * PPM_K, lq);
-  bw[1].load(Wt + (size_t)(16 + li) * PPM_K, lq);
+  const int c = nt * 16 + li;
+  PpmFrag<T> bw, af;
+  bw.load((const T*)b.w + (size_t)c * PPM_K, lq);
   af.load((const T*)b.x + (size_t)(r < M ? r : 0) * PPM_K, lq);
-  float sc[2], sh[2];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    sc[nt] = b.f.scale[nt * 16 + li];
-    sh[nt] = b.f.shift[nt * 16 + li];
-  }
-  f32x4 acc[2];
-  ppm_mma<T, sizeof(T) == 4>(af, bw, acc);
+  const float sc = b.f.scale[c], sh = b.f.shift[c];
+  f32x4 acc;
+  ppm_mma1<T, sizeof(T) == 4>(af, bw, acc);
   T* Y = (T*)b.y;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int c = nt * 16 + li;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int m = t * 16 + lq * 4 + q;
-      const float v = acc[nt][q] * sc[nt] + sh[nt];
-      if (m < M) st1(Y + (size_t)m * b.ldy + c, fmaxf(v, 0.f));
-    }
+  for (int q = 0; q < 4; ++q) {
+    const int m = t * 16 + lq * 4 + q;
+    const float v = acc[q] * sc + sh;
+    if (m < M) st1(Y + (size_t)m * b.ldy + c, fmaxf(v, 0.f));
   }
 }
 
@@ -536,9 +564,9 @@ int ppm_branches_fwd(const PpmFwdArgs& a, int dtype, hipStream_t st) {
     for (int i = 0; i < a.nb; ++i) tiles += (unsigned)((a.b[i].M + 15) / 16);
     ProfScope ps(PK_PPM, st, rows * (a.K + PPM_C) * (dtype == DT_F32 ? 4 : 2),
                  2.0 * a.K * PPM_C * rows);
-    if (dtype == DT_F32) prof_launch(ppm_eval_mma_kernel<float>, tiles, 64, 0, st, a);
-    else if (dtype == DT_F16) prof_launch(ppm_eval_mma_kernel<f16>, tiles, 64, 0, st, a);
-    else prof_launch(ppm_eval_mma_kernel<bf16>, tiles, 64, 0, st, a);
+    if (dtype == DT_F32) prof_launch(ppm_eval_mma_kernel<float>, tiles, 128, 0, st, a);
+    else if (dtype == DT_F16) prof_launch(ppm_eval_mma_kernel<f16>, tiles, 128, 0, st, a);
+    else prof_launch(ppm_eval_mma_kernel<bf16>, tiles, 128, 0, st, a);
     return check_launch("ppm_branches_fwd");
   }
   if (!ppm_check(a.nb, a.K, a.C, maxM, dtype)) return E_INVALID;
