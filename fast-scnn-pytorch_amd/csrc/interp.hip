@@ -112,7 +112,7 @@ __device__ __forceinline__ void st4_nt(f16* p, const float (&v)[4]) {
   __builtin_nontemporal_store(t, (upr_u2*)p);
 }
 
-template <typename TI, typename TO, bool VEC, int RR>
+template <typename TI, typename TO, bool VEC, int RR, int MAXR = UPR_MAXROWS>
 __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
   extern __shared__ float s_rows[];  // [rows][C][Wi + 1] (padded: the staging stores walk c)
   const int ho0 = blockIdx.y * RR, n = blockIdx.z;
@@ -156,29 +156,39 @@ __global__ __launch_bounds__(UPR_THREADS) void up_nchw_rows_kernel(UpArgs a) {
   for (int j = 0; j < 4; ++j) lw[j] = ac_lerp(min(wo0 + j, a.Wo - 1), a.Wi, a.Wo, sw);
   const size_t plane = (size_t)a.Ho * a.Wo;
   TO* yb = (TO*)a.y + (size_t)n * a.C * plane + wo0;
+  // the RR output rows' H-interpolation (staged-row indices and weights), once for every class
+  Lerp lh[RR];
+#pragma unroll
+  for (int q = 0; q < RR; ++q) {
+    lh[q] = ac_lerp(min(ho0 + q, a.Ho - 1), a.Hi, a.Ho, sh);
+    lh[q].i0 -= lo;
+    lh[q].i1 -= lo;
+  }
   for (int c = 0; c < a.C; ++c) {
     // W-interpolation of each staged source row for this thread's 4 columns (aten's inner
     // bracket), computed once and shared by the RR output rows
-    float wr[UPR_MAXROWS][4];
+    float wr[MAXR][4];
 #pragma unroll
-    for (int r = 0; r < UPR_MAXROWS; ++r) {
+    for (int r = 0; r < MAXR; ++r) {
       const float* row = s_rows + min(r, nrows - 1) * CWP + c * WP;
 #pragma unroll
       for (int j = 0; j < 4; ++j) wr[r][j] = lerp2(lw[j].l0, row[lw[j].i0], lw[j].l1, row[lw[j].i1]);
     }
-    for (int ho = ho0; ho <= ho1; ++ho) {
-      const Lerp lh = ac_lerp(ho, a.Hi, a.Ho, sh);
-      const int d0 = lh.i0 - lo, d1 = lh.i1 - lo;
+#pragma unroll
+    for (int q = 0; q < RR; ++q) {
+      const int ho = ho0 + q;
+      if (ho > ho1) break;
+      const int d0 = lh[q].i0, d1 = lh[q].i1;
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float x0 = wr[0][j], x1 = wr[0][j];
 #pragma unroll
-        for (int r = 1; r < UPR_MAXROWS; ++r) {  // register selects, no dynamic indexing
+        for (int r = 1; r < MAXR; ++r) {  // register selects, no dynamic indexing
           x0 = d0 == r ? wr[r][j] : x0;
           x1 = d1 == r ? wr[r][j] : x1;
         }
-        o[j] = lerp2(lh.l0, x0, lh.l1, x1);
+        o[j] = lerp2(lh[q].l0, x0, lh[q].l1, x1);
       }
       TO* yp = yb + c * plane + (size_t)ho * a.Wo;
       if (VEC && wo0 + 4 <= a.Wo) {
@@ -218,9 +228,13 @@ int up_nchw(const UpArgs& a, int in_dtype, int out_dtype, hipStream_t st) {
   if (lds <= 64 * 1024 && a.N <= 65535 && upr_max_rows(a.Hi, a.Ho, RR) <= UPR_MAXROWS) {
     dim3 g((unsigned)cdiv(a.Wo, UPR_COLS), (unsigned)cdiv(a.Ho, RR), (unsigned)a.N);
     const bool vec = a.Wo % 4 == 0;
+    // staged rows per group (3 at cfg2's x8): the W-interpolations and selects of that many
+    const int mr = upr_max_rows(a.Hi, a.Ho, RR);
 #define UPR_LAUNCH(TI, TO)                                                              \
   do {                                                                                  \
-    if (vec) prof_launch(up_nchw_rows_kernel<TI, TO, true, RR>, g, UPR_THREADS, lds, st, a);     \
+    if (vec && mr <= 2) prof_launch(up_nchw_rows_kernel<TI, TO, true, RR, 2>, g, UPR_THREADS, lds, st, a); \
+    else if (vec && mr == 3) prof_launch(up_nchw_rows_kernel<TI, TO, true, RR, 3>, g, UPR_THREADS, lds, st, a); \
+    else if (vec) prof_launch(up_nchw_rows_kernel<TI, TO, true, RR>, g, UPR_THREADS, lds, st, a); \
     else prof_launch(up_nchw_rows_kernel<TI, TO, false, RR>, g, UPR_THREADS, lds, st, a);        \
   } while (0)
     if (in_dtype == DT_F32 && out_dtype == DT_F32) UPR_LAUNCH(float, float);
