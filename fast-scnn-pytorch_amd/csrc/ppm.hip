@@ -306,7 +306,7 @@ __global__ __launch_bounds__(128) void ppm_eval_mma_kernel(PpmFwdArgs a) {
 // gradient's k and of the input gradient's rows — one workgroup per branch was LDS-bound on the
 // 288-row branch's dx (2 LDS reads per FMA on one CU)
 //
-// MMA (16-bit plans, K = 128, M <= 288; one workgroup per branch, r06): the branch's pooled rows are
+// MMA (16-bit plans, K = 128, M <= 288; up to 4 workgroups per branch, r06): the branch's pooled rows are
 // staged in LDS beside dz and W, and both products run on the matrix cores -- dW (32 x K, reduced
 // over M) as 2 x 8 tiles of v_mfma_f32_16x16x32 over 32-row steps, dX (M x K, reduced over the 32
 // channels) as one MFMA per 16 x 16 tile.  (The FMA form's weight gradient walked each k column
@@ -435,7 +435,8 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
     // dW[c][k] = sum_m dz[m][c] x[m][k]: A = dz^T (row c, 8 consecutive m), B = x (col k, same m)
     // (three 32-row steps per iteration, their LDS reads issued together; steps past M add
     //  zero products)
-    for (int t = wave; t < 2 * (K / 16); t += PPM_T / 64) {
+    // (NG workgroups per branch: workgroup gpart takes tiles wave + 8 gpart + 8 NG i)
+    for (int t = wave + 8 * gpart; t < 2 * (K / 16); t += 8 * NG) {
       const int ct = t & 1, kt = t >> 1;
       const int c = ct * 16 + li, k = kt * 16 + li;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -463,11 +464,11 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
     // three tiles per iteration (reads together)
     T* DX = (T*)b.dx;
     const int mt_n = (M + 15) / 16, ntile = mt_n * (K / 16);
-    for (int t0 = wave; t0 < ntile; t0 += 3 * (PPM_T / 64)) {
+    for (int t0 = wave + 8 * gpart; t0 < ntile; t0 += 24 * NG) {
       float av[3][8], bv[3][8];
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const int t = t0 + u * (PPM_T / 64), tt = t < ntile ? t : t0;
+        const int t = t0 + u * 8 * NG, tt = t < ntile ? t : t0;
         const int mt = tt % mt_n, kt = tt / mt_n;
         const int m = mt * 16 + li, k = kt * 16 + li;
         const int mm = m < M ? m : 0;  // (rows past M: garbage rows of A, never stored)
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(PPM_T) void ppm_bwd_kernel(PpmBwdArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const int t = t0 + u * (PPM_T / 64);
+        const int t = t0 + u * 8 * NG;
         const int mt = t % mt_n, kt = t / mt_n;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         Op::mma(Op::pack(av[u]), Op::pack(bv[u]), acc);
@@ -601,10 +602,13 @@ int ppm_branches_bwd(const PpmBwdArgs& a, int dtype, hipStream_t st) {
   b.wg0[0] = 0;
   b.stamps = stamp_region();
   if (dtype != DT_F32 && a.K == PPM_K && maxM <= 288) {  // one workgroup per branch
-    for (int i = 0; i < a.nb; ++i) b.wg0[i + 1] = i + 1;
+    // up to 4 workgroups per branch (one per 64 rows): each recomputes the branch's BN-backward
+    // sums and dz, and takes every NG-th group of 8 dW / dX tiles (the 288-row branch's 144 dX
+    // tiles were 18 per wave on one CU)
+    for (int i = 0; i < a.nb; ++i) b.wg0[i + 1] = b.wg0[i] + std::max(1, std::min(4, a.b[i].M / 64));
     const size_t l2 = lds + 16 + (size_t)maxM * a.K * 2;
-    if (dtype == DT_F16) prof_launch(ppm_bwd_kernel<f16, true>, a.nb, PPM_T, l2, st, b);
-    else prof_launch(ppm_bwd_kernel<bf16, true>, a.nb, PPM_T, l2, st, b);
+    if (dtype == DT_F16) prof_launch(ppm_bwd_kernel<f16, true>, b.wg0[a.nb], PPM_T, l2, st, b);
+    else prof_launch(ppm_bwd_kernel<bf16, true>, b.wg0[a.nb], PPM_T, l2, st, b);
     return check_launch("ppm_branches_bwd");
   }
   for (int i = 0; i < a.nb; ++i) b.wg0[i + 1] = b.wg0[i] + std::max(1, std::min(16, a.b[i].M / 32));
